@@ -1,0 +1,233 @@
+/*
+ * orx.h — C ABI of the MI355X-native render core (liborx.so).
+ *
+ * This is the drop-in boundary for ico-eagleye/OppositeRenderer's
+ * `OptixRenderer` (RenderEngine/renderer/OptixRenderer.h:21-43) and the
+ * parts of `IScene` (RenderEngine/scene/IScene.h:16-29) that the renderer
+ * consumes.  Plain pointers and sizes only; no C++ or torch types cross it.
+ * Errors never throw: every call returns an orx_status and the message of
+ * the last failure is kept per renderer (orx_last_error), replacing the
+ * reference's std::exception(const char*) (OptixRenderer.cpp:816-820).
+ *
+ * Reference entry point -> orx call
+ *   OptixRenderer::OptixRenderer() + initialize(ComputeDevice)
+ *       (OptixRenderer.cpp:81-104, :113-400)              -> orx_create
+ *   OptixRenderer::initScene(IScene&) (:436-485)          -> orx_init_scene
+ *   OptixRenderer::renderNextIteration(...) (:507-821)    -> orx_render_next_iteration
+ *   OptixRenderer::getOutputBuffer(void*) (:860-865)      -> orx_get_output
+ *   getWidth/getHeight/getScreenBufferSizeBytes (:850-870)-> orx_width/orx_height/orx_output_bytes
+ *   OptixRenderer::EMITTED_PHOTONS_PER_ITERATION (.h:43)  -> orx_emitted_photons_per_iteration
+ *   ~OptixRenderer() (:106-111)                           -> orx_destroy
+ */
+#ifndef ORX_H
+#define ORX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORX_ABI_VERSION 1u
+
+typedef struct orx_renderer orx_renderer;
+
+typedef enum {
+    ORX_OK = 0,
+    ORX_ERR_INVALID_ARGUMENT = 1,
+    ORX_ERR_STATE = 2,          /* e.g. initScene before initialize, render before initScene */
+    ORX_ERR_DEVICE = 3,         /* HIP runtime failure */
+    ORX_ERR_NO_LIGHTS = 4,      /* "No lights exists in this scene." (OptixRenderer.cpp:444-447) */
+    ORX_ERR_GRID_TOO_LARGE = 5, /* "Too many cells in SpatialHash.cu" (OptixRenderer_SpatialHash.cu:243-247) */
+    ORX_ERR_OUT_OF_MEMORY = 6,
+    ORX_ERR_UNSUPPORTED = 7
+} orx_status;
+
+/* RenderMethod::E order (RenderEngine/renderer/RenderMethod.h:13-19). */
+typedef enum {
+    ORX_METHOD_PATH_TRACING = 0,
+    ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING = 1,
+    ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING = 2
+} orx_method;
+
+/* Camera inputs (Camera.h:72-79).  The engine derives lookdir / camera_u /
+ * camera_v exactly as Camera::setup (Camera.cpp:333-345). */
+typedef struct {
+    float eye[3];
+    float lookat[3];
+    float up[3];
+    float hfov;     /* degrees */
+    float vfov;     /* degrees */
+    float aperture; /* > 0 enables thin-lens depth of field (helpers/camera.h:11-27) */
+} orx_camera;
+
+/* RenderServerRenderRequestDetails (clientserver/RenderServerRenderRequestDetails.h:15-33). */
+typedef struct {
+    orx_camera camera;
+    int32_t method;  /* orx_method */
+    uint32_t width;
+    uint32_t height;
+    double ppm_alpha;
+} orx_request;
+
+/* Material classes of RenderEngine/material (one per .cpp). */
+typedef enum {
+    ORX_MAT_DIFFUSE = 0,         /* Diffuse(Kd)                           Diffuse.cpp:17-20  */
+    ORX_MAT_DIFFUSE_EMITTER = 1, /* DiffuseEmitter(power, Kd)+inverseArea DiffuseEmitter.cpp:17-25 */
+    ORX_MAT_MIRROR = 2,          /* Mirror(Kr)                            Mirror.cpp:17-20   */
+    ORX_MAT_GLASS = 3,           /* Glass(ior, Kr, Kt)                    Glass.cpp:17-22    */
+    ORX_MAT_GLOSSY = 4           /* Glossy(Kd, Ks, exponent)              Glossy.cpp:16-33   */
+} orx_material_type;
+
+typedef struct {
+    int32_t type;        /* orx_material_type */
+    float Kd[3];         /* diffuse albedo (Diffuse, Glossy, DiffuseEmitter) */
+    float Ks[3];         /* Glossy specular */
+    float Kr[3];         /* Mirror / Glass reflectance */
+    float Kt[3];         /* Glass transmittance */
+    float ior;           /* Glass index of refraction */
+    float exponent;      /* Glossy Phong exponent */
+    float power[3];      /* DiffuseEmitter power (scaled by Kd inside the engine, as the ctor does) */
+    float inverse_area;  /* DiffuseEmitter 1/area of the emitting quad */
+} orx_material;
+
+/* Light::LightType (renderer/Light.h:14-54). */
+typedef enum { ORX_LIGHT_AREA = 0, ORX_LIGHT_POINT = 1, ORX_LIGHT_SPOT = 2 } orx_light_type;
+
+typedef struct {
+    int32_t type;        /* orx_light_type */
+    float power[3];
+    float position[3];   /* area: anchor */
+    float v1[3];         /* area: edge 1 */
+    float v2[3];         /* area: edge 2 */
+    float direction[3];  /* spot */
+    float angle;         /* spot, degrees */
+} orx_light;
+
+/* Flattened scene (replaces IScene::getSceneRootGroup's OptiX node graph).
+ * Deep-copied by orx_init_scene.  Primitive order defines the tie-break of
+ * equal-distance hits (lowest global primitive id wins): quads first, then
+ * spheres, then triangles. */
+typedef struct {
+    uint32_t n_quads;
+    const float* quads;              /* n_quads * 9: anchor, offset1, offset2 (Cornell.cpp:33-64) */
+    const uint32_t* quad_material;   /* n_quads */
+    uint32_t n_spheres;
+    const float* spheres;            /* n_spheres * 4: center xyz, radius (Sphere.cu) */
+    const uint32_t* sphere_material; /* n_spheres */
+    uint32_t n_vertices;
+    const float* vertices;           /* n_vertices * 3 */
+    const float* normals;            /* n_vertices * 3 or NULL (TriangleMesh.cu:56-59) */
+    uint32_t n_triangles;
+    const uint32_t* triangles;       /* n_triangles * 3 vertex indices */
+    const uint32_t* triangle_material;
+    uint32_t n_materials;
+    const orx_material* materials;
+    uint32_t n_lights;
+    const orx_light* lights;         /* IScene::getSceneLights */
+    float aabb_min[3];               /* IScene::getSceneAABB */
+    float aabb_max[3];
+} orx_scene;
+
+/* Compile-time constants of config.h / OptixRenderer.cpp:38-61 as runtime config. */
+typedef struct {
+    uint32_t photon_launch_width;     /* PHOTON_LAUNCH_WIDTH  = 1024 */
+    uint32_t photon_launch_height;    /* PHOTON_LAUNCH_HEIGHT = 1024 */
+    uint32_t max_photon_deposits;     /* MAX_PHOTONS_DEPOSITS_PER_EMITTED = 4 */
+    uint32_t photon_grid_max_size;    /* PHOTON_GRID_MAX_SIZE = 100*100*100 */
+    uint32_t max_photon_trace_depth;  /* MAX_PHOTON_TRACE_DEPTH = 7 */
+    uint32_t max_radiance_trace_depth;/* MAX_RADIANCE_TRACE_DEPTH = 9 */
+    uint32_t vcm_max_path_length;     /* VCM_MAX_PATH_LENGTH = 10 */
+    uint32_t seed;                    /* 0: 574133*clock()+47844152748*time() like SpatialHash.cu:322; else DEBUG_RANDOM_SEED */
+    uint32_t debug_counters;          /* 1: keep per-pixel cells/photons visited (OptixRenderer.cpp:872-953) */
+    uint32_t reserved[7];
+} orx_config;
+
+void orx_default_config(orx_config* cfg);
+
+orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out);
+orx_status orx_init_scene(orx_renderer* r, const orx_scene* scene);
+orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
+                                     uint64_t local_iteration_number, float ppm_radius,
+                                     int create_output, const orx_request* details);
+/* W*H*3 floats into caller-owned host memory; SUM over local iterations. */
+orx_status orx_get_output(orx_renderer* r, float* dst, size_t dst_bytes);
+/* Same, device-to-device into caller-owned device memory on the renderer's
+ * device (used by the multi-GPU harness to hand the buffer to RCCL). */
+orx_status orx_get_output_device(orx_renderer* r, void* dst_device, size_t dst_bytes);
+uint32_t orx_width(const orx_renderer* r);
+uint32_t orx_height(const orx_renderer* r);
+size_t orx_output_bytes(const orx_renderer* r);
+uint32_t orx_emitted_photons_per_iteration(const orx_renderer* r);
+const char* orx_last_error(const orx_renderer* r);
+void orx_destroy(orx_renderer* r);
+
+/* ---- inspection (parity tests, profiling; not part of the reference API) ---- */
+typedef enum {
+    ORX_BUF_RNG = 0,        /* uint32 [slots][6]: xorwow v0..v4, d */
+    ORX_BUF_HITPOINTS = 1,  /* float  [W*H][13]: pos3 normal3 atten3 radiance3 flags(bits) */
+    ORX_BUF_PHOTONS = 2,    /* float  [S][9] grid-sorted photons: power3 position3 direction3 (valid prefix) */
+    ORX_BUF_GRID_OFFSETS = 3,/* uint32 [G+1] */
+    ORX_BUF_INDIRECT = 4,   /* float  [W*H][3] */
+    ORX_BUF_DIRECT = 5,     /* float  [W*H][3] */
+    ORX_BUF_OUTPUT = 6,     /* float  [W*H][3] */
+    ORX_BUF_PHOTON_SLOTS = 7,/* float [S][9] unsorted photon slots: power3 position3 direction3 (0 when cleared) */
+    ORX_BUF_DEBUG_VISITED = 8 /* uint32 [W*H][2]: cells visited, photons visited */
+} orx_buffer_id;
+/* Copies buffer `id` to host; returns the byte size through *out_bytes
+ * (call with dst=NULL to query). */
+orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t dst_bytes, size_t* out_bytes);
+
+/* Passes timed with HIP events on the renderer's stream. */
+typedef enum {
+    ORX_PASS_PPM_EYE = 0,      /* PPM_RAYTRACE_PASS */
+    ORX_PASS_PPM_PHOTON = 1,   /* PPM_PHOTON_PASS (+ fused photon AABB) */
+    ORX_PASS_GRID_HASH = 2,    /* grid setup + calculateHashCellsKernel + histogram */
+    ORX_PASS_GRID_SCAN = 3,    /* exclusive scan -> hashmapOffsetTable */
+    ORX_PASS_GRID_SCATTER = 4, /* sort_by_key as counting-sort scatter */
+    ORX_PASS_PPM_GATHER = 5,   /* PPM_INDIRECT_RADIANCE_ESTIMATION_PASS */
+    ORX_PASS_PPM_DIRECT = 6,   /* PPM_DIRECT_RADIANCE_ESTIMATION_PASS + PPM_OUTPUT_PASS */
+    ORX_PASS_PT = 7,           /* PT_RAYTRACE_PASS */
+    ORX_PASS_VCM_LIGHT = 8,    /* VCM_LIGHT_PASS */
+    ORX_PASS_VCM_CAMERA = 9,   /* VCM_CAMERA_PASS */
+    ORX_PASS_COUNT = 10
+} orx_pass;
+
+typedef struct {
+    uint32_t grid_size[3];
+    float cell_size;
+    float world_origin[3];
+    uint32_t valid_photons;      /* photons in the grid (offset[G]) of the last iteration */
+    uint32_t num_cells;
+    uint64_t photons_visited;    /* gather: photons visited, last iteration (debug counters) */
+    uint64_t cells_visited;      /* gather: (y,z) cell rows visited, last iteration */
+    uint64_t photons_visited_total; /* summed since orx_reset_timing */
+    uint64_t cells_visited_total;
+    uint64_t valid_photons_total;
+    uint32_t timed_iterations;   /* iterations since orx_reset_timing */
+    uint32_t pad;
+    float pass_ms[16];           /* device time per orx_pass summed since orx_reset_timing */
+} orx_stats;
+orx_status orx_get_stats(orx_renderer* r, orx_stats* out);
+/* starts a new timed region for orx_get_stats' *_total and pass_ms fields */
+orx_status orx_reset_timing(orx_renderer* r);
+
+/* Multi-GPU sharding: this renderer owns every RNG-slot row y
+ * with y % world == rank (pixel rows and photon rows).  With world > 1 the
+ * PPM iteration is split by the caller into
+ *   orx_ppm_local_passes   eye pass on own rows, photon pass on own rows, grid over own photons
+ *   (caller all-gathers the compact hitpoints of every rank)
+ *   orx_ppm_gather_all     gather of ALL pixels against own photons -> partial indirect
+ *   (caller reduce-scatters / all-reduces the partial indirect)
+ *   orx_ppm_finish         direct pass + accumulate on own rows
+ * The single-call orx_render_next_iteration is the world == 1 path. */
+orx_status orx_set_shard(orx_renderer* r, uint32_t rank, uint32_t world);
+/* hipStream_t the renderer launches on (as void*), for callers that sync or record events. */
+void* orx_stream(orx_renderer* r);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ORX_H */

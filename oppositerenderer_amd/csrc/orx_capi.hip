@@ -1,0 +1,790 @@
+/*
+ * orx_capi.hip — host side of liborx.so: the OptixRenderer replacement.
+ *
+ * Owns the device buffers and sequences the passes of one progressive
+ * iteration exactly as OptixRenderer::renderNextIteration does
+ * (RenderEngine/renderer/OptixRenderer.cpp:507-821), but as plain HIP
+ * launches on one stream: no OptiX context, no per-launch validation, no
+ * debug-buffer maps (the reference maps ~36 MB of debug counters to the
+ * host every PPM iteration, OptixRenderer.cpp:620/:872-953; here they stay
+ * on the device and are summed in-kernel).
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <ctime>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "orx.h"
+#include "orx_kernels.h"
+
+using namespace orx;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    hipError_t ensure(size_t n) {
+        if (n <= bytes && p) return hipSuccess;
+        release();
+        if (n == 0) n = 16;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+/* host-side BVH over triangles: binned SAH, conservative boxes */
+struct BuildTri {
+    float lo[3], hi[3], c[3];
+};
+
+struct BvhBuilder {
+    std::vector<DevBvhNode> nodes;
+    std::vector<uint32_t> prims;
+    const std::vector<BuildTri>* tris = nullptr;
+
+    static void grow(float* lo, float* hi, const float* l2, const float* h2) {
+        for (int k = 0; k < 3; k++) {
+            lo[k] = std::min(lo[k], l2[k]);
+            hi[k] = std::max(hi[k], h2[k]);
+        }
+    }
+    static float area(const float* lo, const float* hi) {
+        float dx = std::max(0.f, hi[0] - lo[0]), dy = std::max(0.f, hi[1] - lo[1]), dz = std::max(0.f, hi[2] - lo[2]);
+        return dx * dy + dy * dz + dz * dx;
+    }
+    uint32_t build(uint32_t first, uint32_t count) {
+        uint32_t idx = (uint32_t)nodes.size();
+        nodes.push_back(DevBvhNode{});
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (uint32_t i = first; i < first + count; i++) {
+            const BuildTri& t = (*tris)[prims[i]];
+            grow(lo, hi, t.lo, t.hi);
+            grow(clo, chi, t.c, t.c);
+        }
+        /* conservative expansion so that rounding in the slab test can never
+         * cull a primitive the exact test would hit */
+        for (int k = 0; k < 3; k++) {
+            float m = std::max(std::fabs(lo[k]), std::fabs(hi[k]));
+            float e = m * 1e-6f + 1e-20f;
+            nodes[idx].lo[k] = lo[k] - e;
+            nodes[idx].hi[k] = hi[k] + e;
+        }
+        if (count <= 4) {
+            nodes[idx].left_or_first = first;
+            nodes[idx].count_or_right = 0x80000000u | count;
+            return idx;
+        }
+        /* binned SAH on the centroid extent */
+        const int NB = 16;
+        int best_axis = -1, best_split = 0;
+        float best_cost = INFINITY;
+        for (int ax = 0; ax < 3; ax++) {
+            float ext = chi[ax] - clo[ax];
+            if (!(ext > 0)) continue;
+            uint32_t cnt[NB] = {0};
+            float blo[NB][3], bhi[NB][3];
+            for (int b = 0; b < NB; b++)
+                for (int k = 0; k < 3; k++) blo[b][k] = INFINITY, bhi[b][k] = -INFINITY;
+            for (uint32_t i = first; i < first + count; i++) {
+                const BuildTri& t = (*tris)[prims[i]];
+                int b = std::min(NB - 1, (int)((t.c[ax] - clo[ax]) / ext * NB));
+                cnt[b]++;
+                grow(blo[b], bhi[b], t.lo, t.hi);
+            }
+            float rl[NB], rcount[NB];
+            float alo[3] = {INFINITY, INFINITY, INFINITY}, ahi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            uint32_t acc = 0;
+            for (int b = NB - 1; b > 0; b--) {
+                acc += cnt[b];
+                grow(alo, ahi, blo[b], bhi[b]);
+                rl[b] = area(alo, ahi);
+                rcount[b] = (float)acc;
+            }
+            float llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            uint32_t lc = 0;
+            for (int b = 0; b < NB - 1; b++) {
+                lc += cnt[b];
+                grow(llo, lhi, blo[b], bhi[b]);
+                float cost = area(llo, lhi) * (float)lc + rl[b + 1] * rcount[b + 1];
+                if (lc > 0 && lc < count && cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = ax;
+                    best_split = b;
+                }
+            }
+        }
+        uint32_t mid;
+        if (best_axis < 0) {
+            mid = first + count / 2;
+        } else {
+            float ext = chi[best_axis] - clo[best_axis];
+            auto it = std::partition(prims.begin() + first, prims.begin() + first + count, [&](uint32_t p) {
+                const BuildTri& t = (*tris)[p];
+                int b = std::min(NB - 1, (int)((t.c[best_axis] - clo[best_axis]) / ext * NB));
+                return b <= best_split;
+            });
+            mid = (uint32_t)(it - prims.begin());
+            if (mid == first || mid == first + count) mid = first + count / 2;
+        }
+        uint32_t l = build(first, mid - first);
+        uint32_t r = build(mid, first + count - mid);
+        nodes[idx].left_or_first = l;
+        nodes[idx].count_or_right = r;
+        return idx;
+    }
+};
+
+/* host float3 with the same OptiX semantics as the device (f3 is __host__) */
+f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+
+DevLight make_light(const orx_light& L) {
+    /* Light ctors (renderer/Light.cpp:14-49) */
+    DevLight l;
+    std::memset(&l, 0, sizeof l);
+    l.type = L.type;
+    l.power = ld3(L.power);
+    l.position = ld3(L.position);
+    if (L.type == ORX_LIGHT_AREA) {
+        l.v1 = ld3(L.v1);
+        l.v2 = ld3(L.v2);
+        f3 c = cross(l.v1, l.v2);
+        l.normal = normalize(c);
+        l.area = length(c);
+        l.inverseArea = 1.0f / l.area;
+        l.Lemit = (l.power * l.inverseArea) * ORX_1_PI_F;
+    } else if (L.type == ORX_LIGHT_POINT) {
+        l.Lemit = (l.power * 0.25f) * ORX_1_PI_F;
+    } else {
+        l.direction = ld3(L.direction); /* ctor normalises its by-value parameter only (Light.cpp:41) */
+        l.normal = l.direction;
+        l.angle = L.angle;
+        float angleFactor = 1.0f / (1.0f - cosf(l.angle * 180 * ORX_1_PI_F));
+        l.Lemit = ((l.power * 0.25f) * ORX_1_PI_F) * angleFactor;
+    }
+    return l;
+}
+
+float dtor(float d) { return d * ((float)M_PI / 180.f); } /* Camera.cpp:87-90 */
+
+DevCamera camera_setup(const orx_camera& c) {
+    /* Camera::setup (renderer/Camera.cpp:333-345) */
+    DevCamera k;
+    f3 eye = ld3(c.eye), lookat = ld3(c.lookat), up = ld3(c.up);
+    k.eye = eye;
+    k.lookdir = lookat - eye;
+    float lookdir_len = length(k.lookdir);
+    up = normalize(up);
+    f3 cu = normalize(cross(k.lookdir, up));
+    f3 cv = normalize(cross(cu, k.lookdir));
+    float ulen = lookdir_len * tanf(dtor(c.hfov * 0.5f));
+    k.u = cu * ulen;
+    float vlen = lookdir_len * tanf(dtor(c.vfov * 0.5f));
+    k.v = cv * vlen;
+    k.aperture = c.aperture;
+    return k;
+}
+
+enum PassId { P_EYE = 0, P_PHOTON, P_SETUP_HASH, P_SCAN, P_SCATTER, P_GATHER, P_DIRECT, P_PT, P_VCM_LIGHT, P_VCM_CAMERA, P_COUNT };
+constexpr int EV_POOL = 1024; /* timed launches kept per pass between resets */
+
+}  // namespace
+
+struct orx_renderer {
+    int device = 0;
+    orx_config cfg{};
+    hipStream_t stream = nullptr;
+    std::string err;
+    bool scene_ready = false;
+    /* scene */
+    DevBuf d_quads, d_qmat, d_spheres, d_smat, d_triv, d_trin, d_tmat, d_mats, d_lights, d_bvh, d_bvhprims;
+    DevScene scene{};
+    /* frame */
+    uint32_t W = 10, H = 10, RW = 0, RH = 0;
+    uint32_t rank = 0, world = 1;
+    uint32_t rows = 0, rng_rows = 0, prows = 0;
+    bool rng_ready = false;
+    DevBuf d_rng, d_hpA, d_hpB, d_hpC, d_ind, d_dir, d_out, d_dbg;
+    DevBuf d_slotA, d_slotB, d_slotC, d_vmask, d_sortA, d_sortB, d_sortC, d_keys, d_ranks;
+    DevBuf d_hist, d_offsets, d_bbox, d_partials, d_grid;
+    PixelBufs px{};
+    PhotonBufs pb{};
+    /* timing: event pairs per pass since the last orx_reset_timing */
+    std::vector<hipEvent_t> ev[P_COUNT];
+    int ev_n[P_COUNT]{};
+    uint32_t timed_iterations = 0;
+    bool timing = true;
+    uint64_t last_method = 0;
+};
+
+static orx_status set_err(orx_renderer* r, orx_status s, const std::string& m) {
+    if (r) r->err = m;
+    return s;
+}
+#define HIPCHK(r, x)                                                                                      \
+    do {                                                                                                  \
+        hipError_t e_ = (x);                                                                              \
+        if (e_ != hipSuccess)                                                                             \
+            return set_err(r, e_ == hipErrorOutOfMemory ? ORX_ERR_OUT_OF_MEMORY : ORX_ERR_DEVICE,          \
+                           std::string("HIP error in ") + #x + ": " + hipGetErrorString(e_));           \
+    } while (0)
+
+extern "C" {
+
+void orx_default_config(orx_config* c) {
+    std::memset(c, 0, sizeof *c);
+    c->photon_launch_width = 1024;
+    c->photon_launch_height = 1024;
+    c->max_photon_deposits = 4;
+    c->photon_grid_max_size = 100 * 100 * 100;
+    c->max_photon_trace_depth = 7;
+    c->max_radiance_trace_depth = 9;
+    c->vcm_max_path_length = 10;
+    c->seed = 0;
+    c->debug_counters = 1;
+}
+
+orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out) {
+    if (!out) return ORX_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ORX_ERR_DEVICE;
+    if (hip_device < 0 || hip_device >= n) return ORX_ERR_INVALID_ARGUMENT;
+    orx_renderer* r = new (std::nothrow) orx_renderer();
+    if (!r) return ORX_ERR_OUT_OF_MEMORY;
+    r->device = hip_device;
+    if (cfg) r->cfg = *cfg;
+    else orx_default_config(&r->cfg);
+    if (r->cfg.max_photon_deposits == 0 || r->cfg.max_photon_deposits > 8 || r->cfg.photon_launch_width == 0 ||
+        r->cfg.photon_launch_height == 0 || r->cfg.photon_grid_max_size == 0) {
+        delete r;
+        return ORX_ERR_INVALID_ARGUMENT;
+    }
+    if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete r;
+        return ORX_ERR_DEVICE;
+    }
+    *out = r;
+    return ORX_OK;
+}
+
+void orx_destroy(orx_renderer* r) {
+    if (!r) return;
+    hipSetDevice(r->device);
+    if (r->stream) hipStreamSynchronize(r->stream);
+    for (int p = 0; p < P_COUNT; p++)
+        for (hipEvent_t e : r->ev[p]) hipEventDestroy(e);
+    if (r->stream) hipStreamDestroy(r->stream);
+    delete r;
+}
+
+const char* orx_last_error(const orx_renderer* r) { return r ? r->err.c_str() : "null renderer"; }
+void* orx_stream(orx_renderer* r) { return r ? (void*)r->stream : nullptr; }
+
+orx_status orx_set_shard(orx_renderer* r, uint32_t rank, uint32_t world) {
+    if (!r || world == 0 || rank >= world) return ORX_ERR_INVALID_ARGUMENT;
+    r->rank = rank;
+    r->world = world;
+    r->rng_ready = false; /* force re-allocation of the local rows */
+    return ORX_OK;
+}
+
+orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
+    if (!r || !s) return ORX_ERR_INVALID_ARGUMENT;
+    if (s->n_lights == 0 || !s->lights) return set_err(r, ORX_ERR_NO_LIGHTS, "No lights exists in this scene.");
+    if (s->n_materials == 0 || !s->materials) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "scene has no materials");
+    HIPCHK(r, hipSetDevice(r->device));
+    const uint32_t nq = s->n_quads, ns = s->n_spheres, nt = s->n_triangles, nm = s->n_materials;
+    /* validate material indices and triangle vertex indices */
+    for (uint32_t i = 0; i < nq; i++)
+        if (s->quad_material[i] >= nm) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "quad material out of range");
+    for (uint32_t i = 0; i < ns; i++)
+        if (s->sphere_material[i] >= nm) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "sphere material out of range");
+    for (uint32_t i = 0; i < nt; i++) {
+        if (s->triangle_material[i] >= nm) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "triangle material out of range");
+        for (int k = 0; k < 3; k++)
+            if (s->triangles[3 * (size_t)i + k] >= s->n_vertices)
+                return set_err(r, ORX_ERR_INVALID_ARGUMENT, "triangle vertex index out of range");
+    }
+    /* Cornell::createParallelogram (scene/Cornell.cpp:33-64) */
+    std::vector<DevQuad> quads(nq);
+    for (uint32_t i = 0; i < nq; i++) {
+        f3 anchor = ld3(s->quads + 9 * i), o1 = ld3(s->quads + 9 * i + 3), o2 = ld3(s->quads + 9 * i + 6);
+        f3 normal = normalize(cross(o1, o2));
+        float d = dot(normal, anchor);
+        f3 v1 = o1 / dot(o1, o1), v2 = o2 / dot(o2, o2);
+        quads[i] = DevQuad{normal.x, normal.y, normal.z, d, anchor.x, anchor.y, anchor.z, v1.x,
+                           v1.y, v1.z, v2.x, v2.y, v2.z, 0, 0, 0};
+    }
+    std::vector<DevSphere> sph(ns);
+    for (uint32_t i = 0; i < ns; i++)
+        sph[i] = DevSphere{s->spheres[4 * i], s->spheres[4 * i + 1], s->spheres[4 * i + 2], s->spheres[4 * i + 3]};
+    std::vector<DevMaterial> mats(nm);
+    for (uint32_t i = 0; i < nm; i++) {
+        const orx_material& m = s->materials[i];
+        DevMaterial d;
+        std::memset(&d, 0, sizeof d);
+        d.type = m.type;
+        d.Kd = ld3(m.Kd);
+        d.Ks = ld3(m.Ks);
+        d.Kr = ld3(m.Kr);
+        d.Kt = ld3(m.Kt);
+        d.ior = m.ior;
+        d.exponent = m.exponent;
+        if (m.type == ORX_MAT_DIFFUSE_EMITTER) {
+            /* DiffuseEmitter.cpp:17-25, :48-62 */
+            f3 power = ld3(m.power) * d.Kd;
+            d.inverseArea = m.inverse_area;
+            d.powerPerArea = power * m.inverse_area;
+            d.Lemit = (power * m.inverse_area) * ORX_1_PI_F;
+        } else if (m.type == ORX_MAT_GLOSSY) {
+            /* Glossy.cpp:16-30 */
+            f3 sumK = d.Kd + d.Ks;
+            float sumScale = 1.f / maxf(maxf(sumK.x, sumK.y), sumK.z);
+            if (sumScale < 1.f) {
+                d.Kd = d.Kd * sumScale;
+                d.Ks = d.Ks * sumScale;
+            }
+        } else if (m.type < 0 || m.type > ORX_MAT_GLOSSY) {
+            return set_err(r, ORX_ERR_INVALID_ARGUMENT, "unknown material type");
+        }
+        mats[i] = d;
+    }
+    std::vector<DevLight> lights(s->n_lights);
+    for (uint32_t i = 0; i < s->n_lights; i++) lights[i] = make_light(s->lights[i]);
+    /* triangles: per-triangle vertex triplets (float4) + BVH */
+    std::vector<float4> tv((size_t)nt * 3), tn;
+    if (s->normals) tn.resize((size_t)nt * 3);
+    std::vector<BuildTri> bt(nt);
+    for (uint32_t i = 0; i < nt; i++) {
+        BuildTri& b = bt[i];
+        for (int k = 0; k < 3; k++) b.lo[k] = INFINITY, b.hi[k] = -INFINITY;
+        for (int v = 0; v < 3; v++) {
+            uint32_t vi = s->triangles[3 * (size_t)i + v];
+            const float* p = s->vertices + 3 * (size_t)vi;
+            tv[3 * (size_t)i + v] = make_float4(p[0], p[1], p[2], 0.f);
+            if (s->normals) {
+                const float* n = s->normals + 3 * (size_t)vi;
+                tn[3 * (size_t)i + v] = make_float4(n[0], n[1], n[2], 0.f);
+            }
+            for (int k = 0; k < 3; k++) {
+                b.lo[k] = std::min(b.lo[k], p[k]);
+                b.hi[k] = std::max(b.hi[k], p[k]);
+            }
+        }
+        for (int k = 0; k < 3; k++) b.c[k] = 0.5f * (b.lo[k] + b.hi[k]);
+    }
+    BvhBuilder bb;
+    if (nt) {
+        bb.tris = &bt;
+        bb.prims.resize(nt);
+        for (uint32_t i = 0; i < nt; i++) bb.prims[i] = i;
+        bb.nodes.reserve(2 * (size_t)nt / 2 + 1);
+        bb.build(0, nt);
+    }
+    auto up = [&](DevBuf& b, const void* src, size_t bytes) -> hipError_t {
+        hipError_t e = b.ensure(bytes);
+        if (e != hipSuccess) return e;
+        if (bytes) return hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice);
+        return hipSuccess;
+    };
+    HIPCHK(r, up(r->d_quads, quads.data(), quads.size() * sizeof(DevQuad)));
+    HIPCHK(r, up(r->d_qmat, s->quad_material, (size_t)nq * 4));
+    HIPCHK(r, up(r->d_spheres, sph.data(), sph.size() * sizeof(DevSphere)));
+    HIPCHK(r, up(r->d_smat, s->spheres ? s->sphere_material : nullptr, (size_t)ns * 4));
+    HIPCHK(r, up(r->d_triv, tv.data(), tv.size() * sizeof(float4)));
+    HIPCHK(r, up(r->d_trin, tn.data(), tn.size() * sizeof(float4)));
+    HIPCHK(r, up(r->d_tmat, s->triangle_material, (size_t)nt * 4));
+    HIPCHK(r, up(r->d_mats, mats.data(), mats.size() * sizeof(DevMaterial)));
+    HIPCHK(r, up(r->d_lights, lights.data(), lights.size() * sizeof(DevLight)));
+    HIPCHK(r, up(r->d_bvh, bb.nodes.data(), bb.nodes.size() * sizeof(DevBvhNode)));
+    HIPCHK(r, up(r->d_bvhprims, bb.prims.data(), bb.prims.size() * 4));
+    DevScene& S = r->scene;
+    S.nq = nq;
+    S.ns = ns;
+    S.nt = nt;
+    S.quads = r->d_quads.as<DevQuad>();
+    S.qmat = r->d_qmat.as<uint32_t>();
+    S.spheres = r->d_spheres.as<DevSphere>();
+    S.smat = r->d_smat.as<uint32_t>();
+    S.tri_v = r->d_triv.as<float4>();
+    S.tri_n = s->normals ? r->d_trin.as<float4>() : nullptr;
+    S.tmat = r->d_tmat.as<uint32_t>();
+    S.mats = r->d_mats.as<DevMaterial>();
+    S.lights = r->d_lights.as<DevLight>();
+    S.nl = s->n_lights;
+    S.bvh = r->d_bvh.as<DevBvhNode>();
+    S.bvh_prims = r->d_bvhprims.as<uint32_t>();
+    S.bvh_nodes = (uint32_t)bb.nodes.size();
+    /* AAB::getBoundingSphere (math/AAB.cpp:26-33) with Vector3::length's
+     * dot bug a.z*b.x (math/Vector3.cpp:27-30) */
+    f3 lo = ld3(s->aabb_min), hi = ld3(s->aabb_max);
+    f3 center = (lo + hi) * 0.5f;
+    f3 e = hi - center;
+    S.bs_cx = center.x;
+    S.bs_cy = center.y;
+    S.bs_cz = center.z;
+    S.bs_r = sqrtf(e.x * e.x + e.y * e.y + e.z * e.x);
+    r->scene_ready = true;
+    return ORX_OK;
+}
+
+static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
+    const uint32_t PW = r->cfg.photon_launch_width, PH = r->cfg.photon_launch_height, D = r->cfg.max_photon_deposits;
+    r->W = W;
+    r->H = H;
+    r->RW = std::max(PW, W);
+    r->RH = std::max(PH, H);
+    auto local_rows = [&](uint32_t n) { return n > r->rank ? (n - r->rank + r->world - 1) / r->world : 0u; };
+    r->rows = local_rows(H);
+    r->rng_rows = local_rows(r->RH);
+    r->prows = local_rows(PH);
+    const size_t npx = (size_t)r->rows * W;
+    const size_t nslot_rng = (size_t)r->rng_rows * r->RW;
+    const size_t nphot = (size_t)r->prows * PW;
+    const size_t S = nphot * D;
+    const size_t G2 = (size_t)r->cfg.photon_grid_max_size + 2;
+    const size_t nblocks = (G2 + 1023) / 1024 + 1;
+    HIPCHK(r, r->d_rng.ensure(nslot_rng * 24));
+    HIPCHK(r, r->d_hpA.ensure(npx * 16));
+    HIPCHK(r, r->d_hpB.ensure(npx * 16));
+    HIPCHK(r, r->d_hpC.ensure(npx * 8));
+    HIPCHK(r, r->d_ind.ensure(npx * 12));
+    HIPCHK(r, r->d_dir.ensure(npx * 12));
+    HIPCHK(r, r->d_out.ensure(npx * 12));
+    HIPCHK(r, r->d_dbg.ensure(npx * 8));
+    HIPCHK(r, r->d_slotA.ensure(S * 16));
+    HIPCHK(r, r->d_slotB.ensure(S * 16));
+    HIPCHK(r, r->d_slotC.ensure(S * 4));
+    HIPCHK(r, r->d_vmask.ensure(nphot));
+    HIPCHK(r, r->d_sortA.ensure(S * 16));
+    HIPCHK(r, r->d_sortB.ensure(S * 16));
+    HIPCHK(r, r->d_sortC.ensure(S * 4));
+    HIPCHK(r, r->d_keys.ensure(S * 4));
+    HIPCHK(r, r->d_ranks.ensure(S * 4));
+    HIPCHK(r, r->d_hist.ensure(G2 * 4));
+    HIPCHK(r, r->d_offsets.ensure(G2 * 4));
+    HIPCHK(r, r->d_bbox.ensure(6 * 4));
+    HIPCHK(r, r->d_partials.ensure(nblocks * 4));
+    HIPCHK(r, r->d_grid.ensure(sizeof(GridParams)));
+    HIPCHK(r, hipMemsetAsync(r->d_hist.p, 0, G2 * 4, r->stream));
+    HIPCHK(r, hipMemsetAsync(r->d_offsets.p, 0, G2 * 4, r->stream));
+    HIPCHK(r, hipMemsetAsync(r->d_vmask.p, 0, nphot, r->stream));
+    HIPCHK(r, hipMemsetAsync(r->d_grid.p, 0, sizeof(GridParams), r->stream));
+    HIPCHK(r, hipMemsetAsync(r->d_out.p, 0, npx * 12, r->stream));
+    uint32_t bbox_init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+    HIPCHK(r, hipMemcpyAsync(r->d_bbox.p, bbox_init, sizeof bbox_init, hipMemcpyHostToDevice, r->stream));
+
+    PixelBufs& px = r->px;
+    px.W = W;
+    px.H = H;
+    px.rank = r->rank;
+    px.world = r->world;
+    px.rows = r->rows;
+    px.RW = r->RW;
+    for (int k = 0; k < 6; k++) px.rng.p[k] = r->d_rng.as<uint32_t>() + k * nslot_rng;
+    px.hpA = r->d_hpA.as<float4>();
+    px.hpB = r->d_hpB.as<float4>();
+    px.hpC = r->d_hpC.as<float2>();
+    px.indirect = r->d_ind.as<float>();
+    px.direct = r->d_dir.as<float>();
+    px.output = r->d_out.as<float>();
+    px.dbg = r->cfg.debug_counters ? r->d_dbg.as<uint32_t>() : nullptr;
+    PhotonBufs& pb = r->pb;
+    pb.PW = PW;
+    pb.PH = PH;
+    pb.prows = r->prows;
+    pb.D = D;
+    pb.S = (uint32_t)S;
+    pb.gmax = r->cfg.photon_grid_max_size;
+    pb.slotA = r->d_slotA.as<float4>();
+    pb.slotB = r->d_slotB.as<float4>();
+    pb.slotC = r->d_slotC.as<float>();
+    pb.vmask = r->d_vmask.as<uint8_t>();
+    pb.sortA = r->d_sortA.as<float4>();
+    pb.sortB = r->d_sortB.as<float4>();
+    pb.sortC = r->d_sortC.as<float>();
+    pb.keys = r->d_keys.as<uint32_t>();
+    pb.ranks = r->d_ranks.as<uint32_t>();
+    pb.hist = r->d_hist.as<uint32_t>();
+    pb.offsets = r->d_offsets.as<uint32_t>();
+    pb.bbox = r->d_bbox.as<uint32_t>();
+    pb.scan_partials = r->d_partials.as<uint32_t>();
+    pb.grid = r->d_grid.as<GridParams>();
+
+    /* initializeRandomStates (OptixRenderer_SpatialHash.cu:310-347) */
+    uint32_t seed = r->cfg.seed;
+    if (seed == 0) seed = 574133u * (uint32_t)clock() + (uint32_t)(47844152748ull * (uint32_t)time(NULL));
+    launch_rng_init(r->stream, px.rng, r->RW, r->rng_rows, r->rank, r->world, seed);
+    HIPCHK(r, hipGetLastError());
+    r->rng_ready = true;
+    return ORX_OK;
+}
+
+static inline void ev_begin(orx_renderer* r, int p) {
+    if (!r->timing || r->ev_n[p] >= EV_POOL) return;
+    auto& v = r->ev[p];
+    size_t need = 2 * (size_t)r->ev_n[p] + 2;
+    while (v.size() < need) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        v.push_back(e);
+    }
+    hipEventRecord(v[2 * r->ev_n[p]], r->stream);
+}
+static inline void ev_end(orx_renderer* r, int p) {
+    if (!r->timing || r->ev_n[p] >= EV_POOL || r->ev[p].size() < 2 * (size_t)r->ev_n[p] + 2) return;
+    hipEventRecord(r->ev[p][2 * r->ev_n[p] + 1], r->stream);
+    r->ev_n[p]++;
+}
+
+orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
+                                     float ppm_radius, int create_output, const orx_request* det) {
+    (void)create_output; /* ignored by the reference engine too */
+    (void)iteration_number;
+    if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
+    if (!r->scene_ready) return set_err(r, ORX_ERR_STATE, "Traced before OptixRenderer was initialized.");
+    if (det->width == 0 || det->height == 0) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "zero-sized request");
+    if (det->method != ORX_METHOD_PATH_TRACING && det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
+        return set_err(r, ORX_ERR_UNSUPPORTED, "render method not supported by this build");
+    HIPCHK(r, hipSetDevice(r->device));
+    if (det->width != r->W || det->height != r->H || !r->rng_ready) {
+        orx_status st = resize(r, det->width, det->height);
+        if (st != ORX_OK) return st;
+    }
+    r->timed_iterations++;
+    const size_t npx = (size_t)r->rows * r->W;
+    if (local_iteration_number == 0) HIPCHK(r, hipMemsetAsync(r->d_out.p, 0, npx * 12, r->stream));
+    DevCamera cam = camera_setup(det->camera);
+    Consts c;
+    c.max_photon_depth = r->cfg.max_photon_trace_depth;
+    c.max_radiance_depth = r->cfg.max_radiance_trace_depth;
+    c.ppm_radius = ppm_radius;
+    c.ppm_radius2 = ppm_radius * ppm_radius;
+    c.emitted_f = (float)(r->cfg.photon_launch_width * r->cfg.photon_launch_height);
+    c.local_iteration = (uint32_t)(local_iteration_number != 0);
+    if (det->method == ORX_METHOD_PATH_TRACING) {
+        ev_begin(r, P_PT);
+        launch_pt(r->stream, r->scene, cam, r->px, c);
+        ev_end(r, P_PT);
+    } else {
+        ev_begin(r, P_EYE);
+        launch_ppm_eye(r->stream, r->scene, cam, r->px, c);
+        ev_end(r, P_EYE);
+        ev_begin(r, P_PHOTON);
+        launch_ppm_photon(r->stream, r->scene, r->px, r->pb, c);
+        ev_end(r, P_PHOTON);
+        ev_begin(r, P_SETUP_HASH);
+        launch_grid_setup(r->stream, r->pb);
+        launch_grid_hash(r->stream, r->pb);
+        ev_end(r, P_SETUP_HASH);
+        ev_begin(r, P_SCAN);
+        launch_grid_scan(r->stream, r->pb);
+        ev_end(r, P_SCAN);
+        ev_begin(r, P_SCATTER);
+        launch_grid_scatter(r->stream, r->pb);
+        ev_end(r, P_SCATTER);
+        ev_begin(r, P_GATHER);
+        launch_ppm_gather(r->stream, r->px, r->pb, c);
+        ev_end(r, P_GATHER);
+        ev_begin(r, P_DIRECT);
+        launch_ppm_direct_output(r->stream, r->scene, r->px, c);
+        ev_end(r, P_DIRECT);
+    }
+    HIPCHK(r, hipGetLastError());
+    r->last_method = (uint64_t)det->method;
+    return ORX_OK;
+}
+
+static orx_status check_grid_error(orx_renderer* r) {
+    if (r->last_method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING || !r->d_grid.p) return ORX_OK;
+    GridParams g;
+    HIPCHK(r, hipMemcpyAsync(&g, r->d_grid.p, sizeof g, hipMemcpyDeviceToHost, r->stream));
+    HIPCHK(r, hipStreamSynchronize(r->stream));
+    if (g.error)
+        return set_err(r, ORX_ERR_GRID_TOO_LARGE, "Too many cells in SpatialHash.cu, over defined PHOTON_GRID_MAX_SIZE.");
+    return ORX_OK;
+}
+
+orx_status orx_get_output(orx_renderer* r, float* dst, size_t bytes) {
+    if (!r || !dst) return ORX_ERR_INVALID_ARGUMENT;
+    size_t need = (size_t)r->rows * r->W * 12;
+    if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "destination too small");
+    if (!r->d_out.p) return set_err(r, ORX_ERR_STATE, "no frame rendered yet");
+    HIPCHK(r, hipSetDevice(r->device));
+    HIPCHK(r, hipMemcpyAsync(dst, r->d_out.p, need, hipMemcpyDeviceToHost, r->stream));
+    HIPCHK(r, hipStreamSynchronize(r->stream));
+    return check_grid_error(r);
+}
+
+orx_status orx_get_output_device(orx_renderer* r, void* dst, size_t bytes) {
+    if (!r || !dst) return ORX_ERR_INVALID_ARGUMENT;
+    size_t need = (size_t)r->rows * r->W * 12;
+    if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "destination too small");
+    if (!r->d_out.p) return set_err(r, ORX_ERR_STATE, "no frame rendered yet");
+    HIPCHK(r, hipSetDevice(r->device));
+    HIPCHK(r, hipMemcpyAsync(dst, r->d_out.p, need, hipMemcpyDeviceToDevice, r->stream));
+    return ORX_OK;
+}
+
+uint32_t orx_width(const orx_renderer* r) { return r ? r->W : 0; }
+uint32_t orx_height(const orx_renderer* r) { return r ? r->H : 0; }
+size_t orx_output_bytes(const orx_renderer* r) { return r ? (size_t)r->W * r->H * 12 : 0; }
+uint32_t orx_emitted_photons_per_iteration(const orx_renderer* r) {
+    return r ? r->cfg.photon_launch_width * r->cfg.photon_launch_height : 0;
+}
+
+orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes, size_t* out_bytes) {
+    if (!r) return ORX_ERR_INVALID_ARGUMENT;
+    if (!r->rng_ready) return set_err(r, ORX_ERR_STATE, "no frame rendered yet");
+    HIPCHK(r, hipSetDevice(r->device));
+    HIPCHK(r, hipStreamSynchronize(r->stream));
+    GridParams g{};
+    HIPCHK(r, hipMemcpy(&g, r->d_grid.p, sizeof g, hipMemcpyDeviceToHost));
+    const size_t npx = (size_t)r->rows * r->W;
+    const size_t nslot = (size_t)r->rng_rows * r->RW;
+    size_t need = 0;
+    switch (id) {
+    case ORX_BUF_RNG: need = nslot * 24; break;
+    case ORX_BUF_HITPOINTS: need = npx * 13 * 4; break;
+    case ORX_BUF_PHOTONS: need = (size_t)g.valid * 36; break;
+    case ORX_BUF_GRID_OFFSETS: need = ((size_t)g.G + 1) * 4; break;
+    case ORX_BUF_INDIRECT: case ORX_BUF_DIRECT: case ORX_BUF_OUTPUT: need = npx * 12; break;
+    case ORX_BUF_PHOTON_SLOTS: need = (size_t)r->pb.S * 36; break;
+    case ORX_BUF_DEBUG_VISITED: need = npx * 8; break;
+    default: return set_err(r, ORX_ERR_INVALID_ARGUMENT, "unknown buffer id");
+    }
+    if (out_bytes) *out_bytes = need;
+    if (!dst) return ORX_OK;
+    if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "destination too small");
+    auto d2h = [&](void* h, const void* d, size_t n) { return hipMemcpy(h, d, n, hipMemcpyDeviceToHost); };
+    switch (id) {
+    case ORX_BUF_RNG: {
+        std::vector<uint32_t> planes(nslot * 6);
+        HIPCHK(r, d2h(planes.data(), r->d_rng.p, nslot * 24));
+        uint32_t* o = (uint32_t*)dst;
+        for (size_t i = 0; i < nslot; i++)
+            for (int k = 0; k < 6; k++) o[6 * i + k] = planes[k * nslot + i];
+        break;
+    }
+    case ORX_BUF_HITPOINTS: {
+        std::vector<float4> A(npx), B(npx);
+        std::vector<float2> Cc(npx);
+        HIPCHK(r, d2h(A.data(), r->d_hpA.p, npx * 16));
+        HIPCHK(r, d2h(B.data(), r->d_hpB.p, npx * 16));
+        HIPCHK(r, d2h(Cc.data(), r->d_hpC.p, npx * 8));
+        float* o = (float*)dst;
+        for (size_t i = 0; i < npx; i++) {
+            uint32_t flags;
+            std::memcpy(&flags, &A[i].w, 4);
+            bool ns = (flags & PRD_HIT_NON_SPECULAR) != 0;
+            float v[13] = {A[i].x, A[i].y, A[i].z,
+                           ns ? B[i].x : 0.f, ns ? B[i].y : 0.f, ns ? B[i].z : 0.f,
+                           B[i].w, Cc[i].x, Cc[i].y,
+                           ns ? 0.f : B[i].x, ns ? 0.f : B[i].y, ns ? 0.f : B[i].z, A[i].w};
+            std::memcpy(o + 13 * i, v, sizeof v);
+        }
+        break;
+    }
+    case ORX_BUF_PHOTONS: case ORX_BUF_PHOTON_SLOTS: {
+        size_t n = id == ORX_BUF_PHOTONS ? (size_t)g.valid : (size_t)r->pb.S;
+        std::vector<float4> A(n), B(n);
+        std::vector<float> Cc(n);
+        std::vector<uint8_t> vm(id == ORX_BUF_PHOTONS ? 0 : (size_t)r->prows * r->cfg.photon_launch_width);
+        const void* sa = id == ORX_BUF_PHOTONS ? r->d_sortA.p : r->d_slotA.p;
+        const void* sb = id == ORX_BUF_PHOTONS ? r->d_sortB.p : r->d_slotB.p;
+        const void* sc = id == ORX_BUF_PHOTONS ? r->d_sortC.p : r->d_slotC.p;
+        if (n) {
+            HIPCHK(r, d2h(A.data(), sa, n * 16));
+            HIPCHK(r, d2h(B.data(), sb, n * 16));
+            HIPCHK(r, d2h(Cc.data(), sc, n * 4));
+        }
+        if (!vm.empty()) HIPCHK(r, d2h(vm.data(), r->d_vmask.p, vm.size()));
+        float* o = (float*)dst;
+        const uint32_t D = r->cfg.max_photon_deposits;
+        for (size_t i = 0; i < n; i++) {
+            bool valid = id == ORX_BUF_PHOTONS || ((vm[i / D] >> (i % D)) & 1u);
+            float v[9] = {A[i].w, B[i].w, Cc[i], A[i].x, A[i].y, A[i].z, B[i].x, B[i].y, B[i].z};
+            if (!valid) std::memset(v, 0, sizeof v);
+            std::memcpy(o + 9 * i, v, sizeof v);
+        }
+        break;
+    }
+    case ORX_BUF_GRID_OFFSETS: HIPCHK(r, d2h(dst, r->d_offsets.p, need)); break;
+    case ORX_BUF_INDIRECT: HIPCHK(r, d2h(dst, r->d_ind.p, need)); break;
+    case ORX_BUF_DIRECT: HIPCHK(r, d2h(dst, r->d_dir.p, need)); break;
+    case ORX_BUF_OUTPUT: HIPCHK(r, d2h(dst, r->d_out.p, need)); break;
+    case ORX_BUF_DEBUG_VISITED: HIPCHK(r, d2h(dst, r->d_dbg.p, need)); break;
+    }
+    return ORX_OK;
+}
+
+orx_status orx_get_stats(orx_renderer* r, orx_stats* out) {
+    if (!r || !out) return ORX_ERR_INVALID_ARGUMENT;
+    std::memset(out, 0, sizeof *out);
+    HIPCHK(r, hipSetDevice(r->device));
+    HIPCHK(r, hipStreamSynchronize(r->stream));
+    if (r->d_grid.p) {
+        GridParams g;
+        HIPCHK(r, hipMemcpy(&g, r->d_grid.p, sizeof g, hipMemcpyDeviceToHost));
+        out->grid_size[0] = g.gx;
+        out->grid_size[1] = g.gy;
+        out->grid_size[2] = g.gz;
+        out->cell_size = g.cell;
+        out->world_origin[0] = g.ox;
+        out->world_origin[1] = g.oy;
+        out->world_origin[2] = g.oz;
+        out->valid_photons = g.valid;
+        out->num_cells = g.G;
+        out->photons_visited = g.photons_visited;
+        out->cells_visited = g.cells_visited;
+        out->photons_visited_total = g.photons_visited_total;
+        out->cells_visited_total = g.cells_visited_total;
+        out->valid_photons_total = g.valid_total;
+    }
+    for (int p = 0; p < P_COUNT; p++) {
+        double tot = 0.0;
+        for (int k = 0; k < r->ev_n[p]; k++) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, r->ev[p][2 * k], r->ev[p][2 * k + 1]) == hipSuccess) tot += ms;
+        }
+        out->pass_ms[p] = (float)tot;
+    }
+    out->timed_iterations = r->timed_iterations;
+    return check_grid_error(r);
+}
+
+orx_status orx_reset_timing(orx_renderer* r) {
+    if (!r) return ORX_ERR_INVALID_ARGUMENT;
+    HIPCHK(r, hipSetDevice(r->device));
+    HIPCHK(r, hipStreamSynchronize(r->stream));
+    for (int p = 0; p < P_COUNT; p++) r->ev_n[p] = 0;
+    r->timed_iterations = 0;
+    if (r->d_grid.p) {
+        GridParams g;
+        HIPCHK(r, hipMemcpy(&g, r->d_grid.p, sizeof g, hipMemcpyDeviceToHost));
+        g.photons_visited_total = 0;
+        g.cells_visited_total = 0;
+        g.valid_total = 0;
+        HIPCHK(r, hipMemcpy(r->d_grid.p, &g, sizeof g, hipMemcpyHostToDevice));
+    }
+    return ORX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,635 @@
+/*
+ * orx_device.h — gfx950 device-side building blocks of the render core.
+ *
+ * Replaces the OptiX device runtime + helper headers of the reference:
+ *   helpers/random.h (cuRAND XORWOW), helpers/samplers.h, helpers/helpers.h,
+ *   helpers/camera.h, helpers/light.h (getLightContribution),
+ *   geometry_instance/{parallelogram,Sphere,TriangleMesh}.cu (intersection),
+ *   OptiX closest-hit / any-hit dispatch (flattened into switch-on-material).
+ * Float expressions keep the reference's operand order; the library is built
+ * with -ffp-contract=off and correctly rounded div/sqrt so the kernels agree
+ * bit for bit with the CPU oracle on every control-flow decision.
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "orx_detmath.h"
+
+namespace orx {
+
+/* ------------------------------------------------------------------ */
+/* float3 with OptiX semantics                                          */
+/* ------------------------------------------------------------------ */
+struct f3 {
+    float x, y, z;
+};
+__host__ __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__host__ __device__ __forceinline__ f3 mk1(float a) { return f3{a, a, a}; }
+__host__ __device__ __forceinline__ f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__host__ __device__ __forceinline__ f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__host__ __device__ __forceinline__ f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+__host__ __device__ __forceinline__ f3 operator*(f3 a, float s) { return f3{a.x * s, a.y * s, a.z * s}; }
+__host__ __device__ __forceinline__ f3 operator*(float s, f3 a) { return f3{s * a.x, s * a.y, s * a.z}; }
+__host__ __device__ __forceinline__ f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
+/* optix float3 / float = a * (1.0f / s) */
+__host__ __device__ __forceinline__ f3 operator/(f3 a, float s) {
+    float inv = 1.0f / s;
+    return a * inv;
+}
+__host__ __device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__host__ __device__ __forceinline__ f3 cross(f3 a, f3 b) {
+    return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__host__ __device__ __forceinline__ float length(f3 a) { return sqrtf(dot(a, a)); }
+__host__ __device__ __forceinline__ f3 normalize(f3 a) {
+    float inv = 1.0f / sqrtf(dot(a, a));
+    return a * inv;
+}
+__host__ __device__ __forceinline__ float maxf(float a, float b) { return a > b ? a : b; }
+__host__ __device__ __forceinline__ float fmax3(f3 a) { return fmaxf(fmaxf(a.x, a.y), a.z); }
+__host__ __device__ __forceinline__ float favgf(f3 v) { return (v.x + v.y + v.z) * 0.3333333333f; }
+__host__ __device__ __forceinline__ f3 reflect(f3 i, f3 n) { return i - (n * 2.0f) * dot(n, i); }
+__host__ __device__ __forceinline__ bool isnan3(f3 v) { return v.x != v.x || v.y != v.y || v.z != v.z; }
+
+__host__ __device__ inline bool refract(f3& r, f3 i, f3 n, float ior) {
+    f3 nn = n;
+    float negNdotV = dot(i, nn);
+    float eta;
+    if (negNdotV > 0.0f) {
+        eta = ior;
+        nn = -n;
+        negNdotV = -negNdotV;
+    } else {
+        eta = 1.f / ior;
+    }
+    const float k = 1.f - eta * eta * (1.f - negNdotV * negNdotV);
+    if (k < 0.0f) {
+        r = mk1(0.f);
+        return false;
+    }
+    r = normalize(i * eta - nn * (eta * negNdotV + sqrtf(k)));
+    return true;
+}
+
+/* ------------------------------------------------------------------ */
+/* RadiancePRD flags (renderer/RadiancePRD.h:30-35)                    */
+/* ------------------------------------------------------------------ */
+constexpr uint32_t PRD_HIT_EMITTER = 1u << 31;
+constexpr uint32_t PRD_ERROR = 1u << 30;
+constexpr uint32_t PRD_MISS = 1u << 29;
+constexpr uint32_t PRD_HIT_SPECULAR = 1u << 28;
+constexpr uint32_t PRD_HIT_NON_SPECULAR = 1u << 27;
+constexpr uint32_t PRD_PATH_TRACING = 1u << 26;
+constexpr float RT_DEFAULT_MAX = 1.e27f;
+
+/* ------------------------------------------------------------------ */
+/* cuRAND XORWOW state, kept in registers; SoA planes in HBM           */
+/* ------------------------------------------------------------------ */
+struct Rng {
+    uint32_t v0, v1, v2, v3, v4, d;
+};
+struct RngPlanes {
+    uint32_t* p[6]; /* v0..v4, d : [slots] each, coalesced dword access */
+};
+__device__ __forceinline__ Rng rng_load(const RngPlanes& P, size_t s) {
+    return Rng{P.p[0][s], P.p[1][s], P.p[2][s], P.p[3][s], P.p[4][s], P.p[5][s]};
+}
+__device__ __forceinline__ void rng_store(const RngPlanes& P, size_t s, const Rng& r) {
+    P.p[0][s] = r.v0; P.p[1][s] = r.v1; P.p[2][s] = r.v2;
+    P.p[3][s] = r.v3; P.p[4][s] = r.v4; P.p[5][s] = r.d;
+}
+/* curand_init(seed, 0, 0) — subsequence and offset 0: no skip-ahead */
+__host__ __device__ __forceinline__ Rng rng_init(uint64_t seed) {
+    uint32_t s0 = ((uint32_t)seed) ^ 0xaad26b49u;
+    uint32_t s1 = ((uint32_t)(seed >> 32)) ^ 0xf7dcefddu;
+    uint32_t t0 = 1099087573u * s0;
+    uint32_t t1 = 2591861531u * s1;
+    Rng r;
+    r.d = 6615241u + t1 + t0;
+    r.v0 = 123456789u + t0;
+    r.v1 = 362436069u ^ t0;
+    r.v2 = 521288629u + t1;
+    r.v3 = 88675123u ^ t1;
+    r.v4 = 5783321u + t0;
+    return r;
+}
+__host__ __device__ __forceinline__ uint32_t rng_next(Rng& s) {
+    uint32_t t = s.v0 ^ (s.v0 >> 2);
+    s.v0 = s.v1;
+    s.v1 = s.v2;
+    s.v2 = s.v3;
+    s.v3 = s.v4;
+    s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+    s.d += 362437u;
+    return s.v4 + s.d;
+}
+/* getRandomUniformFloat (helpers/random.h:65-69): curand_uniform is
+ * x*2^-32 + 2^-33 which nvcc contracts into one FMA. */
+__device__ __forceinline__ float rnd(Rng& s) {
+    uint32_t x = rng_next(s);
+    float u = __builtin_fmaf((float)x, 2.3283064e-10f, 2.3283064e-10f / 2.0f);
+    return maxf(u - ORX_FLT_EPSILON, 0.0f);
+}
+
+/* ------------------------------------------------------------------ */
+/* samplers (helpers/samplers.h, helpers.h:119-134)                    */
+/* ------------------------------------------------------------------ */
+__device__ __forceinline__ void create_coordinate_system(f3 N, f3& U, f3& V) {
+    if (fabsf(N.x) > fabsf(N.y)) {
+        float invLength = 1.f / sqrtf(N.x * N.x + N.z * N.z);
+        U = mk(-N.z * invLength, 0.f, N.x * invLength);
+    } else {
+        float invLength = 1.f / sqrtf(N.y * N.y + N.z * N.z);
+        U = mk(0.f, N.z * invLength, -N.y * invLength);
+    }
+    V = cross(N, U);
+}
+/* sampleUnitHemisphereCos (samplers.h:24-43) */
+__device__ __forceinline__ f3 sample_hemisphere_cos(f3 normal, float sx, float sy) {
+    float theta = orx_acosf(sqrtf(sx));
+    float phi = 2.0f * ORX_PI_F * sy;
+    float st = orx_sinf(theta);
+    float xs = st * orx_cosf(phi);
+    float ys = orx_cosf(theta);
+    float zs = st * orx_sinf(phi);
+    f3 U, V;
+    create_coordinate_system(normal, U, V);
+    return normalize(U * xs + normal * ys + V * zs);
+}
+/* sampleUnitHemisphere (samplers.h:46-57) */
+__device__ __forceinline__ f3 sample_hemisphere(f3 normal, float sx, float sy) {
+    f3 U, V;
+    create_coordinate_system(normal, U, V);
+    float phi = 2.0f * ORX_PI_F * sx;
+    float r = sqrtf(sy);
+    float x = r * orx_cosf(phi);
+    float y = r * orx_sinf(phi);
+    float z = 1.0f - x * x - y * y;
+    z = z > 0.0f ? sqrtf(z) : 0.0f;
+    return normalize(U * x + V * y + normal * z);
+}
+/* sampleUnitSphere (samplers.h:59-72) */
+__device__ __forceinline__ f3 sample_unit_sphere(float sx, float sy) {
+    f3 v;
+    v.z = 1.f - 2.f * sx;
+    float phi = 2 * ORX_PI_F * sy;
+    float r = sqrtf(1.f - v.z * v.z);
+    v.x = r * orx_cosf(phi);
+    v.y = r * orx_sinf(phi);
+    return v;
+}
+/* sampleDisc (samplers.h:74-93) */
+__device__ __forceinline__ f3 sample_disc(float sx, float sy, f3 center, float radius, f3 normal) {
+    f3 U, V;
+    create_coordinate_system(normal, U, V);
+    float r = sqrtf(sx);
+    float theta = 2.f * ORX_PI_F * sy;
+    float x = r * orx_cosf(theta);
+    float y = r * orx_sinf(theta);
+    return center + (U * x + V * y) * radius;
+}
+
+/* ------------------------------------------------------------------ */
+/* scene                                                               */
+/* ------------------------------------------------------------------ */
+enum : int32_t { MAT_DIFFUSE = 0, MAT_EMITTER = 1, MAT_MIRROR = 2, MAT_GLASS = 3, MAT_GLOSSY = 4 };
+enum : int32_t { LIGHT_AREA = 0, LIGHT_POINT = 1, LIGHT_SPOT = 2 };
+
+struct DevMaterial {
+    int32_t type;
+    f3 Kd, Ks, Kr, Kt;
+    float ior, exponent;
+    f3 powerPerArea, Lemit;
+    float inverseArea;
+};
+struct DevLight {
+    int32_t type;
+    f3 power, position, v1, v2, normal, Lemit; /* Lemit doubles as intensity */
+    f3 direction;
+    float area, inverseArea, angle;
+};
+/* parallelogram: plane (n,d), anchor, v1/|v1|^2, v2/|v2|^2 (Cornell.cpp:45-56) */
+struct DevQuad {
+    float nx, ny, nz, d;
+    float ax, ay, az, v1x;
+    float v1y, v1z, v2x, v2y;
+    float v2z, pad0, pad1, pad2;
+};
+struct DevSphere {
+    float cx, cy, cz, r;
+};
+/* BVH node: 32 B, two children per node; leaves hold a primitive range */
+struct DevBvhNode {
+    float lo[3];
+    uint32_t left_or_first; /* inner: left child index; leaf: first prim in prim_index */
+    float hi[3];
+    uint32_t count_or_right; /* leaf: 0x80000000 | count; inner: right child */
+};
+
+struct DevScene {
+    uint32_t nq, ns, nt;
+    const DevQuad* quads;
+    const uint32_t* qmat;
+    const DevSphere* spheres;
+    const uint32_t* smat;
+    const float4* tri_v;       /* [nt][3] vertex positions (xyz, w unused) */
+    const float4* tri_n;       /* [nt][3] vertex normals or NULL */
+    const uint32_t* tmat;
+    const DevMaterial* mats;
+    const DevLight* lights;
+    uint32_t nl;
+    /* bounding sphere (AAB::getBoundingSphere with Vector3::length bug) */
+    float bs_cx, bs_cy, bs_cz, bs_r;
+    /* triangle BVH (nt > 0) */
+    const DevBvhNode* bvh;
+    const uint32_t* bvh_prims;
+    uint32_t bvh_nodes;
+};
+
+struct Hit {
+    float t;
+    int32_t prim; /* global id: quads, spheres, triangles */
+    float b, g;   /* triangle barycentrics */
+    f3 sn;        /* sphere normal attribute */
+};
+
+/* parallelogram.cu:49-76 */
+__device__ __forceinline__ bool isect_quad(const DevQuad& q, f3 o, f3 d, float tmin, float tmax, float& tout) {
+    f3 n = mk(q.nx, q.ny, q.nz);
+    float dt = dot(d, n);
+    float t = (q.d - dot(n, o)) / dt;
+    if (t > tmin && t < tmax) {
+        f3 p = o + d * t;
+        f3 vi = p - mk(q.ax, q.ay, q.az);
+        float a1 = dot(mk(q.v1x, q.v1y, q.v1z), vi);
+        if (a1 >= 0 && a1 <= 1) {
+            float a2 = dot(mk(q.v2x, q.v2y, q.v2z), vi);
+            if (a2 >= 0 && a2 <= 1) {
+                tout = t;
+                return true;
+            }
+        }
+    }
+    return false;
+}
+/* Sphere.cu:32-56 */
+__device__ __forceinline__ bool isect_sphere(const DevSphere& s, f3 o, f3 d, float tmin, float tmax, float& tout,
+                                             f3& nout) {
+    f3 O = o - mk(s.cx, s.cy, s.cz);
+    float b = dot(O, d);
+    float c = dot(O, O) - s.r * s.r;
+    float disc = b * b - c;
+    if (disc > 0.0f) {
+        float sdisc = sqrtf(disc);
+        float root1 = (-b - sdisc);
+        if (root1 > tmin && root1 < tmax) {
+            tout = root1;
+            nout = (O + d * root1) / s.r;
+            return true;
+        }
+        float root2 = (-b + sdisc);
+        if (root2 > tmin && root2 < tmax) {
+            tout = root2;
+            nout = (O + d * root2) / s.r;
+            return true;
+        }
+    }
+    return false;
+}
+/* OptiX intersect_triangle_branchless (TriangleMesh.cu:46) */
+__device__ __forceinline__ bool isect_tri(f3 p0, f3 p1, f3 p2, f3 o, f3 d, float tmin, float tmax, float& tout,
+                                          float& bout, float& gout) {
+    f3 e0 = p1 - p0;
+    f3 e1 = p0 - p2;
+    f3 n = cross(e1, e0);
+    f3 e2 = (p0 - o) * (1.0f / dot(n, d));
+    f3 i = cross(d, e2);
+    float beta = dot(i, e1);
+    float gamma = dot(i, e0);
+    float t = dot(n, e2);
+    if ((t < tmax) & (t > tmin) & (beta >= 0.0f) & (gamma >= 0.0f) & (beta + gamma <= 1)) {
+        tout = t;
+        bout = beta;
+        gout = gamma;
+        return true;
+    }
+    return false;
+}
+__device__ __forceinline__ f3 ld_f3(const float4& v) { return mk(v.x, v.y, v.z); }
+
+/* slab test: does the ray enter [lo,hi] before tmax? (tie-safe: <=) */
+__device__ __forceinline__ bool box_hit(const DevBvhNode& n, f3 o, f3 inv, float tmin, float tmax, float& tenter) {
+    float tx0 = (n.lo[0] - o.x) * inv.x, tx1 = (n.hi[0] - o.x) * inv.x;
+    float ty0 = (n.lo[1] - o.y) * inv.y, ty1 = (n.hi[1] - o.y) * inv.y;
+    float tz0 = (n.lo[2] - o.z) * inv.z, tz1 = (n.hi[2] - o.z) * inv.z;
+    float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+    float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    tenter = t0;
+    return t0 <= t1;
+}
+
+/* Closest hit over all primitives; equal t resolves to the lowest global
+ * primitive id, which is OptiX NoAccel's child order (Cornell.cpp:183-189)
+ * and is independent of traversal order, so BVH and brute force agree. */
+__device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& h) {
+    float best = tmax;
+    int32_t bp = -1;
+    float t;
+    for (uint32_t i = 0; i < S.nq; i++) {
+        if (isect_quad(S.quads[i], o, d, tmin, best, t)) {
+            best = t;
+            bp = (int32_t)i;
+        }
+    }
+    f3 sn = mk1(0);
+    for (uint32_t i = 0; i < S.ns; i++) {
+        f3 n;
+        if (isect_sphere(S.spheres[i], o, d, tmin, best, t, n)) {
+            best = t;
+            bp = (int32_t)(S.nq + i);
+            sn = n;
+        }
+    }
+    float bb = 0, bg = 0;
+    if (S.nt) {
+        const uint32_t base = S.nq + S.ns;
+        f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        uint32_t stack[64];
+        int sp = 0;
+        uint32_t node = 0;
+        for (;;) {
+            const DevBvhNode n = S.bvh[node];
+            float te;
+            bool visit = box_hit(n, o, inv, tmin, best, te);
+            if (visit && (n.count_or_right & 0x80000000u)) {
+                uint32_t first = n.left_or_first, cnt = n.count_or_right & 0x7fffffffu;
+                for (uint32_t k = 0; k < cnt; k++) {
+                    uint32_t ti = S.bvh_prims[first + k];
+                    float b, g;
+                    f3 p0 = ld_f3(S.tri_v[3 * ti]), p1 = ld_f3(S.tri_v[3 * ti + 1]), p2 = ld_f3(S.tri_v[3 * ti + 2]);
+                    /* accept t < best, or t == best from a lower primitive id */
+                    float lim = bp >= 0 ? orx_as_float(orx_as_uint(best) + 1u) : best;
+                    if (isect_tri(p0, p1, p2, o, d, tmin, lim, t, b, g) && (t < best || (int32_t)(base + ti) < bp)) {
+                        best = t;
+                        bp = (int32_t)(base + ti);
+                        bb = b;
+                        bg = g;
+                    }
+                }
+                if (sp == 0) break;
+                node = stack[--sp];
+            } else if (visit) {
+                stack[sp++] = n.count_or_right;
+                node = n.left_or_first;
+            } else {
+                if (sp == 0) break;
+                node = stack[--sp];
+            }
+        }
+    }
+    if (bp < 0) return false;
+    h.t = best;
+    h.prim = bp;
+    h.b = bb;
+    h.g = bg;
+    h.sn = sn;
+    return true;
+}
+/* any hit in (tmin,tmax): every material's RayType::SHADOW any-hit is
+ * gatherAnyHitOnNonEmitter (Material.cpp:18-26, DirectRadianceEstimation.cu:79-83) */
+__device__ inline bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, float tmax) {
+    float t;
+    for (uint32_t i = 0; i < S.nq; i++)
+        if (isect_quad(S.quads[i], o, d, tmin, tmax, t)) return true;
+    for (uint32_t i = 0; i < S.ns; i++) {
+        f3 n;
+        if (isect_sphere(S.spheres[i], o, d, tmin, tmax, t, n)) return true;
+    }
+    if (S.nt) {
+        f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        uint32_t stack[64];
+        int sp = 0;
+        uint32_t node = 0;
+        for (;;) {
+            const DevBvhNode n = S.bvh[node];
+            float te;
+            bool visit = box_hit(n, o, inv, tmin, tmax, te);
+            if (visit && (n.count_or_right & 0x80000000u)) {
+                uint32_t first = n.left_or_first, cnt = n.count_or_right & 0x7fffffffu;
+                for (uint32_t k = 0; k < cnt; k++) {
+                    uint32_t ti = S.bvh_prims[first + k];
+                    float b, g;
+                    if (isect_tri(ld_f3(S.tri_v[3 * ti]), ld_f3(S.tri_v[3 * ti + 1]), ld_f3(S.tri_v[3 * ti + 2]), o, d,
+                                  tmin, tmax, t, b, g))
+                        return true;
+                }
+                if (sp == 0) break;
+                node = stack[--sp];
+            } else if (visit) {
+                stack[sp++] = n.count_or_right;
+                node = n.left_or_first;
+            } else {
+                if (sp == 0) break;
+                node = stack[--sp];
+            }
+        }
+    }
+    return false;
+}
+
+__device__ __forceinline__ uint32_t prim_material(const DevScene& S, int32_t p) {
+    if ((uint32_t)p < S.nq) return S.qmat[p];
+    if ((uint32_t)p < S.nq + S.ns) return S.smat[p - S.nq];
+    return S.tmat[p - S.nq - S.ns];
+}
+/* world shading normal as the closest-hit programs see it:
+ * normalize(rtTransformNormal(shadingNormal)) with identity transforms. */
+__device__ __forceinline__ f3 shading_normal(const DevScene& S, const Hit& h) {
+    if ((uint32_t)h.prim < S.nq) {
+        const DevQuad& q = S.quads[h.prim];
+        return normalize(mk(q.nx, q.ny, q.nz));
+    }
+    if ((uint32_t)h.prim < S.nq + S.ns) return normalize(h.sn);
+    uint32_t ti = (uint32_t)h.prim - S.nq - S.ns;
+    if (S.tri_n) {
+        f3 n0 = ld_f3(S.tri_n[3 * ti]), n1 = ld_f3(S.tri_n[3 * ti + 1]), n2 = ld_f3(S.tri_n[3 * ti + 2]);
+        return normalize(normalize(n1 * h.b + n2 * h.g + n0 * (1.0f - h.b - h.g)));
+    }
+    f3 p0 = ld_f3(S.tri_v[3 * ti]), p1 = ld_f3(S.tri_v[3 * ti + 1]), p2 = ld_f3(S.tri_v[3 * ti + 2]);
+    return normalize(normalize(cross(p0 - p2, p1 - p0)));
+}
+/* geometric normal as the VCM closest-hit programs see it */
+__device__ __forceinline__ f3 geometric_normal(const DevScene& S, const Hit& h) {
+    if ((uint32_t)h.prim < S.nq) {
+        const DevQuad& q = S.quads[h.prim];
+        return normalize(mk(q.nx, q.ny, q.nz));
+    }
+    if ((uint32_t)h.prim < S.nq + S.ns) return normalize(h.sn);
+    uint32_t ti = (uint32_t)h.prim - S.nq - S.ns;
+    f3 p0 = ld_f3(S.tri_v[3 * ti]), p1 = ld_f3(S.tri_v[3 * ti + 1]), p2 = ld_f3(S.tri_v[3 * ti + 2]);
+    return normalize(normalize(cross(p0 - p2, p1 - p0)));
+}
+
+/* ------------------------------------------------------------------ */
+/* camera (Camera.cpp:333-345 derived on the host; helpers/camera.h)   */
+/* ------------------------------------------------------------------ */
+struct DevCamera {
+    f3 eye, lookdir, u, v;
+    float aperture;
+};
+/* RayGeneratorPPM.cu:40-48 / RayGeneratorPT.cu:53-61 + modifyRayForDepthOfField */
+__device__ __forceinline__ void primary_ray(const DevCamera& cam, uint32_t x, uint32_t y, uint32_t W, uint32_t H,
+                                            Rng& rs, f3& o, f3& d) {
+    float sx = rnd(rs);
+    float sy = rnd(rs);
+    float dx = ((float)x + sx) / (float)W * 2.0f - 1.0f;
+    float dy = ((float)y + sy) / (float)H * 2.0f - 1.0f;
+    f3 origin = cam.eye;
+    f3 dir = normalize(cam.u * dx + cam.v * dy + cam.lookdir);
+    if (cam.aperture > 0) {
+        f3 focal = cam.eye + cam.lookdir;
+        f3 camLookDir = normalize(cam.lookdir);
+        float focalPlaneT = (dot(camLookDir, focal) - dot(camLookDir, cam.eye)) / dot(camLookDir, dir);
+        f3 lookAt = origin + dir * focalPlaneT;
+        float ux = rnd(rs);
+        float uy = rnd(rs);
+        float rr = sqrtf(ux);
+        float th = 2.f * ORX_PI_F * uy;
+        float discx = rr * orx_cosf(th);
+        float discy = rr * orx_sinf(th);
+        origin = origin + ((cam.u * discx) * cam.aperture + (cam.v * discy) * cam.aperture);
+        dir = normalize(lookAt - origin);
+    }
+    o = origin;
+    d = dir;
+}
+
+/* ------------------------------------------------------------------ */
+/* radiance ray: RadiancePRD through the closest-hit programs          */
+/* ------------------------------------------------------------------ */
+struct RadiancePRD {
+    f3 attenuation, radiance;
+    uint32_t depth;
+    f3 position, normal;
+    uint32_t flags;
+    f3 newdir;
+};
+
+__device__ __forceinline__ float glass_reflect_factor(f3 d, f3 N, float n1, float n2, f3& refr, bool& valid) {
+    valid = refract(refr, d, N, n2 / n1);
+    float cosI = -dot(d, N);
+    float cosT = -dot(refr, N);
+    float refl = 1.f;
+    if (valid) {
+        float rp = (n2 * cosI - n1 * cosT) / (n2 * cosI + n1 * cosT);
+        float rs = (n1 * cosI - n2 * cosT) / (n1 * cosI + n2 * cosT);
+        refl = (rp * rp + rs * rs) / 2.f;
+    }
+    return refl;
+}
+
+/* Iterative form of the rtTrace(RADIANCE) recursion: Diffuse.cu:71-87,
+ * Glossy.cu:74-90, DiffuseEmitter.cu:40-51, Mirror.cu:50-63, Glass.cu:90-143,
+ * miss RayGeneratorPPM.cu:72-77. */
+__device__ inline void trace_radiance(const DevScene& S, uint32_t maxd, f3 o, f3 d, float tmin, RadiancePRD& prd,
+                                      Rng& rs) {
+    for (;;) {
+        Hit h;
+        if (!trace_closest(S, o, d, tmin, RT_DEFAULT_MAX, h)) {
+            prd.flags = PRD_MISS;
+            prd.attenuation = mk1(0.f);
+            prd.radiance = mk1(0.f);
+            return;
+        }
+        const DevMaterial& m = S.mats[prim_material(S, h.prim)];
+        f3 hitPoint = o + d * h.t;
+        f3 N = shading_normal(S, h);
+        if (m.type == MAT_DIFFUSE || m.type == MAT_GLOSSY) {
+            prd.flags |= PRD_HIT_NON_SPECULAR;
+            prd.attenuation = prd.attenuation * m.Kd;
+            prd.normal = N;
+            prd.position = hitPoint;
+            prd.depth++;
+            if (prd.flags & PRD_PATH_TRACING) {
+                float s0 = rnd(rs);
+                float s1 = rnd(rs);
+                prd.newdir = sample_hemisphere_cos(N, s0, s1);
+            }
+            return;
+        } else if (m.type == MAT_EMITTER) {
+            prd.flags |= PRD_HIT_EMITTER;
+            if (dot(N, -d) < 0.f) return;
+            f3 Le = m.powerPerArea / ORX_PI_F;
+            prd.radiance = prd.radiance + prd.attenuation * Le;
+            return;
+        } else if (m.type == MAT_MIRROR) {
+            prd.depth++;
+            if (prd.depth <= maxd) {
+                prd.attenuation = prd.attenuation * m.Kr;
+                d = reflect(d, N);
+                o = hitPoint;
+                tmin = 0.0001f;
+                continue;
+            }
+            return;
+        } else { /* glass */
+            bool outside = dot(N, d) < 0;
+            f3 Nn = outside ? N : -N;
+            float n1 = outside ? 1.0f : m.ior, n2 = outside ? m.ior : 1.0f;
+            f3 refr;
+            bool valid;
+            float refl = glass_reflect_factor(d, Nn, n1, n2, refr, valid);
+            float sample = rnd(rs);
+            f3 nd;
+            if (sample <= refl) {
+                nd = reflect(d, Nn);
+            } else {
+                nd = refr;
+                prd.attenuation = prd.attenuation * ((n2 * n2) / (n1 * n1));
+            }
+            prd.flags |= PRD_HIT_SPECULAR;
+            prd.flags &= ~PRD_HIT_NON_SPECULAR;
+            prd.depth++;
+            if (prd.depth <= maxd) {
+                o = hitPoint;
+                d = nd;
+                tmin = 0.0001f;
+                continue;
+            }
+            prd.attenuation = prd.attenuation * 0.f;
+            return;
+        }
+    }
+}
+
+/* getLightContribution (helpers/light.h:29-87) */
+__device__ inline f3 light_contribution(const DevScene& S, const DevLight& light, f3 pos, f3 normal, Rng& rs) {
+    float lightFactor = 1;
+    f3 pointOnLight;
+    if (light.type == LIGHT_AREA) {
+        float sx = rnd(rs);
+        float sy = rnd(rs);
+        pointOnLight = light.position + light.v1 * sx + light.v2 * sy;
+    } else if (light.type == LIGHT_POINT) {
+        pointOnLight = light.position;
+        lightFactor *= 1.f / 4.f;
+    } else {
+        return mk1(0);
+    }
+    f3 towardsLight = pointOnLight - pos;
+    float lightDistance = length(towardsLight);
+    towardsLight = towardsLight / lightDistance;
+    float n_dot_l = maxf(0, dot(normal, towardsLight));
+    lightFactor *= n_dot_l / (ORX_PI_F * lightDistance * lightDistance);
+    if (light.type == LIGHT_AREA) lightFactor *= maxf(0, dot(-towardsLight, light.normal));
+    if (lightFactor > 0.0f) {
+        float tmax = (float)((double)lightDistance - 0.0001);
+        float att = trace_any(S, pos, towardsLight, 0.0001f, tmax) ? 0.0f : 1.0f;
+        lightFactor *= att;
+        return light.power * lightFactor;
+    }
+    return mk1(0);
+}
+
+}  // namespace orx

@@ -1,0 +1,94 @@
+/*
+ * orx_kernels.h — launch interface between the host orchestration
+ * (orx_capi.cpp) and the gfx950 kernels (orx_kernels.hip).
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "orx_device.h"
+
+namespace orx {
+
+/* Device-resident uniform grid parameters, produced by k_grid_setup from the
+ * photon AABB without a host round trip (the reference copies the thrust
+ * reduction result to the host, OptixRenderer_SpatialHash.cu:219-236). */
+struct GridParams {
+    float ox, oy, oz;   /* photonsWorldOrigo (padded AABB min) */
+    float cell;         /* photonsGridCellSize */
+    uint32_t gx, gy, gz;
+    uint32_t G;         /* number of cells */
+    uint32_t valid;     /* photons in cells (offsets[G]) */
+    uint32_t error;     /* 1: G > PHOTON_GRID_MAX_SIZE */
+    uint32_t any_valid;
+    uint32_t pad;
+    uint64_t photons_visited;   /* this iteration */
+    uint64_t cells_visited;
+    uint64_t photons_visited_total; /* since orx_reset_timing */
+    uint64_t cells_visited_total;
+    uint64_t valid_total;
+};
+
+/* Per-frame pixel state. Pixel (x,y) of rank r is stored at local row
+ * j = (y - r)/world (row-interleaved ownership). */
+struct PixelBufs {
+    uint32_t W, H;      /* full image */
+    uint32_t rank, world;
+    uint32_t rows;      /* local rows = number of y with y % world == rank */
+    uint32_t RW;        /* RNG buffer width (slot = y*RW + x, global y) */
+    RngPlanes rng;      /* local RNG rows: slot index = j*RW + x */
+    float4* hpA;        /* pos.xyz, flags bits */
+    float4* hpB;        /* normal.xyz (non-specular hit) | radiance.xyz, atten.x */
+    float2* hpC;        /* atten.y, atten.z */
+    float* indirect;    /* [rows*W*3] */
+    float* direct;      /* [rows*W*3] */
+    float* output;      /* [rows*W*3] running SUM */
+    uint32_t* dbg;      /* [rows*W*2] cells/photons visited, or NULL */
+};
+
+struct PhotonBufs {
+    uint32_t PW, PH;    /* photon launch (full) */
+    uint32_t prows;     /* local photon rows */
+    uint32_t D;         /* max deposits per emitted photon */
+    uint32_t S;         /* local slots = prows*PW*D */
+    uint32_t gmax;      /* PHOTON_GRID_MAX_SIZE */
+    float4* slotA;      /* [S] pos.xyz, power.x */
+    float4* slotB;      /* [S] dir.xyz, power.y */
+    float* slotC;       /* [S] power.z */
+    uint8_t* vmask;     /* [S/D] bit k: deposit k stored with fmaxf(power) > 0 */
+    float4* sortA;      /* grid-ordered copies */
+    float4* sortB;
+    float* sortC;
+    uint32_t* keys;     /* [S] */
+    uint32_t* ranks;    /* [S] */
+    uint32_t* hist;     /* [gmax+2] */
+    uint32_t* offsets;  /* [gmax+2] */
+    uint32_t* bbox;     /* [6] ordered-float min xyz, max xyz */
+    uint32_t* scan_partials; /* [ceil((gmax+2)/1024)+1] */
+    GridParams* grid;
+};
+
+struct Consts {
+    uint32_t max_photon_depth;
+    uint32_t max_radiance_depth;
+    float ppm_radius;
+    float ppm_radius2;
+    float emitted_f;    /* emittedPhotonsPerIterationFloat (global count) */
+    uint32_t local_iteration;
+};
+
+void launch_rng_init(hipStream_t s, RngPlanes rng, uint32_t RW, uint32_t rows, uint32_t rank, uint32_t world,
+                     uint32_t seed);
+void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c);
+void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c);
+void launch_grid_setup(hipStream_t s, const PhotonBufs& pb);
+void launch_grid_hash(hipStream_t s, const PhotonBufs& pb);
+void launch_grid_scan(hipStream_t s, const PhotonBufs& pb);
+void launch_grid_scatter(hipStream_t s, const PhotonBufs& pb);
+/* gathers `rows` pixel rows whose hitpoints are in hp{A,B,C} against the
+ * local photon grid; writes indirect (and debug counters) */
+void launch_ppm_gather(hipStream_t s, const PixelBufs& px, const PhotonBufs& pb, const Consts& c);
+void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c);
+void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c);
+
+}  // namespace orx

@@ -1,0 +1,656 @@
+/*
+ * orx_kernels.hip — gfx950 kernels of the render core.
+ *
+ * One kernel per reference OptiX entry point / Thrust step:
+ *   k_rng_init          initRandomStateBuffer  (OptixRenderer_SpatialHash.cu:310-334)
+ *   k_ppm_eye           PPM_RAYTRACE_PASS      (ppm/RayGeneratorPPM.cu:31-66)
+ *   k_ppm_photon        PPM_PHOTON_PASS        (ppm/PhotonGenerator.cu:81-128 + material
+ *                       closest-hit photon programs) fused with the photon AABB
+ *                       reduction of getPhotonsBoundingBox (SpatialHash.cu:123-128)
+ *   k_grid_setup        cell size / grid dims  (SpatialHash.cu:229-249), on device
+ *   k_grid_hash         calculateHashCellsKernel (SpatialHash.cu:152-173) + histogram
+ *   k_scan_*            exclusive_scan of the histogram (SpatialHash.cu:202-207)
+ *   k_grid_scatter      sort_by_key as a counting-sort scatter (SpatialHash.cu:193-196)
+ *   k_ppm_gather        PPM_INDIRECT_RADIANCE_ESTIMATION_PASS (ppm/IndirectRadianceEstimation.cu:69-227)
+ *   k_ppm_direct_output PPM_DIRECT + PPM_OUTPUT (ppm/DirectRadianceEstimation.cu:29-77, ppm/Output.cu:32-37)
+ *   k_pt                PT_RAYTRACE_PASS       (pt/RayGeneratorPT.cu:46-131)
+ * Wave size is 64 on CDNA4; block reductions below are written for it.
+ */
+#include "orx_kernels.h"
+
+namespace orx {
+
+/* ------------------------------------------------------------------ */
+/* helpers                                                             */
+/* ------------------------------------------------------------------ */
+__device__ __forceinline__ uint32_t f2ord(float f) {
+    uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+__device__ __forceinline__ float wave_min(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ void store_hitpoint(const PixelBufs& px, size_t i, const RadiancePRD& prd) {
+    /* Union: non-specular hits carry normal, others carry radiance (the
+     * unused one is identically zero in RayGeneratorPPM's PRD). */
+    bool ns = (prd.flags & PRD_HIT_NON_SPECULAR) != 0;
+    f3 nr = ns ? prd.normal : prd.radiance;
+    px.hpA[i] = make_float4(prd.position.x, prd.position.y, prd.position.z, __uint_as_float(prd.flags));
+    px.hpB[i] = make_float4(nr.x, nr.y, nr.z, prd.attenuation.x);
+    px.hpC[i] = make_float2(prd.attenuation.y, prd.attenuation.z);
+}
+
+/* ------------------------------------------------------------------ */
+/* RNG init: curand_init(seed + slot, 0, 0)                            */
+/* ------------------------------------------------------------------ */
+__global__ __launch_bounds__(256) void k_rng_init(RngPlanes rng, uint32_t RW, uint32_t rows, uint32_t rank,
+                                                  uint32_t world, uint32_t seed) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t n = (size_t)rows * RW;
+    if (i >= n) return;
+    uint32_t j = (uint32_t)(i / RW), x = (uint32_t)(i % RW);
+    uint32_t y = rank + world * j;
+    uint32_t gslot = y * RW + x;
+    rng_store(rng, i, rng_init((uint64_t)(uint32_t)(seed + gslot)));
+}
+void launch_rng_init(hipStream_t s, RngPlanes rng, uint32_t RW, uint32_t rows, uint32_t rank, uint32_t world,
+                     uint32_t seed) {
+    size_t n = (size_t)rows * RW;
+    hipLaunchKernelGGL(k_rng_init, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rng, RW, rows, rank, world,
+                       seed);
+}
+
+/* ------------------------------------------------------------------ */
+/* PPM eye pass                                                        */
+/* ------------------------------------------------------------------ */
+__global__ __launch_bounds__(256) void k_ppm_eye(DevScene S, DevCamera cam, PixelBufs px, Consts c) {
+    uint32_t x = blockIdx.x * 16 + (threadIdx.x & 15);
+    uint32_t j = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= px.W || j >= px.rows) return;
+    uint32_t y = px.rank + px.world * j;
+    size_t slot = (size_t)j * px.RW + x;
+    Rng rs = rng_load(px.rng, slot);
+    RadiancePRD prd;
+    prd.attenuation = mk1(1.0f);
+    prd.radiance = mk1(0.f);
+    prd.depth = 0;
+    prd.flags = 0;
+    prd.position = mk1(0.f);
+    prd.normal = mk1(0.f);
+    prd.newdir = mk1(0.f);
+    f3 o, d;
+    primary_ray(cam, x, y, px.W, px.H, rs, o, d);
+    trace_radiance(S, c.max_radiance_depth, o, d, 0.001f, prd, rs);
+    store_hitpoint(px, (size_t)j * px.W + x, prd);
+    rng_store(px.rng, slot, rs);
+}
+void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c) {
+    dim3 grid((px.W + 15) / 16, (px.rows + 15) / 16);
+    hipLaunchKernelGGL(k_ppm_eye, grid, dim3(256), 0, s, S, cam, px, c);
+}
+
+/* ------------------------------------------------------------------ */
+/* PPM photon pass (+ AABB of the valid deposits)                      */
+/* ------------------------------------------------------------------ */
+__global__ __launch_bounds__(256) void k_ppm_photon(DevScene S, PixelBufs px, PhotonBufs pb, Consts c) {
+    __shared__ float red[6][4];
+    const uint32_t x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const uint32_t j = blockIdx.y * 4 + (threadIdx.x >> 6);
+    float lo_x = INFINITY, lo_y = INFINITY, lo_z = INFINITY;
+    float hi_x = -INFINITY, hi_y = -INFINITY, hi_z = -INFINITY;
+    if (x < pb.PW && j < pb.prows) {
+        const uint32_t y = px.rank + px.world * j;
+        (void)y;
+        const uint32_t p_local = j * pb.PW + x;
+        const uint32_t pm_index = p_local * pb.D;
+        size_t slot = (size_t)j * px.RW + x;
+        Rng rs = rng_load(px.rng, slot);
+        /* PhotonGenerator.cu:91-107 */
+        int lightIndex = 0;
+        if (S.nl > 1) {
+            float sample = rnd(rs);
+            int li = (int)(sample * (float)S.nl);
+            lightIndex = li < (int)(S.nl - 1) ? li : (int)(S.nl - 1);
+        }
+        const DevLight& L = S.lights[lightIndex];
+        float powerScale = (float)S.nl;
+        f3 power = L.power * powerScale;
+        f3 origin = L.position, dir = mk1(0.f);
+        float photonPowerFactor = 1.f;
+        float s1x = rnd(rs), s1y = rnd(rs);
+        /* generatePhotonOriginAndDirection (PhotonGenerator.cu:40-79) */
+        if (L.type == LIGHT_AREA) {
+            float s2x = rnd(rs), s2y = rnd(rs);
+            origin = origin + (L.v1 * s1x + L.v2 * s1y);
+            dir = sample_hemisphere(L.normal, s2x, s2y);
+        } else if (L.type == LIGHT_POINT) {
+            f3 bc = mk(S.bs_cx, S.bs_cy, S.bs_cz);
+            f3 sceneCenterToLight = L.position - bc;
+            float lightDistance = length(sceneCenterToLight);
+            sceneCenterToLight = sceneCenterToLight / lightDistance;
+            bool wellOutside = (double)lightDistance > 1.5 * (double)S.bs_r;
+            if (wellOutside) {
+                f3 pointOnDisc = sample_disc(s1x, s1y, bc, S.bs_r, sceneCenterToLight);
+                dir = normalize(pointOnDisc - origin);
+                float rr = S.bs_r * S.bs_r + lightDistance * lightDistance;
+                photonPowerFactor = (1 - lightDistance * (1.0f / sqrtf(rr))) / 2.f;
+            } else {
+                dir = sample_unit_sphere(s1x, s1y);
+            }
+        } else {
+            f3 pointOnDisc = sample_disc(s1x, s1y, origin + L.direction, orx_sinf(L.angle / 2), L.direction);
+            dir = normalize(pointOnDisc - origin);
+        }
+        power = power * photonPowerFactor;
+
+        /* photon closest-hit chain: Diffuse.cu:92-135, Glossy.cu:94-137,
+         * Mirror.cu:65-77, Glass.cu:164-205, DiffuseEmitter.cu:56-59 */
+        uint32_t numStored = 0, depth = 0, mask = 0;
+        float weight = 1.0f;
+        float tmin = 0.0001f;
+        f3 o = origin, d = dir;
+        for (;;) {
+            Hit h;
+            if (!trace_closest(S, o, d, tmin, RT_DEFAULT_MAX, h)) break;
+            const DevMaterial& m = S.mats[prim_material(S, h.prim)];
+            f3 hitPoint = o + d * h.t;
+            if (m.type == MAT_DIFFUSE || m.type == MAT_GLOSSY) {
+                f3 N = shading_normal(S, h);
+                if (depth >= 1 && numStored < pb.D) {
+                    uint32_t si = pm_index + numStored;
+                    pb.slotA[si] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, power.x);
+                    pb.slotB[si] = make_float4(d.x, d.y, d.z, power.y);
+                    pb.slotC[si] = power.z;
+                    if (fmax3(power) > 0) {
+                        mask |= 1u << numStored;
+                        lo_x = fminf(lo_x, hitPoint.x); lo_y = fminf(lo_y, hitPoint.y); lo_z = fminf(lo_z, hitPoint.z);
+                        hi_x = fmaxf(hi_x, hitPoint.x); hi_y = fmaxf(hi_y, hitPoint.y); hi_z = fmaxf(hi_z, hitPoint.z);
+                    }
+                    numStored++;
+                }
+                power = power * m.Kd;
+                weight *= fmax3(m.Kd);
+                if (depth >= 3) {
+                    float probContinue = favgf(m.Kd);
+                    float probSample = rnd(rs);
+                    if (probSample >= probContinue) break;
+                    power = power / probContinue;
+                }
+                depth++;
+                if (depth >= c.max_photon_depth || (double)weight < 0.001) break;
+                if (numStored >= pb.D) break;
+                float s0 = rnd(rs);
+                float s1 = rnd(rs);
+                d = sample_hemisphere_cos(N, s0, s1);
+                o = hitPoint;
+                tmin = 0.0001f;
+            } else if (m.type == MAT_EMITTER) {
+                break;
+            } else if (m.type == MAT_MIRROR) {
+                f3 N = shading_normal(S, h);
+                depth++;
+                if (depth <= c.max_photon_depth) {
+                    power = power * m.Kr;
+                    d = reflect(d, N);
+                    o = hitPoint;
+                    tmin = 0.0001f;
+                    continue;
+                }
+                break;
+            } else {
+                f3 wsn = shading_normal(S, h);
+                bool outside = dot(wsn, d) < 0;
+                f3 N = outside ? wsn : -wsn;
+                float n1 = outside ? 1.0f : m.ior, n2 = outside ? m.ior : 1.0f;
+                f3 refr;
+                bool valid;
+                float refl = glass_reflect_factor(d, N, n1, n2, refr, valid);
+                float sample = rnd(rs);
+                f3 nd = (sample <= refl) ? reflect(d, N) : refr;
+                depth++;
+                if (depth <= c.max_photon_depth) {
+                    o = hitPoint;
+                    d = nd;
+                    tmin = 0.0001f;
+                    continue;
+                }
+                break;
+            }
+        }
+        pb.vmask[p_local] = (uint8_t)mask;
+        rng_store(px.rng, slot, rs);
+    }
+    /* block AABB -> device-wide ordered-int atomics */
+    lo_x = wave_min(lo_x); lo_y = wave_min(lo_y); lo_z = wave_min(lo_z);
+    hi_x = wave_max(hi_x); hi_y = wave_max(hi_y); hi_z = wave_max(hi_z);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+        red[0][w] = lo_x; red[1][w] = lo_y; red[2][w] = lo_z;
+        red[3][w] = hi_x; red[4][w] = hi_y; red[5][w] = hi_z;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        int k = threadIdx.x;
+        float v = red[k][0];
+        for (int q = 1; q < 4; q++) v = k < 3 ? fminf(v, red[k][q]) : fmaxf(v, red[k][q]);
+        if (k < 3) {
+            if (v != INFINITY) atomicMin(&pb.bbox[k], f2ord(v));
+        } else {
+            if (v != -INFINITY) atomicMax(&pb.bbox[k], f2ord(v));
+        }
+    }
+}
+void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c) {
+    dim3 grid((pb.PW + 63) / 64, (pb.prows + 3) / 4);
+    hipLaunchKernelGGL(k_ppm_photon, grid, dim3(256), 0, s, S, px, pb, c);
+}
+
+/* ------------------------------------------------------------------ */
+/* grid setup: createUniformGridPhotonMap host math, on one thread     */
+/* ------------------------------------------------------------------ */
+__global__ void k_grid_setup(PhotonBufs pb) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint32_t b[6];
+    for (int k = 0; k < 6; k++) b[k] = pb.bbox[k];
+    bool any = b[0] != 0xffffffffu; /* min initialised to ord(+max) */
+    f3 lo, hi;
+    if (any) {
+        lo = mk(ord2f(b[0]), ord2f(b[1]), ord2f(b[2]));
+        hi = mk(ord2f(b[3]), ord2f(b[4]), ord2f(b[5]));
+    } else {
+        lo = mk1(0.f);
+        hi = mk1(0.f);
+    }
+    /* reset for the next photon pass */
+    for (int k = 0; k < 3; k++) {
+        pb.bbox[k] = 0xffffffffu;
+        pb.bbox[3 + k] = 0u;
+    }
+    /* padAABB (SpatialHash.cu:135-141) */
+    lo = mk(lo.x - 0.0000001f, lo.y - 0.0000001f, lo.z - 0.0000001f);
+    hi = mk(hi.x + 0.0000001f, hi.y + 0.0000001f, hi.z + 0.0000001f);
+    f3 ext = hi - lo;
+    /* getSmallestPossibleCellSize (SpatialHash.cu:62-71) */
+    float sceneVolume = ext.x * ext.y * ext.z;
+    float minVolumePerCell = sceneVolume / (float)pb.gmax;
+    float radiusC = orx_powf(minVolumePerCell, 1.0f / 3.0f);
+    f3 ncf = ext / radiusC;
+    uint32_t nx = orx_f2u_sat(orx_floorf(ncf.x)), ny = orx_f2u_sat(orx_floorf(ncf.y)),
+             nz = orx_f2u_sat(orx_floorf(ncf.z));
+    f3 each = mk(ext.x / (float)nx, ext.y / (float)ny, ext.z / (float)nz);
+    float smallest = fmax3(each);
+    float cellSize = (float)((double)smallest + 0.001);
+    /* calculateGridSize (SpatialHash.cu:42-50) */
+    f3 f = ext / cellSize;
+    uint32_t gx = orx_f2u_sat(orx_ceilf(f.x)), gy = orx_f2u_sat(orx_ceilf(f.y)), gz = orx_f2u_sat(orx_ceilf(f.z));
+    gx = gx < 1 ? 1 : gx;
+    gy = gy < 1 ? 1 : gy;
+    gz = gz < 1 ? 1 : gz;
+    uint64_t G = (uint64_t)gx * gy * gz;
+    GridParams* g = pb.grid;
+    g->ox = lo.x; g->oy = lo.y; g->oz = lo.z;
+    g->cell = cellSize;
+    g->gx = gx; g->gy = gy; g->gz = gz;
+    g->any_valid = any;
+    g->photons_visited = 0;
+    g->cells_visited = 0;
+    if (G > pb.gmax) {
+        g->error = 1;
+        g->G = 0;
+    } else {
+        g->error = 0;
+        g->G = (uint32_t)G;
+    }
+}
+void launch_grid_setup(hipStream_t s, const PhotonBufs& pb) {
+    hipLaunchKernelGGL(k_grid_setup, dim3(1), dim3(64), 0, s, pb);
+}
+
+/* ------------------------------------------------------------------ */
+/* hash + histogram (atomic rank = position inside the cell)           */
+/* ------------------------------------------------------------------ */
+__global__ __launch_bounds__(256) void k_grid_hash(PhotonBufs pb) {
+    const GridParams g = *pb.grid;
+    const uint32_t invalid = g.G + 1;
+    const float inv = 1.f / g.cell;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < pb.S; s += gridDim.x * blockDim.x) {
+        uint32_t p = s / pb.D, k = s - p * pb.D;
+        uint32_t key = invalid, rank = 0;
+        if (g.G && ((pb.vmask[p] >> k) & 1u)) {
+            float4 a = pb.slotA[s];
+            f3 pp = (mk(a.x, a.y, a.z) - mk(g.ox, g.oy, g.oz)) * inv;
+            uint32_t cx = orx_f2u_sat(orx_floorf(pp.x));
+            uint32_t cy = orx_f2u_sat(orx_floorf(pp.y));
+            uint32_t cz = orx_f2u_sat(orx_floorf(pp.z));
+            key = cx + cy * g.gx + cz * g.gx * g.gy;
+            if (key > g.G) key = g.G;
+            rank = atomicAdd(&pb.hist[key], 1u);
+        }
+        pb.keys[s] = key;
+        pb.ranks[s] = rank;
+    }
+}
+void launch_grid_hash(hipStream_t s, const PhotonBufs& pb) {
+    unsigned blocks = (pb.S + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_grid_hash, dim3(blocks), dim3(256), 0, s, pb);
+}
+
+/* ------------------------------------------------------------------ */
+/* exclusive scan of hist[0..G] -> offsets[0..G]; zeroes hist          */
+/* ------------------------------------------------------------------ */
+constexpr int SCAN_BLOCK = 1024; /* elements per block: 256 threads x 4 */
+
+__device__ __forceinline__ uint32_t block_exclusive_scan_256(uint32_t v, uint32_t* total) {
+    __shared__ uint32_t ws[4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) ws[w] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int q = 0; q < w; q++) pre += ws[q];
+    *total = ws[0] + ws[1] + ws[2] + ws[3];
+    __syncthreads();
+    return pre + x - v;
+}
+
+__global__ __launch_bounds__(256) void k_scan_reduce(PhotonBufs pb) {
+    const uint32_t n = pb.grid->G + 1;
+    uint32_t base = blockIdx.x * SCAN_BLOCK + threadIdx.x * 4;
+    uint32_t sum = 0;
+    if (blockIdx.x * SCAN_BLOCK < n) {
+        for (int k = 0; k < 4; k++)
+            if (base + k < n) sum += pb.hist[base + k];
+    }
+    uint32_t total;
+    (void)block_exclusive_scan_256(sum, &total);
+    if (threadIdx.x == 0) pb.scan_partials[blockIdx.x] = total;
+}
+__global__ __launch_bounds__(256) void k_scan_partials(PhotonBufs pb, uint32_t nblocks) {
+    /* single block: exclusive scan of the per-block totals */
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nblocks; base += 256) {
+        uint32_t i = base + threadIdx.x;
+        uint32_t v = i < nblocks ? pb.scan_partials[i] : 0;
+        uint32_t total;
+        uint32_t ex = block_exclusive_scan_256(v, &total);
+        if (i < nblocks) pb.scan_partials[i] = carry + ex;
+        carry += total;
+        __syncthreads();
+    }
+}
+__global__ __launch_bounds__(256) void k_scan_apply(PhotonBufs pb) {
+    const uint32_t G = pb.grid->G;
+    const uint32_t n = G + 1;
+    if (blockIdx.x * SCAN_BLOCK >= n) return;
+    uint32_t base = blockIdx.x * SCAN_BLOCK + threadIdx.x * 4;
+    uint32_t v[4];
+    uint32_t sum = 0;
+    for (int k = 0; k < 4; k++) {
+        v[k] = (base + k < n) ? pb.hist[base + k] : 0;
+        sum += v[k];
+    }
+    uint32_t total;
+    uint32_t ex = block_exclusive_scan_256(sum, &total) + pb.scan_partials[blockIdx.x];
+    for (int k = 0; k < 4; k++) {
+        if (base + k < n) {
+            pb.offsets[base + k] = ex;
+            pb.hist[base + k] = 0; /* consumed: ready for the next iteration */
+            if (base + k == G) {
+                pb.grid->valid = ex;
+                pb.grid->valid_total += ex;
+            }
+        }
+        ex += v[k];
+    }
+}
+void launch_grid_scan(hipStream_t s, const PhotonBufs& pb) {
+    uint32_t nblocks = (pb.gmax + 2 + SCAN_BLOCK - 1) / SCAN_BLOCK;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nblocks), dim3(256), 0, s, pb);
+    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(256), 0, s, pb, nblocks);
+    hipLaunchKernelGGL(k_scan_apply, dim3(nblocks), dim3(256), 0, s, pb);
+}
+
+/* ------------------------------------------------------------------ */
+/* scatter photons into cell order                                     */
+/* ------------------------------------------------------------------ */
+__global__ __launch_bounds__(256) void k_grid_scatter(PhotonBufs pb) {
+    const uint32_t G = pb.grid->G;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < pb.S; s += gridDim.x * blockDim.x) {
+        uint32_t key = pb.keys[s];
+        if (key > G) continue;
+        uint32_t dst = pb.offsets[key] + pb.ranks[s];
+        pb.sortA[dst] = pb.slotA[s];
+        pb.sortB[dst] = pb.slotB[s];
+        pb.sortC[dst] = pb.slotC[s];
+    }
+}
+void launch_grid_scatter(hipStream_t s, const PhotonBufs& pb) {
+    unsigned blocks = (pb.S + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_grid_scatter, dim3(blocks), dim3(256), 0, s, pb);
+}
+
+/* ------------------------------------------------------------------ */
+/* indirect radiance estimate: uniform-grid gather                     */
+/* ------------------------------------------------------------------ */
+__global__ __launch_bounds__(256) void k_ppm_gather(PixelBufs px, PhotonBufs pb, Consts c) {
+    const uint32_t x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const uint32_t j = blockIdx.y * 16 + (threadIdx.x >> 4);
+    const GridParams g = *pb.grid;
+    uint32_t dC = 0, dP = 0;
+    if (x < px.W && j < px.rows) {
+        const size_t i = (size_t)j * px.W + x;
+        const float4 A = px.hpA[i];
+        const float4 B = px.hpB[i];
+        const float2 Cc = px.hpC[i];
+        const uint32_t flags = __float_as_uint(A.w);
+        f3 acc = mk1(0.0f);
+        if ((flags & PRD_HIT_NON_SPECULAR) && g.G) {
+            const f3 pos = mk(A.x, A.y, A.z);
+            const f3 nrm = mk(B.x, B.y, B.z);
+            const float radius2 = c.ppm_radius2;
+            const float radius = c.ppm_radius;
+            const float invCellSize = 1.f / g.cell;
+            const f3 np = pos - mk(g.ox, g.oy, g.oz);
+            int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
+            int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
+            int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
+            uint32_t x_lo = (uint32_t)(ixl > 0 ? ixl : 0);
+            uint32_t y_lo = (uint32_t)(iyl > 0 ? iyl : 0);
+            uint32_t z_lo = (uint32_t)(izl > 0 ? izl : 0);
+            uint32_t ux = orx_f2u_sat((np.x + radius) * invCellSize);
+            uint32_t uy = orx_f2u_sat((np.y + radius) * invCellSize);
+            uint32_t uz = orx_f2u_sat((np.z + radius) * invCellSize);
+            uint32_t x_hi = (g.gx - 1) < ux ? (g.gx - 1) : ux;
+            uint32_t y_hi = (g.gy - 1) < uy ? (g.gy - 1) : uy;
+            uint32_t z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
+            if (x_lo <= x_hi) {
+                const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
+                for (uint32_t z = z_lo; z <= z_hi; z++) {
+                    for (uint32_t yy = y_lo; yy <= y_hi; yy++) {
+                        uint32_t from = x_lo + yy * g.gx + z * g.gx * g.gy;
+                        uint32_t to = from + (x_hi - x_lo);
+                        uint32_t off = pb.offsets[from];
+                        uint32_t offTo = pb.offsets[to + 1];
+                        dC++;
+                        dP += offTo - off;
+                        for (uint32_t k = off; k < offTo; k++) {
+                            const float4 pa = pb.sortA[k];
+                            f3 diff = pos - mk(pa.x, pa.y, pa.z);
+                            float distance2 = dot(diff, diff);
+                            if (distance2 <= radius2) {
+                                const float4 pbv = pb.sortB[k];
+                                if (dot(-mk(pbv.x, pbv.y, pbv.z), nrm) >= 0) {
+                                    float wgt = alpha * (1 - (1 - orx_expf(-beta * distance2 / (2 * radius2))) /
+                                                                 (1 - expNegativeBeta));
+                                    f3 pw = mk(pa.w, pbv.w, pb.sortC[k]);
+                                    acc = acc + pw * wgt;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        const f3 att = mk(B.w, Cc.x, Cc.y);
+        float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
+        float s2 = 1.0f / c.emitted_f;
+        f3 ind = ((acc * att) * s1) * s2;
+        px.indirect[3 * i + 0] = ind.x;
+        px.indirect[3 * i + 1] = ind.y;
+        px.indirect[3 * i + 2] = ind.z;
+        if (px.dbg) {
+            px.dbg[2 * i] = dC;
+            px.dbg[2 * i + 1] = dP;
+        }
+    }
+    uint64_t sp = wave_sum_u64(dP), sc = wave_sum_u64(dC);
+    if ((threadIdx.x & 63) == 0 && sp) {
+        atomicAdd((unsigned long long*)&pb.grid->photons_visited, (unsigned long long)sp);
+        atomicAdd((unsigned long long*)&pb.grid->cells_visited, (unsigned long long)sc);
+        atomicAdd((unsigned long long*)&pb.grid->photons_visited_total, (unsigned long long)sp);
+        atomicAdd((unsigned long long*)&pb.grid->cells_visited_total, (unsigned long long)sc);
+    }
+}
+void launch_ppm_gather(hipStream_t s, const PixelBufs& px, const PhotonBufs& pb, const Consts& c) {
+    dim3 grid((px.W + 15) / 16, (px.rows + 15) / 16);
+    hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), 0, s, px, pb, c);
+}
+
+/* ------------------------------------------------------------------ */
+/* direct radiance (4 shadow samples) + output accumulation            */
+/* ------------------------------------------------------------------ */
+__global__ __launch_bounds__(256) void k_ppm_direct_output(DevScene S, PixelBufs px, Consts c) {
+    const uint32_t x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const uint32_t j = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= px.W || j >= px.rows) return;
+    const size_t i = (size_t)j * px.W + x;
+    const float4 A = px.hpA[i];
+    const float4 B = px.hpB[i];
+    const float2 Cc = px.hpC[i];
+    const uint32_t flags = __float_as_uint(A.w);
+    f3 direct;
+    if (!(flags & PRD_HIT_NON_SPECULAR)) {
+        f3 rad = mk(B.x, B.y, B.z);
+        if ((flags & PRD_HIT_EMITTER) && !(flags & PRD_HIT_SPECULAR))
+            direct = mk(fminf(rad.x, 1.f), fminf(rad.y, 1.f), fminf(rad.z, 1.f));
+        else
+            direct = rad;
+    } else {
+        const size_t slot = (size_t)j * px.RW + x;
+        Rng rs = rng_load(px.rng, slot);
+        const int numLights = (int)S.nl;
+        const f3 pos = mk(A.x, A.y, A.z), nrm = mk(B.x, B.y, B.z);
+        f3 avg = mk1(0.f);
+        for (int s = 0; s < 4; s++) {
+            float sample = rnd(rs);
+            int li = (int)(sample * (float)numLights);
+            int randomLightIndex = li < numLights - 1 ? li : numLights - 1;
+            float scale = (float)numLights;
+            f3 lc = light_contribution(S, S.lights[randomLightIndex], pos, nrm, rs);
+            avg = avg + lc * scale;
+        }
+        direct = (mk(B.w, Cc.x, Cc.y) * avg) / (float)4;
+        rng_store(px.rng, slot, rs);
+    }
+    px.direct[3 * i + 0] = direct.x;
+    px.direct[3 * i + 1] = direct.y;
+    px.direct[3 * i + 2] = direct.z;
+    f3 ind = mk(px.indirect[3 * i], px.indirect[3 * i + 1], px.indirect[3 * i + 2]);
+    f3 fin = direct + ind;
+    f3 out = fin;
+    if (c.local_iteration != 0) out = mk(px.output[3 * i], px.output[3 * i + 1], px.output[3 * i + 2]) + fin;
+    px.output[3 * i + 0] = out.x;
+    px.output[3 * i + 1] = out.y;
+    px.output[3 * i + 2] = out.z;
+}
+void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c) {
+    dim3 grid((px.W + 15) / 16, (px.rows + 15) / 16);
+    hipLaunchKernelGGL(k_ppm_direct_output, grid, dim3(256), 0, s, S, px, c);
+}
+
+/* ------------------------------------------------------------------ */
+/* path tracing                                                        */
+/* ------------------------------------------------------------------ */
+__global__ __launch_bounds__(256) void k_pt(DevScene S, DevCamera cam, PixelBufs px, Consts c) {
+    const uint32_t x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const uint32_t j = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= px.W || j >= px.rows) return;
+    const uint32_t y = px.rank + px.world * j;
+    const size_t i = (size_t)j * px.W + x;
+    const size_t slot = (size_t)j * px.RW + x;
+    /* the PRD copy and the global slot start from the same state and are
+     * advanced independently (RayGeneratorPT.cu:52, :89, :111, :130) */
+    Rng G = rng_load(px.rng, slot);
+    Rng rs = G;
+    const int numLights = (int)S.nl;
+    RadiancePRD prd;
+    prd.attenuation = mk1(1.0f);
+    prd.radiance = mk1(0.f);
+    prd.depth = 0;
+    prd.flags = 0;
+    prd.position = mk1(0.f);
+    prd.normal = mk1(0.f);
+    prd.newdir = mk1(0.f);
+    f3 o, d;
+    primary_ray(cam, x, y, px.W, px.H, rs, o, d);
+    f3 fin = mk1(0);
+    for (int it = 0; it < 5; it++) {
+        prd.flags = PRD_PATH_TRACING;
+        trace_radiance(S, c.max_radiance_depth, o, d, 0.001f, prd, rs);
+        if (prd.flags & PRD_HIT_EMITTER) {
+            if ((prd.flags & PRD_HIT_SPECULAR) || it == 0) fin = prd.radiance;
+            break;
+        } else if (prd.flags & PRD_HIT_NON_SPECULAR) {
+            f3 accum = mk1(0);
+            int li = (int)(rnd(G) * (float)numLights);
+            float scale = (float)numLights;
+            f3 lc = light_contribution(S, S.lights[li], prd.position, prd.normal, rs) * scale;
+            accum = accum + lc;
+            f3 direct = (prd.attenuation * accum) / (float)1;
+            fin = fin + direct;
+            o = prd.position;
+            d = prd.newdir;
+        } else {
+            break;
+        }
+        if (it >= 3) {
+            float sample = rnd(G);
+            float p = fmax3(prd.attenuation);
+            if (sample > p) break;
+            prd.attenuation = prd.attenuation / p;
+        }
+    }
+    if (!isnan3(fin)) {
+        f3 out = fin;
+        if (c.local_iteration != 0) out = mk(px.output[3 * i], px.output[3 * i + 1], px.output[3 * i + 2]) + fin;
+        px.output[3 * i + 0] = out.x;
+        px.output[3 * i + 1] = out.y;
+        px.output[3 * i + 2] = out.z;
+    }
+    rng_store(px.rng, slot, rs);
+}
+void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c) {
+    dim3 grid((px.W + 15) / 16, (px.rows + 15) / 16);
+    hipLaunchKernelGGL(k_pt, grid, dim3(256), 0, s, S, cam, px, c);
+}
+
+}  // namespace orx

@@ -1,0 +1,1246 @@
+/*
+ * orx_oracle.c — plain-C restatement of OppositeRenderer's progressive photon
+ * mapping (PPM) and path tracing (PT) passes.  TEST INFRASTRUCTURE ONLY (see
+ * orx_oracle.h).  Every function cites the reference file:line it follows;
+ * float expressions keep the reference's operand order because the build
+ * runs with -ffp-contract=off and the GPU kernels evaluate the same order.
+ *
+ * OptiX vector semantics used throughout (optixu_math_namespace.h, OptiX 3.x):
+ *   dot(a,b) = a.x*b.x + a.y*b.y + a.z*b.z
+ *   normalize(v) = v * (1.0f / sqrtf(dot(v,v)))
+ *   float3 / float  = float3 * (1.0f / s)
+ *   reflect(i,n) = i - 2*n*dot(n,i)
+ * CUDA fast-math transcendentals are replaced by orx_detmath.h (see there).
+ */
+#include "orx_oracle.h"
+#include "orx_detmath.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ------------------------------------------------------------------ */
+/* float3                                                              */
+/* ------------------------------------------------------------------ */
+typedef struct { float x, y, z; } v3;
+
+static inline v3 mk(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 mk1(float a) { return mk(a, a, a); }
+static inline v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+static inline v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 mul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline v3 scl(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+static inline v3 sub_s(v3 a, float s) { return mk(a.x - s, a.y - s, a.z - s); }
+static inline v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }
+static inline v3 divs(v3 a, float s) { float inv = 1.0f / s; return scl(a, inv); }
+static inline v3 divv(v3 a, v3 b) { return mk(a.x / b.x, a.y / b.y, a.z / b.z); }
+static inline float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline v3 cross(v3 a, v3 b) {
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+static inline float length(v3 a) { return sqrtf(dot(a, a)); }
+static inline v3 normalize(v3 a) { float inv = 1.0f / sqrtf(dot(a, a)); return scl(a, inv); }
+static inline float maxf(float a, float b) { return a > b ? a : b; } /* helpers.h:143-146 */
+static inline float fmax3(v3 a) { return fmaxf(fmaxf(a.x, a.y), a.z); }
+static inline v3 vmin(v3 a, v3 b) { return mk(fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z)); }
+static inline v3 vmax(v3 a, v3 b) { return mk(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z)); }
+static inline float favgf(v3 v) { return (v.x + v.y + v.z) * 0.3333333333f; } /* helpers.h:163-166 */
+static inline v3 reflect(v3 i, v3 n) { return sub(i, scl(scl(n, 2.0f), dot(n, i))); }
+static inline int isnan3(v3 v) { return v.x != v.x || v.y != v.y || v.z != v.z; }
+
+/* OptiX refract (optixu_math_namespace.h) */
+static int refract(v3* r, v3 i, v3 n, float ior) {
+    v3 nn = n;
+    float negNdotV = dot(i, nn);
+    float eta;
+    if (negNdotV > 0.0f) {
+        eta = ior;
+        nn = neg(n);
+        negNdotV = -negNdotV;
+    } else {
+        eta = 1.f / ior;
+    }
+    const float k = 1.f - eta * eta * (1.f - negNdotV * negNdotV);
+    if (k < 0.0f) {
+        *r = mk1(0.f);
+        return 0;
+    }
+    *r = normalize(sub(scl(i, eta), scl(nn, eta * negNdotV + sqrtf(k))));
+    return 1;
+}
+
+/* ------------------------------------------------------------------ */
+/* cuRAND XORWOW (curand_kernel.h, CUDA 5.5) and helpers/random.h      */
+/* ------------------------------------------------------------------ */
+void orc_xorwow_init(uint64_t seed, uint32_t st[6]) {
+    uint32_t s0 = ((uint32_t)seed) ^ 0xaad26b49u;
+    uint32_t s1 = ((uint32_t)(seed >> 32)) ^ 0xf7dcefddu;
+    uint32_t t0 = 1099087573u * s0;
+    uint32_t t1 = 2591861531u * s1;
+    st[5] = 6615241u + t1 + t0;
+    st[0] = 123456789u + t0;
+    st[1] = 362436069u ^ t0;
+    st[2] = 521288629u + t1;
+    st[3] = 88675123u ^ t1;
+    st[4] = 5783321u + t0;
+}
+uint32_t orc_xorwow_next(uint32_t st[6]) {
+    uint32_t t = st[0] ^ (st[0] >> 2);
+    st[0] = st[1];
+    st[1] = st[2];
+    st[2] = st[3];
+    st[3] = st[4];
+    st[4] = (st[4] ^ (st[4] << 4)) ^ (t ^ (t << 1));
+    st[5] += 362437u;
+    return st[4] + st[5];
+}
+/* getRandomUniformFloat: max(curand_uniform - FLT_EPSILON, 0) (helpers/random.h:65-69);
+ * curand_uniform = x*2^-32 + 2^-33, contracted to one FMA by nvcc. */
+float orc_uniform(uint32_t st[6]) {
+    uint32_t x = orc_xorwow_next(st);
+    float u = fmaf((float)x, 2.3283064e-10f, 2.3283064e-10f / 2.0f);
+    return maxf(u - ORX_FLT_EPSILON, 0.0f);
+}
+
+/* ------------------------------------------------------------------ */
+/* samplers (helpers/samplers.h, helpers/helpers.h)                    */
+/* ------------------------------------------------------------------ */
+static void create_coordinate_system(v3 N, v3* U, v3* V) { /* helpers.h:119-134 */
+    if (fabsf(N.x) > fabsf(N.y)) {
+        float invLength = 1.f / sqrtf(N.x * N.x + N.z * N.z);
+        *U = mk(-N.z * invLength, 0.f, N.x * invLength);
+    } else {
+        float invLength = 1.f / sqrtf(N.y * N.y + N.z * N.z);
+        *U = mk(0.f, N.z * invLength, -N.y * invLength);
+    }
+    *V = cross(N, *U);
+}
+/* samplers.h:24-43 (no pdf outputs, no bias) */
+static v3 sample_hemisphere_cos(v3 normal, float sx, float sy) {
+    float theta = orx_acosf(sqrtf(sx));
+    float phi = 2.0f * ORX_PI_F * sy;
+    float st = orx_sinf(theta);
+    float xs = st * orx_cosf(phi);
+    float ys = orx_cosf(theta);
+    float zs = st * orx_sinf(phi);
+    v3 U, V;
+    create_coordinate_system(normal, &U, &V);
+    return normalize(add(add(scl(U, xs), scl(normal, ys)), scl(V, zs)));
+}
+/* samplers.h:46-57 */
+static v3 sample_hemisphere(v3 normal, float sx, float sy) {
+    v3 U, V;
+    create_coordinate_system(normal, &U, &V);
+    float phi = 2.0f * ORX_PI_F * sx;
+    float r = sqrtf(sy);
+    float x = r * orx_cosf(phi);
+    float y = r * orx_sinf(phi);
+    float z = 1.0f - x * x - y * y;
+    z = z > 0.0f ? sqrtf(z) : 0.0f;
+    return normalize(add(add(scl(U, x), scl(V, y)), scl(normal, z)));
+}
+/* samplers.h:59-72 */
+static v3 sample_unit_sphere(float sx, float sy) {
+    v3 v;
+    v.z = 1.f - 2.f * sx;
+    float phi = 2 * ORX_PI_F * sy;
+    float r = sqrtf(1.f - v.z * v.z);
+    v.x = r * orx_cosf(phi);
+    v.y = r * orx_sinf(phi);
+    return v;
+}
+/* samplers.h:74-93 */
+static v3 sample_disc(float sx, float sy, v3 center, float radius, v3 normal) {
+    v3 U, V;
+    create_coordinate_system(normal, &U, &V);
+    float r = sqrtf(sx);
+    float theta = 2.f * ORX_PI_F * sy;
+    float x = r * orx_cosf(theta);
+    float y = r * orx_sinf(theta);
+    return add(center, scl(add(scl(U, x), scl(V, y)), radius));
+}
+
+void orc_sample_unit_hemisphere_cos(const float n[3], float u1, float u2, float out[3]) {
+    v3 r = sample_hemisphere_cos(ld3(n), u1, u2);
+    out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+void orc_sample_unit_hemisphere(const float n[3], float u1, float u2, float out[3]) {
+    v3 r = sample_hemisphere(ld3(n), u1, u2);
+    out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+
+/* ------------------------------------------------------------------ */
+/* scene                                                               */
+/* ------------------------------------------------------------------ */
+#define ORC_RT_DEFAULT_MAX 1.e27f /* optix_device.h RT_DEFAULT_MAX */
+#define PRD_HIT_EMITTER (1u << 31)
+#define PRD_ERROR (1u << 30)
+#define PRD_MISS (1u << 29)
+#define PRD_HIT_SPECULAR (1u << 28)
+#define PRD_HIT_NON_SPECULAR (1u << 27)
+#define PRD_PATH_TRACING (1u << 26)
+
+typedef struct {
+    int type;
+    v3 Kd, Ks, Kr, Kt;
+    float ior, exponent;
+    v3 powerPerArea, Lemit;
+    float inverseArea;
+} mat_t;
+
+typedef struct {
+    int type;
+    v3 power, position, v1, v2, normal, Lemit; /* Lemit doubles as intensity (Light.h union) */
+    v3 direction;
+    float area, inverseArea, angle;
+} light_t;
+
+typedef struct { v3 n; float d; v3 anchor, v1, v2; } quadp_t;
+typedef struct { v3 c; float r; } sphere_t;
+
+typedef struct { v3 position, normal, attenuation, radiance; uint32_t flags; } hitpoint_t;
+typedef struct { v3 power, position, direction; } photon_t; /* Photon.h:10-33 */
+
+struct orc_renderer {
+    orx_config cfg;
+    char err[512];
+    int scene_ready;
+    /* scene */
+    uint32_t nq, ns, nt, nv, nm, nl;
+    quadp_t* quads; uint32_t* qmat;
+    sphere_t* sph; uint32_t* smat;
+    v3* verts; v3* vnorm; int has_normals;
+    uint32_t* tris; uint32_t* tmat;
+    mat_t* mats;
+    light_t* lights;
+    v3 aabb_min, aabb_max;
+    v3 bs_center; float bs_radius;
+    /* frame */
+    uint32_t W, H, RW, RH;
+    int rng_ready;
+    uint32_t* rng; /* [RW*RH][6] */
+    hitpoint_t* hp;
+    photon_t* photons; uint32_t* keys; photon_t* sort_tmp;
+    uint32_t* offsets; uint32_t* hist;
+    v3* indirect; v3* direct; v3* output;
+    uint32_t* dbg; /* [W*H][2] */
+    /* grid state */
+    uint32_t gsize[3]; float cell; v3 origo; uint32_t ncells; uint32_t valid;
+    uint64_t sum_photons_visited, sum_cells_visited;
+};
+
+static orx_status fail(orc_renderer* r, orx_status s, const char* msg) {
+    if (r) snprintf(r->err, sizeof r->err, "%s", msg);
+    return s;
+}
+
+const char* orc_last_error(const orc_renderer* r) { return r ? r->err : "null renderer"; }
+
+void orc_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
+orx_status orc_create(const orx_config* cfg, orc_renderer** out) {
+    if (!out) return ORX_ERR_INVALID_ARGUMENT;
+    orc_renderer* r = (orc_renderer*)calloc(1, sizeof *r);
+    if (!r) return ORX_ERR_OUT_OF_MEMORY;
+    if (cfg) r->cfg = *cfg;
+    else orc_default_config(&r->cfg);
+    r->W = 10; r->H = 10; /* OptixRenderer ctor m_width(10), m_height(10) */
+    *out = r;
+    return ORX_OK;
+}
+
+static void free_scene(orc_renderer* r) {
+    free(r->quads); free(r->qmat); free(r->sph); free(r->smat);
+    free(r->verts); free(r->vnorm); free(r->tris); free(r->tmat);
+    free(r->mats); free(r->lights);
+    r->quads = NULL; r->qmat = NULL; r->sph = NULL; r->smat = NULL; r->verts = NULL;
+    r->vnorm = NULL; r->tris = NULL; r->tmat = NULL; r->mats = NULL; r->lights = NULL;
+}
+static void free_frame(orc_renderer* r) {
+    free(r->rng); free(r->hp); free(r->photons); free(r->keys); free(r->sort_tmp);
+    free(r->offsets); free(r->hist); free(r->indirect); free(r->direct); free(r->output); free(r->dbg);
+    r->rng = NULL; r->hp = NULL; r->photons = NULL; r->keys = NULL; r->sort_tmp = NULL;
+    r->offsets = NULL; r->hist = NULL; r->indirect = NULL; r->direct = NULL; r->output = NULL; r->dbg = NULL;
+}
+void orc_destroy(orc_renderer* r) {
+    if (!r) return;
+    free_scene(r);
+    free_frame(r);
+    free(r);
+}
+
+/* Light ctors (renderer/Light.cpp:14-49) */
+static light_t make_light(const orx_light* L) {
+    light_t l;
+    memset(&l, 0, sizeof l);
+    l.type = L->type;
+    l.power = ld3(L->power);
+    l.position = ld3(L->position);
+    if (L->type == ORX_LIGHT_AREA) {
+        l.v1 = ld3(L->v1);
+        l.v2 = ld3(L->v2);
+        v3 c = cross(l.v1, l.v2);
+        l.normal = normalize(c);
+        l.area = length(c);
+        l.inverseArea = 1.0f / l.area;
+        l.Lemit = scl(scl(l.power, l.inverseArea), ORX_1_PI_F);
+    } else if (L->type == ORX_LIGHT_POINT) {
+        l.Lemit = scl(scl(l.power, 0.25f), ORX_1_PI_F); /* intensity */
+    } else {
+        /* SPOT: the ctor normalises its by-value parameter, not the member (Light.cpp:41) */
+        l.direction = ld3(L->direction);
+        l.normal = l.direction;
+        l.angle = L->angle;
+        float angleFactor = 1.0f / (1.0f - cosf(l.angle * 180 * ORX_1_PI_F));
+        l.Lemit = scl(scl(scl(l.power, 0.25f), ORX_1_PI_F), angleFactor);
+    }
+    return l;
+}
+
+/* Vector3::length with the reference's dot bug a.z*b.x (math/Vector3.cpp:27-30) */
+static float vector3_buggy_length(v3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.x); }
+
+orx_status orc_init_scene(orc_renderer* r, const orx_scene* s) {
+    if (!r || !s) return ORX_ERR_INVALID_ARGUMENT;
+    if (s->n_lights == 0) return fail(r, ORX_ERR_NO_LIGHTS, "No lights exists in this scene.");
+    free_scene(r);
+    r->nq = s->n_quads; r->ns = s->n_spheres; r->nt = s->n_triangles; r->nv = s->n_vertices;
+    r->nm = s->n_materials; r->nl = s->n_lights;
+    r->quads = (quadp_t*)calloc(r->nq + 1, sizeof(quadp_t));
+    r->qmat = (uint32_t*)calloc(r->nq + 1, 4);
+    for (uint32_t i = 0; i < r->nq; i++) {
+        /* Cornell::createParallelogram (scene/Cornell.cpp:33-64) */
+        v3 anchor = ld3(s->quads + 9 * i), o1 = ld3(s->quads + 9 * i + 3), o2 = ld3(s->quads + 9 * i + 6);
+        v3 normal = normalize(cross(o1, o2));
+        r->quads[i].n = normal;
+        r->quads[i].d = dot(normal, anchor);
+        r->quads[i].anchor = anchor;
+        r->quads[i].v1 = divs(o1, dot(o1, o1));
+        r->quads[i].v2 = divs(o2, dot(o2, o2));
+        r->qmat[i] = s->quad_material[i];
+    }
+    r->sph = (sphere_t*)calloc(r->ns + 1, sizeof(sphere_t));
+    r->smat = (uint32_t*)calloc(r->ns + 1, 4);
+    for (uint32_t i = 0; i < r->ns; i++) {
+        r->sph[i].c = ld3(s->spheres + 4 * i);
+        r->sph[i].r = s->spheres[4 * i + 3];
+        r->smat[i] = s->sphere_material[i];
+    }
+    r->verts = (v3*)calloc(r->nv + 1, sizeof(v3));
+    r->vnorm = (v3*)calloc(r->nv + 1, sizeof(v3));
+    r->has_normals = s->normals != NULL;
+    for (uint32_t i = 0; i < r->nv; i++) {
+        r->verts[i] = ld3(s->vertices + 3 * i);
+        if (s->normals) r->vnorm[i] = ld3(s->normals + 3 * i);
+    }
+    r->tris = (uint32_t*)calloc(3 * (size_t)r->nt + 3, 4);
+    r->tmat = (uint32_t*)calloc(r->nt + 1, 4);
+    if (r->nt) {
+        memcpy(r->tris, s->triangles, 12 * (size_t)r->nt);
+        memcpy(r->tmat, s->triangle_material, 4 * (size_t)r->nt);
+    }
+    r->mats = (mat_t*)calloc(r->nm + 1, sizeof(mat_t));
+    for (uint32_t i = 0; i < r->nm; i++) {
+        const orx_material* m = &s->materials[i];
+        mat_t* d = &r->mats[i];
+        d->type = m->type;
+        d->Kd = ld3(m->Kd); d->Ks = ld3(m->Ks); d->Kr = ld3(m->Kr); d->Kt = ld3(m->Kt);
+        d->ior = m->ior; d->exponent = m->exponent;
+        if (m->type == ORX_MAT_DIFFUSE_EMITTER) {
+            /* DiffuseEmitter.cpp:17-25, :48-62 */
+            v3 power = mul(ld3(m->power), d->Kd);
+            d->inverseArea = m->inverse_area;
+            d->powerPerArea = scl(power, m->inverse_area);
+            d->Lemit = scl(scl(power, m->inverse_area), ORX_1_PI_F);
+        }
+        if (m->type == ORX_MAT_GLOSSY) {
+            /* Glossy.cpp:16-30 energy clamp */
+            v3 sumK = add(d->Kd, d->Ks);
+            float sumScale = 1.f / maxf(maxf(sumK.x, sumK.y), sumK.z);
+            if (sumScale < 1.f) { d->Kd = scl(d->Kd, sumScale); d->Ks = scl(d->Ks, sumScale); }
+        }
+    }
+    r->lights = (light_t*)calloc(r->nl + 1, sizeof(light_t));
+    for (uint32_t i = 0; i < r->nl; i++) r->lights[i] = make_light(&s->lights[i]);
+    r->aabb_min = ld3(s->aabb_min);
+    r->aabb_max = ld3(s->aabb_max);
+    /* AAB::getBoundingSphere (math/AAB.cpp:26-33) */
+    v3 center = scl(add(r->aabb_min, r->aabb_max), 0.5f);
+    r->bs_center = center;
+    r->bs_radius = vector3_buggy_length(sub(r->aabb_max, center));
+    r->scene_ready = 1;
+    return ORX_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* ray casting (geometry_instance: parallelogram, Sphere, TriangleMesh) */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    float t;
+    int32_t prim; /* global id: quads, spheres, triangles */
+    v3 gn, sn;    /* geometricNormal / shadingNormal attributes */
+} hit_t;
+
+/* parallelogram.cu:49-76 */
+static inline int isect_quad(const quadp_t* q, v3 o, v3 d, float tmin, float tmax, float* tout) {
+    v3 n = q->n;
+    float dt = dot(d, n);
+    float t = (q->d - dot(n, o)) / dt;
+    if (t > tmin && t < tmax) {
+        v3 p = add(o, scl(d, t));
+        v3 vi = sub(p, q->anchor);
+        float a1 = dot(q->v1, vi);
+        if (a1 >= 0 && a1 <= 1) {
+            float a2 = dot(q->v2, vi);
+            if (a2 >= 0 && a2 <= 1) { *tout = t; return 1; }
+        }
+    }
+    return 0;
+}
+/* Sphere.cu:32-56 — returns the reported root, normal through *n */
+static inline int isect_sphere(const sphere_t* s, v3 o, v3 d, float tmin, float tmax, float* tout, v3* nout) {
+    v3 O = sub(o, s->c);
+    float b = dot(O, d);
+    float c = dot(O, O) - s->r * s->r;
+    float disc = b * b - c;
+    if (disc > 0.0f) {
+        float sdisc = sqrtf(disc);
+        float root1 = (-b - sdisc);
+        if (root1 > tmin && root1 < tmax) {
+            *tout = root1;
+            *nout = divs(add(O, scl(d, root1)), s->r);
+            return 1;
+        }
+        float root2 = (-b + sdisc);
+        if (root2 > tmin && root2 < tmax) {
+            *tout = root2;
+            *nout = divs(add(O, scl(d, root2)), s->r);
+            return 1;
+        }
+    }
+    return 0;
+}
+/* OptiX intersect_triangle_branchless (optixu_math_namespace.h), TriangleMesh.cu:35-54 */
+static inline int isect_tri(v3 p0, v3 p1, v3 p2, v3 o, v3 d, float tmin, float tmax, float* tout, v3* nout,
+                            float* bout, float* gout) {
+    v3 e0 = sub(p1, p0);
+    v3 e1 = sub(p0, p2);
+    v3 n = cross(e1, e0);
+    v3 e2 = scl(sub(p0, o), 1.0f / dot(n, d));
+    v3 i = cross(d, e2);
+    float beta = dot(i, e1);
+    float gamma = dot(i, e0);
+    float t = dot(n, e2);
+    if ((t < tmax) & (t > tmin) & (beta >= 0.0f) & (gamma >= 0.0f) & (beta + gamma <= 1)) {
+        *tout = t; *nout = n; *bout = beta; *gout = gamma;
+        return 1;
+    }
+    return 0;
+}
+
+/* closest hit; equal t -> lowest primitive id (NoAccel child order, Cornell.cpp:183-189) */
+static int trace_closest(const orc_renderer* r, v3 o, v3 d, float tmin, float tmax, hit_t* h) {
+    float best = tmax;
+    int32_t bp = -1;
+    float t;
+    for (uint32_t i = 0; i < r->nq; i++)
+        if (isect_quad(&r->quads[i], o, d, tmin, best, &t)) { best = t; bp = (int32_t)i; }
+    v3 sn_s = mk1(0);
+    for (uint32_t i = 0; i < r->ns; i++) {
+        v3 n;
+        if (isect_sphere(&r->sph[i], o, d, tmin, best, &t, &n)) { best = t; bp = (int32_t)(r->nq + i); sn_s = n; }
+    }
+    float tb = 0, tg = 0;
+    v3 tn = mk1(0);
+    for (uint32_t i = 0; i < r->nt; i++) {
+        const uint32_t* ix = r->tris + 3 * (size_t)i;
+        v3 n; float b, g;
+        if (isect_tri(r->verts[ix[0]], r->verts[ix[1]], r->verts[ix[2]], o, d, tmin, best, &t, &n, &b, &g)) {
+            best = t; bp = (int32_t)(r->nq + r->ns + i); tn = n; tb = b; tg = g;
+        }
+    }
+    if (bp < 0) return 0;
+    h->t = best;
+    h->prim = bp;
+    if ((uint32_t)bp < r->nq) {
+        h->gn = h->sn = r->quads[bp].n;
+    } else if ((uint32_t)bp < r->nq + r->ns) {
+        h->gn = h->sn = sn_s;
+    } else {
+        uint32_t ti = (uint32_t)bp - r->nq - r->ns;
+        const uint32_t* ix = r->tris + 3 * (size_t)ti;
+        if (r->has_normals) {
+            v3 n0 = r->vnorm[ix[0]], n1 = r->vnorm[ix[1]], n2 = r->vnorm[ix[2]];
+            h->sn = normalize(add(add(scl(n1, tb), scl(n2, tg)), scl(n0, 1.0f - tb - tg)));
+        } else {
+            h->sn = normalize(tn);
+        }
+        h->gn = normalize(tn);
+    }
+    return 1;
+}
+static uint32_t prim_material(const orc_renderer* r, int32_t p) {
+    if ((uint32_t)p < r->nq) return r->qmat[p];
+    if ((uint32_t)p < r->nq + r->ns) return r->smat[p - r->nq];
+    return r->tmat[p - r->nq - r->ns];
+}
+/* shadow ray: any hit in (tmin, tmax) occludes (every material carries
+ * gatherAnyHitOnNonEmitter for RayType::SHADOW, Material.cpp:18-26, which
+ * DiffuseEmitter.cpp:33 installs last and so overrides gatherAnyHitOnEmitter) */
+static int trace_any(const orc_renderer* r, v3 o, v3 d, float tmin, float tmax) {
+    float t;
+    for (uint32_t i = 0; i < r->nq; i++)
+        if (isect_quad(&r->quads[i], o, d, tmin, tmax, &t)) return 1;
+    for (uint32_t i = 0; i < r->ns; i++) {
+        v3 n;
+        if (isect_sphere(&r->sph[i], o, d, tmin, tmax, &t, &n)) return 1;
+    }
+    for (uint32_t i = 0; i < r->nt; i++) {
+        const uint32_t* ix = r->tris + 3 * (size_t)i;
+        v3 n; float b, g;
+        if (isect_tri(r->verts[ix[0]], r->verts[ix[1]], r->verts[ix[2]], o, d, tmin, tmax, &t, &n, &b, &g)) return 1;
+    }
+    return 0;
+}
+
+int32_t orc_trace_closest(orc_renderer* r, const float o[3], const float d[3], float tmin, float tmax, float* t_out) {
+    hit_t h;
+    if (!trace_closest(r, ld3(o), ld3(d), tmin, tmax, &h)) return -1;
+    if (t_out) *t_out = h.t;
+    return h.prim;
+}
+int32_t orc_trace_any(orc_renderer* r, const float o[3], const float d[3], float tmin, float tmax) {
+    return trace_any(r, ld3(o), ld3(d), tmin, tmax);
+}
+
+/* ------------------------------------------------------------------ */
+/* camera (renderer/Camera.cpp:333-345)                                */
+/* ------------------------------------------------------------------ */
+typedef struct { v3 eye, lookdir, u, v; float aperture; } cam_t;
+
+static float dtor(float d) { return d * ((float)M_PI / 180.f); } /* Camera.cpp:87-90 */
+
+static cam_t camera_setup(const orx_camera* c) {
+    cam_t k;
+    v3 eye = ld3(c->eye), lookat = ld3(c->lookat), up = ld3(c->up);
+    k.eye = eye;
+    k.lookdir = sub(lookat, eye);
+    float lookdir_len = length(k.lookdir);
+    up = normalize(up);
+    v3 cu = normalize(cross(k.lookdir, up));
+    v3 cv = normalize(cross(cu, k.lookdir));
+    float ulen = lookdir_len * tanf(dtor(c->hfov * 0.5f));
+    k.u = scl(cu, ulen);
+    float vlen = lookdir_len * tanf(dtor(c->vfov * 0.5f));
+    k.v = scl(cv, vlen);
+    k.aperture = c->aperture;
+    return k;
+}
+void orc_camera_setup(const orx_camera* cam, float lookdir[3], float u[3], float v[3]) {
+    cam_t k = camera_setup(cam);
+    lookdir[0] = k.lookdir.x; lookdir[1] = k.lookdir.y; lookdir[2] = k.lookdir.z;
+    u[0] = k.u.x; u[1] = k.u.y; u[2] = k.u.z;
+    v[0] = k.v.x; v[1] = k.v.y; v[2] = k.v.z;
+}
+
+/* RayGeneratorPPM.cu:40-48 / RayGeneratorPT.cu:53-61 + helpers/camera.h:11-27 */
+static void primary_ray(const cam_t* cam, uint32_t x, uint32_t y, uint32_t W, uint32_t H, uint32_t* rs, v3* o, v3* d) {
+    float sx = orc_uniform(rs);
+    float sy = orc_uniform(rs);
+    float dx = ((float)x + sx) / (float)W * 2.0f - 1.0f;
+    float dy = ((float)y + sy) / (float)H * 2.0f - 1.0f;
+    v3 origin = cam->eye;
+    v3 dir = normalize(add(add(scl(cam->u, dx), scl(cam->v, dy)), cam->lookdir));
+    if (cam->aperture > 0) {
+        v3 focal = add(cam->eye, cam->lookdir);
+        v3 camLookDir = normalize(cam->lookdir);
+        float focalPlaneT = (dot(camLookDir, focal) - dot(camLookDir, cam->eye)) / dot(camLookDir, dir);
+        v3 lookAt = add(origin, scl(dir, focalPlaneT));
+        float ux = orc_uniform(rs);
+        float uy = orc_uniform(rs);
+        float rr = sqrtf(ux);
+        float th = 2.f * ORX_PI_F * uy;
+        float discx = rr * orx_cosf(th);
+        float discy = rr * orx_sinf(th);
+        origin = add(origin, add(scl(scl(cam->u, discx), cam->aperture), scl(scl(cam->v, discy), cam->aperture)));
+        dir = normalize(sub(lookAt, origin));
+    }
+    *o = origin;
+    *d = dir;
+}
+
+/* ------------------------------------------------------------------ */
+/* radiance rays: RadiancePRD + material closest-hit programs          */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    v3 attenuation, radiance;
+    uint32_t depth;
+    v3 position, normal;
+    uint32_t flags;
+    v3 newdir; /* randomNewDirection / Le union */
+    uint32_t* rs;
+} rprd_t;
+
+/* Iterative form of the recursive rtTrace(RADIANCE) chain: Mirror/Glass
+ * closest-hit programs tail-recurse (Mirror.cu:50-63, Glass.cu:90-143). */
+static void trace_radiance(const orc_renderer* r, v3 o, v3 d, float tmin, rprd_t* prd) {
+    const uint32_t maxd = r->cfg.max_radiance_trace_depth;
+    for (;;) {
+        hit_t h;
+        if (!trace_closest(r, o, d, tmin, ORC_RT_DEFAULT_MAX, &h)) {
+            /* miss (RayGeneratorPPM.cu:72-77, RayGeneratorPT.cu:144-150) */
+            prd->flags = PRD_MISS;
+            prd->attenuation = mk1(0.f);
+            prd->radiance = mk1(0.f);
+            return;
+        }
+        const mat_t* m = &r->mats[prim_material(r, h.prim)];
+        v3 hitPoint = add(o, scl(d, h.t));
+        if (m->type == ORX_MAT_DIFFUSE || m->type == ORX_MAT_GLOSSY) {
+            /* Diffuse.cu:71-87, Glossy.cu:74-90 */
+            v3 N = normalize(h.sn);
+            prd->flags |= PRD_HIT_NON_SPECULAR;
+            prd->attenuation = mul(prd->attenuation, m->Kd);
+            prd->normal = N;
+            prd->position = hitPoint;
+            prd->depth++;
+            if (prd->flags & PRD_PATH_TRACING) {
+                float s0 = orc_uniform(prd->rs);
+                float s1 = orc_uniform(prd->rs);
+                prd->newdir = sample_hemisphere_cos(N, s0, s1);
+            }
+            return;
+        } else if (m->type == ORX_MAT_DIFFUSE_EMITTER) {
+            /* DiffuseEmitter.cu:40-51 */
+            v3 N = normalize(h.sn);
+            prd->flags |= PRD_HIT_EMITTER;
+            if (dot(N, neg(d)) < 0.f) return;
+            v3 Le = divs(m->powerPerArea, ORX_PI_F);
+            prd->radiance = add(prd->radiance, mul(prd->attenuation, Le));
+            return;
+        } else if (m->type == ORX_MAT_MIRROR) {
+            /* Mirror.cu:50-63 */
+            v3 N = normalize(h.sn);
+            prd->depth++;
+            if (prd->depth <= maxd) {
+                prd->attenuation = mul(prd->attenuation, m->Kr);
+                d = reflect(d, N);
+                o = hitPoint;
+                tmin = 0.0001f;
+                continue;
+            }
+            return;
+        } else { /* ORX_MAT_GLASS, Glass.cu:90-143 */
+            v3 wsn = normalize(h.sn);
+            int outside = dot(wsn, d) < 0;
+            v3 N = outside ? wsn : neg(wsn);
+            float n1 = outside ? 1.0f : m->ior, n2 = outside ? m->ior : 1.0f;
+            v3 refr;
+            int valid = refract(&refr, d, N, n2 / n1);
+            float cosI = -dot(d, N);
+            float cosT = -dot(refr, N);
+            float refl = 1.f;
+            if (valid) {
+                float rp = (n2 * cosI - n1 * cosT) / (n2 * cosI + n1 * cosT);
+                float rsv = (n1 * cosI - n2 * cosT) / (n1 * cosI + n2 * cosT);
+                refl = (rp * rp + rsv * rsv) / 2.f;
+            }
+            float sample = orc_uniform(prd->rs);
+            int isReflected = sample <= refl;
+            v3 nd;
+            if (isReflected) nd = reflect(d, N);
+            else {
+                nd = refr;
+                prd->attenuation = scl(prd->attenuation, (n2 * n2) / (n1 * n1));
+            }
+            prd->flags |= PRD_HIT_SPECULAR;
+            prd->flags &= ~PRD_HIT_NON_SPECULAR;
+            prd->depth++;
+            if (prd->depth <= maxd) {
+                o = hitPoint; d = nd; tmin = 0.0001f;
+                continue;
+            }
+            prd->attenuation = scl(prd->attenuation, 0.f);
+            return;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* frame buffers                                                       */
+/* ------------------------------------------------------------------ */
+static orx_status resize(orc_renderer* r, uint32_t W, uint32_t H) {
+    free_frame(r);
+    const uint32_t PW = r->cfg.photon_launch_width, PH = r->cfg.photon_launch_height;
+    r->W = W; r->H = H;
+    r->RW = PW > W ? PW : W;
+    r->RH = PH > H ? PH : H;
+    size_t npx = (size_t)W * H;
+    size_t S = (size_t)PW * PH * r->cfg.max_photon_deposits;
+    size_t G = r->cfg.photon_grid_max_size;
+    r->rng = (uint32_t*)malloc((size_t)r->RW * r->RH * 6 * 4);
+    r->hp = (hitpoint_t*)calloc(npx, sizeof(hitpoint_t));
+    r->photons = (photon_t*)calloc(S, sizeof(photon_t));
+    r->sort_tmp = (photon_t*)calloc(S, sizeof(photon_t));
+    r->keys = (uint32_t*)calloc(S, 4);
+    r->offsets = (uint32_t*)calloc(G + 2, 4);
+    r->hist = (uint32_t*)calloc(G + 3, 4);
+    r->indirect = (v3*)calloc(npx, sizeof(v3));
+    r->direct = (v3*)calloc(npx, sizeof(v3));
+    r->output = (v3*)calloc(npx, sizeof(v3));
+    r->dbg = (uint32_t*)calloc(npx * 2, 4);
+    if (!r->rng || !r->hp || !r->photons || !r->sort_tmp || !r->keys || !r->offsets || !r->hist ||
+        !r->indirect || !r->direct || !r->output || !r->dbg)
+        return fail(r, ORX_ERR_OUT_OF_MEMORY, "oracle: out of memory");
+    /* initializeRandomStates (OptixRenderer_SpatialHash.cu:310-347) */
+    uint32_t seed = r->cfg.seed;
+    if (seed == 0) seed = 574133u * (uint32_t)clock() + (uint32_t)(47844152748ull * (uint32_t)time(NULL));
+    size_t n = (size_t)r->RW * r->RH;
+#pragma omp parallel for schedule(static)
+    for (long long i = 0; i < (long long)n; i++) orc_xorwow_init((uint64_t)(uint32_t)(seed + (uint32_t)i), r->rng + 6 * i);
+    r->rng_ready = 1;
+    return ORX_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* PPM passes                                                          */
+/* ------------------------------------------------------------------ */
+/* RayGeneratorPPM.cu:31-66 */
+static void ppm_eye_pass(orc_renderer* r, const cam_t* cam) {
+    const uint32_t W = r->W, H = r->H;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (long long y = 0; y < (long long)H; y++) {
+        for (uint32_t x = 0; x < W; x++) {
+            uint32_t rs[6];
+            uint32_t* g = r->rng + 6 * ((size_t)y * r->RW + x);
+            memcpy(rs, g, 24);
+            rprd_t prd;
+            memset(&prd, 0, sizeof prd);
+            prd.attenuation = mk1(1.0f);
+            prd.rs = rs;
+            v3 o, d;
+            primary_ray(cam, x, (uint32_t)y, W, H, rs, &o, &d);
+            trace_radiance(r, o, d, 0.001f, &prd);
+            hitpoint_t* h = &r->hp[(size_t)y * W + x];
+            h->position = prd.position;
+            h->normal = prd.normal;
+            h->attenuation = prd.attenuation;
+            h->radiance = prd.radiance;
+            h->flags = prd.flags;
+            memcpy(g, rs, 24);
+        }
+    }
+}
+
+/* Photon closest-hit chain (Diffuse.cu:92-135, Mirror.cu:65-77, Glass.cu:164-205,
+ * DiffuseEmitter.cu:56-59) in iterative form. */
+static void trace_photon(const orc_renderer* r, v3 o, v3 d, v3 power, uint32_t pm_index, uint32_t* rs) {
+    const uint32_t maxDeposits = r->cfg.max_photon_deposits;
+    const uint32_t maxDepth = r->cfg.max_photon_trace_depth;
+    uint32_t numStored = 0, depth = 0;
+    float weight = 1.0f;
+    float tmin = 0.0001f;
+    for (;;) {
+        hit_t h;
+        if (!trace_closest(r, o, d, tmin, ORC_RT_DEFAULT_MAX, &h)) return; /* PhotonGenerator.cu:132-135 */
+        const mat_t* m = &r->mats[prim_material(r, h.prim)];
+        v3 hitPoint = add(o, scl(d, h.t));
+        if (m->type == ORX_MAT_DIFFUSE || m->type == ORX_MAT_GLOSSY) {
+            v3 N = normalize(h.sn);
+            if (depth >= 1 && numStored < maxDeposits) {
+                photon_t* p = &r->photons[pm_index + numStored];
+                p->power = power;
+                p->position = hitPoint;
+                p->direction = d;
+                numStored++;
+            }
+            power = mul(power, m->Kd);
+            weight *= fmax3(m->Kd);
+            if (depth >= 3) { /* PHOTON_TRACING_RR_START_DEPTH */
+                float probContinue = favgf(m->Kd);
+                float probSample = orc_uniform(rs);
+                if (probSample >= probContinue) return;
+                power = divs(power, probContinue);
+            }
+            depth++;
+            if (depth >= maxDepth || (double)weight < 0.001) return;
+            if (numStored >= maxDeposits) return;
+            float s0 = orc_uniform(rs);
+            float s1 = orc_uniform(rs);
+            d = sample_hemisphere_cos(N, s0, s1);
+            o = hitPoint;
+            tmin = 0.0001f;
+        } else if (m->type == ORX_MAT_DIFFUSE_EMITTER) {
+            return; /* depth++ only */
+        } else if (m->type == ORX_MAT_MIRROR) {
+            v3 N = normalize(h.sn);
+            depth++;
+            if (depth <= maxDepth) {
+                power = mul(power, m->Kr);
+                d = reflect(d, N);
+                o = hitPoint;
+                tmin = 0.0001f;
+                continue;
+            }
+            return;
+        } else { /* glass */
+            v3 wsn = normalize(h.sn);
+            int outside = dot(wsn, d) < 0;
+            v3 N = outside ? wsn : neg(wsn);
+            float n1 = outside ? 1.0f : m->ior, n2 = outside ? m->ior : 1.0f;
+            v3 refr;
+            int valid = refract(&refr, d, N, n2 / n1);
+            float cosI = -dot(d, N);
+            float cosT = -dot(refr, N);
+            float refl = 1.f;
+            if (valid) {
+                float rp = (n2 * cosI - n1 * cosT) / (n2 * cosI + n1 * cosT);
+                float rsv = (n1 * cosI - n2 * cosT) / (n1 * cosI + n2 * cosT);
+                refl = (rp * rp + rsv * rsv) / 2.f;
+            }
+            float sample = orc_uniform(rs);
+            v3 nd = (sample <= refl) ? reflect(d, N) : refr;
+            depth++;
+            if (depth <= maxDepth) {
+                o = hitPoint; d = nd; tmin = 0.0001f;
+                continue;
+            }
+            return;
+        }
+    }
+}
+
+/* PhotonGenerator.cu:40-79 + :81-128 */
+static void ppm_photon_pass(orc_renderer* r) {
+    const uint32_t PW = r->cfg.photon_launch_width, PH = r->cfg.photon_launch_height;
+    const uint32_t maxDeposits = r->cfg.max_photon_deposits;
+    const uint32_t nl = r->nl;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (long long y = 0; y < (long long)PH; y++) {
+        for (uint32_t x = 0; x < PW; x++) {
+            uint32_t pm_index = ((uint32_t)y * PW + x) * maxDeposits;
+            uint32_t* g = r->rng + 6 * ((size_t)y * r->RW + x);
+            uint32_t rs[6];
+            memcpy(rs, g, 24);
+            int lightIndex = 0;
+            if (nl > 1) {
+                float sample = orc_uniform(rs);
+                int li = (int)(sample * nl);
+                lightIndex = li < (int)(nl - 1) ? li : (int)(nl - 1);
+            }
+            const light_t* L = &r->lights[lightIndex];
+            float powerScale = (float)nl;
+            v3 power = scl(L->power, powerScale);
+            v3 origin = L->position, dir = mk1(0);
+            float photonPowerFactor = 1.f;
+            float s1x = orc_uniform(rs), s1y = orc_uniform(rs);
+            if (L->type == ORX_LIGHT_AREA) {
+                float s2x = orc_uniform(rs), s2y = orc_uniform(rs);
+                origin = add(origin, add(scl(L->v1, s1x), scl(L->v2, s1y)));
+                dir = sample_hemisphere(L->normal, s2x, s2y);
+            } else if (L->type == ORX_LIGHT_POINT) {
+                v3 sceneCenterToLight = sub(L->position, r->bs_center);
+                float lightDistance = length(sceneCenterToLight);
+                sceneCenterToLight = divs(sceneCenterToLight, lightDistance);
+                int wellOutside = (double)lightDistance > 1.5 * (double)r->bs_radius;
+                if (wellOutside) {
+                    v3 pointOnDisc = sample_disc(s1x, s1y, r->bs_center, r->bs_radius, sceneCenterToLight);
+                    dir = normalize(sub(pointOnDisc, origin));
+                    float rr = r->bs_radius * r->bs_radius + lightDistance * lightDistance;
+                    photonPowerFactor = (1 - lightDistance * (1.0f / sqrtf(rr))) / 2.f;
+                } else {
+                    dir = sample_unit_sphere(s1x, s1y);
+                }
+            } else { /* SPOT */
+                v3 pointOnDisc = sample_disc(s1x, s1y, add(origin, L->direction), orx_sinf(L->angle / 2), L->direction);
+                dir = normalize(sub(pointOnDisc, origin));
+            }
+            power = scl(power, photonPowerFactor);
+            for (uint32_t i = 0; i < maxDeposits; i++) {
+                r->photons[pm_index + i].position = mk1(0.0f);
+                r->photons[pm_index + i].power = mk1(0.0f);
+            }
+            trace_photon(r, origin, dir, power, pm_index, rs);
+            memcpy(g, rs, 24);
+        }
+    }
+}
+
+/* OptixRenderer_SpatialHash.cu:62-71 (host code: glibc-free detmath pow) */
+static float smallest_possible_cell_size(v3 ext, uint32_t maxGridSize) {
+    float sceneVolume = ext.x * ext.y * ext.z;
+    float minVolumePerCell = sceneVolume / (float)maxGridSize;
+    float radiusC = orx_powf(minVolumePerCell, 1.0f / 3.0f);
+    v3 numCellsF = divs(ext, radiusC);
+    uint32_t nx = orx_f2u_sat(orx_floorf(numCellsF.x));
+    uint32_t ny = orx_f2u_sat(orx_floorf(numCellsF.y));
+    uint32_t nz = orx_f2u_sat(orx_floorf(numCellsF.z));
+    v3 each = mk(ext.x / (float)nx, ext.y / (float)ny, ext.z / (float)nz);
+    return fmax3(each);
+}
+
+/* createUniformGridPhotonMap (OptixRenderer_SpatialHash.cu:209-282) */
+static orx_status ppm_build_grid(orc_renderer* r) {
+    const size_t S = (size_t)r->cfg.photon_launch_width * r->cfg.photon_launch_height * r->cfg.max_photon_deposits;
+    photon_t* ph = r->photons;
+    /* getPhotonsBoundingBox: transform_reduce over valid photons (:123-128) */
+    int any = 0;
+    v3 lo = ph[0].position, hi = ph[0].position;
+    for (size_t i = 0; i < S; i++) {
+        if (fmax3(ph[i].power) > 0) {
+            if (!any) { lo = hi = ph[i].position; any = 1; }
+            else { lo = vmin(lo, ph[i].position); hi = vmax(hi, ph[i].position); }
+        }
+    }
+    if (!any) { lo = mk1(0); hi = mk1(0); }
+    /* padAABB (:135-141) */
+    lo = sub_s(lo, 0.0000001f);
+    hi = mk(hi.x + 0.0000001f, hi.y + 0.0000001f, hi.z + 0.0000001f);
+    v3 ext = sub(hi, lo);
+    float smallest = smallest_possible_cell_size(ext, r->cfg.photon_grid_max_size);
+    float cellSize = (float)((double)smallest + 0.001);
+    /* calculateGridSize (:42-50) */
+    v3 f = divs(ext, cellSize);
+    uint32_t g[3] = {orx_f2u_sat(orx_ceilf(f.x)), orx_f2u_sat(orx_ceilf(f.y)), orx_f2u_sat(orx_ceilf(f.z))};
+    for (int k = 0; k < 3; k++) if (g[k] < 1) g[k] = 1;
+    uint64_t G64 = (uint64_t)g[0] * g[1] * g[2];
+    if (G64 > r->cfg.photon_grid_max_size)
+        return fail(r, ORX_ERR_GRID_TOO_LARGE, "Too many cells in SpatialHash.cu, over defined PHOTON_GRID_MAX_SIZE.");
+    uint32_t G = (uint32_t)G64;
+    r->gsize[0] = g[0]; r->gsize[1] = g[1]; r->gsize[2] = g[2];
+    r->cell = cellSize; r->origo = lo; r->ncells = G;
+    const uint32_t invalid = G + 1;
+    memset(r->hist, 0, (size_t)(G + 2) * 4);
+    const float inv = 1.f / cellSize;
+    /* calculateHashCellsKernel (:152-173) */
+    for (size_t i = 0; i < S; i++) {
+        uint32_t key;
+        if (fmax3(ph[i].power) > 0) {
+            v3 pp = scl(sub(ph[i].position, lo), inv);
+            uint32_t gx = orx_f2u_sat(orx_floorf(pp.x));
+            uint32_t gy = orx_f2u_sat(orx_floorf(pp.y));
+            uint32_t gz = orx_f2u_sat(orx_floorf(pp.z));
+            key = gx + gy * g[0] + gz * g[0] * g[1];
+            if (key > G) key = G; /* out-of-grid edge: parked past the last cell, never gathered */
+            r->hist[key]++;
+        } else {
+            key = invalid;
+        }
+        r->keys[i] = key;
+    }
+    /* exclusive_scan of G+1 entries (:202-207) */
+    uint32_t run = 0;
+    for (uint32_t c = 0; c <= G; c++) { r->offsets[c] = run; run += r->hist[c]; }
+    r->valid = r->offsets[G];
+    /* sort_by_key, stable (:193-196): counting sort over keys 0..G+1 */
+    uint32_t* pos = (uint32_t*)malloc((size_t)(G + 2) * 4);
+    uint32_t acc = 0;
+    for (uint32_t c = 0; c <= G; c++) { pos[c] = acc; acc += r->hist[c]; }
+    pos[G + 1] = acc;
+    for (size_t i = 0; i < S; i++) r->sort_tmp[pos[r->keys[i]]++] = ph[i];
+    free(pos);
+    photon_t* t = r->photons; r->photons = r->sort_tmp; r->sort_tmp = t;
+    return ORX_OK;
+}
+
+/* IndirectRadianceEstimation.cu:54-67, :69-129, :211-221 */
+static void ppm_gather(orc_renderer* r, float ppmRadius, float ppmRadiusSquared, float emittedF) {
+    const uint32_t W = r->W, H = r->H;
+    const uint32_t gx = r->gsize[0], gy = r->gsize[1], gz = r->gsize[2];
+    const v3 origo = r->origo;
+    const float cell = r->cell;
+    uint64_t sumP = 0, sumC = 0;
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : sumP, sumC)
+    for (long long y = 0; y < (long long)H; y++) {
+        for (uint32_t x = 0; x < W; x++) {
+            size_t px = (size_t)y * W + x;
+            const hitpoint_t rec = r->hp[px];
+            v3 acc = mk1(0.0f);
+            uint32_t dP = 0, dC = 0;
+            if (rec.flags & PRD_HIT_NON_SPECULAR) {
+                float radius2 = ppmRadiusSquared;
+                float radius = ppmRadius;
+                float invCellSize = 1.f / cell;
+                v3 np = sub(rec.position, origo);
+                int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
+                int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
+                int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
+                uint32_t x_lo = (uint32_t)(ixl > 0 ? ixl : 0);
+                uint32_t y_lo = (uint32_t)(iyl > 0 ? iyl : 0);
+                uint32_t z_lo = (uint32_t)(izl > 0 ? izl : 0);
+                uint32_t ux = orx_f2u_sat((np.x + radius) * invCellSize);
+                uint32_t uy = orx_f2u_sat((np.y + radius) * invCellSize);
+                uint32_t uz = orx_f2u_sat((np.z + radius) * invCellSize);
+                uint32_t x_hi = (gx - 1) < ux ? (gx - 1) : ux;
+                uint32_t y_hi = (gy - 1) < uy ? (gy - 1) : uy;
+                uint32_t z_hi = (gz - 1) < uz ? (gz - 1) : uz;
+                if (x_lo <= x_hi) {
+                    for (uint32_t z = z_lo; z <= z_hi; z++) {
+                        for (uint32_t yy = y_lo; yy <= y_hi; yy++) {
+                            uint32_t from = x_lo + yy * gx + z * gx * gy;
+                            uint32_t to = from + (x_hi - x_lo);
+                            uint32_t offset = r->offsets[from];
+                            uint32_t offsetTo = r->offsets[to + 1];
+                            uint32_t numPhotons = offsetTo - offset;
+                            dC++;
+                            for (uint32_t i = offset; i < offset + numPhotons; i++) {
+                                const photon_t* p = &r->photons[i];
+                                v3 diff = sub(rec.position, p->position);
+                                float distance2 = dot(diff, diff);
+                                if (distance2 <= radius2 && dot(neg(p->direction), rec.normal) >= 0) {
+                                    const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
+                                    float wgt = alpha * (1 - (1 - orx_expf(-beta * distance2 / (2 * radius2))) / (1 - expNegativeBeta));
+                                    acc = add(acc, scl(p->power, wgt));
+                                }
+                                dP++;
+                            }
+                        }
+                    }
+                }
+            }
+            float s1 = 1.0f / (ORX_PI_F * ppmRadiusSquared);
+            float s2 = 1.0f / emittedF;
+            r->indirect[px] = scl(scl(mul(acc, rec.attenuation), s1), s2);
+            r->dbg[2 * px] = dC;
+            r->dbg[2 * px + 1] = dP;
+            sumP += dP;
+            sumC += dC;
+        }
+    }
+    r->sum_photons_visited = sumP;
+    r->sum_cells_visited = sumC;
+}
+
+/* helpers/light.h:29-87 */
+static v3 light_contribution(const orc_renderer* r, const light_t* light, v3 pos, v3 normal, uint32_t* rs) {
+    float lightFactor = 1;
+    v3 pointOnLight = mk1(0);
+    if (light->type == ORX_LIGHT_AREA) {
+        float sx = orc_uniform(rs), sy = orc_uniform(rs);
+        pointOnLight = add(add(light->position, scl(light->v1, sx)), scl(light->v2, sy));
+    } else if (light->type == ORX_LIGHT_POINT) {
+        pointOnLight = light->position;
+        lightFactor *= 1.f / 4.f;
+    } else {
+        return mk1(0); /* SPOT: lightFactor = 0 */
+    }
+    v3 towardsLight = sub(pointOnLight, pos);
+    float lightDistance = length(towardsLight);
+    towardsLight = divs(towardsLight, lightDistance);
+    float n_dot_l = maxf(0, dot(normal, towardsLight));
+    lightFactor *= n_dot_l / (ORX_PI_F * lightDistance * lightDistance);
+    if (light->type == ORX_LIGHT_AREA) lightFactor *= maxf(0, dot(neg(towardsLight), light->normal));
+    if (lightFactor > 0.0f) {
+        float tmax = (float)((double)lightDistance - 0.0001);
+        float att = trace_any(r, pos, towardsLight, 0.0001f, tmax) ? 0.0f : 1.0f;
+        lightFactor *= att;
+        return scl(light->power, lightFactor);
+    }
+    return mk1(0);
+}
+
+/* DirectRadianceEstimation.cu:29-77 */
+static void ppm_direct(orc_renderer* r) {
+    const uint32_t W = r->W, H = r->H;
+    const int numLights = (int)r->nl;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (long long y = 0; y < (long long)H; y++) {
+        for (uint32_t x = 0; x < W; x++) {
+            size_t px = (size_t)y * W + x;
+            const hitpoint_t rec = r->hp[px];
+            if (!(rec.flags & PRD_HIT_NON_SPECULAR)) {
+                if ((rec.flags & PRD_HIT_EMITTER) && !(rec.flags & PRD_HIT_SPECULAR))
+                    r->direct[px] = mk(fminf(rec.radiance.x, 1), fminf(rec.radiance.y, 1), fminf(rec.radiance.z, 1));
+                else
+                    r->direct[px] = rec.radiance;
+                continue;
+            }
+            uint32_t* rs = r->rng + 6 * ((size_t)y * r->RW + x);
+            v3 avg = mk1(0.f);
+            for (int s = 0; s < 4; s++) {
+                float sample = orc_uniform(rs);
+                int li = (int)(sample * numLights);
+                int randomLightIndex = li < numLights - 1 ? li : numLights - 1;
+                float scale = (float)numLights;
+                v3 c = light_contribution(r, &r->lights[randomLightIndex], rec.position, rec.normal, rs);
+                avg = add(avg, scl(c, scale));
+            }
+            r->direct[px] = divs(mul(rec.attenuation, avg), (float)4);
+        }
+    }
+}
+
+/* Output.cu:32-37 */
+static void ppm_output(orc_renderer* r, uint64_t local) {
+    size_t n = (size_t)r->W * r->H;
+    for (size_t i = 0; i < n; i++) {
+        v3 f = add(r->direct[i], r->indirect[i]);
+        r->output[i] = local == 0 ? f : add(r->output[i], f);
+    }
+}
+
+/* RayGeneratorPT.cu:46-131 */
+static void pt_pass(orc_renderer* r, const cam_t* cam, uint64_t local) {
+    const uint32_t W = r->W, H = r->H;
+    const int numLights = (int)r->nl;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (long long y = 0; y < (long long)H; y++) {
+        for (uint32_t x = 0; x < W; x++) {
+            size_t px = (size_t)y * W + x;
+            uint32_t* G = r->rng + 6 * ((size_t)y * r->RW + x);
+            uint32_t rs[6];
+            memcpy(rs, G, 24);
+            rprd_t prd;
+            memset(&prd, 0, sizeof prd);
+            prd.attenuation = mk1(1.0f);
+            prd.rs = rs;
+            v3 o, d;
+            primary_ray(cam, x, (uint32_t)y, W, H, rs, &o, &d);
+            v3 fin = mk1(0);
+            for (int i = 0; i < 5; i++) {
+                prd.flags = PRD_PATH_TRACING;
+                trace_radiance(r, o, d, 0.001f, &prd);
+                if (prd.flags & PRD_HIT_EMITTER) {
+                    if ((prd.flags & PRD_HIT_SPECULAR) || i == 0) fin = prd.radiance;
+                    break;
+                } else if (prd.flags & PRD_HIT_NON_SPECULAR) {
+                    v3 accum = mk1(0);
+                    int li = (int)(orc_uniform(G) * numLights);
+                    float scale = (float)numLights;
+                    v3 c = scl(light_contribution(r, &r->lights[li], prd.position, prd.normal, rs), scale);
+                    accum = add(accum, c);
+                    v3 direct = divs(mul(prd.attenuation, accum), (float)1);
+                    fin = add(fin, direct);
+                    o = prd.position;
+                    d = prd.newdir;
+                } else {
+                    break;
+                }
+                if (i >= 3) { /* PATH_TRACING_RR_START_DEPTH */
+                    float sample = orc_uniform(G);
+                    float p = fmax3(prd.attenuation);
+                    if (sample > p) break;
+                    prd.attenuation = divs(prd.attenuation, p);
+                }
+            }
+            if (!isnan3(fin)) r->output[px] = local == 0 ? fin : add(r->output[px], fin);
+            memcpy(G, rs, 24);
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* OptixRenderer::renderNextIteration (OptixRenderer.cpp:507-821)     */
+/* ------------------------------------------------------------------ */
+orx_status orc_render_next_iteration(orc_renderer* r, uint64_t iter, uint64_t local, float ppmRadius,
+                                     int create_output, const orx_request* det) {
+    (void)create_output;
+    if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
+    if (!r->scene_ready) return fail(r, ORX_ERR_STATE, "Traced before OptixRenderer was initialized.");
+    if (det->width == 0 || det->height == 0) return fail(r, ORX_ERR_INVALID_ARGUMENT, "zero-sized request");
+    if (det->width != r->W || det->height != r->H || !r->rng_ready) {
+        orx_status s = resize(r, det->width, det->height);
+        if (s != ORX_OK) return s;
+    }
+    if (local == 0) memset(r->output, 0, (size_t)r->W * r->H * sizeof(v3));
+    cam_t cam = camera_setup(&det->camera);
+    (void)iter;
+    if (det->method == ORX_METHOD_PATH_TRACING) {
+        pt_pass(r, &cam, local);
+    } else if (det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING) {
+        ppm_eye_pass(r, &cam);
+        const float ppmRadiusSquared = ppmRadius * ppmRadius;
+        ppm_photon_pass(r);
+        orx_status s = ppm_build_grid(r);
+        if (s != ORX_OK) return s;
+        float emittedF = (float)(r->cfg.photon_launch_width * r->cfg.photon_launch_height);
+        ppm_gather(r, ppmRadius, ppmRadiusSquared, emittedF);
+        ppm_direct(r);
+        ppm_output(r, local);
+    } else {
+        return fail(r, ORX_ERR_UNSUPPORTED, "oracle: VCM not implemented yet");
+    }
+    return ORX_OK;
+}
+
+orx_status orc_get_output(orc_renderer* r, float* dst, size_t bytes) {
+    size_t need = (size_t)r->W * r->H * 12;
+    if (!dst || bytes < need) return ORX_ERR_INVALID_ARGUMENT;
+    memcpy(dst, r->output, need);
+    return ORX_OK;
+}
+
+orx_status orc_read_buffer(orc_renderer* r, int32_t id, void* dst, size_t bytes, size_t* out_bytes) {
+    size_t npx = (size_t)r->W * r->H;
+    size_t need = 0;
+    switch (id) {
+    case ORX_BUF_RNG: need = (size_t)r->RW * r->RH * 24; break;
+    case ORX_BUF_HITPOINTS: need = npx * 13 * 4; break;
+    case ORX_BUF_PHOTONS: need = (size_t)r->valid * 36; break;
+    case ORX_BUF_GRID_OFFSETS: need = ((size_t)r->ncells + 1) * 4; break;
+    case ORX_BUF_INDIRECT: case ORX_BUF_DIRECT: case ORX_BUF_OUTPUT: need = npx * 12; break;
+    case ORX_BUF_DEBUG_VISITED: need = npx * 8; break;
+    default: return fail(r, ORX_ERR_INVALID_ARGUMENT, "unknown buffer id");
+    }
+    if (out_bytes) *out_bytes = need;
+    if (!dst) return ORX_OK;
+    if (bytes < need) return fail(r, ORX_ERR_INVALID_ARGUMENT, "destination too small");
+    switch (id) {
+    case ORX_BUF_RNG: memcpy(dst, r->rng, need); break;
+    case ORX_BUF_HITPOINTS: {
+        float* f = (float*)dst;
+        for (size_t i = 0; i < npx; i++) {
+            const hitpoint_t* h = &r->hp[i];
+            float v[13] = {h->position.x, h->position.y, h->position.z, h->normal.x, h->normal.y, h->normal.z,
+                           h->attenuation.x, h->attenuation.y, h->attenuation.z, h->radiance.x, h->radiance.y,
+                           h->radiance.z, orx_as_float(h->flags)};
+            memcpy(f + 13 * i, v, sizeof v);
+        }
+        break;
+    }
+    case ORX_BUF_PHOTONS: memcpy(dst, r->photons, need); break;
+    case ORX_BUF_GRID_OFFSETS: memcpy(dst, r->offsets, need); break;
+    case ORX_BUF_INDIRECT: memcpy(dst, r->indirect, need); break;
+    case ORX_BUF_DIRECT: memcpy(dst, r->direct, need); break;
+    case ORX_BUF_OUTPUT: memcpy(dst, r->output, need); break;
+    case ORX_BUF_DEBUG_VISITED: memcpy(dst, r->dbg, need); break;
+    }
+    return ORX_OK;
+}
+
+orx_status orc_get_stats(orc_renderer* r, orx_stats* out) {
+    memset(out, 0, sizeof *out);
+    out->grid_size[0] = r->gsize[0]; out->grid_size[1] = r->gsize[1]; out->grid_size[2] = r->gsize[2];
+    out->cell_size = r->cell;
+    out->world_origin[0] = r->origo.x; out->world_origin[1] = r->origo.y; out->world_origin[2] = r->origo.z;
+    out->valid_photons = r->valid;
+    out->num_cells = r->ncells;
+    out->photons_visited = r->sum_photons_visited;
+    out->cells_visited = r->sum_cells_visited;
+    return ORX_OK;
+}
+
+void orc_default_config(orx_config* c) {
+    memset(c, 0, sizeof *c);
+    c->photon_launch_width = 1024;
+    c->photon_launch_height = 1024;
+    c->max_photon_deposits = 4;
+    c->photon_grid_max_size = 100 * 100 * 100;
+    c->max_photon_trace_depth = 7;
+    c->max_radiance_trace_depth = 9;
+    c->vcm_max_path_length = 10;
+    c->seed = 0;
+    c->debug_counters = 1;
+}

@@ -1,0 +1,58 @@
+/*
+ * orx_oracle.h — CPU restatement of OppositeRenderer's render core.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the parity checker and the
+ * CPU baseline of bench.py; nothing in the product (liborx.so, the
+ * oppositerenderer_amd package) may link, load or call it.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg use it.
+ *
+ * Parity status: the reference (OptiX 3.6 / CUDA 5.5 / Windows) cannot be
+ * built or run in this environment and ships no tests, fixtures or golden
+ * vectors, so this restatement is pinned only by
+ * known-answer tests of its building blocks (cuRAND XORWOW constants,
+ * analytic intersection and sampling identities, grid invariants) and by
+ * golden images it generated itself (tests/golden/).  Against the reference
+ * binary itself parity is UNPINNED.
+ *
+ * The API mirrors include/orx.h so that tests drive the oracle and the HIP
+ * renderer through the same calls.
+ */
+#ifndef ORX_ORACLE_H
+#define ORX_ORACLE_H
+
+#include "orx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_renderer orc_renderer;
+
+orx_status orc_create(const orx_config* cfg, orc_renderer** out);
+orx_status orc_init_scene(orc_renderer* r, const orx_scene* scene);
+orx_status orc_render_next_iteration(orc_renderer* r, uint64_t iteration_number,
+                                     uint64_t local_iteration_number, float ppm_radius,
+                                     int create_output, const orx_request* details);
+orx_status orc_get_output(orc_renderer* r, float* dst, size_t dst_bytes);
+orx_status orc_read_buffer(orc_renderer* r, int32_t id, void* dst, size_t dst_bytes, size_t* out_bytes);
+orx_status orc_get_stats(orc_renderer* r, orx_stats* out);
+const char* orc_last_error(const orc_renderer* r);
+void orc_destroy(orc_renderer* r);
+void orc_set_threads(int n);
+void orc_default_config(orx_config* cfg);
+
+/* building blocks exposed for known-answer tests */
+void orc_xorwow_init(uint64_t seed, uint32_t state[6]);
+uint32_t orc_xorwow_next(uint32_t state[6]);
+float orc_uniform(uint32_t state[6]); /* getRandomUniformFloat (helpers/random.h:65-69) */
+/* closest hit against the current scene: returns prim id or -1, writes t */
+int32_t orc_trace_closest(orc_renderer* r, const float o[3], const float d[3], float tmin, float tmax, float* t_out);
+int32_t orc_trace_any(orc_renderer* r, const float o[3], const float d[3], float tmin, float tmax);
+void orc_sample_unit_hemisphere_cos(const float n[3], float u1, float u2, float out[3]);
+void orc_sample_unit_hemisphere(const float n[3], float u1, float u2, float out[3]);
+void orc_camera_setup(const orx_camera* cam, float lookdir[3], float u[3], float v[3]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
