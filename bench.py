@@ -38,6 +38,7 @@ def parse():
     p.add_argument("--scene", default="Cornell")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=20.0)
+    p.add_argument("--gather-variant", type=int, default=0)
     return p.parse_args()
 
 
@@ -50,12 +51,14 @@ def gather_bytes_per_launch(W, H, valid_photons, num_cells):
 
 
 def cpu_baseline(scene, args, W, H, P, seconds):
-    """Oracle (oracle/liborx_oracle.so, OpenMP) on a bounded sample: the same
-    scene/resolution/seed, one PPM iteration with a photon launch scaled down
-    until it fits the time budget; Mpaths/s counts the same paths definition."""
+    """Oracle (oracle/liborx_oracle.so, OpenMP, the CPU restatement of the
+    reference passes) on the host cores: the same scene, resolution, photon
+    count and seed as the GPU line; one warm-up iteration, then timed
+    iterations until `seconds` of CPU wall time or 8 iterations."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     from oppositerenderer_amd import _abi
+    from oppositerenderer_amd.renderer import next_ppm_radius
 
     cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     lib = oracle_lib.load()
@@ -65,29 +68,28 @@ def cpu_baseline(scene, args, W, H, P, seconds):
     req.camera = cam.to_abi()
     req.method = _abi.PROGRESSIVE_PHOTON_MAPPING
     req.width, req.height, req.ppm_alpha = W, H, 2.0 / 3.0
-    # probe at a small sample, then size the real sample to the budget
-    sw, sh, sp = max(64, W // 8), max(64, H // 8), max(64, P // 8)
-    best = None
-    for attempt in range(3):
-        cfg = _abi.default_config(seed=1645301512, photon_launch_width=sp, photon_launch_height=sp)
-        r = oracle_lib.OracleRenderer(cfg)
-        r.init_scene(scene)
-        req.width, req.height = sw, sh
-        r.render_next_iteration(0, 0, scene.initial_ppm_radius(), req)  # warm-up (allocation, RNG init)
+    cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P)
+    r = oracle_lib.OracleRenderer(cfg)
+    r.init_scene(scene)
+    radius = scene.initial_ppm_radius()
+    r.render_next_iteration(0, 0, radius, req)  # warm-up: allocation + RNG init
+    radius = next_ppm_radius(radius, 0)
+    times = []
+    t_start = time.perf_counter()
+    it = 1
+    while it <= 8 and (time.perf_counter() - t_start) < seconds:
         t0 = time.perf_counter()
-        r.render_next_iteration(1, 1, scene.initial_ppm_radius(), req)
-        dt = time.perf_counter() - t0
-        r.close()
-        best = (sw, sh, sp, dt)
-        if dt * 4 > seconds or (sw >= W and sp >= P):
-            break
-        grow = min(4.0, (seconds / 2) / max(dt, 1e-3))
-        s = max(1.0, grow ** 0.5)
-        sw, sh, sp = min(W, int(sw * s)), min(H, int(sh * s)), min(P, int(sp * s))
-    sw, sh, sp, dt = best
-    paths = sw * sh + sp * sp
-    return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": cores, "kind": "port",
-            "sample": f"oracle PPM iteration {sw}x{sh} px + {sp}x{sp} photons, {scene.name}, {dt:.2f}s"}
+        r.render_next_iteration(it, it, radius, req)
+        times.append(time.perf_counter() - t0)
+        radius = next_ppm_radius(radius, it)
+        it += 1
+    r.close()
+    t = float(np.median(times))
+    paths = W * H + P * P
+    return {"value": round(paths / t / 1e6, 3), "unit": "Mpaths/s", "cores": cores, "kind": "port",
+            "ms_per_step": round(t * 1e3, 2),
+            "sample": f"oracle (C/OpenMP restatement) full {scene.name} {W}x{H} PPM, {P * P} photons/iter, "
+                      f"median of {len(times)} iterations after 1 warm-up"}
 
 
 def main():
@@ -104,7 +106,8 @@ def main():
 
     W, H, P = args.width, args.height, args.photon_launch
     scene = scenes.scene_by_name(args.scene)
-    cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P)
+    cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P,
+                              gather_variant=args.gather_variant)
     r = OptixRenderer(cfg)
     r.initialize(local_rank)
     r.initScene(scene)
@@ -155,6 +158,7 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "bytes_per_launch": int(gbytes), "avg_launch_ms": round(gms, 4),
                      "photons_visited_per_launch": int(visited_avg),
+                     "photons_staged_per_launch": int(st.gather_staged_total / max(1, st.timed_iterations)),
                      "visited_photon_GBps": round(visited_avg * 36 / (gms * 1e-3) / 1e9, 1) if gms > 0 else None},
         "passes_ms": {k: round(v, 4) for k, v in per_pass.items() if v > 0},
         "dominant_pass": dominant,

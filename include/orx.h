@@ -141,7 +141,8 @@ typedef struct {
     uint32_t vcm_max_path_length;     /* VCM_MAX_PATH_LENGTH = 10 */
     uint32_t seed;                    /* 0: 574133*clock()+47844152748*time() like SpatialHash.cu:322; else DEBUG_RANDOM_SEED */
     uint32_t debug_counters;          /* 1: keep per-pixel cells/photons visited (OptixRenderer.cpp:872-953) */
-    uint32_t reserved[7];
+    uint32_t gather_variant;          /* 0: wave-cooperative LDS gather (default), 1: one thread per pixel */
+    uint32_t reserved[6];
 } orx_config;
 
 void orx_default_config(orx_config* cfg);
@@ -205,6 +206,7 @@ typedef struct {
     uint64_t photons_visited_total; /* summed since orx_reset_timing */
     uint64_t cells_visited_total;
     uint64_t valid_photons_total;
+    uint64_t gather_staged_total;   /* cooperative gather: photons staged through LDS, summed over waves */
     uint32_t timed_iterations;   /* iterations since orx_reset_timing */
     uint32_t pad;
     float pass_ms[16];           /* device time per orx_pass summed since orx_reset_timing */

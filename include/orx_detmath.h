@@ -56,14 +56,21 @@ static inline ORX_HD uint64_t orx_as_u64(double d) {
     union { uint64_t u; double d; } c; c.d = d; return c.u;
 }
 
-/* floor without relying on libm: exact for every float. */
+/* floor without relying on libm: exact for every float (v_floor_f32 on gfx950
+ * is exact too, so device code uses it). */
 static inline ORX_HD float orx_floorf(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_floorf(x);
+#endif
     if (!(x < 8388608.0f && x > -8388608.0f)) return x; /* |x| >= 2^23 or NaN: integral */
     int32_t i = (int32_t)x;                               /* truncation toward zero */
     float t = (float)i;
     return (t > x) ? t - 1.0f : t;
 }
 static inline ORX_HD float orx_ceilf(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_ceilf(x);
+#endif
     if (!(x < 8388608.0f && x > -8388608.0f)) return x;
     int32_t i = (int32_t)x;
     float t = (float)i;
@@ -140,6 +147,22 @@ static inline ORX_HD float orx_cosf(float x) {
 }
 
 /* ---- exp : Cody-Waite by ln2, degree-6 polynomial on [-ln2/2, ln2/2] ---- */
+/* Branch-free core, exact same arithmetic as orx_expf for x in [-87, 88]
+ * (normal results); the photon-gather weight only feeds it [-1, 0]. */
+static inline ORX_HD float orx_expf_core(float x) {
+    float kf = orx_floorf(x * 1.44269504088896341f + 0.5f);
+    float r = x - kf * 0.693359375f;
+    r = r - kf * -2.12194440e-4f;
+    float p = 1.9875691500e-4f;
+    p = p * r + 1.3981999507e-3f;
+    p = p * r + 8.3334519073e-3f;
+    p = p * r + 4.1665795894e-2f;
+    p = p * r + 1.6666665459e-1f;
+    p = p * r + 5.0000001201e-1f;
+    float e = (r + (r * r) * p) + 1.0f;
+    int32_t k = (int32_t)kf;
+    return e * orx_as_float((uint32_t)(k + 127) << 23);
+}
 static inline ORX_HD float orx_expf(float x) {
     if (!(x == x)) return x;
     if (x > 88.72283f) return orx_as_float(0x7f800000u);

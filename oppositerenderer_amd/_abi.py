@@ -90,7 +90,7 @@ class OrxConfig(C.Structure):
                 ("max_photon_deposits", C.c_uint32), ("photon_grid_max_size", C.c_uint32),
                 ("max_photon_trace_depth", C.c_uint32), ("max_radiance_trace_depth", C.c_uint32),
                 ("vcm_max_path_length", C.c_uint32), ("seed", C.c_uint32),
-                ("debug_counters", C.c_uint32), ("reserved", C.c_uint32 * 7)]
+                ("debug_counters", C.c_uint32), ("gather_variant", C.c_uint32), ("reserved", C.c_uint32 * 6)]
 
 
 class OrxStats(C.Structure):
@@ -98,7 +98,7 @@ class OrxStats(C.Structure):
                 ("valid_photons", C.c_uint32), ("num_cells", C.c_uint32),
                 ("photons_visited", C.c_uint64), ("cells_visited", C.c_uint64),
                 ("photons_visited_total", C.c_uint64), ("cells_visited_total", C.c_uint64),
-                ("valid_photons_total", C.c_uint64),
+                ("valid_photons_total", C.c_uint64), ("gather_staged_total", C.c_uint64),
                 ("timed_iterations", C.c_uint32), ("pad", C.c_uint32), ("pass_ms", C.c_float * 16)]
 
 

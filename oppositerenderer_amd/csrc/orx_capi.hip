@@ -601,7 +601,7 @@ orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
         launch_grid_scatter(r->stream, r->pb);
         ev_end(r, P_SCATTER);
         ev_begin(r, P_GATHER);
-        launch_ppm_gather(r->stream, r->px, r->pb, c);
+        launch_ppm_gather(r->stream, r->px, r->pb, c, (int)r->cfg.gather_variant);
         ev_end(r, P_GATHER);
         ev_begin(r, P_DIRECT);
         launch_ppm_direct_output(r->stream, r->scene, r->px, c);
@@ -757,6 +757,7 @@ orx_status orx_get_stats(orx_renderer* r, orx_stats* out) {
         out->photons_visited_total = g.photons_visited_total;
         out->cells_visited_total = g.cells_visited_total;
         out->valid_photons_total = g.valid_total;
+        out->gather_staged_total = g.union_photons_total;
     }
     for (int p = 0; p < P_COUNT; p++) {
         double tot = 0.0;
@@ -782,6 +783,7 @@ orx_status orx_reset_timing(orx_renderer* r) {
         g.photons_visited_total = 0;
         g.cells_visited_total = 0;
         g.valid_total = 0;
+        g.union_photons_total = 0;
         HIPCHK(r, hipMemcpy(r->d_grid.p, &g, sizeof g, hipMemcpyHostToDevice));
     }
     return ORX_OK;

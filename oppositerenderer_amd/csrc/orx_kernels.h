@@ -27,6 +27,7 @@ struct GridParams {
     uint64_t photons_visited_total; /* since orx_reset_timing */
     uint64_t cells_visited_total;
     uint64_t valid_total;
+    uint64_t union_photons_total; /* coop gather: photons staged per wave, summed */
 };
 
 /* Per-frame pixel state. Pixel (x,y) of rank r is stored at local row
@@ -87,7 +88,8 @@ void launch_grid_scan(hipStream_t s, const PhotonBufs& pb);
 void launch_grid_scatter(hipStream_t s, const PhotonBufs& pb);
 /* gathers `rows` pixel rows whose hitpoints are in hp{A,B,C} against the
  * local photon grid; writes indirect (and debug counters) */
-void launch_ppm_gather(hipStream_t s, const PixelBufs& px, const PhotonBufs& pb, const Consts& c);
+/* variant 0: wave-cooperative (default); 1: one thread per pixel */
+void launch_ppm_gather(hipStream_t s, const PixelBufs& px, const PhotonBufs& pb, const Consts& c, int variant);
 void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c);
 void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c);
 

@@ -452,8 +452,10 @@ void launch_grid_scatter(hipStream_t s, const PhotonBufs& pb) {
 /* indirect radiance estimate: uniform-grid gather                     */
 /* ------------------------------------------------------------------ */
 __global__ __launch_bounds__(256) void k_ppm_gather(PixelBufs px, PhotonBufs pb, Consts c) {
-    const uint32_t x = blockIdx.x * 16 + (threadIdx.x & 15);
-    const uint32_t j = blockIdx.y * 16 + (threadIdx.x >> 4);
+    /* block = 16x16 pixels as four 8x8 wave tiles (neighbouring lanes share photons in L1) */
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (l & 7);
+    const uint32_t j = blockIdx.y * 16 + (w >> 1) * 8 + (l >> 3);
     const GridParams g = *pb.grid;
     uint32_t dC = 0, dP = 0;
     if (x < px.W && j < px.rows) {
@@ -484,6 +486,8 @@ __global__ __launch_bounds__(256) void k_ppm_gather(PixelBufs px, PhotonBufs pb,
             uint32_t z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
             if (x_lo <= x_hi) {
                 const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
+                const float inv2r2 = 1.0f / (2 * radius2);
+                const float invDen = 1.0f / (1 - expNegativeBeta);
                 for (uint32_t z = z_lo; z <= z_hi; z++) {
                     for (uint32_t yy = y_lo; yy <= y_hi; yy++) {
                         uint32_t from = x_lo + yy * g.gx + z * g.gx * g.gy;
@@ -499,8 +503,8 @@ __global__ __launch_bounds__(256) void k_ppm_gather(PixelBufs px, PhotonBufs pb,
                             if (distance2 <= radius2) {
                                 const float4 pbv = pb.sortB[k];
                                 if (dot(-mk(pbv.x, pbv.y, pbv.z), nrm) >= 0) {
-                                    float wgt = alpha * (1 - (1 - orx_expf(-beta * distance2 / (2 * radius2))) /
-                                                                 (1 - expNegativeBeta));
+                                    float e = orx_expf_core((-beta * distance2) * inv2r2);
+                                    float wgt = alpha * (1 - (1 - e) * invDen);
                                     f3 pw = mk(pa.w, pbv.w, pb.sortC[k]);
                                     acc = acc + pw * wgt;
                                 }
@@ -530,9 +534,158 @@ __global__ __launch_bounds__(256) void k_ppm_gather(PixelBufs px, PhotonBufs pb,
         atomicAdd((unsigned long long*)&pb.grid->cells_visited_total, (unsigned long long)sc);
     }
 }
-void launch_ppm_gather(hipStream_t s, const PixelBufs& px, const PhotonBufs& pb, const Consts& c) {
-    dim3 grid((px.W + 15) / 16, (px.rows + 15) / 16);
-    hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), 0, s, px, pb, c);
+/* Wave-cooperative gather: one 64-lane wave owns an 8x8 pixel tile.  For
+ * every (z,y) cell row that any lane's window touches, the wave stages the
+ * row's photons (the union of the lanes' contiguous sub-ranges) through LDS
+ * in chunks of 64 with one coalesced load per lane, then every lane tests
+ * every staged photon against its own [offset[from], offset[to+1]) range
+ * and radius.  Each pixel therefore visits exactly the photons of the
+ * per-pixel loop above, in the same order (rows in z,y order, photons in
+ * grid order), so the sums are bit-identical to k_ppm_gather; only the
+ * photon loads are shared and the inner loop is divergence-free. */
+__global__ __launch_bounds__(64) void k_ppm_gather_coop(PixelBufs px, PhotonBufs pb, Consts c) {
+    __shared__ float4 sA[64];
+    __shared__ float4 sB[64];
+    __shared__ float sC[64];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t x = blockIdx.x * 8 + (lane & 7);
+    const uint32_t j = blockIdx.y * 8 + (lane >> 3);
+    const GridParams g = *pb.grid;
+    const bool inimg = x < px.W && j < px.rows;
+    const size_t i = (size_t)j * px.W + x;
+    float4 A = make_float4(0, 0, 0, 0), B = A;
+    float2 Cc = make_float2(0, 0);
+    if (inimg) {
+        A = px.hpA[i];
+        B = px.hpB[i];
+        Cc = px.hpC[i];
+    }
+    const uint32_t flags = __float_as_uint(A.w);
+    const f3 pos = mk(A.x, A.y, A.z);
+    const f3 nrm = mk(B.x, B.y, B.z);
+    const float radius2 = c.ppm_radius2;
+    const float radius = c.ppm_radius;
+    uint32_t x_lo = 1, x_hi = 0, y_lo = 1, y_hi = 0, z_lo = 1, z_hi = 0;
+    bool active = false;
+    if (inimg && (flags & PRD_HIT_NON_SPECULAR) && g.G) {
+        const float invCellSize = 1.f / g.cell;
+        const f3 np = pos - mk(g.ox, g.oy, g.oz);
+        int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
+        int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
+        int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
+        x_lo = (uint32_t)(ixl > 0 ? ixl : 0);
+        y_lo = (uint32_t)(iyl > 0 ? iyl : 0);
+        z_lo = (uint32_t)(izl > 0 ? izl : 0);
+        uint32_t ux = orx_f2u_sat((np.x + radius) * invCellSize);
+        uint32_t uy = orx_f2u_sat((np.y + radius) * invCellSize);
+        uint32_t uz = orx_f2u_sat((np.z + radius) * invCellSize);
+        x_hi = (g.gx - 1) < ux ? (g.gx - 1) : ux;
+        y_hi = (g.gy - 1) < uy ? (g.gy - 1) : uy;
+        z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
+        active = x_lo <= x_hi && y_lo <= y_hi && z_lo <= z_hi;
+    }
+    /* union of the lanes' (z,y) row windows */
+    uint32_t uz_lo = active ? z_lo : 0xffffffffu, uz_hi = active ? z_hi : 0u;
+    uint32_t uy_lo = active ? y_lo : 0xffffffffu, uy_hi = active ? y_hi : 0u;
+    for (int o = 32; o > 0; o >>= 1) {
+        uz_lo = min(uz_lo, (uint32_t)__shfl_xor((int)uz_lo, o, 64));
+        uz_hi = max(uz_hi, (uint32_t)__shfl_xor((int)uz_hi, o, 64));
+        uy_lo = min(uy_lo, (uint32_t)__shfl_xor((int)uy_lo, o, 64));
+        uy_hi = max(uy_hi, (uint32_t)__shfl_xor((int)uy_hi, o, 64));
+    }
+    /* wave-uniform by construction: make it visible to the compiler (scalar loop control) */
+    uz_lo = __builtin_amdgcn_readfirstlane(uz_lo);
+    uz_hi = __builtin_amdgcn_readfirstlane(uz_hi);
+    uy_lo = __builtin_amdgcn_readfirstlane(uy_lo);
+    uy_hi = __builtin_amdgcn_readfirstlane(uy_hi);
+    f3 acc = mk1(0.0f);
+    uint32_t dC = 0, dP = 0, dU = 0;
+    const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
+    const float inv2r2 = 1.0f / (2 * radius2);
+    const float invDen = 1.0f / (1 - expNegativeBeta);
+    if (uz_lo <= uz_hi) {
+        for (uint32_t z = uz_lo; z <= uz_hi; z++) {
+            for (uint32_t yy = uy_lo; yy <= uy_hi; yy++) {
+                const bool row_in = active && z >= z_lo && z <= z_hi && yy >= y_lo && yy <= y_hi;
+                uint32_t lo = 0xffffffffu, hi = 0u;
+                if (row_in) {
+                    uint32_t from = x_lo + yy * g.gx + z * g.gx * g.gy;
+                    uint32_t to = from + (x_hi - x_lo);
+                    lo = pb.offsets[from];
+                    hi = pb.offsets[to + 1];
+                    dC++;
+                    dP += hi - lo;
+                }
+                uint32_t rlo = lo, rhi = row_in ? hi : 0u;
+                for (int o = 32; o > 0; o >>= 1) {
+                    rlo = min(rlo, (uint32_t)__shfl_xor((int)rlo, o, 64));
+                    rhi = max(rhi, (uint32_t)__shfl_xor((int)rhi, o, 64));
+                }
+                rlo = __builtin_amdgcn_readfirstlane(rlo);
+                rhi = __builtin_amdgcn_readfirstlane(rhi);
+                for (uint32_t base = rlo; base < rhi; base += 64) {
+                    const uint32_t n = min(64u, rhi - base);
+                    if (lane < n) {
+                        sA[lane] = pb.sortA[base + lane];
+                        sB[lane] = pb.sortB[base + lane];
+                        sC[lane] = pb.sortC[base + lane];
+                    }
+                    __syncthreads();
+                    const uint32_t t_lo = lo > base ? lo - base : 0u;
+                    const uint32_t t_hi = hi > base ? min(hi - base, n) : 0u;
+                    dU += n;
+                    for (uint32_t t = 0; t < n; t++) {
+                        const float4 pa = sA[t];
+                        const float4 pbv = sB[t];
+                        const float pc = sC[t];
+                        f3 diff = pos - mk(pa.x, pa.y, pa.z);
+                        float distance2 = dot(diff, diff);
+                        /* predicated, not branched: exp argument stays in [-beta/2, 0] */
+                        bool take = t >= t_lo && t < t_hi && distance2 <= radius2 &&
+                                    dot(-mk(pbv.x, pbv.y, pbv.z), nrm) >= 0;
+                        float e = orx_expf_core((-beta * fminf(distance2, radius2)) * inv2r2);
+                        float wgt = alpha * (1 - (1 - e) * invDen);
+                        f3 pw = mk(pa.w, pbv.w, pc);
+                        f3 nacc = acc + pw * wgt;
+                        acc.x = take ? nacc.x : acc.x;
+                        acc.y = take ? nacc.y : acc.y;
+                        acc.z = take ? nacc.z : acc.z;
+                    }
+                    __syncthreads();
+                }
+            }
+        }
+    }
+    if (inimg) {
+        const f3 att = mk(B.w, Cc.x, Cc.y);
+        float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
+        float s2 = 1.0f / c.emitted_f;
+        f3 ind = ((acc * att) * s1) * s2;
+        px.indirect[3 * i + 0] = ind.x;
+        px.indirect[3 * i + 1] = ind.y;
+        px.indirect[3 * i + 2] = ind.z;
+        if (px.dbg) {
+            px.dbg[2 * i] = dC;
+            px.dbg[2 * i + 1] = dP;
+        }
+    }
+    uint64_t sp = wave_sum_u64(dP), sc = wave_sum_u64(dC);
+    if (lane == 0 && sp) {
+        atomicAdd((unsigned long long*)&pb.grid->union_photons_total, (unsigned long long)dU);
+        atomicAdd((unsigned long long*)&pb.grid->photons_visited, (unsigned long long)sp);
+        atomicAdd((unsigned long long*)&pb.grid->cells_visited, (unsigned long long)sc);
+        atomicAdd((unsigned long long*)&pb.grid->photons_visited_total, (unsigned long long)sp);
+        atomicAdd((unsigned long long*)&pb.grid->cells_visited_total, (unsigned long long)sc);
+    }
+}
+void launch_ppm_gather(hipStream_t s, const PixelBufs& px, const PhotonBufs& pb, const Consts& c, int variant) {
+    if (variant == 1) {
+        dim3 grid((px.W + 15) / 16, (px.rows + 15) / 16);
+        hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), 0, s, px, pb, c);
+    } else {
+        dim3 grid((px.W + 7) / 8, (px.rows + 7) / 8);
+        hipLaunchKernelGGL(k_ppm_gather_coop, grid, dim3(64), 0, s, px, pb, c);
+    }
 }
 
 /* ------------------------------------------------------------------ */

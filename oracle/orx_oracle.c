@@ -986,6 +986,9 @@ static void ppm_gather(orc_renderer* r, float ppmRadius, float ppmRadiusSquared,
                 uint32_t x_hi = (gx - 1) < ux ? (gx - 1) : ux;
                 uint32_t y_hi = (gy - 1) < uy ? (gy - 1) : uy;
                 uint32_t z_hi = (gz - 1) < uz ? (gz - 1) : uz;
+                const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
+                const float inv2r2 = 1.0f / (2 * radius2);
+                const float invDen = 1.0f / (1 - expNegativeBeta);
                 if (x_lo <= x_hi) {
                     for (uint32_t z = z_lo; z <= z_hi; z++) {
                         for (uint32_t yy = y_lo; yy <= y_hi; yy++) {
@@ -1000,8 +1003,11 @@ static void ppm_gather(orc_renderer* r, float ppmRadius, float ppmRadiusSquared,
                                 v3 diff = sub(rec.position, p->position);
                                 float distance2 = dot(diff, diff);
                                 if (distance2 <= radius2 && dot(neg(p->direction), rec.normal) >= 0) {
-                                    const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
-                                    float wgt = alpha * (1 - (1 - orx_expf(-beta * distance2 / (2 * radius2))) / (1 - expNegativeBeta));
+                                    /* photonPower (:59-67); its two divisions compile to div.approx
+                                     * under -use_fast_math and are restated as multiplications by
+                                     * the IEEE reciprocal of the (loop-invariant) divisor */
+                                    float e = orx_expf((-beta * distance2) * inv2r2);
+                                    float wgt = alpha * (1 - (1 - e) * invDen);
                                     acc = add(acc, scl(p->power, wgt));
                                 }
                                 dP++;

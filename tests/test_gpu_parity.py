@@ -30,6 +30,7 @@ def make_pair(scene, W, H, P, method, **cfg):
     gpu = OptixRenderer(c)
     gpu.initialize(0)
     gpu.initScene(scene)
+    cfg.pop("gather_variant", None)
     c2 = _abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P, **cfg)
     ora = oracle_lib.OracleRenderer(c2)
     ora.init_scene(scene)
@@ -78,11 +79,12 @@ def check_ppm_iteration(gpu, ora):
     np.testing.assert_allclose(gi, oi, rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("gather_variant", [0, 1])
 @pytest.mark.parametrize("scene_name,W,H,P", [("Cornell", 64, 64, 128), ("Cornell", 96, 80, 64),
                                               ("CornellSmall", 64, 64, 128)])
-def test_ppm_parity(scene_name, W, H, P):
+def test_ppm_parity(scene_name, W, H, P, gather_variant):
     scene = scenes.scene_by_name(scene_name)
-    gpu, ora, det = make_pair(scene, W, H, P, _abi.PROGRESSIVE_PHOTON_MAPPING)
+    gpu, ora, det = make_pair(scene, W, H, P, _abi.PROGRESSIVE_PHOTON_MAPPING, gather_variant=gather_variant)
     radius = scene.initial_ppm_radius()
     req = det.to_abi()
     for it in range(3):
