@@ -141,7 +141,7 @@ typedef struct {
     uint32_t vcm_max_path_length;     /* VCM_MAX_PATH_LENGTH = 10 */
     uint32_t seed;                    /* 0: 574133*clock()+47844152748*time() like SpatialHash.cu:322; else DEBUG_RANDOM_SEED */
     uint32_t debug_counters;          /* 1: keep per-pixel cells/photons visited (OptixRenderer.cpp:872-953) */
-    uint32_t gather_variant;          /* 0: wave-cooperative LDS gather (default), 1: one thread per pixel */
+    uint32_t gather_variant;          /* 0: one thread per pixel in 8x8 wave tiles (default), 1: wave-cooperative LDS staging */
     uint32_t reserved[6];
 } orx_config;
 

@@ -88,7 +88,7 @@ void launch_grid_scan(hipStream_t s, const PhotonBufs& pb);
 void launch_grid_scatter(hipStream_t s, const PhotonBufs& pb);
 /* gathers `rows` pixel rows whose hitpoints are in hp{A,B,C} against the
  * local photon grid; writes indirect (and debug counters) */
-/* variant 0: wave-cooperative (default); 1: one thread per pixel */
+/* variant 0: one thread per pixel, 8x8 wave tiles (default); 1: wave-cooperative LDS staging */
 void launch_ppm_gather(hipStream_t s, const PixelBufs& px, const PhotonBufs& pb, const Consts& c, int variant);
 void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c);
 void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c);

@@ -679,7 +679,7 @@ __global__ __launch_bounds__(64) void k_ppm_gather_coop(PixelBufs px, PhotonBufs
     }
 }
 void launch_ppm_gather(hipStream_t s, const PixelBufs& px, const PhotonBufs& pb, const Consts& c, int variant) {
-    if (variant == 1) {
+    if (variant == 0) {
         dim3 grid((px.W + 15) / 16, (px.rows + 15) / 16);
         hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), 0, s, px, pb, c);
     } else {
