@@ -39,6 +39,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=20.0)
     p.add_argument("--gather-variant", type=int, default=0)
+    p.add_argument("--force-sharded", action="store_true",
+                   help="run the torch.distributed/RCCL sharded path even with one rank (tests the N>1 code)")
     return p.parse_args()
 
 
@@ -97,7 +99,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus > 1 or world > 1:
+    if args.gpus > 1 or world > 1 or args.force_sharded:
         from oppositerenderer_amd import multigpu
         return multigpu.bench_main(args, METRIC)
 

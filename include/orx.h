@@ -215,18 +215,42 @@ orx_status orx_get_stats(orx_renderer* r, orx_stats* out);
 /* starts a new timed region for orx_get_stats' *_total and pass_ms fields */
 orx_status orx_reset_timing(orx_renderer* r);
 
-/* Multi-GPU sharding: this renderer owns every RNG-slot row y
- * with y % world == rank (pixel rows and photon rows).  With world > 1 the
- * PPM iteration is split by the caller into
- *   orx_ppm_local_passes   eye pass on own rows, photon pass on own rows, grid over own photons
- *   (caller all-gathers the compact hitpoints of every rank)
- *   orx_ppm_gather_all     gather of ALL pixels against own photons -> partial indirect
- *   (caller reduce-scatters / all-reduces the partial indirect)
- *   orx_ppm_finish         direct pass + accumulate on own rows
- * The single-call orx_render_next_iteration is the world == 1 path. */
+/* ---- Multi-GPU sharding ----
+ * Rank `rank` of `world` owns every RNG-slot row y with y % world == rank:
+ * its pixel rows and its photon-launch rows (photon thread (x,y) aliases RNG
+ * slot (x,y), OptixRenderer_SpatialHash.cu:310-334), so RNG states never
+ * leave their GPU.  cfg.photon_launch_height is the GLOBAL launch height.
+ * One PPM iteration of a sharded renderer is driven by the caller:
+ *   orx_ppm_local_passes      eye pass (own pixel rows), photon pass (own rows), photon grid (own photons)
+ *   orx_export_hitpoints      own hitpoints -> caller buffer (orx_hitpoint_export_bytes)
+ *   (caller all-gathers the export buffers of all ranks, rank-major)
+ *   orx_ppm_gather_external   gather every rank's hitpoints against the own grid -> partial indirect
+ *   (caller reduce-scatters (sum) the partial indirect buffers, rank-major blocks)
+ *   orx_ppm_finish            direct pass + output accumulation on own rows
+ * The sum over ranks of the partial gathers equals the single-GPU gather up
+ * to fp32 summation order (the gather is linear in the photon set and its
+ * normalisation uses the global emitted count).  orx_render_next_iteration
+ * is the world == 1 composition of the same phases.  With world > 1,
+ * orx_get_output returns only the rank's own rows (local row j = global
+ * row rank + j*world). */
 orx_status orx_set_shard(orx_renderer* r, uint32_t rank, uint32_t world);
-/* hipStream_t the renderer launches on (as void*), for callers that sync or record events. */
+/* hipStream_t the renderer launches on (as void*). */
 void* orx_stream(orx_renderer* r);
+/* Launch on a caller-provided hipStream_t (e.g. torch's current stream); NULL restores the own stream. */
+orx_status orx_set_stream(orx_renderer* r, void* hip_stream);
+/* rows owned by this rank for the current resolution, and ceil(H/world) */
+uint32_t orx_local_rows(const orx_renderer* r);
+uint32_t orx_max_local_rows(const orx_renderer* r);
+size_t orx_hitpoint_export_bytes(const orx_renderer* r); /* max_local_rows * W * 40 */
+orx_status orx_ppm_local_passes(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
+                                float ppm_radius, const orx_request* details);
+orx_status orx_export_hitpoints(orx_renderer* r, void* dst_device, size_t dst_bytes);
+/* hitpoints_device: `segments` export buffers back to back; indirect_device:
+ * segments * max_local_rows * W * 3 floats */
+orx_status orx_ppm_gather_external(orx_renderer* r, const void* hitpoints_device, uint32_t segments,
+                                   void* indirect_device, size_t indirect_bytes);
+/* indirect_device: max_local_rows * W * 3 floats for the own rows */
+orx_status orx_ppm_finish(orx_renderer* r, const void* indirect_device, size_t indirect_bytes);
 
 #ifdef __cplusplus
 }

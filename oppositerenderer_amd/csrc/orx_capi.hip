@@ -218,9 +218,10 @@ struct orx_renderer {
     /* frame */
     uint32_t W = 10, H = 10, RW = 0, RH = 0;
     uint32_t rank = 0, world = 1;
-    uint32_t rows = 0, rng_rows = 0, prows = 0;
+    uint32_t rows = 0, max_rows = 0, rng_rows = 0, prows = 0;
     bool rng_ready = false;
-    DevBuf d_rng, d_hpA, d_hpB, d_hpC, d_ind, d_dir, d_out, d_dbg;
+    hipStream_t ext_stream = nullptr; /* caller-provided stream (orx_set_stream) */
+    DevBuf d_rng, d_hp, d_ind, d_dir, d_out, d_dbg;
     DevBuf d_slotA, d_slotB, d_slotC, d_vmask, d_sortA, d_sortB, d_sortC, d_keys, d_ranks;
     DevBuf d_hist, d_offsets, d_bbox, d_partials, d_grid;
     PixelBufs px{};
@@ -231,6 +232,7 @@ struct orx_renderer {
     uint32_t timed_iterations = 0;
     bool timing = true;
     uint64_t last_method = 0;
+    Consts last_consts{};
 };
 
 static orx_status set_err(orx_renderer* r, orx_status s, const std::string& m) {
@@ -455,20 +457,20 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     r->rows = local_rows(H);
     r->rng_rows = local_rows(r->RH);
     r->prows = local_rows(PH);
+    r->max_rows = (H + r->world - 1) / r->world;
     const size_t npx = (size_t)r->rows * W;
+    const size_t nhp = (size_t)r->max_rows * W; /* hitpoint planes padded to max_rows */
     const size_t nslot_rng = (size_t)r->rng_rows * r->RW;
     const size_t nphot = (size_t)r->prows * PW;
     const size_t S = nphot * D;
     const size_t G2 = (size_t)r->cfg.photon_grid_max_size + 2;
     const size_t nblocks = (G2 + 1023) / 1024 + 1;
     HIPCHK(r, r->d_rng.ensure(nslot_rng * 24));
-    HIPCHK(r, r->d_hpA.ensure(npx * 16));
-    HIPCHK(r, r->d_hpB.ensure(npx * 16));
-    HIPCHK(r, r->d_hpC.ensure(npx * 8));
-    HIPCHK(r, r->d_ind.ensure(npx * 12));
-    HIPCHK(r, r->d_dir.ensure(npx * 12));
-    HIPCHK(r, r->d_out.ensure(npx * 12));
-    HIPCHK(r, r->d_dbg.ensure(npx * 8));
+    HIPCHK(r, r->d_hp.ensure(nhp * 40));
+    HIPCHK(r, r->d_ind.ensure(nhp * 12));
+    HIPCHK(r, r->d_dir.ensure(nhp * 12));
+    HIPCHK(r, r->d_out.ensure(nhp * 12));
+    HIPCHK(r, r->d_dbg.ensure(nhp * 8));
     HIPCHK(r, r->d_slotA.ensure(S * 16));
     HIPCHK(r, r->d_slotB.ensure(S * 16));
     HIPCHK(r, r->d_slotC.ensure(S * 4));
@@ -487,7 +489,8 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, hipMemsetAsync(r->d_offsets.p, 0, G2 * 4, r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_vmask.p, 0, nphot, r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_grid.p, 0, sizeof(GridParams), r->stream));
-    HIPCHK(r, hipMemsetAsync(r->d_out.p, 0, npx * 12, r->stream));
+    HIPCHK(r, hipMemsetAsync(r->d_out.p, 0, nhp * 12, r->stream));
+    HIPCHK(r, hipMemsetAsync(r->d_hp.p, 0, nhp * 40, r->stream)); /* pad rows: flags 0 */
     uint32_t bbox_init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
     HIPCHK(r, hipMemcpyAsync(r->d_bbox.p, bbox_init, sizeof bbox_init, hipMemcpyHostToDevice, r->stream));
 
@@ -499,9 +502,10 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     px.rows = r->rows;
     px.RW = r->RW;
     for (int k = 0; k < 6; k++) px.rng.p[k] = r->d_rng.as<uint32_t>() + k * nslot_rng;
-    px.hpA = r->d_hpA.as<float4>();
-    px.hpB = r->d_hpB.as<float4>();
-    px.hpC = r->d_hpC.as<float2>();
+    px.hpA = r->d_hp.as<float4>();
+    px.hpB = r->d_hp.as<float4>() + nhp;
+    px.hpC = (float2*)(r->d_hp.as<float4>() + 2 * nhp);
+    px.seg_rows = r->max_rows;
     px.indirect = r->d_ind.as<float>();
     px.direct = r->d_dir.as<float>();
     px.output = r->d_out.as<float>();
@@ -546,12 +550,74 @@ static inline void ev_begin(orx_renderer* r, int p) {
         if (hipEventCreate(&e) != hipSuccess) return;
         v.push_back(e);
     }
-    hipEventRecord(v[2 * r->ev_n[p]], r->stream);
+    hipEventRecord(v[2 * r->ev_n[p]], r->ext_stream ? r->ext_stream : r->stream);
 }
 static inline void ev_end(orx_renderer* r, int p) {
     if (!r->timing || r->ev_n[p] >= EV_POOL || r->ev[p].size() < 2 * (size_t)r->ev_n[p] + 2) return;
-    hipEventRecord(r->ev[p][2 * r->ev_n[p] + 1], r->stream);
+    hipEventRecord(r->ev[p][2 * r->ev_n[p] + 1], r->ext_stream ? r->ext_stream : r->stream);
     r->ev_n[p]++;
+}
+
+static inline hipStream_t cur_stream(orx_renderer* r) { return r->ext_stream ? r->ext_stream : r->stream; }
+
+static Consts make_consts(orx_renderer* r, float ppm_radius, uint64_t local_iteration_number) {
+    Consts c;
+    c.max_photon_depth = r->cfg.max_photon_trace_depth;
+    c.max_radiance_depth = r->cfg.max_radiance_trace_depth;
+    c.ppm_radius = ppm_radius;
+    c.ppm_radius2 = ppm_radius * ppm_radius;
+    /* emittedPhotonsPerIterationFloat: global launch (all ranks) */
+    c.emitted_f = (float)(r->cfg.photon_launch_width * r->cfg.photon_launch_height);
+    c.local_iteration = (uint32_t)(local_iteration_number != 0);
+    return c;
+}
+
+/* resize / RNG init / output clear common to every method (OptixRenderer.cpp:531-557) */
+static orx_status begin_iteration(orx_renderer* r, uint64_t local_iteration_number, const orx_request* det) {
+    if (!r->scene_ready) return set_err(r, ORX_ERR_STATE, "Traced before OptixRenderer was initialized.");
+    if (det->width == 0 || det->height == 0) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "zero-sized request");
+    HIPCHK(r, hipSetDevice(r->device));
+    if (det->width != r->W || det->height != r->H || !r->rng_ready) {
+        orx_status st = resize(r, det->width, det->height);
+        if (st != ORX_OK) return st;
+        if (r->ext_stream) HIPCHK(r, hipStreamSynchronize(r->stream)); /* resize work ran on the own stream */
+    }
+    r->timed_iterations++;
+    if (local_iteration_number == 0)
+        HIPCHK(r, hipMemsetAsync(r->d_out.p, 0, (size_t)r->max_rows * r->W * 12, cur_stream(r)));
+    return ORX_OK;
+}
+
+static GatherIn local_gather_in(orx_renderer* r) {
+    GatherIn gi;
+    gi.base = (const uint8_t*)r->d_hp.p;
+    gi.seg_bytes = (size_t)r->max_rows * r->W * 40;
+    gi.segments = 1;
+    gi.seg_rows = r->max_rows;
+    gi.W = r->W;
+    gi.indirect = r->d_ind.as<float>();
+    gi.dbg = r->cfg.debug_counters ? r->d_dbg.as<uint32_t>() : nullptr;
+    return gi;
+}
+
+static void ppm_local_passes(orx_renderer* r, const DevCamera& cam, const Consts& c) {
+    hipStream_t st = cur_stream(r);
+    ev_begin(r, P_EYE);
+    launch_ppm_eye(st, r->scene, cam, r->px, c);
+    ev_end(r, P_EYE);
+    ev_begin(r, P_PHOTON);
+    launch_ppm_photon(st, r->scene, r->px, r->pb, c);
+    ev_end(r, P_PHOTON);
+    ev_begin(r, P_SETUP_HASH);
+    launch_grid_setup(st, r->pb);
+    launch_grid_hash(st, r->pb);
+    ev_end(r, P_SETUP_HASH);
+    ev_begin(r, P_SCAN);
+    launch_grid_scan(st, r->pb);
+    ev_end(r, P_SCAN);
+    ev_begin(r, P_SCATTER);
+    launch_grid_scatter(st, r->pb);
+    ev_end(r, P_SCATTER);
 }
 
 orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
@@ -559,64 +625,121 @@ orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
     (void)create_output; /* ignored by the reference engine too */
     (void)iteration_number;
     if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
-    if (!r->scene_ready) return set_err(r, ORX_ERR_STATE, "Traced before OptixRenderer was initialized.");
-    if (det->width == 0 || det->height == 0) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "zero-sized request");
     if (det->method != ORX_METHOD_PATH_TRACING && det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
         return set_err(r, ORX_ERR_UNSUPPORTED, "render method not supported by this build");
-    HIPCHK(r, hipSetDevice(r->device));
-    if (det->width != r->W || det->height != r->H || !r->rng_ready) {
-        orx_status st = resize(r, det->width, det->height);
-        if (st != ORX_OK) return st;
-    }
-    r->timed_iterations++;
-    const size_t npx = (size_t)r->rows * r->W;
-    if (local_iteration_number == 0) HIPCHK(r, hipMemsetAsync(r->d_out.p, 0, npx * 12, r->stream));
+    if (det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world > 1)
+        return set_err(r, ORX_ERR_STATE, "sharded PPM runs through orx_ppm_local_passes/_gather_external/_finish");
+    orx_status s0 = begin_iteration(r, local_iteration_number, det);
+    if (s0 != ORX_OK) return s0;
     DevCamera cam = camera_setup(det->camera);
-    Consts c;
-    c.max_photon_depth = r->cfg.max_photon_trace_depth;
-    c.max_radiance_depth = r->cfg.max_radiance_trace_depth;
-    c.ppm_radius = ppm_radius;
-    c.ppm_radius2 = ppm_radius * ppm_radius;
-    c.emitted_f = (float)(r->cfg.photon_launch_width * r->cfg.photon_launch_height);
-    c.local_iteration = (uint32_t)(local_iteration_number != 0);
+    Consts c = make_consts(r, ppm_radius, local_iteration_number);
+    hipStream_t st = cur_stream(r);
     if (det->method == ORX_METHOD_PATH_TRACING) {
         ev_begin(r, P_PT);
-        launch_pt(r->stream, r->scene, cam, r->px, c);
+        launch_pt(st, r->scene, cam, r->px, c);
         ev_end(r, P_PT);
     } else {
-        ev_begin(r, P_EYE);
-        launch_ppm_eye(r->stream, r->scene, cam, r->px, c);
-        ev_end(r, P_EYE);
-        ev_begin(r, P_PHOTON);
-        launch_ppm_photon(r->stream, r->scene, r->px, r->pb, c);
-        ev_end(r, P_PHOTON);
-        ev_begin(r, P_SETUP_HASH);
-        launch_grid_setup(r->stream, r->pb);
-        launch_grid_hash(r->stream, r->pb);
-        ev_end(r, P_SETUP_HASH);
-        ev_begin(r, P_SCAN);
-        launch_grid_scan(r->stream, r->pb);
-        ev_end(r, P_SCAN);
-        ev_begin(r, P_SCATTER);
-        launch_grid_scatter(r->stream, r->pb);
-        ev_end(r, P_SCATTER);
+        ppm_local_passes(r, cam, c);
         ev_begin(r, P_GATHER);
-        launch_ppm_gather(r->stream, r->px, r->pb, c, (int)r->cfg.gather_variant);
+        launch_ppm_gather(st, local_gather_in(r), r->pb, c, (int)r->cfg.gather_variant);
         ev_end(r, P_GATHER);
         ev_begin(r, P_DIRECT);
-        launch_ppm_direct_output(r->stream, r->scene, r->px, c);
+        launch_ppm_direct_output(st, r->scene, r->px, c);
         ev_end(r, P_DIRECT);
     }
     HIPCHK(r, hipGetLastError());
     r->last_method = (uint64_t)det->method;
+    r->last_consts = c;
+    return ORX_OK;
+}
+
+orx_status orx_ppm_local_passes(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
+                                float ppm_radius, const orx_request* det) {
+    (void)iteration_number;
+    if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
+    if (det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
+        return set_err(r, ORX_ERR_INVALID_ARGUMENT, "orx_ppm_local_passes needs a PPM request");
+    orx_status s0 = begin_iteration(r, local_iteration_number, det);
+    if (s0 != ORX_OK) return s0;
+    DevCamera cam = camera_setup(det->camera);
+    Consts c = make_consts(r, ppm_radius, local_iteration_number);
+    ppm_local_passes(r, cam, c);
+    HIPCHK(r, hipGetLastError());
+    r->last_method = (uint64_t)det->method;
+    r->last_consts = c;
+    return ORX_OK;
+}
+
+orx_status orx_export_hitpoints(orx_renderer* r, void* dst, size_t bytes) {
+    if (!r || !dst) return ORX_ERR_INVALID_ARGUMENT;
+    size_t need = (size_t)r->max_rows * r->W * 40;
+    if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "destination too small");
+    HIPCHK(r, hipSetDevice(r->device));
+    HIPCHK(r, hipMemcpyAsync(dst, r->d_hp.p, need, hipMemcpyDeviceToDevice, cur_stream(r)));
+    return ORX_OK;
+}
+
+orx_status orx_ppm_gather_external(orx_renderer* r, const void* hp, uint32_t segments, void* indirect, size_t bytes) {
+    if (!r || !hp || !indirect || segments == 0) return ORX_ERR_INVALID_ARGUMENT;
+    if (!r->rng_ready) return set_err(r, ORX_ERR_STATE, "no local passes yet");
+    size_t need = (size_t)segments * r->max_rows * r->W * 12;
+    if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "indirect buffer too small");
+    HIPCHK(r, hipSetDevice(r->device));
+    GatherIn gi;
+    gi.base = (const uint8_t*)hp;
+    gi.seg_bytes = (size_t)r->max_rows * r->W * 40;
+    gi.segments = segments;
+    gi.seg_rows = r->max_rows;
+    gi.W = r->W;
+    gi.indirect = (float*)indirect;
+    gi.dbg = nullptr;
+    ev_begin(r, P_GATHER);
+    launch_ppm_gather(cur_stream(r), gi, r->pb, r->last_consts, (int)r->cfg.gather_variant);
+    ev_end(r, P_GATHER);
+    HIPCHK(r, hipGetLastError());
+    return ORX_OK;
+}
+
+orx_status orx_ppm_finish(orx_renderer* r, const void* indirect, size_t bytes) {
+    if (!r || !indirect) return ORX_ERR_INVALID_ARGUMENT;
+    size_t need = (size_t)r->max_rows * r->W * 12;
+    if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "indirect buffer too small");
+    HIPCHK(r, hipSetDevice(r->device));
+    hipStream_t st = cur_stream(r);
+    HIPCHK(r, hipMemcpyAsync(r->d_ind.p, indirect, need, hipMemcpyDeviceToDevice, st));
+    ev_begin(r, P_DIRECT);
+    launch_ppm_direct_output(st, r->scene, r->px, r->last_consts);
+    ev_end(r, P_DIRECT);
+    HIPCHK(r, hipGetLastError());
+    return ORX_OK;
+}
+
+orx_status orx_set_stream(orx_renderer* r, void* stream) {
+    if (!r) return ORX_ERR_INVALID_ARGUMENT;
+    HIPCHK(r, hipSetDevice(r->device));
+    if (r->ext_stream && r->ext_stream != (hipStream_t)stream) HIPCHK(r, hipStreamSynchronize(r->ext_stream));
+    HIPCHK(r, hipStreamSynchronize(r->stream));
+    r->ext_stream = (hipStream_t)stream;
+    return ORX_OK;
+}
+uint32_t orx_local_rows(const orx_renderer* r) { return r ? r->rows : 0; }
+uint32_t orx_max_local_rows(const orx_renderer* r) { return r ? (r->H + r->world - 1) / r->world : 0; }
+size_t orx_hitpoint_export_bytes(const orx_renderer* r) {
+    return r ? (size_t)((r->H + r->world - 1) / r->world) * r->W * 40 : 0;
+}
+
+static orx_status sync_all(orx_renderer* r) {
+    HIPCHK(r, hipStreamSynchronize(r->stream));
+    if (r->ext_stream) HIPCHK(r, hipStreamSynchronize(r->ext_stream));
     return ORX_OK;
 }
 
 static orx_status check_grid_error(orx_renderer* r) {
     if (r->last_method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING || !r->d_grid.p) return ORX_OK;
     GridParams g;
-    HIPCHK(r, hipMemcpyAsync(&g, r->d_grid.p, sizeof g, hipMemcpyDeviceToHost, r->stream));
-    HIPCHK(r, hipStreamSynchronize(r->stream));
+    orx_status s0 = sync_all(r);
+    if (s0 != ORX_OK) return s0;
+    HIPCHK(r, hipMemcpy(&g, r->d_grid.p, sizeof g, hipMemcpyDeviceToHost));
     if (g.error)
         return set_err(r, ORX_ERR_GRID_TOO_LARGE, "Too many cells in SpatialHash.cu, over defined PHOTON_GRID_MAX_SIZE.");
     return ORX_OK;
@@ -628,8 +751,9 @@ orx_status orx_get_output(orx_renderer* r, float* dst, size_t bytes) {
     if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "destination too small");
     if (!r->d_out.p) return set_err(r, ORX_ERR_STATE, "no frame rendered yet");
     HIPCHK(r, hipSetDevice(r->device));
-    HIPCHK(r, hipMemcpyAsync(dst, r->d_out.p, need, hipMemcpyDeviceToHost, r->stream));
-    HIPCHK(r, hipStreamSynchronize(r->stream));
+    orx_status s0 = sync_all(r);
+    if (s0 != ORX_OK) return s0;
+    HIPCHK(r, hipMemcpy(dst, r->d_out.p, need, hipMemcpyDeviceToHost));
     return check_grid_error(r);
 }
 
@@ -639,7 +763,7 @@ orx_status orx_get_output_device(orx_renderer* r, void* dst, size_t bytes) {
     if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "destination too small");
     if (!r->d_out.p) return set_err(r, ORX_ERR_STATE, "no frame rendered yet");
     HIPCHK(r, hipSetDevice(r->device));
-    HIPCHK(r, hipMemcpyAsync(dst, r->d_out.p, need, hipMemcpyDeviceToDevice, r->stream));
+    HIPCHK(r, hipMemcpyAsync(dst, r->d_out.p, need, hipMemcpyDeviceToDevice, cur_stream(r)));
     return ORX_OK;
 }
 
@@ -654,7 +778,10 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
     if (!r) return ORX_ERR_INVALID_ARGUMENT;
     if (!r->rng_ready) return set_err(r, ORX_ERR_STATE, "no frame rendered yet");
     HIPCHK(r, hipSetDevice(r->device));
-    HIPCHK(r, hipStreamSynchronize(r->stream));
+    {
+        orx_status s0 = sync_all(r);
+        if (s0 != ORX_OK) return s0;
+    }
     GridParams g{};
     HIPCHK(r, hipMemcpy(&g, r->d_grid.p, sizeof g, hipMemcpyDeviceToHost));
     const size_t npx = (size_t)r->rows * r->W;
@@ -684,11 +811,12 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
         break;
     }
     case ORX_BUF_HITPOINTS: {
+        const size_t nhp = (size_t)r->max_rows * r->W;
         std::vector<float4> A(npx), B(npx);
         std::vector<float2> Cc(npx);
-        HIPCHK(r, d2h(A.data(), r->d_hpA.p, npx * 16));
-        HIPCHK(r, d2h(B.data(), r->d_hpB.p, npx * 16));
-        HIPCHK(r, d2h(Cc.data(), r->d_hpC.p, npx * 8));
+        HIPCHK(r, d2h(A.data(), r->d_hp.p, npx * 16));
+        HIPCHK(r, d2h(B.data(), r->d_hp.as<float4>() + nhp, npx * 16));
+        HIPCHK(r, d2h(Cc.data(), r->d_hp.as<float4>() + 2 * nhp, npx * 8));
         float* o = (float*)dst;
         for (size_t i = 0; i < npx; i++) {
             uint32_t flags;
@@ -739,7 +867,10 @@ orx_status orx_get_stats(orx_renderer* r, orx_stats* out) {
     if (!r || !out) return ORX_ERR_INVALID_ARGUMENT;
     std::memset(out, 0, sizeof *out);
     HIPCHK(r, hipSetDevice(r->device));
-    HIPCHK(r, hipStreamSynchronize(r->stream));
+    {
+        orx_status s0 = sync_all(r);
+        if (s0 != ORX_OK) return s0;
+    }
     if (r->d_grid.p) {
         GridParams g;
         HIPCHK(r, hipMemcpy(&g, r->d_grid.p, sizeof g, hipMemcpyDeviceToHost));
@@ -774,7 +905,10 @@ orx_status orx_get_stats(orx_renderer* r, orx_stats* out) {
 orx_status orx_reset_timing(orx_renderer* r) {
     if (!r) return ORX_ERR_INVALID_ARGUMENT;
     HIPCHK(r, hipSetDevice(r->device));
-    HIPCHK(r, hipStreamSynchronize(r->stream));
+    {
+        orx_status s0 = sync_all(r);
+        if (s0 != ORX_OK) return s0;
+    }
     for (int p = 0; p < P_COUNT; p++) r->ev_n[p] = 0;
     r->timed_iterations = 0;
     if (r->d_grid.p) {

@@ -38,9 +38,13 @@ struct PixelBufs {
     uint32_t rows;      /* local rows = number of y with y % world == rank */
     uint32_t RW;        /* RNG buffer width (slot = y*RW + x, global y) */
     RngPlanes rng;      /* local RNG rows: slot index = j*RW + x */
+    /* hitpoints: one segment of seg_rows rows laid out as planes
+     * [A: seg_rows*W float4][B: seg_rows*W float4][C: seg_rows*W float2]
+     * (the multi-GPU export format, 40 B per pixel) */
     float4* hpA;        /* pos.xyz, flags bits */
     float4* hpB;        /* normal.xyz (non-specular hit) | radiance.xyz, atten.x */
     float2* hpC;        /* atten.y, atten.z */
+    uint32_t seg_rows;  /* rows per hitpoint segment (= ceil(H/world)) */
     float* indirect;    /* [rows*W*3] */
     float* direct;      /* [rows*W*3] */
     float* output;      /* [rows*W*3] running SUM */
@@ -88,8 +92,17 @@ void launch_grid_scan(hipStream_t s, const PhotonBufs& pb);
 void launch_grid_scatter(hipStream_t s, const PhotonBufs& pb);
 /* gathers `rows` pixel rows whose hitpoints are in hp{A,B,C} against the
  * local photon grid; writes indirect (and debug counters) */
+/* Hitpoints to gather: `segments` segments of seg_rows x W pixels, each in the
+ * plane layout of PixelBufs (segment k starts at base + k*seg_bytes). */
+struct GatherIn {
+    const uint8_t* base;
+    size_t seg_bytes;
+    uint32_t segments, seg_rows, W;
+    float* indirect;    /* [segments*seg_rows*W*3] */
+    uint32_t* dbg;      /* [segments*seg_rows*W*2] or NULL */
+};
 /* variant 0: one thread per pixel, 8x8 wave tiles (default); 1: wave-cooperative LDS staging */
-void launch_ppm_gather(hipStream_t s, const PixelBufs& px, const PhotonBufs& pb, const Consts& c, int variant);
+void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, int variant);
 void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c);
 void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c);
 

@@ -451,18 +451,37 @@ void launch_grid_scatter(hipStream_t s, const PhotonBufs& pb) {
 /* ------------------------------------------------------------------ */
 /* indirect radiance estimate: uniform-grid gather                     */
 /* ------------------------------------------------------------------ */
-__global__ __launch_bounds__(256) void k_ppm_gather(PixelBufs px, PhotonBufs pb, Consts c) {
+struct HpRef {
+    const float4* A;
+    const float4* B;
+    const float2* C;
+    size_t li;
+};
+__device__ __forceinline__ HpRef hp_ref(const GatherIn& gi, uint32_t j, uint32_t x) {
+    uint32_t seg = j / gi.seg_rows, lj = j - seg * gi.seg_rows;
+    const size_t plane = (size_t)gi.seg_rows * gi.W;
+    const uint8_t* b = gi.base + seg * gi.seg_bytes;
+    HpRef r;
+    r.A = (const float4*)b;
+    r.B = (const float4*)(b + plane * 16);
+    r.C = (const float2*)(b + plane * 32);
+    r.li = (size_t)lj * gi.W + x;
+    return r;
+}
+
+__global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, Consts c) {
     /* block = 16x16 pixels as four 8x8 wave tiles (neighbouring lanes share photons in L1) */
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (l & 7);
     const uint32_t j = blockIdx.y * 16 + (w >> 1) * 8 + (l >> 3);
     const GridParams g = *pb.grid;
     uint32_t dC = 0, dP = 0;
-    if (x < px.W && j < px.rows) {
-        const size_t i = (size_t)j * px.W + x;
-        const float4 A = px.hpA[i];
-        const float4 B = px.hpB[i];
-        const float2 Cc = px.hpC[i];
+    if (x < gi.W && j < gi.segments * gi.seg_rows) {
+        const size_t i = (size_t)j * gi.W + x;
+        const HpRef hr = hp_ref(gi, j, x);
+        const float4 A = hr.A[hr.li];
+        const float4 B = hr.B[hr.li];
+        const float2 Cc = hr.C[hr.li];
         const uint32_t flags = __float_as_uint(A.w);
         f3 acc = mk1(0.0f);
         if ((flags & PRD_HIT_NON_SPECULAR) && g.G) {
@@ -518,12 +537,12 @@ __global__ __launch_bounds__(256) void k_ppm_gather(PixelBufs px, PhotonBufs pb,
         float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
         float s2 = 1.0f / c.emitted_f;
         f3 ind = ((acc * att) * s1) * s2;
-        px.indirect[3 * i + 0] = ind.x;
-        px.indirect[3 * i + 1] = ind.y;
-        px.indirect[3 * i + 2] = ind.z;
-        if (px.dbg) {
-            px.dbg[2 * i] = dC;
-            px.dbg[2 * i + 1] = dP;
+        gi.indirect[3 * i + 0] = ind.x;
+        gi.indirect[3 * i + 1] = ind.y;
+        gi.indirect[3 * i + 2] = ind.z;
+        if (gi.dbg) {
+            gi.dbg[2 * i] = dC;
+            gi.dbg[2 * i + 1] = dP;
         }
     }
     uint64_t sp = wave_sum_u64(dP), sc = wave_sum_u64(dC);
@@ -543,7 +562,7 @@ __global__ __launch_bounds__(256) void k_ppm_gather(PixelBufs px, PhotonBufs pb,
  * per-pixel loop above, in the same order (rows in z,y order, photons in
  * grid order), so the sums are bit-identical to k_ppm_gather; only the
  * photon loads are shared and the inner loop is divergence-free. */
-__global__ __launch_bounds__(64) void k_ppm_gather_coop(PixelBufs px, PhotonBufs pb, Consts c) {
+__global__ __launch_bounds__(64) void k_ppm_gather_coop(GatherIn gi, PhotonBufs pb, Consts c) {
     __shared__ float4 sA[64];
     __shared__ float4 sB[64];
     __shared__ float sC[64];
@@ -551,14 +570,15 @@ __global__ __launch_bounds__(64) void k_ppm_gather_coop(PixelBufs px, PhotonBufs
     const uint32_t x = blockIdx.x * 8 + (lane & 7);
     const uint32_t j = blockIdx.y * 8 + (lane >> 3);
     const GridParams g = *pb.grid;
-    const bool inimg = x < px.W && j < px.rows;
-    const size_t i = (size_t)j * px.W + x;
+    const bool inimg = x < gi.W && j < gi.segments * gi.seg_rows;
+    const size_t i = (size_t)j * gi.W + x;
     float4 A = make_float4(0, 0, 0, 0), B = A;
     float2 Cc = make_float2(0, 0);
     if (inimg) {
-        A = px.hpA[i];
-        B = px.hpB[i];
-        Cc = px.hpC[i];
+        const HpRef hr = hp_ref(gi, j, x);
+        A = hr.A[hr.li];
+        B = hr.B[hr.li];
+        Cc = hr.C[hr.li];
     }
     const uint32_t flags = __float_as_uint(A.w);
     const f3 pos = mk(A.x, A.y, A.z);
@@ -661,12 +681,12 @@ __global__ __launch_bounds__(64) void k_ppm_gather_coop(PixelBufs px, PhotonBufs
         float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
         float s2 = 1.0f / c.emitted_f;
         f3 ind = ((acc * att) * s1) * s2;
-        px.indirect[3 * i + 0] = ind.x;
-        px.indirect[3 * i + 1] = ind.y;
-        px.indirect[3 * i + 2] = ind.z;
-        if (px.dbg) {
-            px.dbg[2 * i] = dC;
-            px.dbg[2 * i + 1] = dP;
+        gi.indirect[3 * i + 0] = ind.x;
+        gi.indirect[3 * i + 1] = ind.y;
+        gi.indirect[3 * i + 2] = ind.z;
+        if (gi.dbg) {
+            gi.dbg[2 * i] = dC;
+            gi.dbg[2 * i + 1] = dP;
         }
     }
     uint64_t sp = wave_sum_u64(dP), sc = wave_sum_u64(dC);
@@ -678,13 +698,14 @@ __global__ __launch_bounds__(64) void k_ppm_gather_coop(PixelBufs px, PhotonBufs
         atomicAdd((unsigned long long*)&pb.grid->cells_visited_total, (unsigned long long)sc);
     }
 }
-void launch_ppm_gather(hipStream_t s, const PixelBufs& px, const PhotonBufs& pb, const Consts& c, int variant) {
+void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, int variant) {
+    const uint32_t rows = gi.segments * gi.seg_rows;
     if (variant == 0) {
-        dim3 grid((px.W + 15) / 16, (px.rows + 15) / 16);
-        hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), 0, s, px, pb, c);
+        dim3 grid((gi.W + 15) / 16, (rows + 15) / 16);
+        hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), 0, s, gi, pb, c);
     } else {
-        dim3 grid((px.W + 7) / 8, (px.rows + 7) / 8);
-        hipLaunchKernelGGL(k_ppm_gather_coop, grid, dim3(64), 0, s, px, pb, c);
+        dim3 grid((gi.W + 7) / 8, (rows + 7) / 8);
+        hipLaunchKernelGGL(k_ppm_gather_coop, grid, dim3(64), 0, s, gi, pb, c);
     }
 }
 

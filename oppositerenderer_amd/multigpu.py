@@ -1,0 +1,204 @@
+"""Multi-GPU progressive photon mapping: one process per GPU, torch.distributed
+(backend "nccl" = RCCL over xGMI on MI355X; "gloo" for the CPU tests).
+
+Sharding (option A) — rank g of N owns every RNG-slot row
+y with y % N == g, i.e. its pixel rows AND its photon-launch rows (photon
+thread (x,y) aliases RNG slot (x,y), OptixRenderer_SpatialHash.cu:310-334),
+so RNG state never crosses GPUs.  Per PPM iteration:
+
+  1. local passes   eye rays for own pixel rows, own photon batch, photon grid over own photons
+  2. all-gather     compact hitpoints (40 B/pixel) of every rank           (RCCL all_gather)
+  3. gather         ALL pixels against the own photon grid -> partial indirect radiance
+  4. reduce-scatter partial indirect, summed, to the row owners            (RCCL reduce_scatter)
+  5. finish         direct light + running-sum output on own rows
+
+The gather is linear in the photon set and normalises by the global emitted
+count, so the result equals one GPU running the union photon launch, up to
+fp32 summation order.  Scaling is WEAK: each rank traces a full
+photon_launch_width x photon_launch_height batch (global launch height =
+N x per-rank height) and 1/N of the eye/direct pixels.
+
+Backends: `DeviceShard` drives liborx.so with torch device tensors on the
+renderer's (= torch's current) stream; tests drive the CPU oracle through
+the same phase API with gloo (tests/test_multigpu_gloo.py).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import time
+
+import numpy as np
+
+
+def local_rows(H, rank, world):
+    return (H - rank + world - 1) // world if H > rank else 0
+
+
+def assemble_rows(blocks, W, H, world):
+    """blocks[g]: [max_rows, W, 3] of rank g (local row j = global row g + j*world)."""
+    img = np.zeros((H, W, 3), np.float32)
+    for g, b in enumerate(blocks):
+        n = local_rows(H, g, world)
+        img[g::world] = b[:n]
+    return img
+
+
+class ShardedPPM:
+    """Runs the 5-step sharded iteration for any backend exposing
+    local_passes / export_hitpoints / gather_external / finish / alloc."""
+
+    def __init__(self, backend, dist, world, rank, W, H):
+        self.b, self.dist, self.world, self.rank, self.W, self.H = backend, dist, world, rank, W, H
+        self.max_rows = (H + world - 1) // world
+        self.hp_local = backend.alloc(self.max_rows * W * 10)               # 40 B/px as float32
+        self.hp_all = backend.alloc(world * self.max_rows * W * 10)
+        self.ind_partial = backend.alloc(world * self.max_rows * W * 3)
+        self.ind_local = backend.alloc(self.max_rows * W * 3)
+        self.gloo = dist.get_backend() == "gloo"
+
+    def iteration(self, it, local_it, radius, request):
+        d = self.dist
+        self.b.local_passes(it, local_it, radius, request)
+        self.b.export_hitpoints(self.hp_local)
+        if self.gloo:
+            parts = list(self.hp_all.chunk(self.world))
+            d.all_gather(parts, self.hp_local)
+        else:
+            d.all_gather_into_tensor(self.hp_all, self.hp_local)
+        self.b.gather_external(self.hp_all, self.world, self.ind_partial)
+        if self.gloo:  # gloo has no reduce_scatter: all_reduce + own block
+            d.all_reduce(self.ind_partial)
+            blk = self.max_rows * self.W * 3
+            self.ind_local.copy_(self.ind_partial[self.rank * blk:(self.rank + 1) * blk])
+        else:
+            d.reduce_scatter_tensor(self.ind_local, self.ind_partial)
+        self.b.finish(self.ind_local)
+
+    def image(self):
+        """Full running-sum image on every rank (collective)."""
+        out = self.b.output_local_tensor(self.max_rows)
+        parts = [out.clone() for _ in range(self.world)]
+        self.dist.all_gather(parts, out)
+        blocks = [p.detach().cpu().numpy().reshape(self.max_rows, self.W, 3) for p in parts]
+        return assemble_rows(blocks, self.W, self.H, self.world)
+
+
+class DeviceShard:
+    """liborx.so backend: buffers are torch device tensors, kernels run on torch's current stream."""
+
+    def __init__(self, renderer, torch, device):
+        self.r, self.torch, self.device = renderer, torch, device
+        lib = renderer._lib
+        for name, args, res in (
+            ("orx_set_stream", [C.c_void_p, C.c_void_p], C.c_int),
+            ("orx_ppm_local_passes", [C.c_void_p, C.c_uint64, C.c_uint64, C.c_float, C.c_void_p], C.c_int),
+            ("orx_export_hitpoints", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
+            ("orx_ppm_gather_external", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t], C.c_int),
+            ("orx_ppm_finish", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
+        ):
+            f = getattr(lib, name)
+            f.argtypes, f.restype = args, res
+        self.lib = lib
+        stream = torch.cuda.current_stream(device).cuda_stream
+        renderer._check(lib.orx_set_stream(renderer._h, C.c_void_p(stream)))
+
+    def alloc(self, nfloat):
+        return self.torch.zeros(nfloat, dtype=self.torch.float32, device=self.device)
+
+    def local_passes(self, it, local_it, radius, request):
+        self.r._check(self.lib.orx_ppm_local_passes(self.r._h, it, local_it, radius, C.byref(request)))
+
+    def export_hitpoints(self, t):
+        self.r._check(self.lib.orx_export_hitpoints(self.r._h, C.c_void_p(t.data_ptr()), t.numel() * 4))
+
+    def gather_external(self, hp_all, segments, out):
+        self.r._check(self.lib.orx_ppm_gather_external(self.r._h, C.c_void_p(hp_all.data_ptr()), segments,
+                                                       C.c_void_p(out.data_ptr()), out.numel() * 4))
+
+    def finish(self, ind_local):
+        self.r._check(self.lib.orx_ppm_finish(self.r._h, C.c_void_p(ind_local.data_ptr()), ind_local.numel() * 4))
+
+    def output_local_tensor(self, max_rows):
+        t = self.alloc(max_rows * self.r.getWidth() * 3)
+        self.r.getOutputBufferDevice(t.data_ptr(), t.numel() * 4)
+        return t
+
+
+def bench_main(args, metric):
+    """bench.py --gpus N under torchrun: weak scaling, one rank per GPU."""
+    import torch
+    import torch.distributed as dist
+
+    from . import _abi, scenes
+    from .renderer import OptixRenderer, RenderRequestDetails, next_ppm_radius
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    W, H, P = args.width, args.height, args.photon_launch
+    scene = scenes.scene_by_name(args.scene)
+    cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P * world,
+                              gather_variant=args.gather_variant)
+    r = OptixRenderer(cfg)
+    r.initialize(local_rank)
+    r.set_shard(rank, world)
+    r.initScene(scene)
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    det = RenderRequestDetails(cam, scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W, H)
+    req = det.to_abi()
+    dev = torch.device("cuda", local_rank)
+    backend = DeviceShard(r, torch, dev)
+    radius = scene.initial_ppm_radius()
+    sharded = ShardedPPM(backend, dist, world, rank, W, H)
+    it = 0
+    for _ in range(max(1, args.warmup)):
+        sharded.iteration(it, it, radius, req)
+        radius = next_ppm_radius(radius, it)
+        it += 1
+    torch.cuda.synchronize()
+    dist.barrier()
+    r.reset_timing()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sharded.iteration(it, it, radius, req)
+        radius = next_ppm_radius(radius, it)
+        it += 1
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_max = float(t.item())
+    st = r.stats()
+    if rank == 0:
+        paths = W * H + P * P * world
+        per_pass = {name: st.pass_ms[i] / max(1, st.timed_iterations) for i, name in enumerate(_abi.PASS_NAMES)}
+        gms = per_pass["ppm_gather"]
+        valid_avg = st.valid_photons_total / max(1, st.timed_iterations)
+        gbytes = W * H * (40 + 12) + valid_avg * 36 + (st.num_cells + 1) * 4
+        achieved = gbytes / (gms * 1e-3) / 1e9 if gms > 0 else 0.0
+        out = {
+            "metric": metric, "value": round(paths * args.steps / t_max / 1e6, 3), "unit": "Mpaths/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(t_max * 1e3 / args.steps, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (built-in Cornell scene, seeded XORWOW streams)",
+            "config": {"workload": f"{scene.name} {W}x{H} PPM, {P * P} photons/iter per GPU (weak scaling)",
+                       "scene": scene.name, "width": W, "height": H, "photons_per_iteration": P * P * world,
+                       "paths_per_iteration": paths,
+                       "parallelism": f"row-interleaved RNG/pixel/photon ownership x{world}, "
+                                      "RCCL all_gather(hitpoints) + reduce_scatter(indirect)"},
+            "roofline": {"kernel": "k_ppm_gather", "bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0,
+                         "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": None,
+                         "bytes_per_launch": int(gbytes), "avg_launch_ms": round(gms, 4)},
+            "passes_ms": {k: round(v, 4) for k, v in per_pass.items() if v > 0},
+        }
+        print(json.dumps(out))
+    r.destroy()
+    dist.barrier()
+    dist.destroy_process_group()

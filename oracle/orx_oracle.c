@@ -221,8 +221,11 @@ struct orc_renderer {
     light_t* lights;
     v3 aabb_min, aabb_max;
     v3 bs_center; float bs_radius;
-    /* frame */
+    /* frame; sharding: this renderer owns RNG/pixel/photon rows y % world == rank */
     uint32_t W, H, RW, RH;
+    uint32_t rank, world, rows, max_rows, prows;
+    float last_radius, last_radius2;
+    uint64_t last_local;
     int rng_ready;
     uint32_t* rng; /* [RW*RH][6] */
     hitpoint_t* hp;
@@ -257,6 +260,7 @@ orx_status orc_create(const orx_config* cfg, orc_renderer** out) {
     if (cfg) r->cfg = *cfg;
     else orc_default_config(&r->cfg);
     r->W = 10; r->H = 10; /* OptixRenderer ctor m_width(10), m_height(10) */
+    r->world = 1;
     *out = r;
     return ORX_OK;
 }
@@ -687,8 +691,11 @@ static orx_status resize(orc_renderer* r, uint32_t W, uint32_t H) {
     r->W = W; r->H = H;
     r->RW = PW > W ? PW : W;
     r->RH = PH > H ? PH : H;
-    size_t npx = (size_t)W * H;
-    size_t S = (size_t)PW * PH * r->cfg.max_photon_deposits;
+    r->rows = H > r->rank ? (H - r->rank + r->world - 1) / r->world : 0;
+    r->max_rows = (H + r->world - 1) / r->world;
+    r->prows = PH > r->rank ? (PH - r->rank + r->world - 1) / r->world : 0;
+    size_t npx = (size_t)r->max_rows * W;
+    size_t S = (size_t)PW * r->prows * r->cfg.max_photon_deposits;
     size_t G = r->cfg.photon_grid_max_size;
     r->rng = (uint32_t*)malloc((size_t)r->RW * r->RH * 6 * 4);
     r->hp = (hitpoint_t*)calloc(npx, sizeof(hitpoint_t));
@@ -721,7 +728,8 @@ static orx_status resize(orc_renderer* r, uint32_t W, uint32_t H) {
 static void ppm_eye_pass(orc_renderer* r, const cam_t* cam) {
     const uint32_t W = r->W, H = r->H;
 #pragma omp parallel for schedule(dynamic, 4)
-    for (long long y = 0; y < (long long)H; y++) {
+    for (long long j = 0; j < (long long)r->rows; j++) {
+        const uint32_t y = r->rank + r->world * (uint32_t)j;
         for (uint32_t x = 0; x < W; x++) {
             uint32_t rs[6];
             uint32_t* g = r->rng + 6 * ((size_t)y * r->RW + x);
@@ -731,9 +739,9 @@ static void ppm_eye_pass(orc_renderer* r, const cam_t* cam) {
             prd.attenuation = mk1(1.0f);
             prd.rs = rs;
             v3 o, d;
-            primary_ray(cam, x, (uint32_t)y, W, H, rs, &o, &d);
+            primary_ray(cam, x, y, W, H, rs, &o, &d);
             trace_radiance(r, o, d, 0.001f, &prd);
-            hitpoint_t* h = &r->hp[(size_t)y * W + x];
+            hitpoint_t* h = &r->hp[(size_t)j * W + x];
             h->position = prd.position;
             h->normal = prd.normal;
             h->attenuation = prd.attenuation;
@@ -827,10 +835,12 @@ static void ppm_photon_pass(orc_renderer* r) {
     const uint32_t PW = r->cfg.photon_launch_width, PH = r->cfg.photon_launch_height;
     const uint32_t maxDeposits = r->cfg.max_photon_deposits;
     const uint32_t nl = r->nl;
+    (void)PH;
 #pragma omp parallel for schedule(dynamic, 4)
-    for (long long y = 0; y < (long long)PH; y++) {
+    for (long long j = 0; j < (long long)r->prows; j++) {
+        const uint32_t y = r->rank + r->world * (uint32_t)j;
         for (uint32_t x = 0; x < PW; x++) {
-            uint32_t pm_index = ((uint32_t)y * PW + x) * maxDeposits;
+            uint32_t pm_index = ((uint32_t)j * PW + x) * maxDeposits;
             uint32_t* g = r->rng + 6 * ((size_t)y * r->RW + x);
             uint32_t rs[6];
             memcpy(rs, g, 24);
@@ -893,7 +903,7 @@ static float smallest_possible_cell_size(v3 ext, uint32_t maxGridSize) {
 
 /* createUniformGridPhotonMap (OptixRenderer_SpatialHash.cu:209-282) */
 static orx_status ppm_build_grid(orc_renderer* r) {
-    const size_t S = (size_t)r->cfg.photon_launch_width * r->cfg.photon_launch_height * r->cfg.max_photon_deposits;
+    const size_t S = (size_t)r->cfg.photon_launch_width * r->prows * r->cfg.max_photon_deposits;
     photon_t* ph = r->photons;
     /* getPhotonsBoundingBox: transform_reduce over valid photons (:123-128) */
     int any = 0;
@@ -955,9 +965,36 @@ static orx_status ppm_build_grid(orc_renderer* r) {
     return ORX_OK;
 }
 
+/* hitpoint source for the gather: the own rows, or `segments` export buffers
+ * (plane layout A: pos+flags float4, B: normal|radiance + atten.x float4,
+ * C: atten.yz float2; seg_rows*W pixels per plane) */
+typedef struct {
+    const hitpoint_t* own;
+    const float* ext;
+    uint32_t seg_rows;
+} hp_src;
+static hitpoint_t hp_fetch(const orc_renderer* r, const hp_src* src, size_t px) {
+    if (src->own) return src->own[px];
+    const size_t plane = (size_t)src->seg_rows * r->W;
+    size_t seg = px / plane, li = px - seg * plane;
+    const float* b = src->ext + seg * plane * 10;
+    const float* A = b + 4 * li;
+    const float* B = b + 4 * plane + 4 * li;
+    const float* Cc = b + 8 * plane + 2 * li;
+    hitpoint_t h;
+    memset(&h, 0, sizeof h);
+    h.position = mk(A[0], A[1], A[2]);
+    memcpy(&h.flags, &A[3], 4);
+    if (h.flags & PRD_HIT_NON_SPECULAR) h.normal = mk(B[0], B[1], B[2]);
+    else h.radiance = mk(B[0], B[1], B[2]);
+    h.attenuation = mk(B[3], Cc[0], Cc[1]);
+    return h;
+}
+
 /* IndirectRadianceEstimation.cu:54-67, :69-129, :211-221 */
-static void ppm_gather(orc_renderer* r, float ppmRadius, float ppmRadiusSquared, float emittedF) {
-    const uint32_t W = r->W, H = r->H;
+static void ppm_gather_src(orc_renderer* r, const hp_src* src, uint32_t rows_total, v3* out, uint32_t* dbg,
+                           float ppmRadius, float ppmRadiusSquared, float emittedF) {
+    const uint32_t W = r->W, H = rows_total;
     const uint32_t gx = r->gsize[0], gy = r->gsize[1], gz = r->gsize[2];
     const v3 origo = r->origo;
     const float cell = r->cell;
@@ -966,7 +1003,7 @@ static void ppm_gather(orc_renderer* r, float ppmRadius, float ppmRadiusSquared,
     for (long long y = 0; y < (long long)H; y++) {
         for (uint32_t x = 0; x < W; x++) {
             size_t px = (size_t)y * W + x;
-            const hitpoint_t rec = r->hp[px];
+            const hitpoint_t rec = hp_fetch(r, src, px);
             v3 acc = mk1(0.0f);
             uint32_t dP = 0, dC = 0;
             if (rec.flags & PRD_HIT_NON_SPECULAR) {
@@ -1018,15 +1055,21 @@ static void ppm_gather(orc_renderer* r, float ppmRadius, float ppmRadiusSquared,
             }
             float s1 = 1.0f / (ORX_PI_F * ppmRadiusSquared);
             float s2 = 1.0f / emittedF;
-            r->indirect[px] = scl(scl(mul(acc, rec.attenuation), s1), s2);
-            r->dbg[2 * px] = dC;
-            r->dbg[2 * px + 1] = dP;
+            out[px] = scl(scl(mul(acc, rec.attenuation), s1), s2);
+            if (dbg) {
+                dbg[2 * px] = dC;
+                dbg[2 * px + 1] = dP;
+            }
             sumP += dP;
             sumC += dC;
         }
     }
     r->sum_photons_visited = sumP;
     r->sum_cells_visited = sumC;
+}
+static void ppm_gather(orc_renderer* r, float ppmRadius, float ppmRadiusSquared, float emittedF) {
+    hp_src src = {r->hp, NULL, 0};
+    ppm_gather_src(r, &src, r->rows, r->indirect, r->dbg, ppmRadius, ppmRadiusSquared, emittedF);
 }
 
 /* helpers/light.h:29-87 */
@@ -1059,12 +1102,13 @@ static v3 light_contribution(const orc_renderer* r, const light_t* light, v3 pos
 
 /* DirectRadianceEstimation.cu:29-77 */
 static void ppm_direct(orc_renderer* r) {
-    const uint32_t W = r->W, H = r->H;
+    const uint32_t W = r->W;
     const int numLights = (int)r->nl;
 #pragma omp parallel for schedule(dynamic, 4)
-    for (long long y = 0; y < (long long)H; y++) {
+    for (long long j = 0; j < (long long)r->rows; j++) {
+        const uint32_t y = r->rank + r->world * (uint32_t)j;
         for (uint32_t x = 0; x < W; x++) {
-            size_t px = (size_t)y * W + x;
+            size_t px = (size_t)j * W + x;
             const hitpoint_t rec = r->hp[px];
             if (!(rec.flags & PRD_HIT_NON_SPECULAR)) {
                 if ((rec.flags & PRD_HIT_EMITTER) && !(rec.flags & PRD_HIT_SPECULAR))
@@ -1090,7 +1134,7 @@ static void ppm_direct(orc_renderer* r) {
 
 /* Output.cu:32-37 */
 static void ppm_output(orc_renderer* r, uint64_t local) {
-    size_t n = (size_t)r->W * r->H;
+    size_t n = (size_t)r->W * r->rows;
     for (size_t i = 0; i < n; i++) {
         v3 f = add(r->direct[i], r->indirect[i]);
         r->output[i] = local == 0 ? f : add(r->output[i], f);
@@ -1102,9 +1146,10 @@ static void pt_pass(orc_renderer* r, const cam_t* cam, uint64_t local) {
     const uint32_t W = r->W, H = r->H;
     const int numLights = (int)r->nl;
 #pragma omp parallel for schedule(dynamic, 4)
-    for (long long y = 0; y < (long long)H; y++) {
+    for (long long j = 0; j < (long long)r->rows; j++) {
+        const uint32_t y = r->rank + r->world * (uint32_t)j;
         for (uint32_t x = 0; x < W; x++) {
-            size_t px = (size_t)y * W + x;
+            size_t px = (size_t)j * W + x;
             uint32_t* G = r->rng + 6 * ((size_t)y * r->RW + x);
             uint32_t rs[6];
             memcpy(rs, G, 24);
@@ -1113,7 +1158,7 @@ static void pt_pass(orc_renderer* r, const cam_t* cam, uint64_t local) {
             prd.attenuation = mk1(1.0f);
             prd.rs = rs;
             v3 o, d;
-            primary_ray(cam, x, (uint32_t)y, W, H, rs, &o, &d);
+            primary_ray(cam, x, y, W, H, rs, &o, &d);
             v3 fin = mk1(0);
             for (int i = 0; i < 5; i++) {
                 prd.flags = PRD_PATH_TRACING;
@@ -1150,22 +1195,32 @@ static void pt_pass(orc_renderer* r, const cam_t* cam, uint64_t local) {
 /* ------------------------------------------------------------------ */
 /* OptixRenderer::renderNextIteration (OptixRenderer.cpp:507-821)     */
 /* ------------------------------------------------------------------ */
-orx_status orc_render_next_iteration(orc_renderer* r, uint64_t iter, uint64_t local, float ppmRadius,
-                                     int create_output, const orx_request* det) {
-    (void)create_output;
-    if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
+static orx_status begin_iteration(orc_renderer* r, uint64_t local, const orx_request* det) {
     if (!r->scene_ready) return fail(r, ORX_ERR_STATE, "Traced before OptixRenderer was initialized.");
     if (det->width == 0 || det->height == 0) return fail(r, ORX_ERR_INVALID_ARGUMENT, "zero-sized request");
     if (det->width != r->W || det->height != r->H || !r->rng_ready) {
         orx_status s = resize(r, det->width, det->height);
         if (s != ORX_OK) return s;
     }
-    if (local == 0) memset(r->output, 0, (size_t)r->W * r->H * sizeof(v3));
-    cam_t cam = camera_setup(&det->camera);
+    if (local == 0) memset(r->output, 0, (size_t)r->W * r->max_rows * sizeof(v3));
+    return ORX_OK;
+}
+
+orx_status orc_render_next_iteration(orc_renderer* r, uint64_t iter, uint64_t local, float ppmRadius,
+                                     int create_output, const orx_request* det) {
+    (void)create_output;
     (void)iter;
+    if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
+    if (det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world > 1)
+        return fail(r, ORX_ERR_STATE, "sharded PPM runs through the phase API");
+    if (det->method != ORX_METHOD_PATH_TRACING && det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
+        return fail(r, ORX_ERR_UNSUPPORTED, "oracle: method not implemented");
+    orx_status s0 = begin_iteration(r, local, det);
+    if (s0 != ORX_OK) return s0;
+    cam_t cam = camera_setup(&det->camera);
     if (det->method == ORX_METHOD_PATH_TRACING) {
         pt_pass(r, &cam, local);
-    } else if (det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING) {
+    } else {
         ppm_eye_pass(r, &cam);
         const float ppmRadiusSquared = ppmRadius * ppmRadius;
         ppm_photon_pass(r);
@@ -1175,21 +1230,79 @@ orx_status orc_render_next_iteration(orc_renderer* r, uint64_t iter, uint64_t lo
         ppm_gather(r, ppmRadius, ppmRadiusSquared, emittedF);
         ppm_direct(r);
         ppm_output(r, local);
-    } else {
-        return fail(r, ORX_ERR_UNSUPPORTED, "oracle: VCM not implemented yet");
     }
     return ORX_OK;
 }
 
+/* ---- sharded phase API (mirrors orx_ppm_* in include/orx.h) ---- */
+orx_status orc_set_shard(orc_renderer* r, uint32_t rank, uint32_t world) {
+    if (!r || world == 0 || rank >= world) return ORX_ERR_INVALID_ARGUMENT;
+    r->rank = rank;
+    r->world = world;
+    r->rng_ready = 0;
+    return ORX_OK;
+}
+uint32_t orc_max_local_rows(const orc_renderer* r) { return (r->H + r->world - 1) / r->world; }
+uint32_t orc_local_rows(const orc_renderer* r) { return r->rows; }
+size_t orc_hitpoint_export_bytes(const orc_renderer* r) { return (size_t)orc_max_local_rows(r) * r->W * 40; }
+
+orx_status orc_ppm_local_passes(orc_renderer* r, uint64_t iter, uint64_t local, float ppmRadius, const orx_request* det) {
+    (void)iter;
+    if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
+    orx_status s0 = begin_iteration(r, local, det);
+    if (s0 != ORX_OK) return s0;
+    cam_t cam = camera_setup(&det->camera);
+    ppm_eye_pass(r, &cam);
+    ppm_photon_pass(r);
+    orx_status s = ppm_build_grid(r);
+    if (s != ORX_OK) return s;
+    r->last_radius = ppmRadius;
+    r->last_radius2 = ppmRadius * ppmRadius;
+    r->last_local = local;
+    return ORX_OK;
+}
+orx_status orc_export_hitpoints(orc_renderer* r, void* dst, size_t bytes) {
+    const size_t plane = (size_t)r->max_rows * r->W;
+    if (!dst || bytes < plane * 40) return ORX_ERR_INVALID_ARGUMENT;
+    float* b = (float*)dst;
+    memset(b, 0, plane * 40);
+    for (size_t i = 0; i < (size_t)r->rows * r->W; i++) {
+        const hitpoint_t* h = &r->hp[i];
+        float* A = b + 4 * i;
+        float* B = b + 4 * plane + 4 * i;
+        float* Cc = b + 8 * plane + 2 * i;
+        A[0] = h->position.x; A[1] = h->position.y; A[2] = h->position.z;
+        memcpy(&A[3], &h->flags, 4);
+        v3 nr = (h->flags & PRD_HIT_NON_SPECULAR) ? h->normal : h->radiance;
+        B[0] = nr.x; B[1] = nr.y; B[2] = nr.z; B[3] = h->attenuation.x;
+        Cc[0] = h->attenuation.y; Cc[1] = h->attenuation.z;
+    }
+    return ORX_OK;
+}
+orx_status orc_ppm_gather_external(orc_renderer* r, const void* hp, uint32_t segments, void* indirect, size_t bytes) {
+    if (!hp || !indirect || bytes < (size_t)segments * r->max_rows * r->W * 12) return ORX_ERR_INVALID_ARGUMENT;
+    hp_src src = {NULL, (const float*)hp, r->max_rows};
+    float emittedF = (float)(r->cfg.photon_launch_width * r->cfg.photon_launch_height);
+    ppm_gather_src(r, &src, segments * r->max_rows, (v3*)indirect, NULL, r->last_radius, r->last_radius2, emittedF);
+    return ORX_OK;
+}
+orx_status orc_ppm_finish(orc_renderer* r, const void* indirect, size_t bytes) {
+    if (!indirect || bytes < (size_t)r->max_rows * r->W * 12) return ORX_ERR_INVALID_ARGUMENT;
+    memcpy(r->indirect, indirect, (size_t)r->rows * r->W * 12);
+    ppm_direct(r);
+    ppm_output(r, r->last_local);
+    return ORX_OK;
+}
+
 orx_status orc_get_output(orc_renderer* r, float* dst, size_t bytes) {
-    size_t need = (size_t)r->W * r->H * 12;
+    size_t need = (size_t)r->W * r->rows * 12;
     if (!dst || bytes < need) return ORX_ERR_INVALID_ARGUMENT;
     memcpy(dst, r->output, need);
     return ORX_OK;
 }
 
 orx_status orc_read_buffer(orc_renderer* r, int32_t id, void* dst, size_t bytes, size_t* out_bytes) {
-    size_t npx = (size_t)r->W * r->H;
+    size_t npx = (size_t)r->W * r->rows;
     size_t need = 0;
     switch (id) {
     case ORX_BUF_RNG: need = (size_t)r->RW * r->RH * 24; break;

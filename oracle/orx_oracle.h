@@ -41,6 +41,16 @@ void orc_destroy(orc_renderer* r);
 void orc_set_threads(int n);
 void orc_default_config(orx_config* cfg);
 
+/* sharded phase API (see include/orx.h "Multi-GPU sharding") */
+orx_status orc_set_shard(orc_renderer* r, uint32_t rank, uint32_t world);
+uint32_t orc_local_rows(const orc_renderer* r);
+uint32_t orc_max_local_rows(const orc_renderer* r);
+size_t orc_hitpoint_export_bytes(const orc_renderer* r);
+orx_status orc_ppm_local_passes(orc_renderer* r, uint64_t iter, uint64_t local, float ppm_radius, const orx_request* det);
+orx_status orc_export_hitpoints(orc_renderer* r, void* dst, size_t bytes);
+orx_status orc_ppm_gather_external(orc_renderer* r, const void* hp, uint32_t segments, void* indirect, size_t bytes);
+orx_status orc_ppm_finish(orc_renderer* r, const void* indirect, size_t bytes);
+
 /* building blocks exposed for known-answer tests */
 void orc_xorwow_init(uint64_t seed, uint32_t state[6]);
 uint32_t orc_xorwow_next(uint32_t state[6]);

@@ -94,3 +94,48 @@ class OracleRenderer:
             self.close()
         except Exception:
             pass
+
+
+class OracleShard:
+    """CPU backend for oppositerenderer_amd.multigpu.ShardedPPM (gloo tests)."""
+
+    def __init__(self, renderer: OracleRenderer, torch):
+        self.r, self.torch = renderer, torch
+        lib = renderer.lib
+        for name, args, res in (
+            ("orc_set_shard", [C.c_void_p, C.c_uint32, C.c_uint32], C.c_int),
+            ("orc_ppm_local_passes", [C.c_void_p, C.c_uint64, C.c_uint64, C.c_float, C.c_void_p], C.c_int),
+            ("orc_export_hitpoints", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
+            ("orc_ppm_gather_external", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t], C.c_int),
+            ("orc_ppm_finish", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
+        ):
+            f = getattr(lib, name)
+            f.argtypes, f.restype = args, res
+        self.lib = lib
+
+    def set_shard(self, rank, world):
+        self.r._check(self.lib.orc_set_shard(self.r.h, rank, world))
+
+    def alloc(self, nfloat):
+        return self.torch.zeros(nfloat, dtype=self.torch.float32)
+
+    def local_passes(self, it, local_it, radius, request):
+        self.r.width, self.r.height = request.width, request.height
+        self.r._check(self.lib.orc_ppm_local_passes(self.r.h, it, local_it, radius, C.byref(request)))
+
+    def export_hitpoints(self, t):
+        self.r._check(self.lib.orc_export_hitpoints(self.r.h, C.c_void_p(t.data_ptr()), t.numel() * 4))
+
+    def gather_external(self, hp_all, segments, out):
+        self.r._check(self.lib.orc_ppm_gather_external(self.r.h, C.c_void_p(hp_all.data_ptr()), segments,
+                                                       C.c_void_p(out.data_ptr()), out.numel() * 4))
+
+    def finish(self, ind_local):
+        self.r._check(self.lib.orc_ppm_finish(self.r.h, C.c_void_p(ind_local.data_ptr()), ind_local.numel() * 4))
+
+    def output_local_tensor(self, max_rows):
+        t = self.alloc(max_rows * self.r.width * 3)
+        n = C.c_size_t()
+        self.r._check(self.lib.orc_read_buffer(self.r.h, 6, None, 0, C.byref(n)))
+        self.r._check(self.lib.orc_read_buffer(self.r.h, 6, C.c_void_p(t.data_ptr()), t.numel() * 4, C.byref(n)))
+        return t
