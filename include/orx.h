@@ -236,14 +236,21 @@ orx_status orx_reset_timing(orx_renderer* r);
 orx_status orx_set_shard(orx_renderer* r, uint32_t rank, uint32_t world);
 /* hipStream_t the renderer launches on (as void*). */
 void* orx_stream(orx_renderer* r);
-/* Launch on a caller-provided hipStream_t (e.g. torch's current stream); NULL restores the own stream. */
-orx_status orx_set_stream(orx_renderer* r, void* hip_stream);
+/* use_external != 0: launch everything on the caller's hipStream_t `hip_stream`
+ * (NULL = the legacy default stream), e.g. torch's current stream, so kernels
+ * and the caller's collectives are ordered; use_external == 0: own stream. */
+orx_status orx_set_stream(orx_renderer* r, void* hip_stream, int use_external);
 /* rows owned by this rank for the current resolution, and ceil(H/world) */
 uint32_t orx_local_rows(const orx_renderer* r);
 uint32_t orx_max_local_rows(const orx_renderer* r);
 size_t orx_hitpoint_export_bytes(const orx_renderer* r); /* max_local_rows * W * 40 */
 orx_status orx_ppm_local_passes(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
                                 float ppm_radius, const orx_request* details);
+/* the two halves of orx_ppm_local_passes, so that the hitpoint all-gather can
+ * overlap the photon pass: eye pass only / photon pass + grid only */
+orx_status orx_ppm_local_eye(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
+                             float ppm_radius, const orx_request* details);
+orx_status orx_ppm_local_photons(orx_renderer* r);
 orx_status orx_export_hitpoints(orx_renderer* r, void* dst_device, size_t dst_bytes);
 /* hitpoints_device: `segments` export buffers back to back; indirect_device:
  * segments * max_local_rows * W * 3 floats */

@@ -221,6 +221,7 @@ struct orx_renderer {
     uint32_t rows = 0, max_rows = 0, rng_rows = 0, prows = 0;
     bool rng_ready = false;
     hipStream_t ext_stream = nullptr; /* caller-provided stream (orx_set_stream) */
+    bool use_ext = false;
     DevBuf d_rng, d_hp, d_ind, d_dir, d_out, d_dbg;
     DevBuf d_slotA, d_slotB, d_slotC, d_vmask, d_sortA, d_sortB, d_sortC, d_keys, d_ranks;
     DevBuf d_hist, d_offsets, d_bbox, d_partials, d_grid;
@@ -550,15 +551,21 @@ static inline void ev_begin(orx_renderer* r, int p) {
         if (hipEventCreate(&e) != hipSuccess) return;
         v.push_back(e);
     }
-    hipEventRecord(v[2 * r->ev_n[p]], r->ext_stream ? r->ext_stream : r->stream);
+    hipEventRecord(v[2 * r->ev_n[p]], r->use_ext ? r->ext_stream : r->stream);
 }
 static inline void ev_end(orx_renderer* r, int p) {
     if (!r->timing || r->ev_n[p] >= EV_POOL || r->ev[p].size() < 2 * (size_t)r->ev_n[p] + 2) return;
-    hipEventRecord(r->ev[p][2 * r->ev_n[p] + 1], r->ext_stream ? r->ext_stream : r->stream);
+    hipEventRecord(r->ev[p][2 * r->ev_n[p] + 1], r->use_ext ? r->ext_stream : r->stream);
     r->ev_n[p]++;
 }
 
-static inline hipStream_t cur_stream(orx_renderer* r) { return r->ext_stream ? r->ext_stream : r->stream; }
+static orx_status sync_all(orx_renderer* r) {
+    HIPCHK(r, hipStreamSynchronize(r->stream));
+    if (r->use_ext) HIPCHK(r, hipStreamSynchronize(r->ext_stream));
+    return ORX_OK;
+}
+
+static inline hipStream_t cur_stream(orx_renderer* r) { return r->use_ext ? r->ext_stream : r->stream; }
 
 static Consts make_consts(orx_renderer* r, float ppm_radius, uint64_t local_iteration_number) {
     Consts c;
@@ -580,7 +587,7 @@ static orx_status begin_iteration(orx_renderer* r, uint64_t local_iteration_numb
     if (det->width != r->W || det->height != r->H || !r->rng_ready) {
         orx_status st = resize(r, det->width, det->height);
         if (st != ORX_OK) return st;
-        if (r->ext_stream) HIPCHK(r, hipStreamSynchronize(r->stream)); /* resize work ran on the own stream */
+        if (r->use_ext) HIPCHK(r, hipStreamSynchronize(r->stream)); /* resize work ran on the own stream */
     }
     r->timed_iterations++;
     if (local_iteration_number == 0)
@@ -600,11 +607,13 @@ static GatherIn local_gather_in(orx_renderer* r) {
     return gi;
 }
 
-static void ppm_local_passes(orx_renderer* r, const DevCamera& cam, const Consts& c) {
-    hipStream_t st = cur_stream(r);
+static void ppm_eye(orx_renderer* r, const DevCamera& cam, const Consts& c) {
     ev_begin(r, P_EYE);
-    launch_ppm_eye(st, r->scene, cam, r->px, c);
+    launch_ppm_eye(cur_stream(r), r->scene, cam, r->px, c);
     ev_end(r, P_EYE);
+}
+static void ppm_photons_grid(orx_renderer* r, const Consts& c) {
+    hipStream_t st = cur_stream(r);
     ev_begin(r, P_PHOTON);
     launch_ppm_photon(st, r->scene, r->px, r->pb, c);
     ev_end(r, P_PHOTON);
@@ -618,6 +627,10 @@ static void ppm_local_passes(orx_renderer* r, const DevCamera& cam, const Consts
     ev_begin(r, P_SCATTER);
     launch_grid_scatter(st, r->pb);
     ev_end(r, P_SCATTER);
+}
+static void ppm_local_passes(orx_renderer* r, const DevCamera& cam, const Consts& c) {
+    ppm_eye(r, cam, c);
+    ppm_photons_grid(r, c);
 }
 
 orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
@@ -670,6 +683,32 @@ orx_status orx_ppm_local_passes(orx_renderer* r, uint64_t iteration_number, uint
     return ORX_OK;
 }
 
+orx_status orx_ppm_local_eye(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
+                             float ppm_radius, const orx_request* det) {
+    (void)iteration_number;
+    if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
+    if (det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
+        return set_err(r, ORX_ERR_INVALID_ARGUMENT, "orx_ppm_local_eye needs a PPM request");
+    orx_status s0 = begin_iteration(r, local_iteration_number, det);
+    if (s0 != ORX_OK) return s0;
+    DevCamera cam = camera_setup(det->camera);
+    Consts c = make_consts(r, ppm_radius, local_iteration_number);
+    ppm_eye(r, cam, c);
+    HIPCHK(r, hipGetLastError());
+    r->last_method = (uint64_t)det->method;
+    r->last_consts = c;
+    return ORX_OK;
+}
+
+orx_status orx_ppm_local_photons(orx_renderer* r) {
+    if (!r) return ORX_ERR_INVALID_ARGUMENT;
+    if (!r->rng_ready) return set_err(r, ORX_ERR_STATE, "orx_ppm_local_eye first");
+    HIPCHK(r, hipSetDevice(r->device));
+    ppm_photons_grid(r, r->last_consts);
+    HIPCHK(r, hipGetLastError());
+    return ORX_OK;
+}
+
 orx_status orx_export_hitpoints(orx_renderer* r, void* dst, size_t bytes) {
     if (!r || !dst) return ORX_ERR_INVALID_ARGUMENT;
     size_t need = (size_t)r->max_rows * r->W * 40;
@@ -714,11 +753,12 @@ orx_status orx_ppm_finish(orx_renderer* r, const void* indirect, size_t bytes) {
     return ORX_OK;
 }
 
-orx_status orx_set_stream(orx_renderer* r, void* stream) {
+orx_status orx_set_stream(orx_renderer* r, void* stream, int use_external) {
     if (!r) return ORX_ERR_INVALID_ARGUMENT;
     HIPCHK(r, hipSetDevice(r->device));
-    if (r->ext_stream && r->ext_stream != (hipStream_t)stream) HIPCHK(r, hipStreamSynchronize(r->ext_stream));
-    HIPCHK(r, hipStreamSynchronize(r->stream));
+    orx_status s0 = sync_all(r);
+    if (s0 != ORX_OK) return s0;
+    r->use_ext = use_external != 0;
     r->ext_stream = (hipStream_t)stream;
     return ORX_OK;
 }
@@ -726,12 +766,6 @@ uint32_t orx_local_rows(const orx_renderer* r) { return r ? r->rows : 0; }
 uint32_t orx_max_local_rows(const orx_renderer* r) { return r ? (r->H + r->world - 1) / r->world : 0; }
 size_t orx_hitpoint_export_bytes(const orx_renderer* r) {
     return r ? (size_t)((r->H + r->world - 1) / r->world) * r->W * 40 : 0;
-}
-
-static orx_status sync_all(orx_renderer* r) {
-    HIPCHK(r, hipStreamSynchronize(r->stream));
-    if (r->ext_stream) HIPCHK(r, hipStreamSynchronize(r->ext_stream));
-    return ORX_OK;
 }
 
 static orx_status check_grid_error(orx_renderer* r) {

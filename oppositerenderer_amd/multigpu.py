@@ -60,13 +60,22 @@ class ShardedPPM:
 
     def iteration(self, it, local_it, radius, request):
         d = self.dist
-        self.b.local_passes(it, local_it, radius, request)
-        self.b.export_hitpoints(self.hp_local)
-        if self.gloo:
-            parts = list(self.hp_all.chunk(self.world))
-            d.all_gather(parts, self.hp_local)
+        if self.gloo or not hasattr(self.b, "local_eye"):
+            self.b.local_passes(it, local_it, radius, request)
+            self.b.export_hitpoints(self.hp_local)
+            if self.gloo:
+                parts = list(self.hp_all.chunk(self.world))
+                d.all_gather(parts, self.hp_local)
+            else:
+                d.all_gather_into_tensor(self.hp_all, self.hp_local)
         else:
-            d.all_gather_into_tensor(self.hp_all, self.hp_local)
+            # eye pass, then the hitpoint all-gather on RCCL's stream overlaps
+            # the photon pass + grid build on the compute stream
+            self.b.local_eye(it, local_it, radius, request)
+            self.b.export_hitpoints(self.hp_local)
+            work = d.all_gather_into_tensor(self.hp_all, self.hp_local, async_op=True)
+            self.b.local_photons()
+            work.wait()
         self.b.gather_external(self.hp_all, self.world, self.ind_partial)
         if self.gloo:  # gloo has no reduce_scatter: all_reduce + own block
             d.all_reduce(self.ind_partial)
@@ -92,8 +101,10 @@ class DeviceShard:
         self.r, self.torch, self.device = renderer, torch, device
         lib = renderer._lib
         for name, args, res in (
-            ("orx_set_stream", [C.c_void_p, C.c_void_p], C.c_int),
+            ("orx_set_stream", [C.c_void_p, C.c_void_p, C.c_int], C.c_int),
             ("orx_ppm_local_passes", [C.c_void_p, C.c_uint64, C.c_uint64, C.c_float, C.c_void_p], C.c_int),
+            ("orx_ppm_local_eye", [C.c_void_p, C.c_uint64, C.c_uint64, C.c_float, C.c_void_p], C.c_int),
+            ("orx_ppm_local_photons", [C.c_void_p], C.c_int),
             ("orx_export_hitpoints", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
             ("orx_ppm_gather_external", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t], C.c_int),
             ("orx_ppm_finish", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
@@ -101,14 +112,26 @@ class DeviceShard:
             f = getattr(lib, name)
             f.argtypes, f.restype = args, res
         self.lib = lib
-        stream = torch.cuda.current_stream(device).cuda_stream
-        renderer._check(lib.orx_set_stream(renderer._h, C.c_void_p(stream)))
+        # one non-blocking stream shared by the renderer, torch ops and the
+        # RCCL collectives (which order themselves after torch's current stream)
+        cur = torch.cuda.current_stream(device)
+        if cur.cuda_stream == 0:
+            torch.cuda.set_stream(torch.cuda.Stream(device))
+            cur = torch.cuda.current_stream(device)
+        self.stream = cur
+        renderer._check(lib.orx_set_stream(renderer._h, C.c_void_p(cur.cuda_stream), 1))
 
     def alloc(self, nfloat):
         return self.torch.zeros(nfloat, dtype=self.torch.float32, device=self.device)
 
     def local_passes(self, it, local_it, radius, request):
         self.r._check(self.lib.orx_ppm_local_passes(self.r._h, it, local_it, radius, C.byref(request)))
+
+    def local_eye(self, it, local_it, radius, request):
+        self.r._check(self.lib.orx_ppm_local_eye(self.r._h, it, local_it, radius, C.byref(request)))
+
+    def local_photons(self):
+        self.r._check(self.lib.orx_ppm_local_photons(self.r._h))
 
     def export_hitpoints(self, t):
         self.r._check(self.lib.orx_export_hitpoints(self.r._h, C.c_void_p(t.data_ptr()), t.numel() * 4))
@@ -137,6 +160,9 @@ def bench_main(args, metric):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL prints its version banner on fd 1: keep stdout for the one JSON line
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     torch.cuda.set_device(local_rank)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     W, H, P = args.width, args.height, args.photon_launch
@@ -198,7 +224,7 @@ def bench_main(args, metric):
                          "bytes_per_launch": int(gbytes), "avg_launch_ms": round(gms, 4)},
             "passes_ms": {k: round(v, 4) for k, v in per_pass.items() if v > 0},
         }
-        print(json.dumps(out))
+        print(json.dumps(out), file=json_out, flush=True)
     r.destroy()
     dist.barrier()
     dist.destroy_process_group()
