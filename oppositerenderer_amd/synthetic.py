@@ -1,0 +1,144 @@
+"""Seeded synthetic "Sponza-class" scene (BASELINE configs[2]/[3] stand-in).
+
+The real Sponza / Conference .dae assets are unavailable (dead Dropbox link,
+README.md:15; assimp absent), so SURVEY.md 8(d) prescribes a procedurally
+tessellated hall: floor, ceiling and walls as triangle grids, two rows of
+smooth-shaded columns, arcades of boxes, Lambert materials, one quad area
+light registered once.  Geometry is generated deterministically from a numpy
+PCG64 stream seeded with 42; nothing is stored as data.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import scenes
+
+f32 = np.float32
+
+
+def _grid(origin, du, dv, nu, nv):
+    """Tessellated parallelogram: (nu x nv) quads -> 2*nu*nv triangles, face normal."""
+    o, du, dv = (np.asarray(a, np.float64) for a in (origin, du, dv))
+    u = np.linspace(0, 1, nu + 1)
+    v = np.linspace(0, 1, nv + 1)
+    uu, vv = np.meshgrid(u, v, indexing="ij")
+    verts = o + uu[..., None] * du + vv[..., None] * dv
+    verts = verts.reshape(-1, 3)
+    n = np.cross(du, dv)
+    n /= np.linalg.norm(n)
+    norms = np.broadcast_to(n, verts.shape)
+    idx = np.arange((nu + 1) * (nv + 1)).reshape(nu + 1, nv + 1)
+    a, b, c, d = idx[:-1, :-1], idx[1:, :-1], idx[1:, 1:], idx[:-1, 1:]
+    tris = np.concatenate([np.stack([a, b, c], -1).reshape(-1, 3), np.stack([a, c, d], -1).reshape(-1, 3)])
+    return verts, norms, tris
+
+
+def _cylinder(center, radius, height, nseg, nstack):
+    """Open cylinder along +y with outward smooth normals."""
+    th = np.linspace(0, 2 * np.pi, nseg + 1)[:-1]
+    y = np.linspace(0, height, nstack + 1)
+    tt, yy = np.meshgrid(th, y, indexing="ij")
+    x = center[0] + radius * np.cos(tt)
+    z = center[2] + radius * np.sin(tt)
+    verts = np.stack([x, center[1] + yy, z], -1).reshape(-1, 3)
+    norms = np.stack([np.cos(tt), np.zeros_like(tt), np.sin(tt)], -1).reshape(-1, 3)
+    idx = np.arange(nseg * (nstack + 1)).reshape(nseg, nstack + 1)
+    nxt = np.roll(idx, -1, axis=0)
+    a, b, c, d = idx[:, :-1], nxt[:, :-1], nxt[:, 1:], idx[:, 1:]
+    # winding so that the geometric normal cross(p0-p2, p1-p0) points outward
+    tris = np.concatenate([np.stack([a, c, b], -1).reshape(-1, 3), np.stack([a, d, c], -1).reshape(-1, 3)])
+    return verts, norms, tris
+
+
+def _box(lo, hi, n):
+    lo, hi = np.asarray(lo, float), np.asarray(hi, float)
+    e = hi - lo
+    parts = []
+    X, Y, Z = np.eye(3)
+    faces = [
+        (lo, Z * e[2], Y * e[1]),                       # x = lo, normal -x
+        (lo + X * e[0], Y * e[1], Z * e[2]),            # x = hi, normal +x
+        (lo, X * e[0], Z * e[2]),                       # y = lo, normal -y
+        (lo + Y * e[1], Z * e[2], X * e[0]),            # y = hi, normal +y
+        (lo, Y * e[1], X * e[0]),                       # z = lo, normal -z
+        (lo + Z * e[2], X * e[0], Y * e[1]),            # z = hi, normal +z
+    ]
+    for o, du, dv in faces:
+        parts.append(_grid(o, du, dv, n, n))
+    return parts
+
+
+def synthetic_hall(grid_n=64, column_seg=64, column_stack=56, box_n=8, seed=42, scale=1.0 / 3.0) -> scenes.Scene:
+    rng = np.random.default_rng(seed)
+    # Sponza-like proportions; `scale` puts the hall in Cornell-like units so that
+    # IScene::getSceneInitialPPMRadiusEstimate (A*3.94e-6, IScene.cpp:51-59),
+    # which grows with the scene's linear size, stays ~1.4 grid cells as in Cornell
+    S = scale
+    L, Wd, Hh = 3000.0 * S, 1300.0 * S, 1400.0 * S
+    sc = scenes.Scene("SyntheticHall")
+    mats = {
+        "floor": sc.add_material(scenes.Diffuse((0.55, 0.50, 0.45))),
+        "wall": sc.add_material(scenes.Diffuse((0.75, 0.70, 0.62))),
+        "ceiling": sc.add_material(scenes.Diffuse((0.8, 0.8, 0.8))),
+        "column": sc.add_material(scenes.Diffuse((0.7, 0.65, 0.55))),
+        "red": sc.add_material(scenes.Diffuse((0.7, 0.12, 0.10))),
+        "green": sc.add_material(scenes.Diffuse((0.15, 0.55, 0.18))),
+        "blue": sc.add_material(scenes.Diffuse((0.15, 0.2, 0.6))),
+    }
+    parts = []  # (verts, norms, tris, material)
+
+    def add(vnt, m):
+        parts.append((*vnt, m))
+
+    add(_grid((0, 0, 0), (0, 0, Wd), (L, 0, 0), grid_n, grid_n), mats["floor"])          # floor, +y
+    add(_grid((0, Hh, 0), (L, 0, 0), (0, 0, Wd), grid_n, grid_n), mats["ceiling"])       # ceiling, -y
+    add(_grid((0, 0, Wd), (0, Hh, 0), (L, 0, 0), grid_n, grid_n), mats["wall"])          # back (z=Wd), -z
+    add(_grid((0, 0, 0), (L, 0, 0), (0, Hh, 0), grid_n, grid_n), mats["wall"])           # front (z=0), +z
+    add(_grid((0, 0, 0), (0, Hh, 0), (0, 0, Wd), grid_n, grid_n), mats["green"])         # x=0, +x
+    add(_grid((L, 0, 0), (0, 0, Wd), (0, Hh, 0), grid_n, grid_n), mats["red"])           # x=L, -x
+    # two colonnades
+    ncol = 12
+    for row, zc in enumerate((Wd * 0.27, Wd * 0.73)):
+        for k in range(ncol):
+            xc = L * (k + 0.5) / ncol + rng.uniform(-8, 8) * S
+            r = (55.0 + rng.uniform(-5, 5)) * S
+            add(_cylinder((xc, 0.0, zc), r, 900.0 * S, column_seg, column_stack), mats["column"])
+            # capital + arcade beam segment as boxes
+            for lo, hi in (((xc - 80 * S, 900 * S, zc - 80 * S), (xc + 80 * S, 960 * S, zc + 80 * S)),):
+                for p in _box(lo, hi, box_n):
+                    add(p, mats["column"])
+        for k in range(ncol - 1):
+            x0 = L * (k + 0.5) / ncol + 80 * S
+            x1 = L * (k + 1.5) / ncol - 80 * S
+            for p in _box((x0, 1040 * S, zc - 60 * S), (x1, 1120 * S, zc + 60 * S), box_n):
+                add(p, mats["column"])
+    # a few coloured blocks on the floor
+    for _ in range(6):
+        x, z = rng.uniform(300 * S, L - 300 * S), rng.uniform(350 * S, Wd - 350 * S)
+        s = rng.uniform(60, 140) * S
+        m = mats[("red", "green", "blue")[rng.integers(0, 3)]]
+        for p in _box((x - s, 0, z - s), (x + s, 2 * s, z + s), box_n):
+            add(p, m)
+    verts, norms, tris, tmat = [], [], [], []
+    base = 0
+    for v, n, t, m in parts:
+        verts.append(v)
+        norms.append(n)
+        tris.append(t + base)
+        tmat.append(np.full(len(t), m, np.uint32))
+        base += len(v)
+    sc.set_mesh(np.concatenate(verts).astype(np.float32), np.concatenate(tris).astype(np.uint32),
+                np.concatenate(tmat), np.concatenate(norms).astype(np.float32))
+    # one quad area light under the ceiling, facing down, registered once
+    anchor = (L * 0.5 - 250.0 * S, Hh - 2.0 * S, Wd * 0.5 - 150.0 * S)
+    v1, v2 = (0.0, 0.0, 300.0 * S), (500.0 * S, 0.0, 0.0)   # cross(v1, v2) = -y
+    light = scenes.AreaLight((3.0e7, 2.8e7, 2.4e7), anchor, v1, v2)
+    sc.lights.append(light)
+    em = sc.add_material(scenes.DiffuseEmitter(light.power, 1.0, light.inverse_area))
+    sc.add_parallelogram(light.position, light.v1, light.v2, em)
+    sc.aabb_min = np.array([-5, -5, -5], np.float32)
+    sc.aabb_max = np.array([L + 5, Hh + 5, Wd + 5], np.float32)
+    sc.default_camera = scenes.Camera(np.array([150.0 * S, 600.0 * S, Wd * 0.5], np.float32),
+                                      np.array([L, 450.0 * S, Wd * 0.5], np.float32),
+                                      np.array([0.0, 1.0, 0.0], np.float32), 60.0, 45.0, 0.0)
+    return sc

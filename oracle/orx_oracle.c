@@ -217,6 +217,8 @@ struct orc_renderer {
     sphere_t* sph; uint32_t* smat;
     v3* verts; v3* vnorm; int has_normals;
     uint32_t* tris; uint32_t* tmat;
+    /* triangle BVH: node i = {lo[3], hi[3], left|first, right|count|leafbit} */
+    float* bvh_box; uint32_t* bvh_a; uint32_t* bvh_b; uint32_t* bvh_prims; uint32_t bvh_n;
     mat_t* mats;
     light_t* lights;
     v3 aabb_min, aabb_max;
@@ -266,6 +268,8 @@ orx_status orc_create(const orx_config* cfg, orc_renderer** out) {
 }
 
 static void free_scene(orc_renderer* r) {
+    free(r->bvh_box); free(r->bvh_a); free(r->bvh_b); free(r->bvh_prims);
+    r->bvh_box = NULL; r->bvh_a = NULL; r->bvh_b = NULL; r->bvh_prims = NULL; r->bvh_n = 0;
     free(r->quads); free(r->qmat); free(r->sph); free(r->smat);
     free(r->verts); free(r->vnorm); free(r->tris); free(r->tmat);
     free(r->mats); free(r->lights);
@@ -316,6 +320,84 @@ static light_t make_light(const orx_light* L) {
 /* Vector3::length with the reference's dot bug a.z*b.x (math/Vector3.cpp:27-30) */
 static float vector3_buggy_length(v3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.x); }
 
+/* ---- triangle BVH (median split on the widest centroid axis) ---- */
+typedef struct { float c; uint32_t i; } cent_t;
+static int cent_cmp(const void* a, const void* b) {
+    float x = ((const cent_t*)a)->c, y = ((const cent_t*)b)->c;
+    if (x < y) return -1;
+    if (x > y) return 1;
+    uint32_t i = ((const cent_t*)a)->i, j = ((const cent_t*)b)->i;
+    return i < j ? -1 : (i > j);
+}
+static uint32_t bvh_build(orc_renderer* r, const float* tlo, const float* thi, uint32_t first, uint32_t count,
+                          cent_t* scratch) {
+    uint32_t idx = r->bvh_n++;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t k = first; k < first + count; k++) {
+        uint32_t t = r->bvh_prims[k];
+        for (int a = 0; a < 3; a++) {
+            float l = tlo[3 * t + a], h = thi[3 * t + a], c = 0.5f * (l + h);
+            if (l < lo[a]) lo[a] = l;
+            if (h > hi[a]) hi[a] = h;
+            if (c < clo[a]) clo[a] = c;
+            if (c > chi[a]) chi[a] = c;
+        }
+    }
+    for (int a = 0; a < 3; a++) { /* conservative box */
+        float m = fmaxf(fabsf(lo[a]), fabsf(hi[a]));
+        float e = m * 2e-6f + 1e-20f;
+        r->bvh_box[6 * idx + a] = lo[a] - e;
+        r->bvh_box[6 * idx + 3 + a] = hi[a] + e;
+    }
+    if (count <= 4) {
+        r->bvh_a[idx] = first;
+        r->bvh_b[idx] = 0x80000000u | count;
+        return idx;
+    }
+    int ax = 0;
+    for (int a = 1; a < 3; a++)
+        if (chi[a] - clo[a] > chi[ax] - clo[ax]) ax = a;
+    for (uint32_t k = 0; k < count; k++) {
+        uint32_t t = r->bvh_prims[first + k];
+        scratch[k].c = 0.5f * (tlo[3 * t + ax] + thi[3 * t + ax]);
+        scratch[k].i = t;
+    }
+    qsort(scratch, count, sizeof(cent_t), cent_cmp);
+    for (uint32_t k = 0; k < count; k++) r->bvh_prims[first + k] = scratch[k].i;
+    uint32_t half = count / 2;
+    uint32_t l = bvh_build(r, tlo, thi, first, half, scratch);
+    uint32_t rr = bvh_build(r, tlo, thi, first + half, count - half, scratch);
+    r->bvh_a[idx] = l;
+    r->bvh_b[idx] = rr;
+    return idx;
+}
+static void build_tri_bvh(orc_renderer* r) {
+    uint32_t nt = r->nt;
+    float* tlo = (float*)malloc(12 * (size_t)nt);
+    float* thi = (float*)malloc(12 * (size_t)nt);
+    for (uint32_t t = 0; t < nt; t++) {
+        for (int a = 0; a < 3; a++) {
+            float v0 = (&r->verts[r->tris[3 * t]].x)[a], v1 = (&r->verts[r->tris[3 * t + 1]].x)[a],
+                  v2 = (&r->verts[r->tris[3 * t + 2]].x)[a];
+            tlo[3 * t + a] = fminf(fminf(v0, v1), v2);
+            thi[3 * t + a] = fmaxf(fmaxf(v0, v1), v2);
+        }
+    }
+    size_t cap = 2 * (size_t)nt + 1;
+    r->bvh_box = (float*)malloc(24 * cap);
+    r->bvh_a = (uint32_t*)malloc(4 * cap);
+    r->bvh_b = (uint32_t*)malloc(4 * cap);
+    r->bvh_prims = (uint32_t*)malloc(4 * (size_t)nt);
+    for (uint32_t t = 0; t < nt; t++) r->bvh_prims[t] = t;
+    cent_t* scratch = (cent_t*)malloc(sizeof(cent_t) * nt);
+    r->bvh_n = 0;
+    bvh_build(r, tlo, thi, 0, nt, scratch);
+    free(scratch);
+    free(tlo);
+    free(thi);
+}
+
 orx_status orc_init_scene(orc_renderer* r, const orx_scene* s) {
     if (!r || !s) return ORX_ERR_INVALID_ARGUMENT;
     if (s->n_lights == 0) return fail(r, ORX_ERR_NO_LIGHTS, "No lights exists in this scene.");
@@ -355,6 +437,7 @@ orx_status orc_init_scene(orc_renderer* r, const orx_scene* s) {
         memcpy(r->tris, s->triangles, 12 * (size_t)r->nt);
         memcpy(r->tmat, s->triangle_material, 4 * (size_t)r->nt);
     }
+    if (r->nt) build_tri_bvh(r);
     r->mats = (mat_t*)calloc(r->nm + 1, sizeof(mat_t));
     for (uint32_t i = 0; i < r->nm; i++) {
         const orx_material* m = &s->materials[i];
@@ -454,6 +537,15 @@ static inline int isect_tri(v3 p0, v3 p1, v3 p2, v3 o, v3 d, float tmin, float t
     return 0;
 }
 
+static inline int bvh_box_hit(const float* bx, v3 o, v3 inv, float tmin, float tmax) {
+    float tx0 = (bx[0] - o.x) * inv.x, tx1 = (bx[3] - o.x) * inv.x;
+    float ty0 = (bx[1] - o.y) * inv.y, ty1 = (bx[4] - o.y) * inv.y;
+    float tz0 = (bx[2] - o.z) * inv.z, tz1 = (bx[5] - o.z) * inv.z;
+    float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+    float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    return t0 <= t1;
+}
+
 /* closest hit; equal t -> lowest primitive id (NoAccel child order, Cornell.cpp:183-189) */
 static int trace_closest(const orc_renderer* r, v3 o, v3 d, float tmin, float tmax, hit_t* h) {
     float best = tmax;
@@ -468,11 +560,36 @@ static int trace_closest(const orc_renderer* r, v3 o, v3 d, float tmin, float tm
     }
     float tb = 0, tg = 0;
     v3 tn = mk1(0);
-    for (uint32_t i = 0; i < r->nt; i++) {
-        const uint32_t* ix = r->tris + 3 * (size_t)i;
-        v3 n; float b, g;
-        if (isect_tri(r->verts[ix[0]], r->verts[ix[1]], r->verts[ix[2]], o, d, tmin, best, &t, &n, &b, &g)) {
-            best = t; bp = (int32_t)(r->nq + r->ns + i); tn = n; tb = b; tg = g;
+    if (r->nt) {
+        const uint32_t base = r->nq + r->ns;
+        v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        uint32_t stack[64];
+        int sp = 0;
+        uint32_t node = 0;
+        for (;;) {
+            const float* bx = r->bvh_box + 6 * node;
+            if (bvh_box_hit(bx, o, inv, tmin, best)) {
+                if (r->bvh_b[node] & 0x80000000u) {
+                    uint32_t first = r->bvh_a[node], cnt = r->bvh_b[node] & 0x7fffffffu;
+                    for (uint32_t k = 0; k < cnt; k++) {
+                        uint32_t i = r->bvh_prims[first + k];
+                        const uint32_t* ix = r->tris + 3 * (size_t)i;
+                        v3 n; float b, g;
+                        /* closest t; equal t -> lower primitive id (brute-force order) */
+                        float lim = bp >= 0 ? nextafterf(best, INFINITY) : best;
+                        if (isect_tri(r->verts[ix[0]], r->verts[ix[1]], r->verts[ix[2]], o, d, tmin, lim, &t, &n, &b, &g) &&
+                            (t < best || (int32_t)(base + i) < bp)) {
+                            best = t; bp = (int32_t)(base + i); tn = n; tb = b; tg = g;
+                        }
+                    }
+                } else {
+                    stack[sp++] = r->bvh_b[node];
+                    node = r->bvh_a[node];
+                    continue;
+                }
+            }
+            if (sp == 0) break;
+            node = stack[--sp];
         }
     }
     if (bp < 0) return 0;
@@ -511,10 +628,31 @@ static int trace_any(const orc_renderer* r, v3 o, v3 d, float tmin, float tmax) 
         v3 n;
         if (isect_sphere(&r->sph[i], o, d, tmin, tmax, &t, &n)) return 1;
     }
-    for (uint32_t i = 0; i < r->nt; i++) {
-        const uint32_t* ix = r->tris + 3 * (size_t)i;
-        v3 n; float b, g;
-        if (isect_tri(r->verts[ix[0]], r->verts[ix[1]], r->verts[ix[2]], o, d, tmin, tmax, &t, &n, &b, &g)) return 1;
+    if (r->nt) {
+        v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        uint32_t stack[64];
+        int sp = 0;
+        uint32_t node = 0;
+        for (;;) {
+            const float* bx = r->bvh_box + 6 * node;
+            if (bvh_box_hit(bx, o, inv, tmin, tmax)) {
+                if (r->bvh_b[node] & 0x80000000u) {
+                    uint32_t first = r->bvh_a[node], cnt = r->bvh_b[node] & 0x7fffffffu;
+                    for (uint32_t k = 0; k < cnt; k++) {
+                        const uint32_t* ix = r->tris + 3 * (size_t)r->bvh_prims[first + k];
+                        v3 n; float b, g;
+                        if (isect_tri(r->verts[ix[0]], r->verts[ix[1]], r->verts[ix[2]], o, d, tmin, tmax, &t, &n, &b, &g))
+                            return 1;
+                    }
+                } else {
+                    stack[sp++] = r->bvh_b[node];
+                    node = r->bvh_a[node];
+                    continue;
+                }
+            }
+            if (sp == 0) break;
+            node = stack[--sp];
+        }
     }
     return 0;
 }
