@@ -131,8 +131,8 @@ def synthetic_hall(grid_n=64, column_seg=64, column_stack=56, box_n=8, seed=42, 
                 np.concatenate(tmat), np.concatenate(norms).astype(np.float32))
     # one quad area light under the ceiling, facing down, registered once
     anchor = (L * 0.5 - 250.0 * S, Hh - 2.0 * S, Wd * 0.5 - 150.0 * S)
-    v1, v2 = (0.0, 0.0, 300.0 * S), (500.0 * S, 0.0, 0.0)   # cross(v1, v2) = -y
-    light = scenes.AreaLight((3.0e7, 2.8e7, 2.4e7), anchor, v1, v2)
+    v1, v2 = (500.0 * S, 0.0, 0.0), (0.0, 0.0, 300.0 * S)   # Light normal = normalize(cross(v1, v2)) = -y
+    light = scenes.AreaLight((3.0e5, 2.8e5, 2.4e5), anchor, v1, v2)
     sc.lights.append(light)
     em = sc.add_material(scenes.DiffuseEmitter(light.power, 1.0, light.inverse_area))
     sc.add_parallelogram(light.position, light.v1, light.v2, em)
