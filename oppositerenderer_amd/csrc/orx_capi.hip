@@ -68,7 +68,14 @@ struct BvhBuilder {
         float dx = std::max(0.f, hi[0] - lo[0]), dy = std::max(0.f, hi[1] - lo[1]), dz = std::max(0.f, hi[2] - lo[2]);
         return dx * dy + dy * dz + dz * dx;
     }
-    uint32_t build(uint32_t first, uint32_t count) {
+    uint32_t max_depth = 0;
+    static uint32_t ceil_log2(uint32_t v) {
+        uint32_t l = 0;
+        while ((1u << l) < v) l++;
+        return l;
+    }
+    uint32_t build(uint32_t first, uint32_t count, uint32_t depth = 0) {
+        if (depth > max_depth) max_depth = depth;
         uint32_t idx = (uint32_t)nodes.size();
         nodes.push_back(DevBvhNode{});
         float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -91,11 +98,13 @@ struct BvhBuilder {
             nodes[idx].count_or_right = 0x80000000u | count;
             return idx;
         }
-        /* binned SAH on the centroid extent */
+        /* binned SAH on the centroid extent; object-median split once the
+         * depth budget (ORX_BVH_STACK) would otherwise be at risk */
         const int NB = 16;
         int best_axis = -1, best_split = 0;
         float best_cost = INFINITY;
-        for (int ax = 0; ax < 3; ax++) {
+        const bool median = depth + ceil_log2((count + 3) / 4) + 2 >= ORX_BVH_STACK;
+        for (int ax = 0; ax < 3 && !median; ax++) {
             float ext = chi[ax] - clo[ax];
             if (!(ext > 0)) continue;
             uint32_t cnt[NB] = {0};
@@ -132,7 +141,13 @@ struct BvhBuilder {
         }
         uint32_t mid;
         if (best_axis < 0) {
+            /* object median along the widest centroid axis */
+            int ax = 0;
+            for (int a = 1; a < 3; a++)
+                if (chi[a] - clo[a] > chi[ax] - clo[ax]) ax = a;
             mid = first + count / 2;
+            std::nth_element(prims.begin() + first, prims.begin() + mid, prims.begin() + first + count,
+                             [&](uint32_t p, uint32_t q) { return (*tris)[p].c[ax] < (*tris)[q].c[ax]; });
         } else {
             float ext = chi[best_axis] - clo[best_axis];
             auto it = std::partition(prims.begin() + first, prims.begin() + first + count, [&](uint32_t p) {
@@ -143,8 +158,8 @@ struct BvhBuilder {
             mid = (uint32_t)(it - prims.begin());
             if (mid == first || mid == first + count) mid = first + count / 2;
         }
-        uint32_t l = build(first, mid - first);
-        uint32_t r = build(mid, first + count - mid);
+        uint32_t l = build(first, mid - first, depth + 1);
+        uint32_t r = build(mid, first + count - mid, depth + 1);
         nodes[idx].left_or_first = l;
         nodes[idx].count_or_right = r;
         return idx;
@@ -371,21 +386,14 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     }
     std::vector<DevLight> lights(s->n_lights);
     for (uint32_t i = 0; i < s->n_lights; i++) lights[i] = make_light(s->lights[i]);
-    /* triangles: per-triangle vertex triplets (float4) + BVH */
-    std::vector<float4> tv((size_t)nt * 3), tn;
-    if (s->normals) tn.resize((size_t)nt * 3);
+    /* triangles: BVH over triangle boxes, then vertex / normal / material
+     * arrays rewritten in leaf order (tri_v[3k].w carries the original id) */
     std::vector<BuildTri> bt(nt);
     for (uint32_t i = 0; i < nt; i++) {
         BuildTri& b = bt[i];
         for (int k = 0; k < 3; k++) b.lo[k] = INFINITY, b.hi[k] = -INFINITY;
         for (int v = 0; v < 3; v++) {
-            uint32_t vi = s->triangles[3 * (size_t)i + v];
-            const float* p = s->vertices + 3 * (size_t)vi;
-            tv[3 * (size_t)i + v] = make_float4(p[0], p[1], p[2], 0.f);
-            if (s->normals) {
-                const float* n = s->normals + 3 * (size_t)vi;
-                tn[3 * (size_t)i + v] = make_float4(n[0], n[1], n[2], 0.f);
-            }
+            const float* p = s->vertices + 3 * (size_t)s->triangles[3 * (size_t)i + v];
             for (int k = 0; k < 3; k++) {
                 b.lo[k] = std::min(b.lo[k], p[k]);
                 b.hi[k] = std::max(b.hi[k], p[k]);
@@ -400,6 +408,26 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
         for (uint32_t i = 0; i < nt; i++) bb.prims[i] = i;
         bb.nodes.reserve(2 * (size_t)nt / 2 + 1);
         bb.build(0, nt);
+        if (bb.max_depth >= ORX_BVH_STACK)
+            return set_err(r, ORX_ERR_INVALID_ARGUMENT, "BVH deeper than the traversal stack");
+    }
+    std::vector<float4> tv((size_t)nt * 3), tn;
+    std::vector<uint32_t> tmat_leaf(nt);
+    if (s->normals) tn.resize((size_t)nt * 3);
+    for (uint32_t k = 0; k < nt; k++) {
+        const uint32_t i = bb.prims[k];
+        tmat_leaf[k] = s->triangle_material[i];
+        for (int v = 0; v < 3; v++) {
+            uint32_t vi = s->triangles[3 * (size_t)i + v];
+            const float* p = s->vertices + 3 * (size_t)vi;
+            float w = 0.f;
+            if (v == 0) std::memcpy(&w, &i, 4);
+            tv[3 * (size_t)k + v] = make_float4(p[0], p[1], p[2], w);
+            if (s->normals) {
+                const float* n = s->normals + 3 * (size_t)vi;
+                tn[3 * (size_t)k + v] = make_float4(n[0], n[1], n[2], 0.f);
+            }
+        }
     }
     auto up = [&](DevBuf& b, const void* src, size_t bytes) -> hipError_t {
         hipError_t e = b.ensure(bytes);
@@ -413,11 +441,10 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     HIPCHK(r, up(r->d_smat, s->spheres ? s->sphere_material : nullptr, (size_t)ns * 4));
     HIPCHK(r, up(r->d_triv, tv.data(), tv.size() * sizeof(float4)));
     HIPCHK(r, up(r->d_trin, tn.data(), tn.size() * sizeof(float4)));
-    HIPCHK(r, up(r->d_tmat, s->triangle_material, (size_t)nt * 4));
+    HIPCHK(r, up(r->d_tmat, tmat_leaf.data(), (size_t)nt * 4));
     HIPCHK(r, up(r->d_mats, mats.data(), mats.size() * sizeof(DevMaterial)));
     HIPCHK(r, up(r->d_lights, lights.data(), lights.size() * sizeof(DevLight)));
     HIPCHK(r, up(r->d_bvh, bb.nodes.data(), bb.nodes.size() * sizeof(DevBvhNode)));
-    HIPCHK(r, up(r->d_bvhprims, bb.prims.data(), bb.prims.size() * 4));
     DevScene& S = r->scene;
     S.nq = nq;
     S.ns = ns;
@@ -433,7 +460,6 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     S.lights = r->d_lights.as<DevLight>();
     S.nl = s->n_lights;
     S.bvh = r->d_bvh.as<DevBvhNode>();
-    S.bvh_prims = r->d_bvhprims.as<uint32_t>();
     S.bvh_nodes = (uint32_t)bb.nodes.size();
     /* AAB::getBoundingSphere (math/AAB.cpp:26-33) with Vector3::length's
      * dot bug a.z*b.x (math/Vector3.cpp:27-30) */

@@ -233,25 +233,33 @@ struct DevScene {
     const uint32_t* qmat;
     const DevSphere* spheres;
     const uint32_t* smat;
-    const float4* tri_v;       /* [nt][3] vertex positions (xyz, w unused) */
-    const float4* tri_n;       /* [nt][3] vertex normals or NULL */
-    const uint32_t* tmat;
+    /* triangles in BVH leaf order: tri_v[3k] = {p0.xyz, original triangle id bits},
+     * tri_v[3k+1] = p1, tri_v[3k+2] = p2 (48 B per triangle, no index indirection) */
+    const float4* tri_v;
+    const float4* tri_n;       /* [nt][3] vertex normals in leaf order, or NULL */
+    const uint32_t* tmat;      /* leaf order */
     const DevMaterial* mats;
     const DevLight* lights;
     uint32_t nl;
     /* bounding sphere (AAB::getBoundingSphere with Vector3::length bug) */
     float bs_cx, bs_cy, bs_cz, bs_r;
-    /* triangle BVH (nt > 0) */
+    /* triangle BVH (nt > 0), depth <= ORX_BVH_STACK */
     const DevBvhNode* bvh;
-    const uint32_t* bvh_prims;
     uint32_t bvh_nodes;
 };
 
+/* Traversal stack: per-lane column of an LDS array [ORX_BVH_STACK][64] owned
+ * by a 64-thread (one-wave) block; entry k of a lane at s[k * 64]. */
+#define ORX_BVH_STACK 32
+#define ORX_STACK_DECL __shared__ uint32_t orx_stack_lds[ORX_BVH_STACK * 64]
+#define ORX_STACK_PTR (&orx_stack_lds[threadIdx.x & 63])
+
 struct Hit {
     float t;
-    int32_t prim; /* global id: quads, spheres, triangles */
-    float b, g;   /* triangle barycentrics */
-    f3 sn;        /* sphere normal attribute */
+    int32_t prim;  /* global id: quads, spheres, triangles (original triangle order) */
+    uint32_t slot; /* triangles: index in leaf order */
+    float b, g;    /* triangle barycentrics */
+    f3 sn;         /* sphere normal attribute */
 };
 
 /* parallelogram.cu:49-76 */
@@ -331,10 +339,14 @@ __device__ __forceinline__ bool box_hit(const DevBvhNode& n, f3 o, f3 inv, float
 
 /* Closest hit over all primitives; equal t resolves to the lowest global
  * primitive id, which is OptiX NoAccel's child order (Cornell.cpp:183-189)
- * and is independent of traversal order, so BVH and brute force agree. */
-__device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& h) {
+ * and is independent of traversal order, so BVH and brute force agree.
+ * Triangles: near-first BVH traversal, children tested at the parent, the
+ * far child pushed on the lane's LDS stack and re-tested against the
+ * (possibly shrunk) closest distance when popped. */
+__device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& h, uint32_t* stk) {
     float best = tmax;
     int32_t bp = -1;
+    uint32_t bslot = 0;
     float t;
     for (uint32_t i = 0; i < S.nq; i++) {
         if (isect_quad(S.quads[i], o, d, tmin, best, t)) {
@@ -354,43 +366,58 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
     float bb = 0, bg = 0;
     if (S.nt) {
         const uint32_t base = S.nq + S.ns;
-        f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-        uint32_t stack[64];
+        const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
         int sp = 0;
         uint32_t node = 0;
-        for (;;) {
+        float te;
+        bool have = box_hit(S.bvh[0], o, inv, tmin, best, te);
+        while (have) {
             const DevBvhNode n = S.bvh[node];
-            float te;
-            bool visit = box_hit(n, o, inv, tmin, best, te);
-            if (visit && (n.count_or_right & 0x80000000u)) {
-                uint32_t first = n.left_or_first, cnt = n.count_or_right & 0x7fffffffu;
-                for (uint32_t k = 0; k < cnt; k++) {
-                    uint32_t ti = S.bvh_prims[first + k];
+            have = false;
+            if (n.count_or_right & 0x80000000u) {
+                const uint32_t first = n.left_or_first, cnt = n.count_or_right & 0x7fffffffu;
+                for (uint32_t k = first; k < first + cnt; k++) {
+                    const float4 v0 = S.tri_v[3 * k], v1 = S.tri_v[3 * k + 1], v2 = S.tri_v[3 * k + 2];
+                    const int32_t gid = (int32_t)(base + __float_as_uint(v0.w));
                     float b, g;
-                    f3 p0 = ld_f3(S.tri_v[3 * ti]), p1 = ld_f3(S.tri_v[3 * ti + 1]), p2 = ld_f3(S.tri_v[3 * ti + 2]);
                     /* accept t < best, or t == best from a lower primitive id */
                     float lim = bp >= 0 ? orx_as_float(orx_as_uint(best) + 1u) : best;
-                    if (isect_tri(p0, p1, p2, o, d, tmin, lim, t, b, g) && (t < best || (int32_t)(base + ti) < bp)) {
+                    if (isect_tri(ld_f3(v0), ld_f3(v1), ld_f3(v2), o, d, tmin, lim, t, b, g) &&
+                        (t < best || gid < bp)) {
                         best = t;
-                        bp = (int32_t)(base + ti);
+                        bp = gid;
+                        bslot = k;
                         bb = b;
                         bg = g;
                     }
                 }
-                if (sp == 0) break;
-                node = stack[--sp];
-            } else if (visit) {
-                stack[sp++] = n.count_or_right;
-                node = n.left_or_first;
             } else {
-                if (sp == 0) break;
-                node = stack[--sp];
+                const DevBvhNode L = S.bvh[n.left_or_first], R = S.bvh[n.count_or_right];
+                float tl, tr;
+                const bool hl = box_hit(L, o, inv, tmin, best, tl);
+                const bool hr = box_hit(R, o, inv, tmin, best, tr);
+                if (hl && hr) {
+                    const bool lf = tl <= tr;
+                    stk[sp * 64] = lf ? n.count_or_right : n.left_or_first;
+                    sp++;
+                    node = lf ? n.left_or_first : n.count_or_right;
+                    have = true;
+                } else if (hl || hr) {
+                    node = hl ? n.left_or_first : n.count_or_right;
+                    have = true;
+                }
+            }
+            while (!have && sp > 0) {
+                sp--;
+                node = stk[sp * 64];
+                have = box_hit(S.bvh[node], o, inv, tmin, best, te);
             }
         }
     }
     if (bp < 0) return false;
     h.t = best;
     h.prim = bp;
+    h.slot = bslot;
     h.b = bb;
     h.g = bg;
     h.sn = sn;
@@ -398,7 +425,7 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
 }
 /* any hit in (tmin,tmax): every material's RayType::SHADOW any-hit is
  * gatherAnyHitOnNonEmitter (Material.cpp:18-26, DirectRadianceEstimation.cu:79-83) */
-__device__ inline bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, float tmax) {
+__device__ inline bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, float tmax, uint32_t* stk) {
     float t;
     for (uint32_t i = 0; i < S.nq; i++)
         if (isect_quad(S.quads[i], o, d, tmin, tmax, t)) return true;
@@ -407,41 +434,51 @@ __device__ inline bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, floa
         if (isect_sphere(S.spheres[i], o, d, tmin, tmax, t, n)) return true;
     }
     if (S.nt) {
-        f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-        uint32_t stack[64];
+        const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
         int sp = 0;
         uint32_t node = 0;
-        for (;;) {
+        float te;
+        bool have = box_hit(S.bvh[0], o, inv, tmin, tmax, te);
+        while (have) {
             const DevBvhNode n = S.bvh[node];
-            float te;
-            bool visit = box_hit(n, o, inv, tmin, tmax, te);
-            if (visit && (n.count_or_right & 0x80000000u)) {
-                uint32_t first = n.left_or_first, cnt = n.count_or_right & 0x7fffffffu;
-                for (uint32_t k = 0; k < cnt; k++) {
-                    uint32_t ti = S.bvh_prims[first + k];
+            have = false;
+            if (n.count_or_right & 0x80000000u) {
+                const uint32_t first = n.left_or_first, cnt = n.count_or_right & 0x7fffffffu;
+                for (uint32_t k = first; k < first + cnt; k++) {
                     float b, g;
-                    if (isect_tri(ld_f3(S.tri_v[3 * ti]), ld_f3(S.tri_v[3 * ti + 1]), ld_f3(S.tri_v[3 * ti + 2]), o, d,
+                    if (isect_tri(ld_f3(S.tri_v[3 * k]), ld_f3(S.tri_v[3 * k + 1]), ld_f3(S.tri_v[3 * k + 2]), o, d,
                                   tmin, tmax, t, b, g))
                         return true;
                 }
-                if (sp == 0) break;
-                node = stack[--sp];
-            } else if (visit) {
-                stack[sp++] = n.count_or_right;
-                node = n.left_or_first;
             } else {
-                if (sp == 0) break;
-                node = stack[--sp];
+                const DevBvhNode L = S.bvh[n.left_or_first], R = S.bvh[n.count_or_right];
+                float tl, tr;
+                const bool hl = box_hit(L, o, inv, tmin, tmax, tl);
+                const bool hr = box_hit(R, o, inv, tmin, tmax, tr);
+                if (hl && hr) {
+                    stk[sp * 64] = n.count_or_right;
+                    sp++;
+                    node = n.left_or_first;
+                    have = true;
+                } else if (hl || hr) {
+                    node = hl ? n.left_or_first : n.count_or_right;
+                    have = true;
+                }
+            }
+            if (!have && sp > 0) {
+                sp--;
+                node = stk[sp * 64];
+                have = true; /* box already known to overlap [tmin, tmax] */
             }
         }
     }
     return false;
 }
 
-__device__ __forceinline__ uint32_t prim_material(const DevScene& S, int32_t p) {
-    if ((uint32_t)p < S.nq) return S.qmat[p];
-    if ((uint32_t)p < S.nq + S.ns) return S.smat[p - S.nq];
-    return S.tmat[p - S.nq - S.ns];
+__device__ __forceinline__ uint32_t prim_material(const DevScene& S, const Hit& h) {
+    if ((uint32_t)h.prim < S.nq) return S.qmat[h.prim];
+    if ((uint32_t)h.prim < S.nq + S.ns) return S.smat[h.prim - S.nq];
+    return S.tmat[h.slot];
 }
 /* world shading normal as the closest-hit programs see it:
  * normalize(rtTransformNormal(shadingNormal)) with identity transforms. */
@@ -451,7 +488,7 @@ __device__ __forceinline__ f3 shading_normal(const DevScene& S, const Hit& h) {
         return normalize(mk(q.nx, q.ny, q.nz));
     }
     if ((uint32_t)h.prim < S.nq + S.ns) return normalize(h.sn);
-    uint32_t ti = (uint32_t)h.prim - S.nq - S.ns;
+    const uint32_t ti = h.slot;
     if (S.tri_n) {
         f3 n0 = ld_f3(S.tri_n[3 * ti]), n1 = ld_f3(S.tri_n[3 * ti + 1]), n2 = ld_f3(S.tri_n[3 * ti + 2]);
         return normalize(normalize(n1 * h.b + n2 * h.g + n0 * (1.0f - h.b - h.g)));
@@ -466,7 +503,7 @@ __device__ __forceinline__ f3 geometric_normal(const DevScene& S, const Hit& h) 
         return normalize(mk(q.nx, q.ny, q.nz));
     }
     if ((uint32_t)h.prim < S.nq + S.ns) return normalize(h.sn);
-    uint32_t ti = (uint32_t)h.prim - S.nq - S.ns;
+    const uint32_t ti = h.slot;
     f3 p0 = ld_f3(S.tri_v[3 * ti]), p1 = ld_f3(S.tri_v[3 * ti + 1]), p2 = ld_f3(S.tri_v[3 * ti + 2]);
     return normalize(normalize(cross(p0 - p2, p1 - p0)));
 }
@@ -533,16 +570,16 @@ __device__ __forceinline__ float glass_reflect_factor(f3 d, f3 N, float n1, floa
  * Glossy.cu:74-90, DiffuseEmitter.cu:40-51, Mirror.cu:50-63, Glass.cu:90-143,
  * miss RayGeneratorPPM.cu:72-77. */
 __device__ inline void trace_radiance(const DevScene& S, uint32_t maxd, f3 o, f3 d, float tmin, RadiancePRD& prd,
-                                      Rng& rs) {
+                                      Rng& rs, uint32_t* stk) {
     for (;;) {
         Hit h;
-        if (!trace_closest(S, o, d, tmin, RT_DEFAULT_MAX, h)) {
+        if (!trace_closest(S, o, d, tmin, RT_DEFAULT_MAX, h, stk)) {
             prd.flags = PRD_MISS;
             prd.attenuation = mk1(0.f);
             prd.radiance = mk1(0.f);
             return;
         }
-        const DevMaterial& m = S.mats[prim_material(S, h.prim)];
+        const DevMaterial& m = S.mats[prim_material(S, h)];
         f3 hitPoint = o + d * h.t;
         f3 N = shading_normal(S, h);
         if (m.type == MAT_DIFFUSE || m.type == MAT_GLOSSY) {
@@ -604,7 +641,8 @@ __device__ inline void trace_radiance(const DevScene& S, uint32_t maxd, f3 o, f3
 }
 
 /* getLightContribution (helpers/light.h:29-87) */
-__device__ inline f3 light_contribution(const DevScene& S, const DevLight& light, f3 pos, f3 normal, Rng& rs) {
+__device__ inline f3 light_contribution(const DevScene& S, const DevLight& light, f3 pos, f3 normal, Rng& rs,
+                                        uint32_t* stk) {
     float lightFactor = 1;
     f3 pointOnLight;
     if (light.type == LIGHT_AREA) {
@@ -625,7 +663,7 @@ __device__ inline f3 light_contribution(const DevScene& S, const DevLight& light
     if (light.type == LIGHT_AREA) lightFactor *= maxf(0, dot(-towardsLight, light.normal));
     if (lightFactor > 0.0f) {
         float tmax = (float)((double)lightDistance - 0.0001);
-        float att = trace_any(S, pos, towardsLight, 0.0001f, tmax) ? 0.0f : 1.0f;
+        float att = trace_any(S, pos, towardsLight, 0.0001f, tmax, stk) ? 0.0f : 1.0f;
         lightFactor *= att;
         return light.power * lightFactor;
     }

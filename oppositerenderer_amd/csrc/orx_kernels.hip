@@ -76,9 +76,10 @@ void launch_rng_init(hipStream_t s, RngPlanes rng, uint32_t RW, uint32_t rows, u
 /* ------------------------------------------------------------------ */
 /* PPM eye pass                                                        */
 /* ------------------------------------------------------------------ */
-__global__ __launch_bounds__(256) void k_ppm_eye(DevScene S, DevCamera cam, PixelBufs px, Consts c) {
-    uint32_t x = blockIdx.x * 16 + (threadIdx.x & 15);
-    uint32_t j = blockIdx.y * 16 + (threadIdx.x >> 4);
+__global__ __launch_bounds__(64) void k_ppm_eye(DevScene S, DevCamera cam, PixelBufs px, Consts c) {
+    ORX_STACK_DECL;
+    uint32_t x = blockIdx.x * 8 + (threadIdx.x & 7);
+    uint32_t j = blockIdx.y * 8 + (threadIdx.x >> 3);
     if (x >= px.W || j >= px.rows) return;
     uint32_t y = px.rank + px.world * j;
     size_t slot = (size_t)j * px.RW + x;
@@ -93,22 +94,22 @@ __global__ __launch_bounds__(256) void k_ppm_eye(DevScene S, DevCamera cam, Pixe
     prd.newdir = mk1(0.f);
     f3 o, d;
     primary_ray(cam, x, y, px.W, px.H, rs, o, d);
-    trace_radiance(S, c.max_radiance_depth, o, d, 0.001f, prd, rs);
+    trace_radiance(S, c.max_radiance_depth, o, d, 0.001f, prd, rs, ORX_STACK_PTR);
     store_hitpoint(px, (size_t)j * px.W + x, prd);
     rng_store(px.rng, slot, rs);
 }
 void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c) {
-    dim3 grid((px.W + 15) / 16, (px.rows + 15) / 16);
-    hipLaunchKernelGGL(k_ppm_eye, grid, dim3(256), 0, s, S, cam, px, c);
+    dim3 grid((px.W + 7) / 8, (px.rows + 7) / 8);
+    hipLaunchKernelGGL(k_ppm_eye, grid, dim3(64), 0, s, S, cam, px, c);
 }
 
 /* ------------------------------------------------------------------ */
 /* PPM photon pass (+ AABB of the valid deposits)                      */
 /* ------------------------------------------------------------------ */
-__global__ __launch_bounds__(256) void k_ppm_photon(DevScene S, PixelBufs px, PhotonBufs pb, Consts c) {
-    __shared__ float red[6][4];
-    const uint32_t x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const uint32_t j = blockIdx.y * 4 + (threadIdx.x >> 6);
+__global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, PhotonBufs pb, Consts c) {
+    ORX_STACK_DECL;
+    const uint32_t x = blockIdx.x * 64 + threadIdx.x;
+    const uint32_t j = blockIdx.y;
     float lo_x = INFINITY, lo_y = INFINITY, lo_z = INFINITY;
     float hi_x = -INFINITY, hi_y = -INFINITY, hi_z = -INFINITY;
     if (x < pb.PW && j < pb.prows) {
@@ -164,8 +165,8 @@ __global__ __launch_bounds__(256) void k_ppm_photon(DevScene S, PixelBufs px, Ph
         f3 o = origin, d = dir;
         for (;;) {
             Hit h;
-            if (!trace_closest(S, o, d, tmin, RT_DEFAULT_MAX, h)) break;
-            const DevMaterial& m = S.mats[prim_material(S, h.prim)];
+            if (!trace_closest(S, o, d, tmin, RT_DEFAULT_MAX, h, ORX_STACK_PTR)) break;
+            const DevMaterial& m = S.mats[prim_material(S, h)];
             f3 hitPoint = o + d * h.t;
             if (m.type == MAT_DIFFUSE || m.type == MAT_GLOSSY) {
                 f3 N = shading_normal(S, h);
@@ -233,29 +234,22 @@ __global__ __launch_bounds__(256) void k_ppm_photon(DevScene S, PixelBufs px, Ph
         pb.vmask[p_local] = (uint8_t)mask;
         rng_store(px.rng, slot, rs);
     }
-    /* block AABB -> device-wide ordered-int atomics */
+    /* wave AABB -> device-wide ordered-int atomics (one lane per component) */
     lo_x = wave_min(lo_x); lo_y = wave_min(lo_y); lo_z = wave_min(lo_z);
     hi_x = wave_max(hi_x); hi_y = wave_max(hi_y); hi_z = wave_max(hi_z);
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0) {
-        red[0][w] = lo_x; red[1][w] = lo_y; red[2][w] = lo_z;
-        red[3][w] = hi_x; red[4][w] = hi_y; red[5][w] = hi_z;
-    }
-    __syncthreads();
-    if (threadIdx.x < 6) {
-        int k = threadIdx.x;
-        float v = red[k][0];
-        for (int q = 1; q < 4; q++) v = k < 3 ? fminf(v, red[k][q]) : fmaxf(v, red[k][q]);
-        if (k < 3) {
-            if (v != INFINITY) atomicMin(&pb.bbox[k], f2ord(v));
+    const uint32_t lane = threadIdx.x;
+    if (lane < 6) {
+        float v = lane == 0 ? lo_x : lane == 1 ? lo_y : lane == 2 ? lo_z : lane == 3 ? hi_x : lane == 4 ? hi_y : hi_z;
+        if (lane < 3) {
+            if (v != INFINITY) atomicMin(&pb.bbox[lane], f2ord(v));
         } else {
-            if (v != -INFINITY) atomicMax(&pb.bbox[k], f2ord(v));
+            if (v != -INFINITY) atomicMax(&pb.bbox[lane], f2ord(v));
         }
     }
 }
 void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c) {
-    dim3 grid((pb.PW + 63) / 64, (pb.prows + 3) / 4);
-    hipLaunchKernelGGL(k_ppm_photon, grid, dim3(256), 0, s, S, px, pb, c);
+    dim3 grid((pb.PW + 63) / 64, pb.prows);
+    hipLaunchKernelGGL(k_ppm_photon, grid, dim3(64), 0, s, S, px, pb, c);
 }
 
 /* ------------------------------------------------------------------ */
@@ -712,9 +706,10 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
 /* ------------------------------------------------------------------ */
 /* direct radiance (4 shadow samples) + output accumulation            */
 /* ------------------------------------------------------------------ */
-__global__ __launch_bounds__(256) void k_ppm_direct_output(DevScene S, PixelBufs px, Consts c) {
-    const uint32_t x = blockIdx.x * 16 + (threadIdx.x & 15);
-    const uint32_t j = blockIdx.y * 16 + (threadIdx.x >> 4);
+__global__ __launch_bounds__(64) void k_ppm_direct_output(DevScene S, PixelBufs px, Consts c) {
+    ORX_STACK_DECL;
+    const uint32_t x = blockIdx.x * 8 + (threadIdx.x & 7);
+    const uint32_t j = blockIdx.y * 8 + (threadIdx.x >> 3);
     if (x >= px.W || j >= px.rows) return;
     const size_t i = (size_t)j * px.W + x;
     const float4 A = px.hpA[i];
@@ -739,7 +734,7 @@ __global__ __launch_bounds__(256) void k_ppm_direct_output(DevScene S, PixelBufs
             int li = (int)(sample * (float)numLights);
             int randomLightIndex = li < numLights - 1 ? li : numLights - 1;
             float scale = (float)numLights;
-            f3 lc = light_contribution(S, S.lights[randomLightIndex], pos, nrm, rs);
+            f3 lc = light_contribution(S, S.lights[randomLightIndex], pos, nrm, rs, ORX_STACK_PTR);
             avg = avg + lc * scale;
         }
         direct = (mk(B.w, Cc.x, Cc.y) * avg) / (float)4;
@@ -757,16 +752,17 @@ __global__ __launch_bounds__(256) void k_ppm_direct_output(DevScene S, PixelBufs
     px.output[3 * i + 2] = out.z;
 }
 void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c) {
-    dim3 grid((px.W + 15) / 16, (px.rows + 15) / 16);
-    hipLaunchKernelGGL(k_ppm_direct_output, grid, dim3(256), 0, s, S, px, c);
+    dim3 grid((px.W + 7) / 8, (px.rows + 7) / 8);
+    hipLaunchKernelGGL(k_ppm_direct_output, grid, dim3(64), 0, s, S, px, c);
 }
 
 /* ------------------------------------------------------------------ */
 /* path tracing                                                        */
 /* ------------------------------------------------------------------ */
-__global__ __launch_bounds__(256) void k_pt(DevScene S, DevCamera cam, PixelBufs px, Consts c) {
-    const uint32_t x = blockIdx.x * 16 + (threadIdx.x & 15);
-    const uint32_t j = blockIdx.y * 16 + (threadIdx.x >> 4);
+__global__ __launch_bounds__(64) void k_pt(DevScene S, DevCamera cam, PixelBufs px, Consts c) {
+    ORX_STACK_DECL;
+    const uint32_t x = blockIdx.x * 8 + (threadIdx.x & 7);
+    const uint32_t j = blockIdx.y * 8 + (threadIdx.x >> 3);
     if (x >= px.W || j >= px.rows) return;
     const uint32_t y = px.rank + px.world * j;
     const size_t i = (size_t)j * px.W + x;
@@ -789,7 +785,7 @@ __global__ __launch_bounds__(256) void k_pt(DevScene S, DevCamera cam, PixelBufs
     f3 fin = mk1(0);
     for (int it = 0; it < 5; it++) {
         prd.flags = PRD_PATH_TRACING;
-        trace_radiance(S, c.max_radiance_depth, o, d, 0.001f, prd, rs);
+        trace_radiance(S, c.max_radiance_depth, o, d, 0.001f, prd, rs, ORX_STACK_PTR);
         if (prd.flags & PRD_HIT_EMITTER) {
             if ((prd.flags & PRD_HIT_SPECULAR) || it == 0) fin = prd.radiance;
             break;
@@ -797,7 +793,7 @@ __global__ __launch_bounds__(256) void k_pt(DevScene S, DevCamera cam, PixelBufs
             f3 accum = mk1(0);
             int li = (int)(rnd(G) * (float)numLights);
             float scale = (float)numLights;
-            f3 lc = light_contribution(S, S.lights[li], prd.position, prd.normal, rs) * scale;
+            f3 lc = light_contribution(S, S.lights[li], prd.position, prd.normal, rs, ORX_STACK_PTR) * scale;
             accum = accum + lc;
             f3 direct = (prd.attenuation * accum) / (float)1;
             fin = fin + direct;
@@ -823,8 +819,8 @@ __global__ __launch_bounds__(256) void k_pt(DevScene S, DevCamera cam, PixelBufs
     rng_store(px.rng, slot, rs);
 }
 void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c) {
-    dim3 grid((px.W + 15) / 16, (px.rows + 15) / 16);
-    hipLaunchKernelGGL(k_pt, grid, dim3(256), 0, s, S, cam, px, c);
+    dim3 grid((px.W + 7) / 8, (px.rows + 7) / 8);
+    hipLaunchKernelGGL(k_pt, grid, dim3(64), 0, s, S, cam, px, c);
 }
 
 }  // namespace orx
