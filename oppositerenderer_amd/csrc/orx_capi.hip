@@ -509,7 +509,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_ranks.ensure(S * 4));
     HIPCHK(r, r->d_hist.ensure(G2 * 4));
     HIPCHK(r, r->d_offsets.ensure(G2 * 4));
-    HIPCHK(r, r->d_bbox.ensure(6 * 4));
+    HIPCHK(r, r->d_bbox.ensure(6 * BBOX_REPLICAS * 4));
     HIPCHK(r, r->d_partials.ensure(nblocks * 4));
     HIPCHK(r, r->d_grid.ensure(sizeof(GridParams)));
     HIPCHK(r, hipMemsetAsync(r->d_hist.p, 0, G2 * 4, r->stream));
@@ -518,8 +518,8 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, hipMemsetAsync(r->d_grid.p, 0, sizeof(GridParams), r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_out.p, 0, nhp * 12, r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_hp.p, 0, nhp * 40, r->stream)); /* pad rows: flags 0 */
-    uint32_t bbox_init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
-    HIPCHK(r, hipMemcpyAsync(r->d_bbox.p, bbox_init, sizeof bbox_init, hipMemcpyHostToDevice, r->stream));
+    HIPCHK(r, hipMemsetAsync(r->d_bbox.p, 0xff, 3 * BBOX_REPLICAS * 4, r->stream));
+    HIPCHK(r, hipMemsetAsync(r->d_bbox.as<uint32_t>() + 3 * BBOX_REPLICAS, 0, 3 * BBOX_REPLICAS * 4, r->stream));
 
     PixelBufs& px = r->px;
     px.W = W;

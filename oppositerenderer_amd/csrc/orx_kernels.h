@@ -51,6 +51,8 @@ struct PixelBufs {
     uint32_t* dbg;      /* [rows*W*2] cells/photons visited, or NULL */
 };
 
+constexpr uint32_t BBOX_REPLICAS = 64;
+
 struct PhotonBufs {
     uint32_t PW, PH;    /* photon launch (full) */
     uint32_t prows;     /* local photon rows */
@@ -68,7 +70,7 @@ struct PhotonBufs {
     uint32_t* ranks;    /* [S] */
     uint32_t* hist;     /* [gmax+2] */
     uint32_t* offsets;  /* [gmax+2] */
-    uint32_t* bbox;     /* [6] ordered-float min xyz, max xyz */
+    uint32_t* bbox;     /* [6][BBOX_REPLICAS] ordered-float min xyz, max xyz */
     uint32_t* scan_partials; /* [ceil((gmax+2)/1024)+1] */
     GridParams* grid;
 };

@@ -237,13 +237,15 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
     /* wave AABB -> device-wide ordered-int atomics (one lane per component) */
     lo_x = wave_min(lo_x); lo_y = wave_min(lo_y); lo_z = wave_min(lo_z);
     hi_x = wave_max(hi_x); hi_y = wave_max(hi_y); hi_z = wave_max(hi_z);
+    /* 64 replicas per component keep same-address atomic contention low */
     const uint32_t lane = threadIdx.x;
+    const uint32_t rep = (blockIdx.x + blockIdx.y * gridDim.x) & (BBOX_REPLICAS - 1);
     if (lane < 6) {
         float v = lane == 0 ? lo_x : lane == 1 ? lo_y : lane == 2 ? lo_z : lane == 3 ? hi_x : lane == 4 ? hi_y : hi_z;
         if (lane < 3) {
-            if (v != INFINITY) atomicMin(&pb.bbox[lane], f2ord(v));
+            if (v != INFINITY) atomicMin(&pb.bbox[lane * BBOX_REPLICAS + rep], f2ord(v));
         } else {
-            if (v != -INFINITY) atomicMax(&pb.bbox[lane], f2ord(v));
+            if (v != -INFINITY) atomicMax(&pb.bbox[lane * BBOX_REPLICAS + rep], f2ord(v));
         }
     }
 }
@@ -256,9 +258,22 @@ void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, co
 /* grid setup: createUniformGridPhotonMap host math, on one thread     */
 /* ------------------------------------------------------------------ */
 __global__ void k_grid_setup(PhotonBufs pb) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    /* lanes k*64..: fold the replicas, then reset them for the next photon pass */
+    __shared__ uint32_t red[6];
+    const uint32_t lane = threadIdx.x;
+    for (int k = 0; k < 6; k++) {
+        uint32_t v = pb.bbox[k * BBOX_REPLICAS + lane];
+        for (int o = 32; o > 0; o >>= 1) {
+            uint32_t w = (uint32_t)__shfl_xor((int)v, o, 64);
+            v = k < 3 ? min(v, w) : max(v, w);
+        }
+        if (lane == 0) red[k] = v;
+        pb.bbox[k * BBOX_REPLICAS + lane] = k < 3 ? 0xffffffffu : 0u;
+    }
+    __syncthreads();
+    if (lane != 0) return;
     uint32_t b[6];
-    for (int k = 0; k < 6; k++) b[k] = pb.bbox[k];
+    for (int k = 0; k < 6; k++) b[k] = red[k];
     bool any = b[0] != 0xffffffffu; /* min initialised to ord(+max) */
     f3 lo, hi;
     if (any) {
@@ -267,11 +282,6 @@ __global__ void k_grid_setup(PhotonBufs pb) {
     } else {
         lo = mk1(0.f);
         hi = mk1(0.f);
-    }
-    /* reset for the next photon pass */
-    for (int k = 0; k < 3; k++) {
-        pb.bbox[k] = 0xffffffffu;
-        pb.bbox[3 + k] = 0u;
     }
     /* padAABB (SpatialHash.cu:135-141) */
     lo = mk(lo.x - 0.0000001f, lo.y - 0.0000001f, lo.z - 0.0000001f);
