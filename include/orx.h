@@ -174,7 +174,13 @@ typedef enum {
     ORX_BUF_DIRECT = 5,     /* float  [W*H][3] */
     ORX_BUF_OUTPUT = 6,     /* float  [W*H][3] */
     ORX_BUF_PHOTON_SLOTS = 7,/* float [S][9] unsorted photon slots: power3 position3 direction3 (0 when cleared) */
-    ORX_BUF_DEBUG_VISITED = 8 /* uint32 [W*H][2]: cells visited, photons visited */
+    ORX_BUF_DEBUG_VISITED = 8,/* uint32 [W*H][2]: cells visited, photons visited */
+    /* VCM (vcm/VCMLightPass.cu, VCMCameraPass.cu); light subpath p = x + y*W pairs with pixel p */
+    ORX_BUF_VCM_VERTEX_COUNT = 9, /* uint32 [W*H]: stored light vertices per subpath (lightSubpathVertexCountBuffer) */
+    ORX_BUF_VCM_VERTICES = 10,    /* float [9][W*H][16]: per vertex slot k, subpath p: pos3 mat(bits) throughput3 dVCM
+                                     normal3 dVC dirFix3 dVM; entries k >= count[p] are stale */
+    ORX_BUF_VCM_SPLAT = 11,       /* float [W*H][3]: this iteration's light-tracing splats (connectCameraT1) */
+    ORX_BUF_VCM_CAMERA = 12       /* float [W*H][3]: this iteration's camera subpath colour (cameraPrd.color) */
 } orx_buffer_id;
 /* Copies buffer `id` to host; returns the byte size through *out_bytes
  * (call with dst=NULL to query). */

@@ -39,6 +39,10 @@ BUF_DIRECT = 5
 BUF_OUTPUT = 6
 BUF_PHOTON_SLOTS = 7
 BUF_DEBUG_VISITED = 8
+BUF_VCM_VERTEX_COUNT = 9
+BUF_VCM_VERTICES = 10
+BUF_VCM_SPLAT = 11
+BUF_VCM_CAMERA = 12
 
 # RadiancePRD.h:30-35 flag bits
 PRD_HIT_EMITTER = 1 << 31

@@ -198,7 +198,7 @@ DevLight make_light(const orx_light& L) {
 
 float dtor(float d) { return d * ((float)M_PI / 180.f); } /* Camera.cpp:87-90 */
 
-DevCamera camera_setup(const orx_camera& c) {
+DevCamera camera_setup(const orx_camera& c, float* ulen_out = nullptr, float* vlen_out = nullptr) {
     /* Camera::setup (renderer/Camera.cpp:333-345) */
     DevCamera k;
     f3 eye = ld3(c.eye), lookat = ld3(c.lookat), up = ld3(c.up);
@@ -213,6 +213,8 @@ DevCamera camera_setup(const orx_camera& c) {
     float vlen = lookdir_len * tanf(dtor(c.vfov * 0.5f));
     k.v = cv * vlen;
     k.aperture = c.aperture;
+    if (ulen_out) *ulen_out = ulen;
+    if (vlen_out) *vlen_out = vlen;
     return k;
 }
 
@@ -249,6 +251,12 @@ struct orx_renderer {
     bool timing = true;
     uint64_t last_method = 0;
     Consts last_consts{};
+    /* VCM: pixelSizeFactor (OptixRenderer.cpp:306, :846), LVC estimate flag (:83, :461, :847) */
+    float psf_x = 1.0f, psf_y = 1.0f;
+    bool vcm_estimated = false;
+    size_t vcm_npx = 0;
+    DevBuf d_vcount, d_vverts, d_vsplat, d_vcam;
+    std::vector<DevLight> host_lights;
 };
 
 static orx_status set_err(orx_renderer* r, orx_status s, const std::string& m) {
@@ -386,6 +394,7 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     }
     std::vector<DevLight> lights(s->n_lights);
     for (uint32_t i = 0; i < s->n_lights; i++) lights[i] = make_light(s->lights[i]);
+    r->host_lights = lights;
     /* triangles: BVH over triangle boxes, then vertex / normal / material
      * arrays rewritten in leaf order (tri_v[3k].w carries the original id) */
     std::vector<BuildTri> bt(nt);
@@ -470,6 +479,7 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     S.bs_cy = center.y;
     S.bs_cz = center.z;
     S.bs_r = sqrtf(e.x * e.x + e.y * e.y + e.z * e.x);
+    r->vcm_estimated = false;
     r->scene_ready = true;
     return ORX_OK;
 }
@@ -610,6 +620,11 @@ static orx_status begin_iteration(orx_renderer* r, uint64_t local_iteration_numb
     if (!r->scene_ready) return set_err(r, ORX_ERR_STATE, "Traced before OptixRenderer was initialized.");
     if (det->width == 0 || det->height == 0) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "zero-sized request");
     HIPCHK(r, hipSetDevice(r->device));
+    if (det->width != r->W || det->height != r->H) { /* resizeBuffers (OptixRenderer.cpp:826-848) */
+        r->psf_x = 1.0f / (float)det->width;
+        r->psf_y = 1.0f / (float)det->height;
+        r->vcm_estimated = false;
+    }
     if (det->width != r->W || det->height != r->H || !r->rng_ready) {
         orx_status st = resize(r, det->width, det->height);
         if (st != ORX_OK) return st;
@@ -659,13 +674,83 @@ static void ppm_local_passes(orx_renderer* r, const DevCamera& cam, const Consts
     ppm_photons_grid(r, c);
 }
 
+/* VCM_BIDIRECTIONAL_PATH_TRACING branch of renderNextIteration (OptixRenderer.cpp:675-795) */
+static orx_status vcm_iteration(orx_renderer* r, const orx_request* det, float ppm_radius) {
+    const size_t npx = (size_t)r->W * r->H;
+    if (r->vcm_npx != npx) {
+        HIPCHK(r, r->d_vcount.ensure(npx * 4));
+        HIPCHK(r, r->d_vverts.ensure(npx * VCM_MAX_VERTS * 64));
+        HIPCHK(r, r->d_vsplat.ensure(npx * 12));
+        HIPCHK(r, r->d_vcam.ensure(npx * 12));
+        HIPCHK(r, hipMemsetAsync(r->d_vcount.p, 0, npx * 4, cur_stream(r)));
+        HIPCHK(r, hipMemsetAsync(r->d_vcam.p, 0, npx * 12, cur_stream(r)));
+        r->vcm_npx = npx;
+    }
+    VcmBufs vb;
+    vb.RW = r->RW;
+    vb.rng = r->px.rng;
+    vb.vcount = r->d_vcount.as<uint32_t>();
+    const size_t plane = npx * VCM_MAX_VERTS;
+    vb.vA = r->d_vverts.as<float4>();
+    vb.vB = vb.vA + plane;
+    vb.vC = vb.vB + plane;
+    vb.vD = vb.vC + plane;
+    vb.splat = r->d_vsplat.as<float>();
+    vb.cam = r->d_vcam.as<float>();
+    vb.output = r->d_out.as<float>();
+    VcmConsts c;
+    float ulen = 0.f, vlen = 0.f;
+    DevCamera cam = camera_setup(det->camera, &ulen, &vlen);
+    c.eye = cam.eye;
+    c.lookdir = cam.lookdir;
+    c.u = cam.u;
+    c.v = cam.v;
+    c.unitU = normalize(cam.u);
+    c.unitV = normalize(cam.v);
+    c.lookdirN = normalize(cam.lookdir);
+    c.lookdirLen = length(cam.lookdir);
+    c.ipsx = 2.0f * ulen;
+    c.ipsy = 2.0f * vlen;
+    c.psfx = r->psf_x;
+    c.psfy = r->psf_y;
+    c.W = r->W;
+    c.H = r->H;
+    c.count = r->W * r->H;
+    c.maxPathLen = r->cfg.vcm_max_path_length;
+    /* etaVCM = (nVM / nVC) * PI * r^2 with nVC = 1, nVM = lightSubPathCount */
+    const float ppmRadiusSquared = ppm_radius * ppm_radius;
+    const float etaVCM = ((float)c.count / (float)1u) * ORX_PI_F * ppmRadiusSquared;
+    c.misVm = 0.f;
+    c.misVc = 1.f / etaVCM;
+    hipStream_t st = cur_stream(r);
+    ev_begin(r, P_VCM_LIGHT);
+    if (!r->vcm_estimated) { /* subpath length estimate launch: advances the RNG, stores nothing */
+        launch_vcm_light(st, r->scene, vb, c, true);
+        r->vcm_estimated = true;
+    }
+    HIPCHK(r, hipMemsetAsync(vb.splat, 0, npx * 12, st));
+    launch_vcm_light(st, r->scene, vb, c, false);
+    ev_end(r, P_VCM_LIGHT);
+    ev_begin(r, P_VCM_CAMERA);
+    launch_vcm_camera(st, r->scene, vb, c);
+    ev_end(r, P_VCM_CAMERA);
+    return ORX_OK;
+}
+
 orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
                                      float ppm_radius, int create_output, const orx_request* det) {
     (void)create_output; /* ignored by the reference engine too */
     (void)iteration_number;
     if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
-    if (det->method != ORX_METHOD_PATH_TRACING && det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
+    if (det->method != ORX_METHOD_PATH_TRACING && det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING &&
+        det->method != ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING)
         return set_err(r, ORX_ERR_UNSUPPORTED, "render method not supported by this build");
+    if (det->method == ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING && r->world > 1)
+        return set_err(r, ORX_ERR_UNSUPPORTED, "VCM runs on one device");
+    if (det->method == ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING)
+        for (const DevLight& l : r->host_lights)
+            if (l.type == LIGHT_SPOT)
+                return set_err(r, ORX_ERR_UNSUPPORTED, "VCM: spot lights are not emitted by lightEmit (helpers/light.h:130)");
     if (det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world > 1)
         return set_err(r, ORX_ERR_STATE, "sharded PPM runs through orx_ppm_local_passes/_gather_external/_finish");
     orx_status s0 = begin_iteration(r, local_iteration_number, det);
@@ -677,6 +762,9 @@ orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
         ev_begin(r, P_PT);
         launch_pt(st, r->scene, cam, r->px, c);
         ev_end(r, P_PT);
+    } else if (det->method == ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING) {
+        orx_status sv = vcm_iteration(r, det, ppm_radius);
+        if (sv != ORX_OK) return sv;
     } else {
         ppm_local_passes(r, cam, c);
         ev_begin(r, P_GATHER);
@@ -855,6 +943,9 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
     case ORX_BUF_INDIRECT: case ORX_BUF_DIRECT: case ORX_BUF_OUTPUT: need = npx * 12; break;
     case ORX_BUF_PHOTON_SLOTS: need = (size_t)r->pb.S * 36; break;
     case ORX_BUF_DEBUG_VISITED: need = npx * 8; break;
+    case ORX_BUF_VCM_VERTEX_COUNT: need = r->vcm_npx * 4; break;
+    case ORX_BUF_VCM_VERTICES: need = r->vcm_npx * VCM_MAX_VERTS * 64; break;
+    case ORX_BUF_VCM_SPLAT: case ORX_BUF_VCM_CAMERA: need = r->vcm_npx * 12; break;
     default: return set_err(r, ORX_ERR_INVALID_ARGUMENT, "unknown buffer id");
     }
     if (out_bytes) *out_bytes = need;
@@ -919,6 +1010,18 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
     case ORX_BUF_DIRECT: HIPCHK(r, d2h(dst, r->d_dir.p, need)); break;
     case ORX_BUF_OUTPUT: HIPCHK(r, d2h(dst, r->d_out.p, need)); break;
     case ORX_BUF_DEBUG_VISITED: HIPCHK(r, d2h(dst, r->d_dbg.p, need)); break;
+    case ORX_BUF_VCM_VERTEX_COUNT: HIPCHK(r, d2h(dst, r->d_vcount.p, need)); break;
+    case ORX_BUF_VCM_SPLAT: HIPCHK(r, d2h(dst, r->d_vsplat.p, need)); break;
+    case ORX_BUF_VCM_CAMERA: HIPCHK(r, d2h(dst, r->d_vcam.p, need)); break;
+    case ORX_BUF_VCM_VERTICES: { /* four float4 planes [9][npx] -> [9][npx][16] */
+        const size_t plane = r->vcm_npx * VCM_MAX_VERTS;
+        std::vector<float4> P(4 * plane);
+        HIPCHK(r, d2h(P.data(), r->d_vverts.p, 4 * plane * 16));
+        float* o = (float*)dst;
+        for (size_t i = 0; i < plane; i++)
+            for (int k = 0; k < 4; k++) std::memcpy(o + 16 * i + 4 * k, &P[k * plane + i], 16);
+        break;
+    }
     }
     return ORX_OK;
 }

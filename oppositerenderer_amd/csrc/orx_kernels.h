@@ -108,4 +108,31 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
 void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c);
 void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c);
 
+/* ---- VCM (orx_vcm.hip) ---- */
+constexpr uint32_t VCM_MAX_VERTS = 9; /* VCM_MAX_PATH_LENGTH - 1 (OptixRenderer.cpp:343-344) */
+/* light subpath p = x + y*W pairs with pixel p; RNG slot y*RW + x serves both */
+struct VcmBufs {
+    uint32_t RW;
+    RngPlanes rng;
+    uint32_t* vcount;   /* [W*H] stored vertices per light subpath */
+    float4* vA;         /* [9][W*H] pos.xyz | material id bits */
+    float4* vB;         /* [9][W*H] throughput.xyz | dVCM */
+    float4* vC;         /* [9][W*H] normal.xyz | dVC */
+    float4* vD;         /* [9][W*H] localDirFix.xyz | dVM */
+    float* splat;       /* [W*H*3] connectCameraT1 accumulation of this iteration */
+    float* cam;         /* [W*H*3] camera subpath colour of this iteration */
+    float* output;      /* [W*H*3] running sum */
+};
+struct VcmConsts {
+    f3 eye, lookdir, u, v;          /* Camera (Camera.cpp:333-345) */
+    f3 unitU, unitV, lookdirN;
+    float lookdirLen, ipsx, ipsy;   /* imagePlaneSize = 2*(ulen, vlen) */
+    float psfx, psfy;               /* pixelSizeFactor (OptixRenderer.cpp:846) */
+    float misVc, misVm;             /* 1/etaVCM, 0 (vcmUseVM = false) */
+    uint32_t W, H, count;           /* count = lightSubpathCount = W*H */
+    uint32_t maxPathLen;
+};
+void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c, bool estimate);
+void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c);
+
 }  // namespace orx

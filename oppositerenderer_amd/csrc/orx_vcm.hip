@@ -1,0 +1,783 @@
+/*
+ * orx_vcm.hip — VCM (bidirectional path tracing with vertex connection) for
+ * gfx950: the reference's VCM_LIGHT_PASS and VCM_CAMERA_PASS launches
+ * (OptixRenderer.cpp:675-795) as two megakernels, one lane per subpath.
+ *
+ * Reference programs restated (RenderEngine/):
+ *   renderer/vcm/VCMLightPass.cu, VCMCameraPass.cu, vcm.h, mis.h,
+ *   renderer/BSDF.h (VcmBSDF), BxDF.h, reflection.h, math/DifferentialGeometry.h,
+ *   helpers/light.h (lightEmit / lightIlluminate), helpers/samplers.h,
+ *   material/{Diffuse,Glossy,Mirror,Glass,DiffuseEmitter}.cu vcmClosestHit*.
+ * Shipped configuration: VCM_UNIFORM_VERTEX_SAMPLING 0, vcmUseVC 1, vcmUseVM 0.
+ *
+ * Data layout (HBM):
+ *   light vertex cache: slot k of subpath p (p = x + y*W) in four float4
+ *   planes [9][W*H] — A: pos.xyz|material, B: throughput.xyz|dVCM,
+ *   C: normal.xyz|dVC, D: localDirFix.xyz|dVM.  The reference appends
+ *   vertices to one atomically-bumped LightVertex array and keeps a
+ *   [W*H][9] index table; camera subpath p only ever reads light subpath p,
+ *   so the direct [k][p] layout needs neither the atomic nor the table and
+ *   every per-k access of a wave is one contiguous 1 KiB run.
+ *   light-tracing splats (connectCameraT1) go to a per-iteration float
+ *   buffer with hardware fp32 atomics; the camera pass folds it into the
+ *   running-sum output together with the camera subpath colour.
+ * The same quirks as the CPU restatement (oracle/orx_oracle_vcm.c.inc) are
+ * reproduced; everything but the splat sums is bit-identical to it.
+ */
+#include "orx_kernels.h"
+
+namespace orx {
+
+constexpr float VCM_EPS_COSINE = 1e-6f;  /* config.h:42 */
+constexpr float VCM_EPS_RAY = 1e-3f;     /* config.h:43 */
+constexpr float VCM_RAY_LEN_MIN = 0.0001f;
+constexpr float VCM_EPS_PHONG = 1e-3f;   /* BxDF.h:253 */
+
+/* BxDF::Type (BxDF.h:47-67) */
+enum : uint32_t {
+    BX_REFLECTION = 1, BX_TRANSMISSION = 2, BX_DIFFUSE = 4, BX_GLOSSY = 8, BX_SPECULAR = 16, BX_ALL = 31,
+    BX_LAMBERTIAN = 32, BX_SPEC_REFLECTION = 64, BX_SPEC_TRANSMISSION = 128, BX_PHONG = 256
+};
+
+__device__ __forceinline__ bool iszero(f3 v) { return v.x == 0.f && v.y == 0.f && v.z == 0.f; }
+__device__ __forceinline__ float luminance_cie(f3 c) { return c.x * 0.2126f + c.y * 0.7152f + c.z * 0.0722f; }
+__device__ __forceinline__ f3 local_reflect(f3 w) { return mk(-w.x, -w.y, w.z); }
+
+/* DifferentialGeometry (math/DifferentialGeometry.h) */
+struct Frame {
+    f3 b, t, n;
+    __device__ __forceinline__ f3 to_world(f3 a) const { return b * a.x + t * a.y + n * a.z; }
+    __device__ __forceinline__ f3 to_local(f3 a) const { return mk(dot(b, a), dot(t, a), dot(n, a)); }
+};
+__device__ __forceinline__ Frame frame_from_normal(f3 nrm) {
+    Frame f;
+    f.n = normalize(nrm);
+    f3 tmp = fabsf(f.n.x) > 0.99f ? mk(0.f, 1.f, 0.f) : mk(1.f, 0.f, 0.f);
+    f.t = normalize(cross(f.n, tmp));
+    f.b = cross(f.t, f.n);
+    return f;
+}
+
+/* FresnelDielectric::evaluate (reflection.h:106-133) */
+__device__ inline float fresnel_dielectric(float cosi, float eta_i, float eta_t) {
+    cosi = fmaxf(-1.0f, fminf(cosi, 1.0f));
+    const bool entering = cosi > 0.0f;
+    float ei = entering ? eta_i : eta_t, et = entering ? eta_t : eta_i;
+    float sint = ei / et * sqrtf(fmaxf(0.0f, 1.0f - cosi * cosi));
+    if (sint >= 1.0f) return 1.0f;
+    cosi = fabsf(cosi);
+    float cost = sqrtf(fmaxf(0.0f, 1.0f - sint * sint));
+    float Rparl = ((et * cosi) - (ei * cost)) / ((et * cosi) + (ei * cost));
+    float Rperp = ((ei * cosi) - (et * cost)) / ((ei * cosi) + (et * cost));
+    return (Rparl * Rparl + Rperp * Rperp) * 0.5f;
+}
+
+struct Bxdf {
+    uint32_t type;
+    f3 R;
+    float exponent;
+    float ei, et;
+    bool dielectric;
+};
+__device__ __forceinline__ bool bx_match(uint32_t type, uint32_t mask) {
+    return (type & BX_ALL & mask) == (type & BX_ALL);
+}
+__device__ __forceinline__ float bx_fresnel(const Bxdf& b, float c) {
+    return b.dielectric ? fresnel_dielectric(c, b.ei, b.et) : 1.0f;
+}
+__device__ __forceinline__ float bx_cont(const Bxdf& b, f3 wo) {
+    const uint32_t k = b.type & ~BX_ALL;
+    if (k == BX_LAMBERTIAN || k == BX_PHONG) return fmaxf(b.R.x, maxf(b.R.y, b.R.z));
+    if (k == BX_SPEC_REFLECTION) return bx_fresnel(b, wo.z) * fmaxf(b.R.x, maxf(b.R.y, b.R.z));
+    return 1.f - bx_fresnel(b, wo.z);
+}
+__device__ __forceinline__ float bx_albedo(const Bxdf& b, f3 wo) {
+    const uint32_t k = b.type & ~BX_ALL;
+    if (k == BX_LAMBERTIAN || k == BX_PHONG) return luminance_cie(b.R);
+    if (k == BX_SPEC_REFLECTION) return bx_fresnel(b, wo.z) * luminance_cie(b.R);
+    return (1.f - bx_fresnel(b, wo.z)) * luminance_cie(b.R);
+}
+__device__ __forceinline__ Bxdf mk_bx(uint32_t type, f3 R, float e = 0.f, float ei = 1.f, float et = 1.f,
+                                      bool diel = false) {
+    Bxdf b;
+    b.type = type; b.R = R; b.exponent = e; b.ei = ei; b.et = et; b.dielectric = diel;
+    return b;
+}
+constexpr uint32_t T_LAMBERT = BX_LAMBERTIAN | BX_REFLECTION | BX_DIFFUSE;
+constexpr uint32_t T_PHONG = BX_PHONG | BX_REFLECTION | BX_GLOSSY;
+constexpr uint32_t T_SREFL = BX_SPEC_REFLECTION | BX_REFLECTION | BX_SPECULAR;
+constexpr uint32_t T_STRANS = BX_SPEC_TRANSMISSION | BX_TRANSMISSION | BX_SPECULAR;
+
+__device__ __forceinline__ float pow_cos_pdf(f3 n, f3 d, float power) {
+    const float cosTheta = fmaxf(0.f, dot(n, d));
+    return (power + 1.f) * orx_powf(cosTheta, power) * (ORX_1_PI_F * 0.5f);
+}
+__device__ inline float bx_pdf(const Bxdf& b, f3 wo, f3 wi, bool rev) {
+    const uint32_t k = b.type & ~BX_ALL;
+    if (k == BX_LAMBERTIAN) {
+        if (wo.z * wi.z > 0.0f) return rev ? fabsf(wo.z) * ORX_1_PI_F : fabsf(wi.z) * ORX_1_PI_F;
+        return 0.f;
+    }
+    if (k == BX_PHONG) {
+        f3 r = local_reflect(wo);
+        if (dot(r, wi) <= VCM_EPS_PHONG) return 0.f;
+        return pow_cos_pdf(r, wi, b.exponent);
+    }
+    return 0.f;
+}
+__device__ inline f3 phong_f(const Bxdf& b, f3 wo, f3 wi, float* pdf) {
+    if (wo.z < VCM_EPS_COSINE || wi.z < VCM_EPS_COSINE) {
+        if (pdf) *pdf = 0.f;
+        return mk1(0.f);
+    }
+    f3 r = local_reflect(wo);
+    float d = dot(r, wi);
+    if (d <= VCM_EPS_PHONG) {
+        if (pdf) *pdf = 0.f;
+        return mk1(0.f);
+    }
+    if (pdf) *pdf = pow_cos_pdf(r, wi, b.exponent);
+    f3 rho = ((b.R * (b.exponent + 2.f)) * 0.5f) * ORX_1_PI_F;
+    return rho * orx_powf(d, b.exponent);
+}
+__device__ inline f3 bx_f(const Bxdf& b, f3 wo, f3 wi) {
+    const uint32_t k = b.type & ~BX_ALL;
+    if (k == BX_LAMBERTIAN) return b.R * ORX_1_PI_F;
+    if (k == BX_PHONG) return phong_f(b, wo, wi, nullptr);
+    return mk1(0.f);
+}
+__device__ inline f3 bx_vcm_f(const Bxdf& b, f3 wo, f3 wi, float& dpdf, float& rpdf) {
+    const uint32_t k = b.type & ~BX_ALL;
+    if (k == BX_LAMBERTIAN) {
+        if (wo.z < VCM_EPS_COSINE || wi.z < VCM_EPS_COSINE) return mk1(0.f);
+        dpdf = fmaxf(0.f, wi.z * ORX_1_PI_F);
+        rpdf = fmaxf(0.f, wo.z * ORX_1_PI_F);
+        return b.R * ORX_1_PI_F;
+    }
+    if (k == BX_PHONG) {
+        float pdf = 0.f;
+        f3 f = phong_f(b, wo, wi, &pdf);
+        dpdf = pdf;
+        rpdf = pdf;
+        return f;
+    }
+    dpdf = 0.f;
+    rpdf = 0.f;
+    return mk1(0.f);
+}
+__device__ inline f3 bx_sample_f(const Bxdf& b, f3 wo, f3& wi, float s0, float s1, float& pdf, bool adjoint) {
+    const uint32_t k = b.type & ~BX_ALL;
+    if (k == BX_LAMBERTIAN) {
+        if (wo.z < VCM_EPS_COSINE) { pdf = 0.f; return mk1(0.f); }
+        /* optixu cosine_sample_hemisphere */
+        const float r = sqrtf(s0);
+        const float phi = 2.0f * ORX_PI_F * s1;
+        wi.x = r * orx_cosf(phi);
+        wi.y = r * orx_sinf(phi);
+        wi.z = sqrtf(fmaxf(0.0f, 1.0f - wi.x * wi.x - wi.y * wi.y));
+        pdf = bx_pdf(b, wo, wi, false);
+        return b.R * ORX_1_PI_F;
+    }
+    if (k == BX_PHONG) {
+        const float phi = 2.f * ORX_PI_F * s0;
+        const float z = orx_powf(s1, 1.f / (b.exponent + 1.f));
+        const float r = sqrtf(1.f - z * z);
+        wi = mk(orx_cosf(phi) * r, orx_sinf(phi) * r, z);
+        if (wo.z < VCM_EPS_COSINE || wi.z < VCM_EPS_COSINE) { pdf = 0.f; return mk1(0.f); }
+        const f3 refl = local_reflect(wo);
+        const Frame dg = frame_from_normal(refl);
+        wi = dg.to_world(wi);
+        const float d = dot(refl, wi);
+        if (d <= VCM_EPS_PHONG) { pdf = 0.f; return mk1(0.f); }
+        pdf = bx_pdf(b, wo, wi, false);
+        f3 rho = ((b.R * (b.exponent + 2.f)) * 0.5f) * ORX_1_PI_F;
+        return rho * orx_powf(d, b.exponent);
+    }
+    if (k == BX_SPEC_REFLECTION) {
+        wi = mk(-wo.x, -wo.y, wo.z);
+        pdf = 1.0f;
+        const float R = bx_fresnel(b, wo.z);
+        return (b.R * R) / fabsf(wi.z);
+    }
+    const bool entering = wo.z > 0.0f;
+    const float ei = entering ? b.ei : b.et, et = entering ? b.et : b.ei;
+    const float sini2 = 1.0f - wo.z * wo.z;
+    const float eta = ei / et;
+    const float sint2 = eta * eta * sini2;
+    if (sint2 >= 1.f) return mk1(0.f); /* pdf left untouched (BxDF.h:496) */
+    float cost = sqrtf(fmaxf(0.f, 1.f - sint2));
+    if (entering) cost = -cost;
+    wi = mk(eta * -wo.x, eta * -wo.y, cost);
+    pdf = 1.f;
+    const float T = 1.f - bx_fresnel(b, wo.z);
+    if (adjoint) return (b.R * T) / fabsf(wi.z);
+    return ((b.R * T) * (eta * eta)) / fabsf(wi.z);
+}
+
+struct VBsdf {
+    Frame dg;
+    f3 gn;
+    f3 fix;
+    Bxdf bx[2];
+    float pick[2];
+    float cont;
+    int n;
+    bool fix_is_light;
+
+    __device__ __forceinline__ void init(f3 world_normal, f3 incident, bool is_light) {
+        dg = frame_from_normal(world_normal);
+        gn = world_normal;
+        fix_is_light = is_light;
+        fix = dg.to_local(incident);
+        n = 0;
+        cont = 0.f;
+        pick[0] = pick[1] = 0.f;
+    }
+    __device__ __forceinline__ void add(const Bxdf& b) {
+        bx[n] = b;
+        float rr = 0.f;
+        rr += bx_cont(b, fix);
+        cont = fminf(1.f, cont + rr);
+        float albedo = 0.f;
+        albedo += bx_albedo(b, fix);
+        pick[n] = albedo;
+        n++;
+    }
+    __device__ __forceinline__ int count(uint32_t mask) const {
+        int c = 0;
+        for (int i = 0; i < n; i++) c += bx_match(bx[i].type, mask) ? 1 : 0;
+        return c;
+    }
+    __device__ __forceinline__ bool is_specular() const { return count(BX_ALL & ~BX_SPECULAR) == 0; }
+    __device__ __forceinline__ float sum_pick(uint32_t mask) const {
+        float c = 0.f;
+        for (int i = 0; i < n; i++)
+            if (bx_match(bx[i].type, mask)) c += pick[i];
+        return c;
+    }
+    /* VcmBSDF::sampleF via vcmSampleF (BSDF.h:411-485) */
+    __device__ f3 sample_f(float sx, float sy, float sz, f3& world_wi, float& pdf, float& cos_out,
+                           uint32_t& sampled) const {
+        int index = 0;
+        float sum = 0.f;
+        const int nMatched = count(BX_ALL);
+        if (nMatched) {
+            sum = sum_pick(BX_ALL);
+            float prev = 0.f;
+            for (int i = 0; i < n; i++) {
+                if (bx_match(bx[i].type, BX_ALL)) {
+                    const float cp = pick[i] / sum;
+                    if (sx < prev + cp) { index = i; break; }
+                    prev += cp;
+                }
+            }
+        }
+        if (sum == 0.f) { pdf = 0.0f; return mk1(0.f); }
+        const Bxdf& b = bx[index];
+        const f3 world_wo = dg.to_world(fix);
+        const f3 wo = dg.to_local(world_wo);
+        f3 wi = mk1(0.f);
+        f3 f = bx_sample_f(b, wo, wi, sy, sz, pdf, fix_is_light);
+        const float q = pick[index] / sum;
+        pdf *= q;
+        if (pdf == 0.0f) { sampled = 0; return mk1(0.f); }
+        sampled = b.type;
+        world_wi = dg.to_world(wi);
+        cos_out = fabsf(wi.z);
+        if (!(b.type & BX_SPECULAR)) {
+            if (nMatched > 1) {
+                for (int i = 0; i < n; i++) {
+                    if (i == index || !bx_match(bx[i].type, BX_ALL)) continue;
+                    float comp = 0.f;
+                    comp += bx_pdf(bx[i], wo, wi, false);
+                    pdf += comp * q;
+                }
+            }
+            uint32_t m2 = BX_ALL;
+            if (dot(gn, world_wi) * dot(gn, world_wo) >= 0.0f) m2 &= ~BX_TRANSMISSION;
+            else m2 &= ~BX_REFLECTION;
+            for (int i = 0; i < n; i++) {
+                if (i == index || !bx_match(bx[i].type, m2)) continue;
+                f = f + bx_f(bx[i], wo, wi);
+            }
+        }
+        return f;
+    }
+    /* VcmBSDF::pdf(dir, All & ~Specular, aEvalRevPdf = true) (BSDF.h:391-407) */
+    __device__ float pdf_rev(f3 world_gen) const {
+        const uint32_t mask = BX_ALL & ~BX_SPECULAR;
+        const f3 wi = dg.to_local(world_gen);
+        const float sum = sum_pick(mask);
+        if (sum == 0.f) return 0.f;
+        float pdf = 0.f;
+        for (int i = 0; i < n; i++) {
+            if (bx_match(bx[i].type, mask)) {
+                float comp = 0.f;
+                comp += bx_pdf(bx[i], fix, wi, true);
+                pdf += comp * pick[i] / sum;
+            }
+        }
+        return pdf;
+    }
+    /* VcmBSDF::vcmF (BSDF.h:488-541) */
+    __device__ f3 vcm_f(f3 world_gen, float& cos_gen, float& dpdf, float& rpdf) const {
+        const f3 gen = dg.to_local(world_gen);
+        const f3 world_fix = dg.to_world(fix);
+        dpdf = 0.f;
+        rpdf = 0.f;
+        if (fix.z < VCM_EPS_COSINE || gen.z < VCM_EPS_COSINE) return mk1(0.f);
+        cos_gen = gen.z;
+        uint32_t mask = BX_ALL;
+        if (dot(gn, world_gen) * dot(gn, world_fix) >= 0.0f) mask &= ~BX_TRANSMISSION;
+        else mask &= ~BX_REFLECTION;
+        const float sum = sum_pick(mask);
+        if (sum == 0.f) return mk1(0.f);
+        f3 f = mk1(0.f);
+        for (int i = 0; i < n; i++) {
+            if (bx_match(bx[i].type, mask)) {
+                float dp = 0.f, rp = 0.f;
+                f = f + bx_vcm_f(bx[i], fix, gen, dp, rp);
+                const float q = pick[i] / sum;
+                dp *= q;
+                rp *= q;
+                dpdf += dp;
+                rpdf += rp;
+            }
+        }
+        return f;
+    }
+};
+
+/* material vcmClosestHit{Light,Camera}: false = program ends the subpath */
+__device__ inline bool material_bsdf(const DevMaterial& m, f3 gn, f3 dir, bool is_light, VBsdf& s, f3& N) {
+    switch (m.type) {
+    case MAT_DIFFUSE:
+        N = gn;
+        s.init(gn, -dir, is_light);
+        s.add(mk_bx(T_LAMBERT, m.Kd));
+        return true;
+    case MAT_GLOSSY:
+        N = gn;
+        s.init(gn, -dir, is_light);
+        s.add(mk_bx(T_LAMBERT, m.Kd));
+        s.add(mk_bx(T_PHONG, m.Ks, m.exponent));
+        return true;
+    case MAT_MIRROR:
+        if (iszero(m.Kr)) return false;
+        N = gn;
+        s.init(gn, -dir, is_light);
+        s.add(mk_bx(T_SREFL, m.Kr));
+        return true;
+    case MAT_GLASS: {
+        const bool outside = dot(gn, dir) < 0;
+        const f3 nn = outside ? gn : -gn;
+        const float n1 = outside ? 1.f : m.ior, n2 = outside ? m.ior : 1.f;
+        const bool krBlack = iszero(m.Kr), ktBlack = iszero(m.Kt);
+        if (krBlack && ktBlack) return false;
+        N = nn;
+        s.init(nn, -dir, is_light);
+        if (!ktBlack) s.add(mk_bx(T_STRANS, m.Kt, 0.f, n1, n2, true));
+        if (!krBlack) s.add(mk_bx(T_SREFL, m.Kr, 0.f, n1, n2, true));
+        return true;
+    }
+    default:
+        return false;
+    }
+}
+
+struct Subpath {
+    f3 origin, direction, throughput, color;
+    uint32_t depth;
+    float dVCM, dVC, dVM;
+    bool done;
+};
+
+__device__ __forceinline__ bool occluded(const DevScene& S, f3 p, f3 d, float tmax, uint32_t* stk) {
+    if (tmax < 3.f * VCM_EPS_RAY) return false;
+    return trace_any(S, p, d, VCM_EPS_RAY, tmax - 2.f * VCM_EPS_RAY, stk);
+}
+__device__ __forceinline__ void mis_on_hit(Subpath& p, float cosIn, float t) {
+    p.dVCM *= t * t;
+    p.dVCM /= cosIn;
+    p.dVC /= cosIn;
+    p.dVM /= cosIn;
+}
+/* sampleScattering (vcm.h:153-202) + updateMisTermsOnScatter (mis.h:110-160) */
+__device__ inline void sample_scattering(Subpath& p, f3 hit, const VBsdf& bs, const VcmConsts& c, Rng& rs) {
+    const float contProb = bs.cont;
+    const float rrSample = rnd(rs);
+    if (contProb < rrSample) { p.done = true; return; }
+    float pdf = 0.f, cosOut = 0.f;
+    const float s0 = rnd(rs);
+    const float s1 = rnd(rs);
+    const float s2 = rnd(rs);
+    uint32_t ev = 0;
+    const f3 f = bs.sample_f(s0, s1, s2, p.direction, pdf, cosOut, ev);
+    if (iszero(f)) return;
+    float rev = pdf;
+    if (!bx_match(ev, BX_SPECULAR)) rev = bs.pdf_rev(p.direction);
+    pdf *= contProb;
+    rev *= contProb;
+    if (ev & BX_SPECULAR) {
+        p.dVCM = 0.f;
+        p.dVC *= cosOut;
+        p.dVM *= cosOut;
+    } else {
+        const float g = cosOut / pdf;
+        p.dVC = g * (p.dVC * rev + p.dVCM + c.misVm);
+        p.dVM = g * (p.dVM * rev + p.dVCM * c.misVc * 1.f + 1.f);
+        p.dVCM = 1.f / pdf;
+    }
+    p.throughput = p.throughput * (f * (cosOut / pdf));
+    p.origin = hit;
+}
+
+/* connectCameraT1 (vcm.h:52-150) */
+__device__ inline void connect_camera(const DevScene& S, const Subpath& L, const VBsdf& bs, f3 hit,
+                                      const VcmConsts& c, float* splat, uint32_t* stk) {
+    f3 dirToCamera = c.eye - hit;
+    if (dot(c.lookdir, -dirToCamera) <= 0.f) return;
+    const float distance = length(dirToCamera);
+    dirToCamera = dirToCamera / distance;
+    const float cosAtCamera = dot(c.lookdirN, -dirToCamera);
+    const float ipd = c.lookdirLen / cosAtCamera;
+    const f3 ippw = c.eye + (-dirToCamera) * ipd;
+    const f3 ipc = c.eye + c.lookdir;
+    const f3 c2p = ippw - ipc;
+    const float pu = dot(c2p, c.unitU);
+    const float pv = dot(c2p, c.unitV);
+    if (!(2.f * fabsf(pu) < c.ipsx && 2.f * fabsf(pv) < c.ipsy)) return;
+    const float pcx = (pu + 0.5f * c.ipsx) / c.ipsx;
+    const float pcy = (pv + 0.5f * c.ipsy) / c.ipsy;
+    uint32_t ix = orx_f2u_sat(pcx * (float)c.W), iy = orx_f2u_sat(pcy * (float)c.H);
+    ix = ix > c.W - 1 ? c.W - 1 : ix;
+    iy = iy > c.H - 1 ? c.H - 1 : iy;
+    float cosToCamera = 0.f, dpdf, rpdf;
+    const f3 f = bs.vcm_f(dirToCamera, cosToCamera, dpdf, rpdf);
+    if (iszero(f)) return;
+    rpdf *= bs.cont;
+    const float i2s = (ipd * ipd) / cosAtCamera;
+    const float pixelArea = c.psfx * c.ipsx * c.psfx * c.ipsy;
+    const float imageSamplePdfA = 1.f / pixelArea;
+    const float cameraPdfW = imageSamplePdfA * i2s;
+    const float cameraPdfA = cameraPdfW * fabsf(cosToCamera) / (distance * distance);
+    const float wLight = (cameraPdfA / (float)c.count) * (c.misVm + L.dVCM + L.dVC * rpdf);
+    const float misWeight = 1.f / (wLight + 1.f);
+    const float conv = 1.f / cameraPdfA;
+    const f3 contrib = ((L.throughput * misWeight) * f) / ((float)c.count * conv);
+    if (!occluded(S, hit, dirToCamera, distance, stk)) {
+        float* o = splat + 3 * ((size_t)iy * c.W + ix);
+        unsafeAtomicAdd(o + 0, contrib.x);
+        unsafeAtomicAdd(o + 1, contrib.y);
+        unsafeAtomicAdd(o + 2, contrib.z);
+    }
+}
+
+/* lightPass (VCMLightPass.cu:52-93), initLightPayload (:120-176), lightHit (vcm.h:210-309) */
+template <bool ESTIMATE>
+__global__ __launch_bounds__(64) void k_vcm_light(DevScene S, VcmBufs vb, VcmConsts c) {
+    ORX_STACK_DECL;
+    uint32_t* stk = ORX_STACK_PTR;
+    const uint32_t p = blockIdx.x * 64u + threadIdx.x;
+    if (p >= c.count) return;
+    const uint32_t x = p % c.W, y = p / c.W;
+    const size_t slot = (size_t)y * vb.RW + x;
+    Rng rs = rng_load(vb.rng, slot);
+    uint32_t nverts = 0;
+    Subpath L;
+    L.throughput = mk1(1.f);
+    L.color = mk1(0.f);
+    L.depth = 0;
+    L.done = false;
+    int li = 0;
+    if (1 < S.nl) {
+        const float s = rnd(rs);
+        li = (int)(s * (float)S.nl);
+        li = li > (int)S.nl - 1 ? (int)S.nl - 1 : li;
+    }
+    const DevLight& light = S.lights[li];
+    const float lightPickPdf = 1.f / (float)S.nl;
+    float emissionPdfW, directPdfW, cosAtLight;
+    f3 radiance;
+    {   /* lightEmit (helpers/light.h:84-138) */
+        const float dx = rnd(rs), dy = rnd(rs);
+        if (light.type == LIGHT_AREA) {
+            const float px = rnd(rs), py = rnd(rs);
+            L.origin = light.position + light.v1 * px + light.v2 * py;
+            const float theta = orx_acosf(sqrtf(dx));
+            const float phi = 2.0f * ORX_PI_F * dy;
+            const float st = orx_sinf(theta);
+            const float xs = st * orx_cosf(phi);
+            float ys = orx_cosf(theta);
+            const float zs = st * orx_sinf(phi);
+            f3 U, V;
+            create_coordinate_system(light.normal, U, V);
+            if (ys < VCM_EPS_COSINE) ys = VCM_EPS_COSINE;
+            emissionPdfW = ys * ORX_1_PI_F;
+            cosAtLight = ys;
+            L.direction = normalize(U * xs + light.normal * ys + V * zs);
+            emissionPdfW *= light.inverseArea;
+            directPdfW = light.inverseArea;
+            radiance = light.Lemit * cosAtLight;
+        } else {
+            L.origin = light.position;
+            f3 toC = mk(S.bs_cx, S.bs_cy, S.bs_cz) - light.position;
+            const float dist = length(toC);
+            toC = toC / dist;
+            if (S.bs_r < dist) {
+                const float theta = orx_asinf(S.bs_r / dist);
+                f3 U, V;
+                create_coordinate_system(toC, U, V);
+                const float cosTheta = orx_cosf(theta);
+                const float z = cosTheta + (1.f - cosTheta) * dx;
+                const float phi = 2 * ORX_PI_F * dy;
+                const float rr = sqrtf(1.f - z * z);
+                const float xx = rr * orx_cosf(phi);
+                const float yy = rr * orx_sinf(phi);
+                emissionPdfW = 1.f / (2.f * ORX_PI_F * (1.f - cosTheta));
+                L.direction = normalize(U * xx + toC * z + V * yy);
+            } else {
+                L.direction = sample_unit_sphere(dx, dy);
+                emissionPdfW = 0.25f * ORX_1_PI_F;
+            }
+            directPdfW = 1.f;
+            cosAtLight = 1.f;
+            radiance = light.Lemit;
+        }
+    }
+    emissionPdfW *= lightPickPdf;
+    directPdfW *= lightPickPdf;
+    L.throughput = radiance / emissionPdfW;
+    L.dVCM = directPdfW / emissionPdfW;
+    L.dVC = light.type == LIGHT_AREA ? cosAtLight / emissionPdfW : 0.f;
+    L.dVM = L.dVC * c.misVc;
+
+    for (;;) {
+        Hit h;
+        if (!trace_closest(S, L.origin, L.direction, VCM_RAY_LEN_MIN, RT_DEFAULT_MAX, h, stk)) break;
+        const uint32_t mi = prim_material(S, h);
+        const DevMaterial& m = S.mats[mi];
+        const f3 hit = L.origin + L.direction * h.t;
+        if (m.type == MAT_EMITTER) break;
+        VBsdf bs;
+        f3 N;
+        if (!material_bsdf(m, geometric_normal(S, h), L.direction, true, bs, N)) break;
+        L.depth++;
+        const float cosIn = dot(N, -L.direction);
+        if (cosIn < VCM_EPS_COSINE) break;
+        mis_on_hit(L, cosIn, h.t);
+        const bool spec = bs.is_specular();
+        if (!spec) {
+            const uint32_t k = nverts++;
+            if (!ESTIMATE && k < VCM_MAX_VERTS) {
+                const size_t o = (size_t)k * c.count + p;
+                vb.vA[o] = make_float4(hit.x, hit.y, hit.z, __uint_as_float(mi));
+                vb.vB[o] = make_float4(L.throughput.x, L.throughput.y, L.throughput.z, L.dVCM);
+                vb.vC[o] = make_float4(N.x, N.y, N.z, L.dVC);
+                vb.vD[o] = make_float4(bs.fix.x, bs.fix.y, bs.fix.z, L.dVM);
+            }
+            if (!ESTIMATE) connect_camera(S, L, bs, hit, c, vb.splat, stk);
+        }
+        if (c.maxPathLen < L.depth + 2) break;
+        sample_scattering(L, hit, bs, c, rs);
+        if (L.done) break;
+    }
+    vb.vcount[p] = nverts;
+    rng_store(vb.rng, slot, rs);
+}
+
+/* connectVertices (vcm.h:315-400) against light vertex k of this subpath */
+__device__ inline void connect_vertex(const DevScene& S, Subpath& C, const VBsdf& cb, f3 hit, const VcmBufs& vb,
+                                      size_t o, const VcmConsts& c, uint32_t* stk) {
+    const float4 A = vb.vA[o];
+    f3 direction = mk(A.x, A.y, A.z) - hit;
+    const float dist2 = dot(direction, direction);
+    const float distance = sqrtf(dist2);
+    direction = direction / distance;
+    float camCos = 0.f, cDir, cRev;
+    const f3 camF = cb.vcm_f(direction, camCos, cDir, cRev);
+    if (iszero(camF)) return;
+    cDir *= cb.cont;
+    cRev *= cb.cont;
+    const float4 Cn = vb.vC[o];
+    const float4 D = vb.vD[o];
+    const DevMaterial& m = S.mats[__float_as_uint(A.w)];
+    VBsdf lb;
+    const f3 N = mk(Cn.x, Cn.y, Cn.z);
+    lb.dg = frame_from_normal(N);
+    lb.gn = N;
+    lb.fix_is_light = true;
+    lb.fix = mk(D.x, D.y, D.z);
+    lb.n = 0;
+    lb.cont = 0.f;
+    lb.add(mk_bx(T_LAMBERT, m.Kd));
+    if (m.type == MAT_GLOSSY) lb.add(mk_bx(T_PHONG, m.Ks, m.exponent));
+    float lightCos = 0.f, lDir, lRev;
+    const f3 lightF = lb.vcm_f(-direction, lightCos, lDir, lRev);
+    if (iszero(lightF)) return;
+    lDir *= lb.cont;
+    lRev *= lb.cont;
+    const float geometryTerm = lightCos * camCos / dist2;
+    if (geometryTerm < 0.f) return;
+    const float camDirPdfA = cDir * fabsf(camCos) / (distance * distance);
+    const float lightDirPdfA = lDir * fabsf(lightCos) / (distance * distance);
+    const float4 B = vb.vB[o];
+    const float wLight = camDirPdfA * (c.misVm * 1.f + B.w + Cn.w * lRev);
+    const float wCamera = lightDirPdfA * (c.misVm * 1.f + C.dVCM + C.dVC * cRev);
+    const float misWeight = 1.f / (wLight + 1.f + wCamera);
+    f3 contrib = ((camF * geometryTerm) * lightF) * 1.f;
+    contrib = contrib * ((C.throughput * misWeight) * mk(B.x, B.y, B.z));
+    if (occluded(S, hit, direction, distance, stk)) return;
+    C.color = C.color + contrib;
+}
+
+/* connectLightSourceS1 (vcm.h:406-488) + lightIlluminate (helpers/light.h:141-203) */
+__device__ inline void connect_light(const DevScene& S, Subpath& C, const VBsdf& cb, f3 hit, const VcmConsts& c,
+                                     Rng& rs, uint32_t* stk) {
+    int li = 0;
+    if (1 < S.nl) {
+        const float s = rnd(rs);
+        li = (int)(s * (float)S.nl);
+        li = li > (int)S.nl - 1 ? (int)S.nl - 1 : li;
+    }
+    const DevLight& light = S.lights[li];
+    const float lightPickProb = 1.f / (float)S.nl;
+    float emissionPdfW, directPdfW, cosAtLight, distance;
+    f3 dirToLight;
+    if (light.type == LIGHT_AREA) {
+        const float px = rnd(rs), py = rnd(rs);
+        const f3 pl = light.position + light.v1 * px + light.v2 * py;
+        dirToLight = pl - hit;
+        distance = length(dirToLight);
+        dirToLight = dirToLight / distance;
+        const float cosThetaLight = dot(light.normal, -dirToLight);
+        if (cosThetaLight < VCM_EPS_COSINE) return;
+        directPdfW = light.inverseArea * (distance * distance) / cosThetaLight;
+        cosAtLight = cosThetaLight;
+        emissionPdfW = light.inverseArea * cosThetaLight * ORX_1_PI_F;
+    } else {
+        dirToLight = light.position - hit;
+        distance = length(dirToLight);
+        dirToLight = dirToLight / distance;
+        const f3 toC = mk(S.bs_cx, S.bs_cy, S.bs_cz) - light.position;
+        const float d = length(toC);
+        if (S.bs_r < d) {
+            const float theta = orx_asinf(S.bs_r / d);
+            emissionPdfW = 1.f / (2.f * ORX_PI_F * (1.f - orx_cosf(theta)));
+        } else {
+            emissionPdfW = 0.25f * ORX_1_PI_F;
+        }
+        directPdfW = distance * distance;
+        cosAtLight = 1.f;
+    }
+    const f3 radiance = light.Lemit;
+    if (iszero(radiance)) return;
+    float cosToLight = 0.f, bDir, bRev;
+    const f3 f = cb.vcm_f(dirToLight, cosToLight, bDir, bRev);
+    if (iszero(f)) return;
+    bDir *= light.type != LIGHT_AREA ? 0.f : cb.cont;
+    bRev *= cb.cont;
+    const float wLight = bDir / (lightPickProb * directPdfW);
+    const float wCamera = (emissionPdfW * cosToLight / (directPdfW * cosAtLight)) * (c.misVm + C.dVCM + C.dVC * bRev);
+    const float misWeight = 1.f / (wLight + 1.f + wCamera);
+    const f3 contrib = (radiance * f) * (misWeight * cosToLight / (lightPickProb * directPdfW));
+    if (iszero(contrib)) return;
+    if (occluded(S, hit, dirToLight, distance, stk)) return;
+    C.color = C.color + contrib * C.throughput;
+}
+
+/* cameraPass (VCMCameraPass.cu:48-80), initCameraPayload (:100-135), cameraHit (vcm.h:527-628) */
+__global__ __launch_bounds__(64) void k_vcm_camera(DevScene S, VcmBufs vb, VcmConsts c) {
+    ORX_STACK_DECL;
+    uint32_t* stk = ORX_STACK_PTR;
+    const uint32_t tilesX = (c.W + 7) / 8;
+    const uint32_t x = (blockIdx.x % tilesX) * 8 + (threadIdx.x & 7);
+    const uint32_t y = (blockIdx.x / tilesX) * 8 + (threadIdx.x >> 3);
+    if (x >= c.W || y >= c.H) return;
+    const uint32_t p = x + y * c.W;
+    const size_t slot = (size_t)y * vb.RW + x;
+    Rng rs = rng_load(vb.rng, slot);
+    Subpath C;
+    C.throughput = mk1(1.0f);
+    C.color = mk1(0.f);
+    C.depth = 0;
+    C.done = false;
+    C.dVC = 0.f;
+    C.dVM = 0.f;
+    const float sx = rnd(rs), sy = rnd(rs);
+    const float dx = ((float)x + sx) / (float)c.W * 2.0f - 1.0f;
+    const float dy = ((float)y + sy) / (float)c.H * 2.0f - 1.0f;
+    C.origin = c.eye;
+    C.direction = normalize(c.u * dx + c.v * dy + c.lookdir);
+    const float cosAtCamera = dot(c.lookdirN, C.direction);
+    const float ipd = c.lookdirLen / cosAtCamera;
+    const float i2s = (ipd * ipd) / cosAtCamera;
+    const float pixelArea = c.psfx * c.ipsx * c.psfx * c.ipsy;
+    const float areaSamplePdf = 1.f / pixelArea;
+    const float cameraPdfW = areaSamplePdf * i2s;
+    C.dVCM = (float)c.count / cameraPdfW;
+    const uint32_t nverts = vb.vcount[p];
+    for (;;) {
+        Hit h;
+        if (!trace_closest(S, C.origin, C.direction, VCM_RAY_LEN_MIN, RT_DEFAULT_MAX, h, stk)) break;
+        const DevMaterial& m = S.mats[prim_material(S, h)];
+        const f3 hit = C.origin + C.direction * h.t;
+        if (m.type == MAT_EMITTER) { /* DiffuseEmitter.cu:95-120 + connectLightSourceS0 (vcm.h:493-522) */
+            C.depth++;
+            if (iszero(m.Lemit)) break;
+            const f3 N = geometric_normal(S, h);
+            if (dot(N, -C.direction) < 0.f) break;
+            const float lightPickProb = 1.f / (float)S.nl;
+            float directPdfA = m.inverseArea;
+            float emissionPdfW = maxf(0.f, dot(N, -C.direction)) * ORX_1_PI_F * m.inverseArea;
+            if (C.depth == 1) {
+                C.color = C.color + C.throughput * m.Lemit;
+                break;
+            }
+            directPdfA *= lightPickProb;
+            emissionPdfW *= lightPickProb;
+            const float wCamera = directPdfA * C.dVCM + emissionPdfW * C.dVC;
+            const float misWeight = 1.f / (1.f + wCamera);
+            C.color = C.color + (C.throughput * misWeight) * m.Lemit;
+            break;
+        }
+        VBsdf bs;
+        f3 N;
+        if (!material_bsdf(m, geometric_normal(S, h), C.direction, false, bs, N)) break;
+        C.depth++;
+        const float cosIn = dot(N, -C.direction);
+        if (cosIn < VCM_EPS_COSINE) break;
+        mis_on_hit(C, cosIn, h.t);
+        if (!bs.is_specular()) {
+            connect_light(S, C, bs, hit, c, rs, stk);
+            const uint32_t nv = nverts < VCM_MAX_VERTS ? nverts : VCM_MAX_VERTS;
+            for (uint32_t k = 0; k < nv; ++k) connect_vertex(S, C, bs, hit, vb, (size_t)k * c.count + p, c, stk);
+        }
+        if (c.maxPathLen <= C.depth) break;
+        sample_scattering(C, hit, bs, c, rs);
+        if (C.done) break;
+    }
+    const size_t o3 = 3 * (size_t)p;
+    vb.cam[o3 + 0] = C.color.x;
+    vb.cam[o3 + 1] = C.color.y;
+    vb.cam[o3 + 2] = C.color.z;
+    const float ox = vb.output[o3 + 0] + vb.splat[o3 + 0];
+    const float oy = vb.output[o3 + 1] + vb.splat[o3 + 1];
+    const float oz = vb.output[o3 + 2] + vb.splat[o3 + 2];
+    vb.output[o3 + 0] = ox + C.color.x;
+    vb.output[o3 + 1] = oy + C.color.y;
+    vb.output[o3 + 2] = oz + C.color.z;
+    rng_store(vb.rng, slot, rs);
+}
+
+void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c, bool estimate) {
+    const uint32_t blocks = (c.count + 63) / 64;
+    if (estimate) hipLaunchKernelGGL(k_vcm_light<true>, dim3(blocks), dim3(64), 0, s, S, vb, c);
+    else hipLaunchKernelGGL(k_vcm_light<false>, dim3(blocks), dim3(64), 0, s, S, vb, c);
+}
+void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
+    const uint32_t blocks = ((c.W + 7) / 8) * ((c.H + 7) / 8);
+    hipLaunchKernelGGL(k_vcm_camera, dim3(blocks), dim3(64), 0, s, S, vb, c);
+}
+
+}  // namespace orx

@@ -149,6 +149,12 @@ def PointLight(power, position):
     return Light(_abi.LIGHT_POINT, np.broadcast_to(np.float32(power), 3).copy(), np.float32(position))
 
 
+def SpotLight(power, position, direction, angle):
+    """Light::Light spot ctor (renderer/Light.cpp:39-49); angle in degrees."""
+    return Light(_abi.LIGHT_SPOT, np.broadcast_to(np.float32(power), 3).copy(), np.float32(position),
+                 direction=np.float32(direction), angle=float(angle))
+
+
 class Scene:
     """Flat scene: what IScene::getSceneRootGroup + getSceneLights + getSceneAABB
     hand to OptixRenderer::initScene (OptixRenderer.cpp:436-485)."""

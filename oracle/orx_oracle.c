@@ -238,6 +238,11 @@ struct orc_renderer {
     /* grid state */
     uint32_t gsize[3]; float cell; v3 origo; uint32_t ncells; uint32_t valid;
     uint64_t sum_photons_visited, sum_cells_visited;
+    /* VCM: pixelSizeFactor (OptixRenderer.cpp:306, :846), LVC-estimated flag (:83, :461, :847) */
+    float psf_x, psf_y;
+    int vcm_estimated;
+    size_t vcm_npx;
+    uint32_t* vcount; float* vverts; v3* vsplat; v3* vcam;
 };
 
 static orx_status fail(orc_renderer* r, orx_status s, const char* msg) {
@@ -262,6 +267,7 @@ orx_status orc_create(const orx_config* cfg, orc_renderer** out) {
     if (cfg) r->cfg = *cfg;
     else orc_default_config(&r->cfg);
     r->W = 10; r->H = 10; /* OptixRenderer ctor m_width(10), m_height(10) */
+    r->psf_x = 1.0f; r->psf_y = 1.0f;
     r->world = 1;
     *out = r;
     return ORX_OK;
@@ -281,6 +287,8 @@ static void free_frame(orc_renderer* r) {
     free(r->offsets); free(r->hist); free(r->indirect); free(r->direct); free(r->output); free(r->dbg);
     r->rng = NULL; r->hp = NULL; r->photons = NULL; r->keys = NULL; r->sort_tmp = NULL;
     r->offsets = NULL; r->hist = NULL; r->indirect = NULL; r->direct = NULL; r->output = NULL; r->dbg = NULL;
+    free(r->vcount); free(r->vverts); free(r->vsplat); free(r->vcam);
+    r->vcount = NULL; r->vverts = NULL; r->vsplat = NULL; r->vcam = NULL; r->vcm_npx = 0;
 }
 void orc_destroy(orc_renderer* r) {
     if (!r) return;
@@ -467,6 +475,7 @@ orx_status orc_init_scene(orc_renderer* r, const orx_scene* s) {
     v3 center = scl(add(r->aabb_min, r->aabb_max), 0.5f);
     r->bs_center = center;
     r->bs_radius = vector3_buggy_length(sub(r->aabb_max, center));
+    r->vcm_estimated = 0;
     r->scene_ready = 1;
     return ORX_OK;
 }
@@ -670,7 +679,7 @@ int32_t orc_trace_any(orc_renderer* r, const float o[3], const float d[3], float
 /* ------------------------------------------------------------------ */
 /* camera (renderer/Camera.cpp:333-345)                                */
 /* ------------------------------------------------------------------ */
-typedef struct { v3 eye, lookdir, u, v; float aperture; } cam_t;
+typedef struct { v3 eye, lookdir, u, v; float aperture, ulen, vlen; } cam_t;
 
 static float dtor(float d) { return d * ((float)M_PI / 180.f); } /* Camera.cpp:87-90 */
 
@@ -688,6 +697,8 @@ static cam_t camera_setup(const orx_camera* c) {
     float vlen = lookdir_len * tanf(dtor(c->vfov * 0.5f));
     k.v = scl(cv, vlen);
     k.aperture = c->aperture;
+    k.ulen = ulen; /* imagePlaneSize = 2 * (ulen, vlen), Camera.cpp:344 */
+    k.vlen = vlen;
     return k;
 }
 void orc_camera_setup(const orx_camera* cam, float lookdir[3], float u[3], float v[3]) {
@@ -1330,12 +1341,19 @@ static void pt_pass(orc_renderer* r, const cam_t* cam, uint64_t local) {
     }
 }
 
+#include "orx_oracle_vcm.c.inc"
+
 /* ------------------------------------------------------------------ */
 /* OptixRenderer::renderNextIteration (OptixRenderer.cpp:507-821)     */
 /* ------------------------------------------------------------------ */
 static orx_status begin_iteration(orc_renderer* r, uint64_t local, const orx_request* det) {
     if (!r->scene_ready) return fail(r, ORX_ERR_STATE, "Traced before OptixRenderer was initialized.");
     if (det->width == 0 || det->height == 0) return fail(r, ORX_ERR_INVALID_ARGUMENT, "zero-sized request");
+    if (det->width != r->W || det->height != r->H) { /* resizeBuffers (OptixRenderer.cpp:826-848) */
+        r->psf_x = 1.0f / (float)det->width;
+        r->psf_y = 1.0f / (float)det->height;
+        r->vcm_estimated = 0;
+    }
     if (det->width != r->W || det->height != r->H || !r->rng_ready) {
         orx_status s = resize(r, det->width, det->height);
         if (s != ORX_OK) return s;
@@ -1351,13 +1369,18 @@ orx_status orc_render_next_iteration(orc_renderer* r, uint64_t iter, uint64_t lo
     if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
     if (det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world > 1)
         return fail(r, ORX_ERR_STATE, "sharded PPM runs through the phase API");
-    if (det->method != ORX_METHOD_PATH_TRACING && det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
+    if (det->method == ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING && r->world > 1)
+        return fail(r, ORX_ERR_UNSUPPORTED, "VCM is single-device");
+    if (det->method != ORX_METHOD_PATH_TRACING && det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING &&
+        det->method != ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING)
         return fail(r, ORX_ERR_UNSUPPORTED, "oracle: method not implemented");
     orx_status s0 = begin_iteration(r, local, det);
     if (s0 != ORX_OK) return s0;
     cam_t cam = camera_setup(&det->camera);
     if (det->method == ORX_METHOD_PATH_TRACING) {
         pt_pass(r, &cam, local);
+    } else if (det->method == ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING) {
+        return vcm_iteration(r, det, ppmRadius);
     } else {
         ppm_eye_pass(r, &cam);
         const float ppmRadiusSquared = ppmRadius * ppmRadius;
@@ -1449,6 +1472,9 @@ orx_status orc_read_buffer(orc_renderer* r, int32_t id, void* dst, size_t bytes,
     case ORX_BUF_GRID_OFFSETS: need = ((size_t)r->ncells + 1) * 4; break;
     case ORX_BUF_INDIRECT: case ORX_BUF_DIRECT: case ORX_BUF_OUTPUT: need = npx * 12; break;
     case ORX_BUF_DEBUG_VISITED: need = npx * 8; break;
+    case ORX_BUF_VCM_VERTEX_COUNT: need = r->vcm_npx * 4; break;
+    case ORX_BUF_VCM_VERTICES: need = r->vcm_npx * VCM_MAX_VERTS * 64; break;
+    case ORX_BUF_VCM_SPLAT: case ORX_BUF_VCM_CAMERA: need = r->vcm_npx * 12; break;
     default: return fail(r, ORX_ERR_INVALID_ARGUMENT, "unknown buffer id");
     }
     if (out_bytes) *out_bytes = need;
@@ -1473,6 +1499,10 @@ orx_status orc_read_buffer(orc_renderer* r, int32_t id, void* dst, size_t bytes,
     case ORX_BUF_DIRECT: memcpy(dst, r->direct, need); break;
     case ORX_BUF_OUTPUT: memcpy(dst, r->output, need); break;
     case ORX_BUF_DEBUG_VISITED: memcpy(dst, r->dbg, need); break;
+    case ORX_BUF_VCM_VERTEX_COUNT: memcpy(dst, r->vcount, need); break;
+    case ORX_BUF_VCM_VERTICES: memcpy(dst, r->vverts, need); break;
+    case ORX_BUF_VCM_SPLAT: memcpy(dst, r->vsplat, need); break;
+    case ORX_BUF_VCM_CAMERA: memcpy(dst, r->vcam, need); break;
     }
     return ORX_OK;
 }
