@@ -159,6 +159,8 @@ def bench_main(args, metric):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if getattr(args, "method", "ppm") != "ppm":
+        raise SystemExit("the sharded bench runs PPM (VCM and PT shard trivially by rows; see DESIGN.md)")
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # RCCL prints its version banner on fd 1: keep stdout for the one JSON line
     json_out = os.fdopen(os.dup(1), "w")
@@ -203,26 +205,33 @@ def bench_main(args, metric):
     t_max = float(t.item())
     st = r.stats()
     if rank == 0:
+        from . import roofline
         paths = W * H + P * P * world
-        per_pass = {name: st.pass_ms[i] / max(1, st.timed_iterations) for i, name in enumerate(_abi.PASS_NAMES)}
-        gms = per_pass["ppm_gather"]
-        valid_avg = st.valid_photons_total / max(1, st.timed_iterations)
-        gbytes = W * H * (40 + 12) + valid_avg * 36 + (st.num_cells + 1) * 4
-        achieved = gbytes / (gms * 1e-3) / 1e9 if gms > 0 else 0.0
+        n_it = max(1, st.timed_iterations)
+        per_pass = {name: st.pass_ms[i] / n_it for i, name in enumerate(_abi.PASS_NAMES)}
+        per_pass = {k: v for k, v in per_pass.items() if v > 0}
+        dominant = max(per_pass, key=per_pass.get)
+        valid_avg = st.valid_photons_total / n_it
+        # rank 0's passes: its own photon batch, its pixel rows (eye/direct), all pixels (gather)
+        pb = roofline.pass_bytes(_abi.PROGRESSIVE_PHOTON_MAPPING, W, H, P * P, valid_avg, st.num_cells)
+        rows0 = local_rows(H, 0, world)
+        for k in ("ppm_eye", "ppm_direct_output"):
+            pb[k] = pb[k] * rows0 / H
+        roof = roofline.roofline(dominant, pb[dominant], per_pass[dominant], None)
         out = {
             "metric": metric, "value": round(paths * args.steps / t_max / 1e6, 3), "unit": "Mpaths/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t_max * 1e3 / args.steps, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic (built-in Cornell scene, seeded XORWOW streams)",
+            "vs_baseline": None, "dtype": "f32",
+            "data": f"synthetic: seeded procedural scene ({scene.name}), XORWOW streams seeded 1645301512",
             "config": {"workload": f"{scene.name} {W}x{H} PPM, {P * P} photons/iter per GPU (weak scaling)",
                        "scene": scene.name, "width": W, "height": H, "photons_per_iteration": P * P * world,
                        "paths_per_iteration": paths,
                        "parallelism": f"row-interleaved RNG/pixel/photon ownership x{world}, "
                                       "RCCL all_gather(hitpoints) + reduce_scatter(indirect)"},
-            "roofline": {"kernel": "k_ppm_gather", "bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0,
-                         "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": None,
-                         "bytes_per_launch": int(gbytes), "avg_launch_ms": round(gms, 4)},
-            "passes_ms": {k: round(v, 4) for k, v in per_pass.items() if v > 0},
+            "roofline": roof,
+            "passes": {k: round(v, 4) for k, v in per_pass.items()},
+            "dominant_pass": dominant,
         }
         print(json.dumps(out), file=json_out, flush=True)
     r.destroy()

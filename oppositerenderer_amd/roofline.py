@@ -1,0 +1,83 @@
+"""Algorithmic HBM bytes per pass launch (DESIGN.md "Roofline"), the units the
+bench's `roofline.achieved` is computed from.
+
+"Algorithmic" = the bytes the pass must move at minimum with this data
+layout: every input read once, every output written once.  BVH node and
+triangle fetches and cache re-reads (a gather visits a grid photon once per
+overlapping pixel) are not algorithmic; they show up in the PMC traffic.
+SURVEY.md 8(d) prices the gather's visited photons (V x 36 B) as HBM bytes;
+on MI355X those re-reads are served by L2/MALL (PMC FETCH_SIZE evidences it),
+so the roofline here counts each resident photon once and reports V x 36 B
+separately as `visited_photon_GBps`.
+"""
+from __future__ import annotations
+
+from . import _abi
+
+R_RNG = 24            # XORWOW state: v0..v4, d (six dword planes); read + written per use
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+KERNELS_OF_PASS = {
+    "ppm_eye": ["k_ppm_eye"],
+    "ppm_photon": ["k_ppm_photon"],
+    "grid_hash": ["k_grid_setup", "k_grid_hash"],
+    "grid_scan": ["k_scan_reduce", "k_scan_partials", "k_scan_apply"],
+    "grid_scatter": ["k_grid_scatter"],
+    "ppm_gather": ["k_ppm_gather", "k_ppm_gather_coop"],
+    "ppm_direct_output": ["k_ppm_direct_output"],
+    "pt": ["k_pt"],
+    "vcm_light": ["k_vcm_light"],
+    "vcm_camera": ["k_vcm_camera"],
+}
+
+
+def paths_per_iteration(method: int, W: int, H: int, photons: int) -> int:
+    """PT W*H; PPM W*H eye + emitted photon paths; VCM 2*W*H."""
+    if method == _abi.PROGRESSIVE_PHOTON_MAPPING:
+        return W * H + photons
+    if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING:
+        return 2 * W * H
+    return W * H
+
+
+def pass_bytes(method: int, W: int, H: int, photons: int, valid: float = 0.0, cells: int = 0,
+               light_vertices: float = 0.0) -> dict:
+    """Bytes per launch of each pass.
+
+    valid: grid-resident photons (deposits with power > 0); cells: grid cells G;
+    light_vertices: stored VCM light vertices per iteration."""
+    N = W * H
+    R2 = 2 * R_RNG
+    if method == _abi.PROGRESSIVE_PHOTON_MAPPING:
+        return {
+            # RNG RMW + one 40 B hitpoint (pos|flags 16, normal-or-radiance|atten.x 16, atten.yz 8)
+            "ppm_eye": N * (R2 + 40),
+            # RNG RMW + 1 B deposit mask per emitted photon + 36 B per stored deposit
+            "ppm_photon": photons * (R2 + 1) + valid * 36,
+            # mask per emitted photon, position 12 B read, key + rank 8 B written, histogram 4 B per photon
+            "grid_hash": photons * 1 + valid * (12 + 8 + 4),
+            # histogram read + zeroed, offsets written
+            "grid_scan": (cells + 2) * 12,
+            # key + rank read, photon 36 B read + written, offset read
+            "grid_scatter": valid * (8 + 36 + 36 + 4),
+            # hitpoint 40 B + indirect 12 B per pixel, each grid photon once, offset table once
+            "ppm_gather": N * (40 + 12) + valid * 36 + (cells + 1) * 4,
+            # hitpoint, RNG RMW, indirect read, direct written, output read + written
+            "ppm_direct_output": N * (40 + R2 + 12 + 12 + 24),
+        }
+    if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING:
+        return {
+            # RNG RMW, vertex count, 64 B per stored light vertex
+            "vcm_light": N * (R2 + 4) + light_vertices * 64,
+            # RNG RMW, vertex count, splat read, camera colour, output RMW, every stored vertex read once
+            "vcm_camera": N * (R2 + 4 + 12 + 12 + 24) + light_vertices * 64,
+        }
+    return {"pt": N * (R2 + 24)}
+
+
+def roofline(pass_name: str, bytes_per_launch: float, ms_per_launch: float, traffic=None) -> dict:
+    achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9 if ms_per_launch > 0 else 0.0
+    return {"kernel": "+".join(KERNELS_OF_PASS.get(pass_name, [pass_name])), "pass": pass_name, "bound": "hbm",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(ms_per_launch, 4)}
