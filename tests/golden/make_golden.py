@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Regenerate the golden fixtures from the CPU oracle (test infrastructure).
+
+The reference ships no fixtures and cannot run here, so these pin
+the oracle against drift: any change to the restatement that alters a result
+shows up as a fixture mismatch.  Each case: seed 1645301512 (config.h:50),
+small image, two iterations.  Usage: python tests/golden/make_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import oracle_lib  # noqa: E402
+from oppositerenderer_amd import _abi, scenes  # noqa: E402
+from oppositerenderer_amd.renderer import next_ppm_radius  # noqa: E402
+
+SEED = 1645301512
+CASES = {
+    # name: (scene, method, W, H, photon launch, iterations, buffers)
+    "cornell_pt": ("Cornell", _abi.PATH_TRACING, 32, 32, 32, 2, ["RNG", "OUTPUT"]),
+    "cornell_ppm": ("Cornell", _abi.PROGRESSIVE_PHOTON_MAPPING, 32, 32, 64, 2,
+                    ["RNG", "HITPOINTS", "GRID_OFFSETS", "DIRECT", "INDIRECT", "OUTPUT"]),
+    "cornellsmall_spheres_ppm": ("CornellSmallSmallSpheres", _abi.PROGRESSIVE_PHOTON_MAPPING, 24, 24, 48, 2,
+                                 ["RNG", "GRID_OFFSETS", "DIRECT", "INDIRECT", "OUTPUT"]),
+    "cornellsmall_spheres_vcm": ("CornellSmallSmallSpheres", _abi.VCM_BIDIRECTIONAL_PATH_TRACING, 24, 24, 32, 2,
+                                 ["RNG", "VCM_VERTEX_COUNT", "VCM_CAMERA", "VCM_SPLAT", "OUTPUT"]),
+    "cornellsmall_glossy_vcm": ("CornellSmallLargeSphere", _abi.VCM_BIDIRECTIONAL_PATH_TRACING, 24, 24, 32, 2,
+                                ["RNG", "VCM_VERTEX_COUNT", "VCM_CAMERA", "VCM_SPLAT", "OUTPUT"]),
+}
+INT_BUFFERS = {"RNG", "GRID_OFFSETS", "VCM_VERTEX_COUNT"}
+
+
+def render(case, renderer_factory):
+    scene_name, method, W, H, P, iters, bufs = CASES[case]
+    scene = scenes.scene_by_name(scene_name)
+    r = renderer_factory(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P), scene)
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    req = _abi.OrxRequest()
+    req.camera = cam.to_abi()
+    req.method, req.width, req.height, req.ppm_alpha = method, W, H, 2.0 / 3.0
+    radius = scene.initial_ppm_radius()
+    for it in range(iters):
+        r.render_next_iteration(it, it, radius, req)
+        radius = next_ppm_radius(radius, it)
+    out = {}
+    for b in bufs:
+        out[b] = r.read_buffer(getattr(_abi, "BUF_" + b), np.uint32 if b in INT_BUFFERS else np.float32)
+    return r, out
+
+
+def oracle_factory(cfg, scene):
+    r = oracle_lib.OracleRenderer(cfg)
+    r.init_scene(scene)
+    return r
+
+
+def main():
+    oracle_lib.load().orc_set_threads(1)
+    for case in CASES:
+        r, out = render(case, oracle_factory)
+        r.close()
+        np.savez_compressed(os.path.join(HERE, case + ".npz"), **out)
+        print(case, {k: v.shape for k, v in out.items()})
+
+
+if __name__ == "__main__":
+    main()
