@@ -214,7 +214,7 @@ typedef struct {
     uint64_t valid_photons_total;
     uint64_t gather_staged_total;   /* cooperative gather: photons staged through LDS, summed over waves */
     uint32_t timed_iterations;   /* iterations since orx_reset_timing */
-    uint32_t pad;
+    uint32_t bvh_stack_entries;  /* LDS traversal stack depth bound of the scene's BVH4 */
     float pass_ms[16];           /* device time per orx_pass summed since orx_reset_timing */
 } orx_stats;
 orx_status orx_get_stats(orx_renderer* r, orx_stats* out);

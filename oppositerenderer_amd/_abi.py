@@ -103,7 +103,7 @@ class OrxStats(C.Structure):
                 ("photons_visited", C.c_uint64), ("cells_visited", C.c_uint64),
                 ("photons_visited_total", C.c_uint64), ("cells_visited_total", C.c_uint64),
                 ("valid_photons_total", C.c_uint64), ("gather_staged_total", C.c_uint64),
-                ("timed_iterations", C.c_uint32), ("pad", C.c_uint32), ("pass_ms", C.c_float * 16)]
+                ("timed_iterations", C.c_uint32), ("bvh_stack_entries", C.c_uint32), ("pass_ms", C.c_float * 16)]
 
 
 PASS_NAMES = ["ppm_eye", "ppm_photon", "grid_hash", "grid_scan", "grid_scatter", "ppm_gather", "ppm_direct_output",

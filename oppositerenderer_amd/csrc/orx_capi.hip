@@ -166,6 +166,104 @@ struct BvhBuilder {
     }
 };
 
+/* Collapse the binary SAH tree into the four-wide quantised BVH the kernels
+ * traverse (DevBvh4).  Each node opens its largest-area inner children until
+ * it has four; child boxes are quantised outward on an 8-bit grid per axis.
+ * `bound` = the most stack entries a traversal can hold: at a node with k
+ * children hit, k-1 are pushed before descending. */
+struct Bvh4Builder {
+    const std::vector<DevBvhNode>* b2 = nullptr;
+    std::vector<DevBvh4> out;
+    bool ok = true;
+
+    static bool leaf(const DevBvhNode& n) { return (n.count_or_right & 0x80000000u) != 0; }
+    static float area(const DevBvhNode& n) {
+        float dx = n.hi[0] - n.lo[0], dy = n.hi[1] - n.lo[1], dz = n.hi[2] - n.lo[2];
+        return dx * dy + dy * dz + dz * dx;
+    }
+    /* outward 8-bit quantisation of [clo, chi] on origin + q * 2^e */
+    static bool quantise(float origin, int e, float clo, float chi, uint32_t& qlo, uint32_t& qhi) {
+        const float sc = std::ldexp(1.0f, e);
+        auto dec = [&](uint32_t q) { return origin + (float)q * sc; };
+        double fl = std::floor(((double)clo - origin) / sc), ch = std::ceil(((double)chi - origin) / sc);
+        qlo = (uint32_t)std::min(255.0, std::max(0.0, fl));
+        qhi = (uint32_t)std::min(255.0, std::max(0.0, ch));
+        while (qlo > 0 && dec(qlo) > clo) qlo--;
+        if (dec(qlo) > clo) return false;
+        while (qhi < 255 && dec(qhi) < chi) qhi++;
+        return dec(qhi) >= chi;
+    }
+    uint32_t build(uint32_t n2, uint32_t& bound) {
+        const std::vector<DevBvhNode>& B = *b2;
+        std::vector<uint32_t> ch;
+        if (leaf(B[n2])) {
+            ch.push_back(n2);
+        } else {
+            ch = {B[n2].left_or_first, B[n2].count_or_right};
+            while (ch.size() < 4) {
+                int bi = -1;
+                float ba = -1.f;
+                for (size_t i = 0; i < ch.size(); i++)
+                    if (!leaf(B[ch[i]]) && area(B[ch[i]]) > ba) ba = area(B[ch[i]]), bi = (int)i;
+                if (bi < 0) break;
+                const uint32_t c = ch[bi];
+                ch[bi] = B[c].left_or_first;
+                ch.push_back(B[c].count_or_right);
+            }
+        }
+        DevBvh4 nd;
+        std::memset(&nd, 0, sizeof nd);
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (uint32_t c : ch)
+            for (int k = 0; k < 3; k++) lo[k] = std::min(lo[k], B[c].lo[k]), hi[k] = std::max(hi[k], B[c].hi[k]);
+        nd.ox = lo[0];
+        nd.oy = lo[1];
+        nd.oz = lo[2];
+        for (int k = 0; k < 3; k++) {
+            const float ext = hi[k] - lo[k];
+            int e = -126;
+            if (ext > 0) {
+                int ee;
+                std::frexp(ext / 255.0f, &ee);
+                e = std::max(-126, ee - 1);
+            }
+            for (;; e++) {
+                if (e > 127) { ok = false; break; }
+                bool good = true;
+                uint32_t ql[4] = {0, 0, 0, 0}, qh[4] = {0, 0, 0, 0};
+                for (size_t i = 0; i < ch.size() && good; i++)
+                    good = quantise(lo[k], e, B[ch[i]].lo[k], B[ch[i]].hi[k], ql[i], qh[i]);
+                if (!good) continue;
+                uint32_t wl = 0, wh = 0;
+                for (int i = 0; i < 4; i++) wl |= ql[i] << (8 * i), wh |= qh[i] << (8 * i);
+                nd.qlo[k] = wl;
+                nd.qhi[k] = wh;
+                nd.exps |= (uint32_t)(e + 127) << (8 * k);
+                break;
+            }
+        }
+        const uint32_t idx = (uint32_t)out.size();
+        out.push_back(nd);
+        uint32_t sub = 0;
+        uint32_t refs[4] = {ORX_EMPTY, ORX_EMPTY, ORX_EMPTY, ORX_EMPTY};
+        for (size_t i = 0; i < ch.size(); i++) {
+            const DevBvhNode& c = B[ch[i]];
+            if (leaf(c)) {
+                const uint32_t cnt = c.count_or_right & 0x7fffffffu;
+                if (cnt == 0 || cnt > 8 || c.left_or_first >= (1u << 28)) ok = false;
+                refs[i] = ORX_LEAF | (c.left_or_first << 3) | (cnt - 1u);
+            } else {
+                uint32_t b = 0;
+                refs[i] = build(ch[i], b);
+                sub = std::max(sub, b);
+            }
+        }
+        for (int i = 0; i < 4; i++) out[idx].child[i] = refs[i];
+        bound = (uint32_t)ch.size() - 1u + sub;
+        return idx;
+    }
+};
+
 /* host float3 with the same OptiX semantics as the device (f3 is __host__) */
 f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
 
@@ -420,6 +518,15 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
         if (bb.max_depth >= ORX_BVH_STACK)
             return set_err(r, ORX_ERR_INVALID_ARGUMENT, "BVH deeper than the traversal stack");
     }
+    Bvh4Builder b4;
+    uint32_t stack_bound = 0;
+    if (nt) {
+        b4.b2 = &bb.nodes;
+        b4.out.reserve(bb.nodes.size() / 2 + 1);
+        b4.build(0, stack_bound);
+        if (!b4.ok) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "BVH4 quantisation failed");
+        if (stack_bound > 96) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "BVH4 traversal stack bound above 96");
+    }
     std::vector<float4> tv((size_t)nt * 3), tn;
     std::vector<uint32_t> tmat_leaf(nt);
     if (s->normals) tn.resize((size_t)nt * 3);
@@ -453,7 +560,7 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     HIPCHK(r, up(r->d_tmat, tmat_leaf.data(), (size_t)nt * 4));
     HIPCHK(r, up(r->d_mats, mats.data(), mats.size() * sizeof(DevMaterial)));
     HIPCHK(r, up(r->d_lights, lights.data(), lights.size() * sizeof(DevLight)));
-    HIPCHK(r, up(r->d_bvh, bb.nodes.data(), bb.nodes.size() * sizeof(DevBvhNode)));
+    HIPCHK(r, up(r->d_bvh, b4.out.data(), b4.out.size() * sizeof(DevBvh4)));
     DevScene& S = r->scene;
     S.nq = nq;
     S.ns = ns;
@@ -468,8 +575,9 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     S.mats = r->d_mats.as<DevMaterial>();
     S.lights = r->d_lights.as<DevLight>();
     S.nl = s->n_lights;
-    S.bvh = r->d_bvh.as<DevBvhNode>();
-    S.bvh_nodes = (uint32_t)bb.nodes.size();
+    S.bvh4 = r->d_bvh.as<DevBvh4>();
+    S.bvh_nodes = (uint32_t)b4.out.size();
+    S.stack_entries = nt ? stack_bound + 1 : 0;
     /* AAB::getBoundingSphere (math/AAB.cpp:26-33) with Vector3::length's
      * dot bug a.z*b.x (math/Vector3.cpp:27-30) */
     f3 lo = ld3(s->aabb_min), hi = ld3(s->aabb_max);
@@ -1062,6 +1170,7 @@ orx_status orx_get_stats(orx_renderer* r, orx_stats* out) {
         out->pass_ms[p] = (float)tot;
     }
     out->timed_iterations = r->timed_iterations;
+    out->bvh_stack_entries = r->scene.stack_entries;
     return check_grid_error(r);
 }
 

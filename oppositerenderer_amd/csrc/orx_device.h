@@ -219,13 +219,31 @@ struct DevQuad {
 struct DevSphere {
     float cx, cy, cz, r;
 };
-/* BVH node: 32 B, two children per node; leaves hold a primitive range */
+/* Binary BVH node (host-side build only): 32 B, leaves hold a primitive range */
 struct DevBvhNode {
     float lo[3];
     uint32_t left_or_first; /* inner: left child index; leaf: first prim in prim_index */
     float hi[3];
     uint32_t count_or_right; /* leaf: 0x80000000 | count; inner: right child */
 };
+
+/* Four-wide BVH node, 64 B (one 64-B segment, four dwordx4 loads), collapsed
+ * from the binary SAH tree.  Child boxes are quantised to 8 bits per bound
+ * against the node's origin with a power-of-two scale per axis, rounded
+ * outward (so every decoded box contains the child's conservative box):
+ *   lo_k(child i) = origin_k + qlo_k[i] * 2^(e_k - 127)
+ * Child reference: inner node index, or ORX_LEAF | first << 3 | (count - 1)
+ * for a triangle range in leaf order, or ORX_EMPTY. */
+struct DevBvh4 {
+    float ox, oy, oz;
+    uint32_t exps;     /* e_x | e_y << 8 | e_z << 16 (biased float exponents of the scales) */
+    uint32_t qlo[3];   /* per axis: byte i = child i */
+    uint32_t qhi[3];
+    uint32_t child[4];
+    uint32_t pad[2];
+};
+constexpr uint32_t ORX_LEAF = 0x80000000u;
+constexpr uint32_t ORX_EMPTY = 0xffffffffu;
 
 struct DevScene {
     uint32_t nq, ns, nt;
@@ -243,16 +261,20 @@ struct DevScene {
     uint32_t nl;
     /* bounding sphere (AAB::getBoundingSphere with Vector3::length bug) */
     float bs_cx, bs_cy, bs_cz, bs_r;
-    /* triangle BVH (nt > 0), depth <= ORX_BVH_STACK */
-    const DevBvhNode* bvh;
+    /* triangle BVH4 (nt > 0); a traversal pushes at most stack_entries refs */
+    const DevBvh4* bvh4;
     uint32_t bvh_nodes;
+    uint32_t stack_entries;
 };
 
-/* Traversal stack: per-lane column of an LDS array [ORX_BVH_STACK][64] owned
- * by a 64-thread (one-wave) block; entry k of a lane at s[k * 64]. */
-#define ORX_BVH_STACK 32
-#define ORX_STACK_DECL __shared__ uint32_t orx_stack_lds[ORX_BVH_STACK * 64]
+/* Traversal stack: per-lane column of a dynamic LDS array [stack_entries][64]
+ * owned by a 64-thread (one-wave) block; entry k of a lane at s[k * 64].  The
+ * depth bound is computed from the tree at orx_init_scene and the launch
+ * passes ORX_STACK_BYTES(S) of dynamic LDS. */
+#define ORX_BVH_STACK 32 /* depth cap of the binary build */
+#define ORX_STACK_DECL extern __shared__ uint32_t orx_stack_lds[]
 #define ORX_STACK_PTR (&orx_stack_lds[threadIdx.x & 63])
+#define ORX_STACK_BYTES(S) ((size_t)(S).stack_entries * 64 * 4)
 
 struct Hit {
     float t;
@@ -326,23 +348,68 @@ __device__ __forceinline__ bool isect_tri(f3 p0, f3 p1, f3 p2, f3 o, f3 d, float
 }
 __device__ __forceinline__ f3 ld_f3(const float4& v) { return mk(v.x, v.y, v.z); }
 
-/* slab test: does the ray enter [lo,hi] before tmax? (tie-safe: <=) */
-__device__ __forceinline__ bool box_hit(const DevBvhNode& n, f3 o, f3 inv, float tmin, float tmax, float& tenter) {
-    float tx0 = (n.lo[0] - o.x) * inv.x, tx1 = (n.hi[0] - o.x) * inv.x;
-    float ty0 = (n.lo[1] - o.y) * inv.y, ty1 = (n.hi[1] - o.y) * inv.y;
-    float tz0 = (n.lo[2] - o.z) * inv.z, tz1 = (n.hi[2] - o.z) * inv.z;
-    float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-    float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
-    tenter = t0;
-    return t0 <= t1;
+/* Per-ray slab-test constants.  A zero direction component is replaced by
+ * +-1e-30 for the box tests only: the tilted ray leaves a conservative box
+ * (>= 1e-20 margin, see the builder) only beyond t = 1e10, so no box the exact
+ * ray reaches is culled; the triangle tests use the exact direction. */
+struct RayBox {
+    f3 o, inv;
+};
+__device__ __forceinline__ RayBox ray_box(f3 o, f3 d) {
+    auto safe = [](float v) { return fabsf(v) > 1e-30f ? v : copysignf(1e-30f, v); };
+    return RayBox{o, mk(1.0f / safe(d.x), 1.0f / safe(d.y), 1.0f / safe(d.z))};
+}
+/* Test the four quantised child boxes of a node against (tmin, tmax):
+ * t = (origin + q*s - o) * inv evaluated as fma(q, s*inv, (origin - o)*inv);
+ * the rounding of that form is far below the builder's 1e-6 relative box
+ * expansion, so the test stays conservative.  Returns entry distances
+ * (+inf for misses) and child refs. */
+__device__ __forceinline__ void node_test(const DevBvh4* nodes, uint32_t idx, const RayBox& rb, float tmin, float tmax,
+                                          float t[4], uint32_t c[4]) {
+    const float4* p = reinterpret_cast<const float4*>(nodes + idx);
+    const float4 A = p[0], B = p[1], C = p[2], D = p[3];
+    const uint32_t ex = __float_as_uint(A.w);
+    const float sx = __uint_as_float((ex & 0xffu) << 23);
+    const float sy = __uint_as_float(((ex >> 8) & 0xffu) << 23);
+    const float sz = __uint_as_float(((ex >> 16) & 0xffu) << 23);
+    const float ax = (A.x - rb.o.x) * rb.inv.x, bx = sx * rb.inv.x;
+    const float ay = (A.y - rb.o.y) * rb.inv.y, by = sy * rb.inv.y;
+    const float az = (A.z - rb.o.z) * rb.inv.z, bz = sz * rb.inv.z;
+    const uint32_t lx = __float_as_uint(B.x), ly = __float_as_uint(B.y), lz = __float_as_uint(B.z);
+    const uint32_t hx = __float_as_uint(B.w), hy = __float_as_uint(C.x), hz = __float_as_uint(C.y);
+    c[0] = __float_as_uint(C.z);
+    c[1] = __float_as_uint(C.w);
+    c[2] = __float_as_uint(D.x);
+    c[3] = __float_as_uint(D.y);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const float tlx = __builtin_fmaf((float)((lx >> (8 * i)) & 0xffu), bx, ax);
+        const float thx = __builtin_fmaf((float)((hx >> (8 * i)) & 0xffu), bx, ax);
+        const float tly = __builtin_fmaf((float)((ly >> (8 * i)) & 0xffu), by, ay);
+        const float thy = __builtin_fmaf((float)((hy >> (8 * i)) & 0xffu), by, ay);
+        const float tlz = __builtin_fmaf((float)((lz >> (8 * i)) & 0xffu), bz, az);
+        const float thz = __builtin_fmaf((float)((hz >> (8 * i)) & 0xffu), bz, az);
+        const float t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
+        const float t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tmax));
+        t[i] = (t0 <= t1 && c[i] != ORX_EMPTY) ? t0 : INFINITY;
+    }
+}
+__device__ __forceinline__ void cswap(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {
+    const bool sw = tb < ta;
+    const float t = sw ? tb : ta;
+    const uint32_t c = sw ? cb : ca;
+    tb = sw ? ta : tb;
+    cb = sw ? ca : cb;
+    ta = t;
+    ca = c;
 }
 
 /* Closest hit over all primitives; equal t resolves to the lowest global
  * primitive id, which is OptiX NoAccel's child order (Cornell.cpp:183-189)
  * and is independent of traversal order, so BVH and brute force agree.
- * Triangles: near-first BVH traversal, children tested at the parent, the
- * far child pushed on the lane's LDS stack and re-tested against the
- * (possibly shrunk) closest distance when popped. */
+ * Triangles: near-first BVH4 traversal; the hit children of a node are
+ * sorted by entry distance, the nearest is taken and the others are pushed
+ * far-to-near on the lane's LDS stack. */
 __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& h, uint32_t* stk) {
     float best = tmax;
     int32_t bp = -1;
@@ -366,16 +433,12 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
     float bb = 0, bg = 0;
     if (S.nt) {
         const uint32_t base = S.nq + S.ns;
-        const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        const RayBox rb = ray_box(o, d);
         int sp = 0;
-        uint32_t node = 0;
-        float te;
-        bool have = box_hit(S.bvh[0], o, inv, tmin, best, te);
-        while (have) {
-            const DevBvhNode n = S.bvh[node];
-            have = false;
-            if (n.count_or_right & 0x80000000u) {
-                const uint32_t first = n.left_or_first, cnt = n.count_or_right & 0x7fffffffu;
+        uint32_t ref = 0; /* root */
+        for (;;) {
+            if (ref & ORX_LEAF) {
+                const uint32_t first = (ref & 0x7fffffffu) >> 3, cnt = (ref & 7u) + 1u;
                 for (uint32_t k = first; k < first + cnt; k++) {
                     const float4 v0 = S.tri_v[3 * k], v1 = S.tri_v[3 * k + 1], v2 = S.tri_v[3 * k + 2];
                     const int32_t gid = (int32_t)(base + __float_as_uint(v0.w));
@@ -392,26 +455,24 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
                     }
                 }
             } else {
-                const DevBvhNode L = S.bvh[n.left_or_first], R = S.bvh[n.count_or_right];
-                float tl, tr;
-                const bool hl = box_hit(L, o, inv, tmin, best, tl);
-                const bool hr = box_hit(R, o, inv, tmin, best, tr);
-                if (hl && hr) {
-                    const bool lf = tl <= tr;
-                    stk[sp * 64] = lf ? n.count_or_right : n.left_or_first;
-                    sp++;
-                    node = lf ? n.left_or_first : n.count_or_right;
-                    have = true;
-                } else if (hl || hr) {
-                    node = hl ? n.left_or_first : n.count_or_right;
-                    have = true;
+                float ct[4];
+                uint32_t cc[4];
+                node_test(S.bvh4, ref, rb, tmin, best, ct, cc);
+                cswap(ct[0], cc[0], ct[1], cc[1]);
+                cswap(ct[2], cc[2], ct[3], cc[3]);
+                cswap(ct[0], cc[0], ct[2], cc[2]);
+                cswap(ct[1], cc[1], ct[3], cc[3]);
+                cswap(ct[1], cc[1], ct[2], cc[2]);
+                if (ct[0] != INFINITY) {
+                    if (ct[3] != INFINITY) stk[(sp++) * 64] = cc[3];
+                    if (ct[2] != INFINITY) stk[(sp++) * 64] = cc[2];
+                    if (ct[1] != INFINITY) stk[(sp++) * 64] = cc[1];
+                    ref = cc[0];
+                    continue;
                 }
             }
-            while (!have && sp > 0) {
-                sp--;
-                node = stk[sp * 64];
-                have = box_hit(S.bvh[node], o, inv, tmin, best, te);
-            }
+            if (sp == 0) break;
+            ref = stk[(--sp) * 64];
         }
     }
     if (bp < 0) return false;
@@ -434,16 +495,12 @@ __device__ inline bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, floa
         if (isect_sphere(S.spheres[i], o, d, tmin, tmax, t, n)) return true;
     }
     if (S.nt) {
-        const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        const RayBox rb = ray_box(o, d);
         int sp = 0;
-        uint32_t node = 0;
-        float te;
-        bool have = box_hit(S.bvh[0], o, inv, tmin, tmax, te);
-        while (have) {
-            const DevBvhNode n = S.bvh[node];
-            have = false;
-            if (n.count_or_right & 0x80000000u) {
-                const uint32_t first = n.left_or_first, cnt = n.count_or_right & 0x7fffffffu;
+        uint32_t ref = 0;
+        for (;;) {
+            if (ref & ORX_LEAF) {
+                const uint32_t first = (ref & 0x7fffffffu) >> 3, cnt = (ref & 7u) + 1u;
                 for (uint32_t k = first; k < first + cnt; k++) {
                     float b, g;
                     if (isect_tri(ld_f3(S.tri_v[3 * k]), ld_f3(S.tri_v[3 * k + 1]), ld_f3(S.tri_v[3 * k + 2]), o, d,
@@ -451,25 +508,24 @@ __device__ inline bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, floa
                         return true;
                 }
             } else {
-                const DevBvhNode L = S.bvh[n.left_or_first], R = S.bvh[n.count_or_right];
-                float tl, tr;
-                const bool hl = box_hit(L, o, inv, tmin, tmax, tl);
-                const bool hr = box_hit(R, o, inv, tmin, tmax, tr);
-                if (hl && hr) {
-                    stk[sp * 64] = n.count_or_right;
-                    sp++;
-                    node = n.left_or_first;
-                    have = true;
-                } else if (hl || hr) {
-                    node = hl ? n.left_or_first : n.count_or_right;
-                    have = true;
+                float ct[4];
+                uint32_t cc[4];
+                node_test(S.bvh4, ref, rb, tmin, tmax, ct, cc);
+                uint32_t next = ORX_EMPTY;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    if (ct[i] != INFINITY) {
+                        if (next != ORX_EMPTY) stk[(sp++) * 64] = next;
+                        next = cc[i];
+                    }
+                }
+                if (next != ORX_EMPTY) {
+                    ref = next;
+                    continue;
                 }
             }
-            if (!have && sp > 0) {
-                sp--;
-                node = stk[sp * 64];
-                have = true; /* box already known to overlap [tmin, tmax] */
-            }
+            if (sp == 0) break;
+            ref = stk[(--sp) * 64];
         }
     }
     return false;

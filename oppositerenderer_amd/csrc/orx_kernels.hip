@@ -100,7 +100,7 @@ __global__ __launch_bounds__(64) void k_ppm_eye(DevScene S, DevCamera cam, Pixel
 }
 void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c) {
     dim3 grid((px.W + 7) / 8, (px.rows + 7) / 8);
-    hipLaunchKernelGGL(k_ppm_eye, grid, dim3(64), 0, s, S, cam, px, c);
+    hipLaunchKernelGGL(k_ppm_eye, grid, dim3(64), ORX_STACK_BYTES(S), s, S, cam, px, c);
 }
 
 /* ------------------------------------------------------------------ */
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
 }
 void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c) {
     dim3 grid((pb.PW + 63) / 64, pb.prows);
-    hipLaunchKernelGGL(k_ppm_photon, grid, dim3(64), 0, s, S, px, pb, c);
+    hipLaunchKernelGGL(k_ppm_photon, grid, dim3(64), ORX_STACK_BYTES(S), s, S, px, pb, c);
 }
 
 /* ------------------------------------------------------------------ */
@@ -763,7 +763,7 @@ __global__ __launch_bounds__(64) void k_ppm_direct_output(DevScene S, PixelBufs 
 }
 void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c) {
     dim3 grid((px.W + 7) / 8, (px.rows + 7) / 8);
-    hipLaunchKernelGGL(k_ppm_direct_output, grid, dim3(64), 0, s, S, px, c);
+    hipLaunchKernelGGL(k_ppm_direct_output, grid, dim3(64), ORX_STACK_BYTES(S), s, S, px, c);
 }
 
 /* ------------------------------------------------------------------ */
@@ -830,7 +830,7 @@ __global__ __launch_bounds__(64) void k_pt(DevScene S, DevCamera cam, PixelBufs 
 }
 void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c) {
     dim3 grid((px.W + 7) / 8, (px.rows + 7) / 8);
-    hipLaunchKernelGGL(k_pt, grid, dim3(64), 0, s, S, cam, px, c);
+    hipLaunchKernelGGL(k_pt, grid, dim3(64), ORX_STACK_BYTES(S), s, S, cam, px, c);
 }
 
 }  // namespace orx

@@ -772,12 +772,12 @@ __global__ __launch_bounds__(64) void k_vcm_camera(DevScene S, VcmBufs vb, VcmCo
 
 void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c, bool estimate) {
     const uint32_t blocks = (c.count + 63) / 64;
-    if (estimate) hipLaunchKernelGGL(k_vcm_light<true>, dim3(blocks), dim3(64), 0, s, S, vb, c);
-    else hipLaunchKernelGGL(k_vcm_light<false>, dim3(blocks), dim3(64), 0, s, S, vb, c);
+    if (estimate) hipLaunchKernelGGL(k_vcm_light<true>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
+    else hipLaunchKernelGGL(k_vcm_light<false>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
 }
 void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
     const uint32_t blocks = ((c.W + 7) / 8) * ((c.H + 7) / 8);
-    hipLaunchKernelGGL(k_vcm_camera, dim3(blocks), dim3(64), 0, s, S, vb, c);
+    hipLaunchKernelGGL(k_vcm_camera, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
 }
 
 }  // namespace orx

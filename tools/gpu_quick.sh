@@ -1,0 +1,7 @@
+# quick GPU check: full GPU test suite, then short hall benches (no CPU baseline)
+set -o pipefail
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 300 python bench.py --steps 16 --warmup 2 --no-cpu-baseline > gpurun_out/q_ppm.json 2> gpurun_out/q_ppm.err && \
+timeout -k 10 300 python bench.py --steps 8 --warmup 2 --no-cpu-baseline --method vcm > gpurun_out/q_vcm.json 2> gpurun_out/q_vcm.err && \
+timeout -k 10 300 python bench.py --steps 16 --warmup 2 --no-cpu-baseline --scene Cornell --width 1024 --height 1024 --photon-launch 1024 > gpurun_out/q_cornell.json 2> gpurun_out/q_cornell.err
+echo "exit=$?" >> gpurun_out/gpu_tests.log
