@@ -519,16 +519,38 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
                         uint32_t offTo = pb.offsets[to + 1];
                         dC++;
                         dP += offTo - off;
-                        for (uint32_t k = off; k < offTo; k++) {
-                            const float4 pa = pb.sortA[k];
-                            f3 diff = pos - mk(pa.x, pa.y, pa.z);
-                            float distance2 = dot(diff, diff);
-                            if (distance2 <= radius2) {
-                                const float4 pbv = pb.sortB[k];
-                                if (dot(-mk(pbv.x, pbv.y, pbv.z), nrm) >= 0) {
-                                    float e = orx_expf_core((-beta * distance2) * inv2r2);
+                        /* batches of 4: the position loads of a batch are issued
+                         * together (4 L2 round trips in flight per lane), then the
+                         * photons are tested and accumulated in grid order */
+                        for (uint32_t k0 = off; k0 < offTo; k0 += 4) {
+                            const uint32_t last = offTo - 1;
+                            float4 pa[4];
+#pragma unroll
+                            for (int q = 0; q < 4; q++) pa[q] = pb.sortA[min(k0 + q, last)];
+                            float d2[4];
+                            bool in[4];
+#pragma unroll
+                            for (int q = 0; q < 4; q++) {
+                                const f3 diff = pos - mk(pa[q].x, pa[q].y, pa[q].z);
+                                d2[q] = dot(diff, diff);
+                                in[q] = (k0 + q < offTo) && d2[q] <= radius2;
+                            }
+                            if (!(in[0] | in[1] | in[2] | in[3])) continue;
+                            float4 pbv[4];
+                            float pcz[4];
+#pragma unroll
+                            for (int q = 0; q < 4; q++) {
+                                if (in[q]) {
+                                    pbv[q] = pb.sortB[k0 + q];
+                                    pcz[q] = pb.sortC[k0 + q];
+                                }
+                            }
+#pragma unroll
+                            for (int q = 0; q < 4; q++) {
+                                if (in[q] && dot(-mk(pbv[q].x, pbv[q].y, pbv[q].z), nrm) >= 0) {
+                                    float e = orx_expf_core((-beta * d2[q]) * inv2r2);
                                     float wgt = alpha * (1 - (1 - e) * invDen);
-                                    f3 pw = mk(pa.w, pbv.w, pb.sortC[k]);
+                                    f3 pw = mk(pa[q].w, pbv[q].w, pcz[q]);
                                     acc = acc + pw * wgt;
                                 }
                             }
