@@ -339,7 +339,7 @@ struct orx_renderer {
     bool use_ext = false;
     DevBuf d_rng, d_hp, d_ind, d_dir, d_out, d_dbg;
     DevBuf d_slotA, d_slotB, d_slotC, d_vmask, d_sortA, d_sortB, d_sortC, d_keys, d_ranks;
-    DevBuf d_hist, d_offsets, d_bbox, d_partials, d_grid;
+    DevBuf d_hist, d_offsets, d_bbox, d_partials, d_grid, d_work;
     PixelBufs px{};
     PhotonBufs pb{};
     /* timing: event pairs per pass since the last orx_reset_timing */
@@ -353,7 +353,7 @@ struct orx_renderer {
     float psf_x = 1.0f, psf_y = 1.0f;
     bool vcm_estimated = false;
     size_t vcm_npx = 0;
-    DevBuf d_vcount, d_vverts, d_vsplat, d_vcam;
+    DevBuf d_vcount, d_vverts, d_vsplat, d_vcam, d_tstats;
     std::vector<DevLight> host_lights;
 };
 
@@ -370,6 +370,16 @@ static orx_status set_err(orx_renderer* r, orx_status s, const std::string& m) {
     } while (0)
 
 extern "C" {
+
+#ifdef ORX_TRAV_STATS
+/* stats build only: [closest: rays, nodes, leaves, tris, any: rays, nodes, leaves, tris]; reset = 1 zeroes */
+int orx_trav_stats_read(orx_renderer* r, unsigned long long* out, int reset) {
+    if (!r || !r->scene.trav_stats || hipDeviceSynchronize() != hipSuccess) return 1;
+    if (hipMemcpy(out, r->scene.trav_stats, 64, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+    if (reset && hipMemset(r->scene.trav_stats, 0, 64) != hipSuccess) return 1;
+    return 0;
+}
+#endif
 
 void orx_default_config(orx_config* c) {
     std::memset(c, 0, sizeof *c);
@@ -578,6 +588,13 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     S.bvh4 = r->d_bvh.as<DevBvh4>();
     S.bvh_nodes = (uint32_t)b4.out.size();
     S.stack_entries = nt ? stack_bound + 1 : 0;
+#ifdef ORX_TRAV_STATS
+    HIPCHK(r, r->d_tstats.ensure(64));
+    HIPCHK(r, hipMemset(r->d_tstats.p, 0, 64));
+    S.trav_stats = r->d_tstats.as<unsigned long long>();
+#else
+    S.trav_stats = nullptr;
+#endif
     /* AAB::getBoundingSphere (math/AAB.cpp:26-33) with Vector3::length's
      * dot bug a.z*b.x (math/Vector3.cpp:27-30) */
     f3 lo = ld3(s->aabb_min), hi = ld3(s->aabb_max);
@@ -630,6 +647,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_bbox.ensure(6 * BBOX_REPLICAS * 4));
     HIPCHK(r, r->d_partials.ensure(nblocks * 4));
     HIPCHK(r, r->d_grid.ensure(sizeof(GridParams)));
+    HIPCHK(r, r->d_work.ensure(64));
     HIPCHK(r, hipMemsetAsync(r->d_hist.p, 0, G2 * 4, r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_offsets.p, 0, G2 * 4, r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_vmask.p, 0, nphot, r->stream));
@@ -676,6 +694,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     pb.bbox = r->d_bbox.as<uint32_t>();
     pb.scan_partials = r->d_partials.as<uint32_t>();
     pb.grid = r->d_grid.as<GridParams>();
+    pb.work = r->d_work.as<uint32_t>();
 
     /* initializeRandomStates (OptixRenderer_SpatialHash.cu:310-347) */
     uint32_t seed = r->cfg.seed;

@@ -244,6 +244,7 @@ struct DevBvh4 {
 };
 constexpr uint32_t ORX_LEAF = 0x80000000u;
 constexpr uint32_t ORX_EMPTY = 0xffffffffu;
+constexpr uint32_t ORX_DONE = 0x7fffffffu; /* traversal sentinel: no node */
 
 struct DevScene {
     uint32_t nq, ns, nt;
@@ -265,6 +266,7 @@ struct DevScene {
     const DevBvh4* bvh4;
     uint32_t bvh_nodes;
     uint32_t stack_entries;
+    unsigned long long* trav_stats; /* [8] in ORX_TRAV_STATS builds, else unused */
 };
 
 /* Traversal stack: per-lane column of a dynamic LDS array [stack_entries][64]
@@ -404,6 +406,24 @@ __device__ __forceinline__ void cswap(float& ta, uint32_t& ca, float& tb, uint32
     ca = c;
 }
 
+/* Optional traversal statistics (build with -DORX_TRAV_STATS): rays, inner
+ * nodes visited, leaves visited, triangle tests — per ray type (closest/any). */
+#ifdef ORX_TRAV_STATS
+#define ORX_TS_DECL uint32_t ts_nodes = 0, ts_leaves = 0, ts_tris = 0
+#define ORX_TS_INC(v, n) (v) += (n)
+#define ORX_TS_FLUSH(base)                                                  \
+    do {                                                                    \
+        atomicAdd(&S.trav_stats[(base) + 0], 1ull);                       \
+        atomicAdd(&S.trav_stats[(base) + 1], (unsigned long long)ts_nodes);  \
+        atomicAdd(&S.trav_stats[(base) + 2], (unsigned long long)ts_leaves); \
+        atomicAdd(&S.trav_stats[(base) + 3], (unsigned long long)ts_tris);   \
+    } while (0)
+#else
+#define ORX_TS_DECL
+#define ORX_TS_INC(v, n)
+#define ORX_TS_FLUSH(base)
+#endif
+
 /* Closest hit over all primitives; equal t resolves to the lowest global
  * primitive id, which is OptiX NoAccel's child order (Cornell.cpp:183-189)
  * and is independent of traversal order, so BVH and brute force agree.
@@ -436,9 +456,34 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
         const RayBox rb = ray_box(o, d);
         int sp = 0;
         uint32_t ref = 0; /* root */
-        for (;;) {
-            if (ref & ORX_LEAF) {
+        ORX_TS_DECL;
+        /* while-while (Aila & Laine 2009): inner nodes until the lane reaches a
+         * leaf, then leaves until the next stack entry is an inner node, so a
+         * wave does not alternate masked node and leaf work every iteration */
+        while (ref != ORX_DONE) {
+            while (!(ref & ORX_LEAF) && ref != ORX_DONE) {
+                float ct[4];
+                uint32_t cc[4];
+                node_test(S.bvh4, ref, rb, tmin, best, ct, cc);
+                ORX_TS_INC(ts_nodes, 1);
+                cswap(ct[0], cc[0], ct[1], cc[1]);
+                cswap(ct[2], cc[2], ct[3], cc[3]);
+                cswap(ct[0], cc[0], ct[2], cc[2]);
+                cswap(ct[1], cc[1], ct[3], cc[3]);
+                cswap(ct[1], cc[1], ct[2], cc[2]);
+                if (ct[0] != INFINITY) {
+                    if (ct[3] != INFINITY) stk[(sp++) * 64] = cc[3];
+                    if (ct[2] != INFINITY) stk[(sp++) * 64] = cc[2];
+                    if (ct[1] != INFINITY) stk[(sp++) * 64] = cc[1];
+                    ref = cc[0];
+                } else {
+                    ref = sp ? stk[(--sp) * 64] : ORX_DONE;
+                }
+            }
+            while (ref & ORX_LEAF) {
                 const uint32_t first = (ref & 0x7fffffffu) >> 3, cnt = (ref & 7u) + 1u;
+                ORX_TS_INC(ts_leaves, 1);
+                ORX_TS_INC(ts_tris, cnt);
                 for (uint32_t k = first; k < first + cnt; k++) {
                     const float4 v0 = S.tri_v[3 * k], v1 = S.tri_v[3 * k + 1], v2 = S.tri_v[3 * k + 2];
                     const int32_t gid = (int32_t)(base + __float_as_uint(v0.w));
@@ -454,26 +499,10 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
                         bg = g;
                     }
                 }
-            } else {
-                float ct[4];
-                uint32_t cc[4];
-                node_test(S.bvh4, ref, rb, tmin, best, ct, cc);
-                cswap(ct[0], cc[0], ct[1], cc[1]);
-                cswap(ct[2], cc[2], ct[3], cc[3]);
-                cswap(ct[0], cc[0], ct[2], cc[2]);
-                cswap(ct[1], cc[1], ct[3], cc[3]);
-                cswap(ct[1], cc[1], ct[2], cc[2]);
-                if (ct[0] != INFINITY) {
-                    if (ct[3] != INFINITY) stk[(sp++) * 64] = cc[3];
-                    if (ct[2] != INFINITY) stk[(sp++) * 64] = cc[2];
-                    if (ct[1] != INFINITY) stk[(sp++) * 64] = cc[1];
-                    ref = cc[0];
-                    continue;
-                }
+                ref = sp ? stk[(--sp) * 64] : ORX_DONE;
             }
-            if (sp == 0) break;
-            ref = stk[(--sp) * 64];
         }
+        ORX_TS_FLUSH(0);
     }
     if (bp < 0) return false;
     h.t = best;
@@ -498,35 +527,39 @@ __device__ inline bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, floa
         const RayBox rb = ray_box(o, d);
         int sp = 0;
         uint32_t ref = 0;
-        for (;;) {
-            if (ref & ORX_LEAF) {
-                const uint32_t first = (ref & 0x7fffffffu) >> 3, cnt = (ref & 7u) + 1u;
-                for (uint32_t k = first; k < first + cnt; k++) {
-                    float b, g;
-                    if (isect_tri(ld_f3(S.tri_v[3 * k]), ld_f3(S.tri_v[3 * k + 1]), ld_f3(S.tri_v[3 * k + 2]), o, d,
-                                  tmin, tmax, t, b, g))
-                        return true;
-                }
-            } else {
+        ORX_TS_DECL;
+        while (ref != ORX_DONE) {
+            while (!(ref & ORX_LEAF) && ref != ORX_DONE) {
                 float ct[4];
                 uint32_t cc[4];
                 node_test(S.bvh4, ref, rb, tmin, tmax, ct, cc);
-                uint32_t next = ORX_EMPTY;
+                ORX_TS_INC(ts_nodes, 1);
+                uint32_t next = ORX_DONE;
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
                     if (ct[i] != INFINITY) {
-                        if (next != ORX_EMPTY) stk[(sp++) * 64] = next;
+                        if (next != ORX_DONE) stk[(sp++) * 64] = next;
                         next = cc[i];
                     }
                 }
-                if (next != ORX_EMPTY) {
-                    ref = next;
-                    continue;
-                }
+                ref = next != ORX_DONE ? next : (sp ? stk[(--sp) * 64] : ORX_DONE);
             }
-            if (sp == 0) break;
-            ref = stk[(--sp) * 64];
+            while (ref & ORX_LEAF) {
+                const uint32_t first = (ref & 0x7fffffffu) >> 3, cnt = (ref & 7u) + 1u;
+                ORX_TS_INC(ts_leaves, 1);
+                for (uint32_t k = first; k < first + cnt; k++) {
+                    float b, g;
+                    ORX_TS_INC(ts_tris, 1);
+                    if (isect_tri(ld_f3(S.tri_v[3 * k]), ld_f3(S.tri_v[3 * k + 1]), ld_f3(S.tri_v[3 * k + 2]), o, d,
+                                  tmin, tmax, t, b, g)) {
+                        ORX_TS_FLUSH(4);
+                        return true;
+                    }
+                }
+                ref = sp ? stk[(--sp) * 64] : ORX_DONE;
+            }
         }
+        ORX_TS_FLUSH(4);
     }
     return false;
 }

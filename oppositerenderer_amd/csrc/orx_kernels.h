@@ -73,6 +73,7 @@ struct PhotonBufs {
     uint32_t* bbox;     /* [6][BBOX_REPLICAS] ordered-float min xyz, max xyz */
     uint32_t* scan_partials; /* [ceil((gmax+2)/1024)+1] */
     GridParams* grid;
+    uint32_t* work;     /* [1] persistent photon pass: next photon index (zeroed before each launch) */
 };
 
 struct Consts {

@@ -16,6 +16,9 @@
  *   k_pt                PT_RAYTRACE_PASS       (pt/RayGeneratorPT.cu:46-131)
  * Wave size is 64 on CDNA4; block reductions below are written for it.
  */
+#include <algorithm>
+#include <cstdlib>
+
 #include "orx_kernels.h"
 
 namespace orx {
@@ -106,140 +109,206 @@ void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, cons
 /* ------------------------------------------------------------------ */
 /* PPM photon pass (+ AABB of the valid deposits)                      */
 /* ------------------------------------------------------------------ */
+/* Photon pass as persistent threads (PhotonGenerator.cu:83-128 + the photon
+ * closest-hit programs).  Each lane carries one photon path; a lane whose
+ * path ends takes the next photon index from a device counter (one atomic
+ * per wave for all the lanes that need work), so the lanes of a wave stay
+ * busy however unequal the path lengths are.  Photon p = j*PW + x always
+ * uses RNG slot (j, x) and deposit slots [p*D, p*D + D), so the result does
+ * not depend on which lane traced it. */
+struct PhotonPath {
+    f3 o, d, power;
+    float weight, tmin;
+    uint32_t p_local, depth, numStored, mask;
+    size_t slot;
+};
+__device__ __forceinline__ void photon_emit(const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, uint32_t p,
+                                            PhotonPath& P, Rng& rs) {
+    const uint32_t j = p / pb.PW, x = p - j * pb.PW;
+    P.p_local = p;
+    P.slot = (size_t)j * px.RW + x;
+    rs = rng_load(px.rng, P.slot);
+    /* PhotonGenerator.cu:91-107 */
+    int lightIndex = 0;
+    if (S.nl > 1) {
+        float sample = rnd(rs);
+        int li = (int)(sample * (float)S.nl);
+        lightIndex = li < (int)(S.nl - 1) ? li : (int)(S.nl - 1);
+    }
+    const DevLight& L = S.lights[lightIndex];
+    float powerScale = (float)S.nl;
+    f3 power = L.power * powerScale;
+    f3 origin = L.position, dir = mk1(0.f);
+    float photonPowerFactor = 1.f;
+    float s1x = rnd(rs), s1y = rnd(rs);
+    /* generatePhotonOriginAndDirection (PhotonGenerator.cu:40-79) */
+    if (L.type == LIGHT_AREA) {
+        float s2x = rnd(rs), s2y = rnd(rs);
+        origin = origin + (L.v1 * s1x + L.v2 * s1y);
+        dir = sample_hemisphere(L.normal, s2x, s2y);
+    } else if (L.type == LIGHT_POINT) {
+        f3 bc = mk(S.bs_cx, S.bs_cy, S.bs_cz);
+        f3 sceneCenterToLight = L.position - bc;
+        float lightDistance = length(sceneCenterToLight);
+        sceneCenterToLight = sceneCenterToLight / lightDistance;
+        bool wellOutside = (double)lightDistance > 1.5 * (double)S.bs_r;
+        if (wellOutside) {
+            f3 pointOnDisc = sample_disc(s1x, s1y, bc, S.bs_r, sceneCenterToLight);
+            dir = normalize(pointOnDisc - origin);
+            float rr = S.bs_r * S.bs_r + lightDistance * lightDistance;
+            photonPowerFactor = (1 - lightDistance * (1.0f / sqrtf(rr))) / 2.f;
+        } else {
+            dir = sample_unit_sphere(s1x, s1y);
+        }
+    } else {
+        f3 pointOnDisc = sample_disc(s1x, s1y, origin + L.direction, orx_sinf(L.angle / 2), L.direction);
+        dir = normalize(pointOnDisc - origin);
+    }
+    P.power = power * photonPowerFactor;
+    P.o = origin;
+    P.d = dir;
+    P.weight = 1.0f;
+    P.tmin = 0.0001f;
+    P.depth = 0;
+    P.numStored = 0;
+    P.mask = 0;
+}
+
+template <bool PERSISTENT>
 __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, PhotonBufs pb, Consts c) {
     ORX_STACK_DECL;
-    const uint32_t x = blockIdx.x * 64 + threadIdx.x;
-    const uint32_t j = blockIdx.y;
+    uint32_t* stk = ORX_STACK_PTR;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t total = pb.prows * pb.PW;
     float lo_x = INFINITY, lo_y = INFINITY, lo_z = INFINITY;
     float hi_x = -INFINITY, hi_y = -INFINITY, hi_z = -INFINITY;
-    if (x < pb.PW && j < pb.prows) {
-        const uint32_t y = px.rank + px.world * j;
-        (void)y;
-        const uint32_t p_local = j * pb.PW + x;
-        const uint32_t pm_index = p_local * pb.D;
-        size_t slot = (size_t)j * px.RW + x;
-        Rng rs = rng_load(px.rng, slot);
-        /* PhotonGenerator.cu:91-107 */
-        int lightIndex = 0;
-        if (S.nl > 1) {
-            float sample = rnd(rs);
-            int li = (int)(sample * (float)S.nl);
-            lightIndex = li < (int)(S.nl - 1) ? li : (int)(S.nl - 1);
-        }
-        const DevLight& L = S.lights[lightIndex];
-        float powerScale = (float)S.nl;
-        f3 power = L.power * powerScale;
-        f3 origin = L.position, dir = mk1(0.f);
-        float photonPowerFactor = 1.f;
-        float s1x = rnd(rs), s1y = rnd(rs);
-        /* generatePhotonOriginAndDirection (PhotonGenerator.cu:40-79) */
-        if (L.type == LIGHT_AREA) {
-            float s2x = rnd(rs), s2y = rnd(rs);
-            origin = origin + (L.v1 * s1x + L.v2 * s1y);
-            dir = sample_hemisphere(L.normal, s2x, s2y);
-        } else if (L.type == LIGHT_POINT) {
-            f3 bc = mk(S.bs_cx, S.bs_cy, S.bs_cz);
-            f3 sceneCenterToLight = L.position - bc;
-            float lightDistance = length(sceneCenterToLight);
-            sceneCenterToLight = sceneCenterToLight / lightDistance;
-            bool wellOutside = (double)lightDistance > 1.5 * (double)S.bs_r;
-            if (wellOutside) {
-                f3 pointOnDisc = sample_disc(s1x, s1y, bc, S.bs_r, sceneCenterToLight);
-                dir = normalize(pointOnDisc - origin);
-                float rr = S.bs_r * S.bs_r + lightDistance * lightDistance;
-                photonPowerFactor = (1 - lightDistance * (1.0f / sqrtf(rr))) / 2.f;
+    PhotonPath P;
+    Rng rs;
+    bool alive = false;
+    /* the wave's private range [next, end) of photon indices, refilled
+     * CHUNK at a time from the device counter (one atomic per chunk) */
+    constexpr uint32_t CHUNK = 256;
+    uint32_t next = 0, end = 0;
+    for (;;) {
+        /* refill: lanes without a path take consecutive photon indices */
+        uint64_t need = __ballot(!alive);
+        if (!PERSISTENT) { /* one photon per lane: block b owns photons [64b, 64b + 64) */
+            if (end == 0) {
+                next = blockIdx.x * 64u;
+                end = next + 64u < total ? next + 64u : total;
+                if (next > end) next = end;
             } else {
-                dir = sample_unit_sphere(s1x, s1y);
+                next = end;
             }
-        } else {
-            f3 pointOnDisc = sample_disc(s1x, s1y, origin + L.direction, orx_sinf(L.angle / 2), L.direction);
-            dir = normalize(pointOnDisc - origin);
         }
-        power = power * photonPowerFactor;
-
-        /* photon closest-hit chain: Diffuse.cu:92-135, Glossy.cu:94-137,
-         * Mirror.cu:65-77, Glass.cu:164-205, DiffuseEmitter.cu:56-59 */
-        uint32_t numStored = 0, depth = 0, mask = 0;
-        float weight = 1.0f;
-        float tmin = 0.0001f;
-        f3 o = origin, d = dir;
-        for (;;) {
+        if (PERSISTENT && need && next >= end && end < total) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(pb.work, CHUNK);
+            base = (uint32_t)__shfl((int)base, 0, 64);
+            next = base < total ? base : total;
+            end = base + CHUNK < total ? base + CHUNK : total;
+            if (base >= total) end = total, next = total;
+        }
+        if (need && next < end) {
+            const uint32_t avail = end - next;
+            const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+            if (!alive && rank < avail) {
+                photon_emit(S, px, pb, next + rank, P, rs);
+                alive = true;
+            }
+            const uint32_t n = (uint32_t)__popcll(need);
+            next += n < avail ? n : avail;
+        }
+        if (!__ballot(alive)) break;
+        if (alive) {
+            /* one bounce: Diffuse.cu:92-135, Glossy.cu:94-137, Mirror.cu:65-77,
+             * Glass.cu:164-205, DiffuseEmitter.cu:56-59 */
+            bool done = false;
             Hit h;
-            if (!trace_closest(S, o, d, tmin, RT_DEFAULT_MAX, h, ORX_STACK_PTR)) break;
-            const DevMaterial& m = S.mats[prim_material(S, h)];
-            f3 hitPoint = o + d * h.t;
-            if (m.type == MAT_DIFFUSE || m.type == MAT_GLOSSY) {
-                f3 N = shading_normal(S, h);
-                if (depth >= 1 && numStored < pb.D) {
-                    uint32_t si = pm_index + numStored;
-                    pb.slotA[si] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, power.x);
-                    pb.slotB[si] = make_float4(d.x, d.y, d.z, power.y);
-                    pb.slotC[si] = power.z;
-                    if (fmax3(power) > 0) {
-                        mask |= 1u << numStored;
-                        lo_x = fminf(lo_x, hitPoint.x); lo_y = fminf(lo_y, hitPoint.y); lo_z = fminf(lo_z, hitPoint.z);
-                        hi_x = fmaxf(hi_x, hitPoint.x); hi_y = fmaxf(hi_y, hitPoint.y); hi_z = fmaxf(hi_z, hitPoint.z);
-                    }
-                    numStored++;
-                }
-                power = power * m.Kd;
-                weight *= fmax3(m.Kd);
-                if (depth >= 3) {
-                    float probContinue = favgf(m.Kd);
-                    float probSample = rnd(rs);
-                    if (probSample >= probContinue) break;
-                    power = power / probContinue;
-                }
-                depth++;
-                if (depth >= c.max_photon_depth || (double)weight < 0.001) break;
-                if (numStored >= pb.D) break;
-                float s0 = rnd(rs);
-                float s1 = rnd(rs);
-                d = sample_hemisphere_cos(N, s0, s1);
-                o = hitPoint;
-                tmin = 0.0001f;
-            } else if (m.type == MAT_EMITTER) {
-                break;
-            } else if (m.type == MAT_MIRROR) {
-                f3 N = shading_normal(S, h);
-                depth++;
-                if (depth <= c.max_photon_depth) {
-                    power = power * m.Kr;
-                    d = reflect(d, N);
-                    o = hitPoint;
-                    tmin = 0.0001f;
-                    continue;
-                }
-                break;
+            if (!trace_closest(S, P.o, P.d, P.tmin, RT_DEFAULT_MAX, h, stk)) {
+                done = true;
             } else {
-                f3 wsn = shading_normal(S, h);
-                bool outside = dot(wsn, d) < 0;
-                f3 N = outside ? wsn : -wsn;
-                float n1 = outside ? 1.0f : m.ior, n2 = outside ? m.ior : 1.0f;
-                f3 refr;
-                bool valid;
-                float refl = glass_reflect_factor(d, N, n1, n2, refr, valid);
-                float sample = rnd(rs);
-                f3 nd = (sample <= refl) ? reflect(d, N) : refr;
-                depth++;
-                if (depth <= c.max_photon_depth) {
-                    o = hitPoint;
-                    d = nd;
-                    tmin = 0.0001f;
-                    continue;
+                const DevMaterial& m = S.mats[prim_material(S, h)];
+                const f3 hitPoint = P.o + P.d * h.t;
+                if (m.type == MAT_DIFFUSE || m.type == MAT_GLOSSY) {
+                    const f3 N = shading_normal(S, h);
+                    if (P.depth >= 1 && P.numStored < pb.D) {
+                        const uint32_t si = P.p_local * pb.D + P.numStored;
+                        pb.slotA[si] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, P.power.x);
+                        pb.slotB[si] = make_float4(P.d.x, P.d.y, P.d.z, P.power.y);
+                        pb.slotC[si] = P.power.z;
+                        if (fmax3(P.power) > 0) {
+                            P.mask |= 1u << P.numStored;
+                            lo_x = fminf(lo_x, hitPoint.x); lo_y = fminf(lo_y, hitPoint.y); lo_z = fminf(lo_z, hitPoint.z);
+                            hi_x = fmaxf(hi_x, hitPoint.x); hi_y = fmaxf(hi_y, hitPoint.y); hi_z = fmaxf(hi_z, hitPoint.z);
+                        }
+                        P.numStored++;
+                    }
+                    P.power = P.power * m.Kd;
+                    P.weight *= fmax3(m.Kd);
+                    if (P.depth >= 3) {
+                        float probContinue = favgf(m.Kd);
+                        float probSample = rnd(rs);
+                        if (probSample >= probContinue) done = true;
+                        else P.power = P.power / probContinue;
+                    }
+                    if (!done) {
+                        P.depth++;
+                        if (P.depth >= c.max_photon_depth || (double)P.weight < 0.001 || P.numStored >= pb.D) {
+                            done = true;
+                        } else {
+                            float s0 = rnd(rs);
+                            float s1 = rnd(rs);
+                            P.d = sample_hemisphere_cos(N, s0, s1);
+                            P.o = hitPoint;
+                            P.tmin = 0.0001f;
+                        }
+                    }
+                } else if (m.type == MAT_EMITTER) {
+                    done = true;
+                } else if (m.type == MAT_MIRROR) {
+                    const f3 N = shading_normal(S, h);
+                    P.depth++;
+                    if (P.depth <= c.max_photon_depth) {
+                        P.power = P.power * m.Kr;
+                        P.d = reflect(P.d, N);
+                        P.o = hitPoint;
+                        P.tmin = 0.0001f;
+                    } else {
+                        done = true;
+                    }
+                } else {
+                    const f3 wsn = shading_normal(S, h);
+                    const bool outside = dot(wsn, P.d) < 0;
+                    const f3 N = outside ? wsn : -wsn;
+                    const float n1 = outside ? 1.0f : m.ior, n2 = outside ? m.ior : 1.0f;
+                    f3 refr;
+                    bool valid;
+                    const float refl = glass_reflect_factor(P.d, N, n1, n2, refr, valid);
+                    const float sample = rnd(rs);
+                    const f3 nd = (sample <= refl) ? reflect(P.d, N) : refr;
+                    P.depth++;
+                    if (P.depth <= c.max_photon_depth) {
+                        P.o = hitPoint;
+                        P.d = nd;
+                        P.tmin = 0.0001f;
+                    } else {
+                        done = true;
+                    }
                 }
-                break;
+            }
+            if (done) {
+                pb.vmask[P.p_local] = (uint8_t)P.mask;
+                rng_store(px.rng, P.slot, rs);
+                alive = false;
             }
         }
-        pb.vmask[p_local] = (uint8_t)mask;
-        rng_store(px.rng, slot, rs);
     }
     /* wave AABB -> device-wide ordered-int atomics (one lane per component) */
     lo_x = wave_min(lo_x); lo_y = wave_min(lo_y); lo_z = wave_min(lo_z);
     hi_x = wave_max(hi_x); hi_y = wave_max(hi_y); hi_z = wave_max(hi_z);
     /* 64 replicas per component keep same-address atomic contention low */
-    const uint32_t lane = threadIdx.x;
-    const uint32_t rep = (blockIdx.x + blockIdx.y * gridDim.x) & (BBOX_REPLICAS - 1);
+    const uint32_t rep = blockIdx.x & (BBOX_REPLICAS - 1);
     if (lane < 6) {
         float v = lane == 0 ? lo_x : lane == 1 ? lo_y : lane == 2 ? lo_z : lane == 3 ? hi_x : lane == 4 ? hi_y : hi_z;
         if (lane < 3) {
@@ -250,8 +319,20 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
     }
 }
 void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c) {
-    dim3 grid((pb.PW + 63) / 64, pb.prows);
-    hipLaunchKernelGGL(k_ppm_photon, grid, dim3(64), ORX_STACK_BYTES(S), s, S, px, pb, c);
+    /* persistent grid: enough one-wave blocks to fill every SIMD several
+     * times over; each block drains the shared photon counter */
+    const uint32_t total = pb.prows * pb.PW;
+    static const int persistent = [] {
+        const char* e = getenv("ORX_PHOTON_PERSISTENT");
+        return e ? atoi(e) : 0;
+    }();
+    if (persistent) {
+        const uint32_t blocks = std::min<uint32_t>((total + 63) / 64, 256u * 4u * 8u);
+        hipMemsetAsync(pb.work, 0, 4, s);
+        hipLaunchKernelGGL(k_ppm_photon<true>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, px, pb, c);
+    } else {
+        hipLaunchKernelGGL(k_ppm_photon<false>, dim3((total + 63) / 64), dim3(64), ORX_STACK_BYTES(S), s, S, px, pb, c);
+    }
 }
 
 /* ------------------------------------------------------------------ */
@@ -473,6 +554,7 @@ __device__ __forceinline__ HpRef hp_ref(const GatherIn& gi, uint32_t j, uint32_t
     return r;
 }
 
+template <int GB>
 __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, Consts c) {
     /* block = 16x16 pixels as four 8x8 wave tiles (neighbouring lanes share photons in L1) */
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -579,6 +661,146 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
         atomicAdd((unsigned long long*)&pb.grid->cells_visited_total, (unsigned long long)sc);
     }
 }
+/* Wave-per-pixel gather: a 64-lane wave owns an 8x8 pixel tile and walks its
+ * 64 pixels one at a time.  For each pixel the lanes split the concatenation
+ * of the pixel's (z,y) cell-row photon ranges — exactly the photons the
+ * reference loop visits (IndirectRadianceEstimation.cu:95-129) — so every
+ * photon load is part of a coalesced 1 KiB run and the loop has no per-lane
+ * trip-count divergence; the lanes' partial sums are then combined by a
+ * fixed xor-butterfly.  Visit counters are the reference's (rows and photons
+ * of the cell window).  Only the fp32 summation order differs from the
+ * per-pixel kernel. */
+__device__ __forceinline__ float rl_f(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ uint32_t rl_u(uint32_t v, int lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ __forceinline__ float wave_sum_f(float v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__global__ __launch_bounds__(256) void k_ppm_gather_wave(GatherIn gi, PhotonBufs pb, Consts c) {
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (l & 7);
+    const uint32_t j = blockIdx.y * 16 + (w >> 1) * 8 + (l >> 3);
+    const GridParams g = *pb.grid;
+    const bool own = x < gi.W && j < gi.segments * gi.seg_rows;
+    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+    float2 Cc = make_float2(0.f, 0.f);
+    if (own) {
+        const HpRef hr = hp_ref(gi, j, x);
+        A = hr.A[hr.li];
+        B = hr.B[hr.li];
+        Cc = hr.C[hr.li];
+    }
+    const uint32_t ownmask = (uint32_t)own;
+    const float radius2 = c.ppm_radius2;
+    const float radius = c.ppm_radius;
+    const float invCellSize = 1.f / g.cell;
+    const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
+    const float inv2r2 = 1.0f / (2 * radius2);
+    const float invDen = 1.0f / (1 - expNegativeBeta);
+    f3 mine = mk1(0.f);
+    uint32_t my_dC = 0, my_dP = 0;
+    for (int pix = 0; pix < 64; pix++) {
+        if (!rl_u(ownmask, pix)) continue;
+        const uint32_t flags = rl_u(__float_as_uint(A.w), pix);
+        if (!((flags & PRD_HIT_NON_SPECULAR) && g.G)) continue;
+        const f3 pos = mk(rl_f(A.x, pix), rl_f(A.y, pix), rl_f(A.z, pix));
+        const f3 nrm = mk(rl_f(B.x, pix), rl_f(B.y, pix), rl_f(B.z, pix));
+        const f3 np = pos - mk(g.ox, g.oy, g.oz);
+        const int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
+        const int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
+        const int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
+        const uint32_t x_lo = (uint32_t)(ixl > 0 ? ixl : 0);
+        const uint32_t y_lo = (uint32_t)(iyl > 0 ? iyl : 0);
+        const uint32_t z_lo = (uint32_t)(izl > 0 ? izl : 0);
+        const uint32_t ux = orx_f2u_sat((np.x + radius) * invCellSize);
+        const uint32_t uy = orx_f2u_sat((np.y + radius) * invCellSize);
+        const uint32_t uz = orx_f2u_sat((np.z + radius) * invCellSize);
+        const uint32_t x_hi = (g.gx - 1) < ux ? (g.gx - 1) : ux;
+        const uint32_t y_hi = (g.gy - 1) < uy ? (g.gy - 1) : uy;
+        const uint32_t z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
+        if (x_lo > x_hi || y_lo > y_hi || z_lo > z_hi) continue;
+        const uint32_t ny = y_hi - y_lo + 1, nrows = ny * (z_hi - z_lo + 1);
+        f3 acc = mk1(0.0f);
+        uint32_t dP = 0;
+        for (uint32_t r0 = 0; r0 < nrows; r0 += 64) {
+            /* lane r describes row r0 + r (z outer, y inner, as the reference) */
+            const uint32_t r = r0 + l;
+            uint32_t base = 0, len = 0;
+            if (r < nrows) {
+                const uint32_t yy = y_lo + r % ny, z = z_lo + r / ny;
+                const uint32_t from = x_lo + yy * g.gx + z * g.gx * g.gy;
+                base = pb.offsets[from];
+                len = pb.offsets[from + (x_hi - x_lo) + 1] - base;
+            }
+            uint32_t incl = len;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = __shfl_up(incl, o, 64);
+                if (l >= (uint32_t)o) incl += v;
+            }
+            const uint32_t excl = incl - len;
+            const uint32_t total = rl_u(incl, 63);
+            const uint32_t nr = nrows - r0 < 64 ? nrows - r0 : 64;
+            dP += total;
+            for (uint32_t g0 = 0; g0 < total; g0 += 64) {
+                const uint32_t gidx = g0 + l;
+                /* last row whose exclusive start is <= gidx */
+                int lo = 0;
+#pragma unroll
+                for (int step = 32; step >= 1; step >>= 1) {
+                    const int mid = lo + step;
+                    const uint32_t v = __shfl(excl, mid & 63, 64);
+                    if ((uint32_t)mid < nr && v <= gidx) lo = mid;
+                }
+                const uint32_t k = __shfl(base, lo, 64) + (gidx - __shfl(excl, lo, 64));
+                if (gidx < total) {
+                    const float4 pa = pb.sortA[k];
+                    const f3 diff = pos - mk(pa.x, pa.y, pa.z);
+                    const float distance2 = dot(diff, diff);
+                    if (distance2 <= radius2) {
+                        const float4 pbv = pb.sortB[k];
+                        if (dot(-mk(pbv.x, pbv.y, pbv.z), nrm) >= 0) {
+                            const float e = orx_expf_core((-beta * distance2) * inv2r2);
+                            const float wgt = alpha * (1 - (1 - e) * invDen);
+                            acc = acc + mk(pa.w, pbv.w, pb.sortC[k]) * wgt;
+                        }
+                    }
+                }
+            }
+        }
+        acc = mk(wave_sum_f(acc.x), wave_sum_f(acc.y), wave_sum_f(acc.z));
+        if (l == (uint32_t)pix) {
+            mine = acc;
+            my_dC = nrows;
+            my_dP = dP;
+        }
+    }
+    if (own) {
+        const size_t i = (size_t)j * gi.W + x;
+        const f3 att = mk(B.w, Cc.x, Cc.y);
+        const float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
+        const float s2 = 1.0f / c.emitted_f;
+        const f3 ind = ((mine * att) * s1) * s2;
+        gi.indirect[3 * i + 0] = ind.x;
+        gi.indirect[3 * i + 1] = ind.y;
+        gi.indirect[3 * i + 2] = ind.z;
+        if (gi.dbg) {
+            gi.dbg[2 * i] = my_dC;
+            gi.dbg[2 * i + 1] = my_dP;
+        }
+    }
+    const uint64_t sp = wave_sum_u64(my_dP), sc = wave_sum_u64(my_dC);
+    if (l == 0 && sp) {
+        atomicAdd((unsigned long long*)&pb.grid->photons_visited, (unsigned long long)sp);
+        atomicAdd((unsigned long long*)&pb.grid->cells_visited, (unsigned long long)sc);
+        atomicAdd((unsigned long long*)&pb.grid->photons_visited_total, (unsigned long long)sp);
+        atomicAdd((unsigned long long*)&pb.grid->cells_visited_total, (unsigned long long)sc);
+    }
+}
+
 /* Wave-cooperative gather: one 64-lane wave owns an 8x8 pixel tile.  For
  * every (z,y) cell row that any lane's window touches, the wave stages the
  * row's photons (the union of the lanes' contiguous sub-ranges) through LDS
@@ -726,9 +948,12 @@ __global__ __launch_bounds__(64) void k_ppm_gather_coop(GatherIn gi, PhotonBufs 
 }
 void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, int variant) {
     const uint32_t rows = gi.segments * gi.seg_rows;
-    if (variant == 0) {
+    if (variant != 1) {
         dim3 grid((gi.W + 15) / 16, (rows + 15) / 16);
-        hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), 0, s, gi, pb, c);
+        if (variant == 2) hipLaunchKernelGGL(k_ppm_gather<8>, grid, dim3(256), 0, s, gi, pb, c);
+        else if (variant == 3) hipLaunchKernelGGL(k_ppm_gather<2>, grid, dim3(256), 0, s, gi, pb, c);
+        else if (variant == 4) hipLaunchKernelGGL(k_ppm_gather_wave, grid, dim3(256), 0, s, gi, pb, c);
+        else hipLaunchKernelGGL(k_ppm_gather<4>, grid, dim3(256), 0, s, gi, pb, c);
     } else {
         dim3 grid((gi.W + 7) / 8, (rows + 7) / 8);
         hipLaunchKernelGGL(k_ppm_gather_coop, grid, dim3(64), 0, s, gi, pb, c);

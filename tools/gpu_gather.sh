@@ -1,0 +1,6 @@
+set -o pipefail
+timeout -k 10 300 python -m pytest tests/test_gpu_parity.py tests/test_golden.py -x -q -k "ppm" > gpurun_out/gpu_tests.log 2>&1 || exit 1
+for v in 0; do
+timeout -k 10 300 python bench.py --steps 16 --warmup 2 --no-cpu-baseline --gather-variant $v > gpurun_out/q_ppm_v$v.json 2> gpurun_out/q_ppm.err || exit 1
+timeout -k 10 300 python bench.py --steps 16 --warmup 2 --no-cpu-baseline --gather-variant $v --scene Cornell --width 1024 --height 1024 --photon-launch 1024 > gpurun_out/q_cornell_v$v.json 2> gpurun_out/q_ppm.err || exit 1
+done

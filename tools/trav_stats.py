@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Traversal statistics on the GPU (build: make -C oppositerenderer_amd/csrc stats).
+Prints per-iteration rays / inner nodes / leaves / triangle tests for closest-hit
+and any-hit traversals of one bench workload."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from oppositerenderer_amd import _abi, renderer, scenes  # noqa: E402
+
+lib = renderer.load_library(os.path.join(ROOT, "oppositerenderer_amd", "liborx_stats.so"))
+lib.orx_trav_stats_read.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
+scene_name = sys.argv[1] if len(sys.argv) > 1 else "SyntheticHall"
+method = {"ppm": 2, "vcm": 1, "pt": 0}[sys.argv[2] if len(sys.argv) > 2 else "ppm"]
+W, H, P = (1920, 1080, 2048) if scene_name.startswith("Synthetic") else (1024, 1024, 1024)
+sc = scenes.scene_by_name(scene_name)
+r = renderer.OptixRenderer(_abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P))
+r.initialize(0)
+r.initScene(sc)
+det = renderer.RenderRequestDetails(sc.default_camera.set_aspect_ratio(W / H), sc.name, method, W, H)
+buf = (C.c_ulonglong * 8)()
+radius = sc.initial_ppm_radius()
+for it in range(3):
+    r.renderNextIteration(it, it, radius, False, det)
+    radius = renderer.next_ppm_radius(radius, it)
+    assert lib.orx_trav_stats_read(r._h, buf, 1) == 0
+    v = list(buf)
+    for name, b in (("closest", 0), ("any", 4)):
+        rays = max(1, v[b])
+        print(f"it{it} {name:8s} rays {v[b]:12d}  nodes/ray {v[b + 1] / rays:6.2f}  leaves/ray {v[b + 2] / rays:6.2f}"
+              f"  tris/ray {v[b + 3] / rays:6.2f}")
+print("bvh stack entries", r.stats().bvh_stack_entries)
