@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <ctime>
 #include <new>
@@ -69,6 +70,11 @@ struct BvhBuilder {
         return dx * dy + dy * dz + dz * dx;
     }
     uint32_t max_depth = 0;
+    /* defaults measured on the 1080p hall (tools/trav_stats.py): SAH leaf
+     * test up to 8 triangles cuts triangle tests/ray 5.9 -> 3.2 */
+    int bins = 32;          /* SAH bins per axis (ORX_BVH_BINS) */
+    uint32_t leaf_max = 8;  /* largest leaf (ORX_BVH_LEAF_MAX, <= 8) */
+    float leaf_sah = 0.6f;  /* node traversal cost relative to a triangle test (ORX_BVH_LEAF_SAH); 0 = leaves of <= leaf_max, no test */
     static uint32_t ceil_log2(uint32_t v) {
         uint32_t l = 0;
         while ((1u << l) < v) l++;
@@ -93,22 +99,22 @@ struct BvhBuilder {
             nodes[idx].lo[k] = lo[k] - e;
             nodes[idx].hi[k] = hi[k] + e;
         }
-        if (count <= 4) {
+        if (count <= 1 || (count <= leaf_max && leaf_sah == 0.f)) {
             nodes[idx].left_or_first = first;
             nodes[idx].count_or_right = 0x80000000u | count;
             return idx;
         }
         /* binned SAH on the centroid extent; object-median split once the
          * depth budget (ORX_BVH_STACK) would otherwise be at risk */
-        const int NB = 16;
+        const int NB = bins;
         int best_axis = -1, best_split = 0;
         float best_cost = INFINITY;
         const bool median = depth + ceil_log2((count + 3) / 4) + 2 >= ORX_BVH_STACK;
         for (int ax = 0; ax < 3 && !median; ax++) {
             float ext = chi[ax] - clo[ax];
             if (!(ext > 0)) continue;
-            uint32_t cnt[NB] = {0};
-            float blo[NB][3], bhi[NB][3];
+            uint32_t cnt[64] = {0};
+            float blo[64][3], bhi[64][3];
             for (int b = 0; b < NB; b++)
                 for (int k = 0; k < 3; k++) blo[b][k] = INFINITY, bhi[b][k] = -INFINITY;
             for (uint32_t i = first; i < first + count; i++) {
@@ -117,7 +123,7 @@ struct BvhBuilder {
                 cnt[b]++;
                 grow(blo[b], bhi[b], t.lo, t.hi);
             }
-            float rl[NB], rcount[NB];
+            float rl[64], rcount[64];
             float alo[3] = {INFINITY, INFINITY, INFINITY}, ahi[3] = {-INFINITY, -INFINITY, -INFINITY};
             uint32_t acc = 0;
             for (int b = NB - 1; b > 0; b--) {
@@ -137,6 +143,15 @@ struct BvhBuilder {
                     best_axis = ax;
                     best_split = b;
                 }
+            }
+        }
+        if (count <= leaf_max) {
+            /* SAH leaf test: split cost Ct + (A_L N_L + A_R N_R)/A vs leaf cost N (Ci = 1) */
+            const float A = area(lo, hi);
+            if (best_axis < 0 || !(A > 0) || leaf_sah + best_cost / A >= (float)count) {
+                nodes[idx].left_or_first = first;
+                nodes[idx].count_or_right = 0x80000000u | count;
+                return idx;
             }
         }
         uint32_t mid;
@@ -338,7 +353,7 @@ struct orx_renderer {
     hipStream_t ext_stream = nullptr; /* caller-provided stream (orx_set_stream) */
     bool use_ext = false;
     DevBuf d_rng, d_hp, d_ind, d_dir, d_out, d_dbg;
-    DevBuf d_slotA, d_slotB, d_slotC, d_vmask, d_sortA, d_sortB, d_sortC, d_keys, d_ranks;
+    DevBuf d_slotA, d_slotB, d_slotC, d_vmask, d_sorted, d_perm, d_keys, d_ranks;
     DevBuf d_hist, d_offsets, d_bbox, d_partials, d_grid, d_work;
     PixelBufs px{};
     PhotonBufs pb{};
@@ -521,6 +536,9 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     BvhBuilder bb;
     if (nt) {
         bb.tris = &bt;
+        if (const char* e = getenv("ORX_BVH_BINS")) bb.bins = std::max(2, std::min(64, atoi(e)));
+        if (const char* e = getenv("ORX_BVH_LEAF_MAX")) bb.leaf_max = (uint32_t)std::max(1, std::min(8, atoi(e)));
+        if (const char* e = getenv("ORX_BVH_LEAF_SAH")) bb.leaf_sah = (float)atof(e);
         bb.prims.resize(nt);
         for (uint32_t i = 0; i < nt; i++) bb.prims[i] = i;
         bb.nodes.reserve(2 * (size_t)nt / 2 + 1);
@@ -637,9 +655,10 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_slotB.ensure(S * 16));
     HIPCHK(r, r->d_slotC.ensure(S * 4));
     HIPCHK(r, r->d_vmask.ensure(nphot));
-    HIPCHK(r, r->d_sortA.ensure(S * 16));
-    HIPCHK(r, r->d_sortB.ensure(S * 16));
-    HIPCHK(r, r->d_sortC.ensure(S * 4));
+    const size_t splane = ((S + 4) + 3) & ~(size_t)3;
+    HIPCHK(r, r->d_sorted.ensure(9 * splane * 4));
+    HIPCHK(r, r->d_perm.ensure(S * 4 + 16));
+    HIPCHK(r, hipMemsetAsync(r->d_sorted.p, 0, 9 * splane * 4, r->stream)); /* tail reads stay finite */
     HIPCHK(r, r->d_keys.ensure(S * 4));
     HIPCHK(r, r->d_ranks.ensure(S * 4));
     HIPCHK(r, r->d_hist.ensure(G2 * 4));
@@ -684,9 +703,9 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     pb.slotB = r->d_slotB.as<float4>();
     pb.slotC = r->d_slotC.as<float>();
     pb.vmask = r->d_vmask.as<uint8_t>();
-    pb.sortA = r->d_sortA.as<float4>();
-    pb.sortB = r->d_sortB.as<float4>();
-    pb.sortC = r->d_sortC.as<float>();
+    pb.sorted = r->d_sorted.as<float>();
+    pb.splane = (uint32_t)splane;
+    pb.perm = r->d_perm.as<uint32_t>();
     pb.keys = r->d_keys.as<uint32_t>();
     pb.ranks = r->d_ranks.as<uint32_t>();
     pb.hist = r->d_hist.as<uint32_t>();
@@ -1108,24 +1127,32 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
         }
         break;
     }
-    case ORX_BUF_PHOTONS: case ORX_BUF_PHOTON_SLOTS: {
-        size_t n = id == ORX_BUF_PHOTONS ? (size_t)g.valid : (size_t)r->pb.S;
+    case ORX_BUF_PHOTONS: {
+        /* nine SoA planes -> [n][power3 position3 direction3] (Photon.h:10-33 order) */
+        const size_t n = g.valid, P = r->pb.splane;
+        std::vector<float> pl(9 * n);
+        for (int q = 0; q < 9 && n; q++) HIPCHK(r, d2h(pl.data() + q * n, r->d_sorted.as<float>() + q * P, n * 4));
+        static const int order[9] = {6, 7, 8, 0, 1, 2, 3, 4, 5};
+        float* o = (float*)dst;
+        for (size_t i = 0; i < n; i++)
+            for (int k = 0; k < 9; k++) o[9 * i + k] = pl[order[k] * n + i];
+        break;
+    }
+    case ORX_BUF_PHOTON_SLOTS: {
+        const size_t n = (size_t)r->pb.S;
         std::vector<float4> A(n), B(n);
         std::vector<float> Cc(n);
-        std::vector<uint8_t> vm(id == ORX_BUF_PHOTONS ? 0 : (size_t)r->prows * r->cfg.photon_launch_width);
-        const void* sa = id == ORX_BUF_PHOTONS ? r->d_sortA.p : r->d_slotA.p;
-        const void* sb = id == ORX_BUF_PHOTONS ? r->d_sortB.p : r->d_slotB.p;
-        const void* sc = id == ORX_BUF_PHOTONS ? r->d_sortC.p : r->d_slotC.p;
+        std::vector<uint8_t> vm((size_t)r->prows * r->cfg.photon_launch_width);
         if (n) {
-            HIPCHK(r, d2h(A.data(), sa, n * 16));
-            HIPCHK(r, d2h(B.data(), sb, n * 16));
-            HIPCHK(r, d2h(Cc.data(), sc, n * 4));
+            HIPCHK(r, d2h(A.data(), r->d_slotA.p, n * 16));
+            HIPCHK(r, d2h(B.data(), r->d_slotB.p, n * 16));
+            HIPCHK(r, d2h(Cc.data(), r->d_slotC.p, n * 4));
         }
         if (!vm.empty()) HIPCHK(r, d2h(vm.data(), r->d_vmask.p, vm.size()));
         float* o = (float*)dst;
         const uint32_t D = r->cfg.max_photon_deposits;
         for (size_t i = 0; i < n; i++) {
-            bool valid = id == ORX_BUF_PHOTONS || ((vm[i / D] >> (i % D)) & 1u);
+            const bool valid = (vm[i / D] >> (i % D)) & 1u;
             float v[9] = {A[i].w, B[i].w, Cc[i], A[i].x, A[i].y, A[i].z, B[i].x, B[i].y, B[i].z};
             if (!valid) std::memset(v, 0, sizeof v);
             std::memcpy(o + 9 * i, v, sizeof v);

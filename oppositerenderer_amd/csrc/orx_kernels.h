@@ -63,9 +63,9 @@ struct PhotonBufs {
     float4* slotB;      /* [S] dir.xyz, power.y */
     float* slotC;       /* [S] power.z */
     uint8_t* vmask;     /* [S/D] bit k: deposit k stored with fmaxf(power) > 0 */
-    float4* sortA;      /* grid-ordered copies */
-    float4* sortB;
-    float* sortC;
+    float* sorted;      /* grid-ordered photons, nine float planes (SoA): x y z | dir x y z | power x y z */
+    uint32_t splane;    /* plane stride in floats (multiple of 4, >= S + 4) */
+    uint32_t* perm;     /* [S] grid position -> photon slot (counting-sort scatter target) */
     uint32_t* keys;     /* [S] */
     uint32_t* ranks;    /* [S] */
     uint32_t* hist;     /* [gmax+2] */

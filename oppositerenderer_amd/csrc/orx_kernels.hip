@@ -521,16 +521,35 @@ __global__ __launch_bounds__(256) void k_grid_scatter(PhotonBufs pb) {
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < pb.S; s += gridDim.x * blockDim.x) {
         uint32_t key = pb.keys[s];
         if (key > G) continue;
-        uint32_t dst = pb.offsets[key] + pb.ranks[s];
-        pb.sortA[dst] = pb.slotA[s];
-        pb.sortB[dst] = pb.slotB[s];
-        pb.sortC[dst] = pb.slotC[s];
+        pb.perm[pb.offsets[key] + pb.ranks[s]] = s;
+    }
+}
+/* grid order -> SoA planes: destination-major, so the nine plane writes are
+ * coalesced and the source reads are whole float4s */
+__global__ __launch_bounds__(256) void k_grid_permute(PhotonBufs pb) {
+    const uint32_t valid = pb.grid->valid;
+    const size_t P = pb.splane;
+    for (uint32_t dst = blockIdx.x * blockDim.x + threadIdx.x; dst < valid; dst += gridDim.x * blockDim.x) {
+        const uint32_t s = pb.perm[dst];
+        const float4 a = pb.slotA[s], b = pb.slotB[s];
+        const float cz = pb.slotC[s];
+        float* o = pb.sorted + dst;
+        o[0] = a.x;
+        o[P] = a.y;
+        o[2 * P] = a.z;
+        o[3 * P] = b.x;
+        o[4 * P] = b.y;
+        o[5 * P] = b.z;
+        o[6 * P] = a.w;
+        o[7 * P] = b.w;
+        o[8 * P] = cz;
     }
 }
 void launch_grid_scatter(hipStream_t s, const PhotonBufs& pb) {
     unsigned blocks = (pb.S + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(k_grid_scatter, dim3(blocks), dim3(256), 0, s, pb);
+    hipLaunchKernelGGL(k_grid_permute, dim3(blocks), dim3(256), 0, s, pb);
 }
 
 /* ------------------------------------------------------------------ */
@@ -554,9 +573,20 @@ __device__ __forceinline__ HpRef hp_ref(const GatherIn& gi, uint32_t j, uint32_t
     return r;
 }
 
-template <int GB>
+/* Per-pixel gather, packed fp32: one lane per pixel (four 8x8 wave tiles per
+ * 256-thread block, so neighbouring lanes share photons in L1).  The (z,y)
+ * cell rows of the window are walked in the reference order
+ * (IndirectRadianceEstimation.cu:95-129); within a row the photons go in
+ * aligned groups of four: one dwordx4 load per SoA plane, distance tests,
+ * normal tests, the kernel weight (photonPower, :59-67) and the
+ * contributions evaluated two photons per instruction (v_pk_add_f32 /
+ * v_pk_mul_f32 — IEEE per component, so every value is bit-identical to the
+ * scalar oracle), then accumulated in photon order. */
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2f lo2(float4 v) { return v2f{v.x, v.y}; }
+__device__ __forceinline__ v2f hi2(float4 v) { return v2f{v.z, v.w}; }
+
 __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, Consts c) {
-    /* block = 16x16 pixels as four 8x8 wave tiles (neighbouring lanes share photons in L1) */
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (l & 7);
     const uint32_t j = blockIdx.y * 16 + (w >> 1) * 8 + (l >> 3);
@@ -569,82 +599,98 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
         const float4 B = hr.B[hr.li];
         const float2 Cc = hr.C[hr.li];
         const uint32_t flags = __float_as_uint(A.w);
-        f3 acc = mk1(0.0f);
+        float ax = 0.f, ay = 0.f, az = 0.f;
         if ((flags & PRD_HIT_NON_SPECULAR) && g.G) {
             const f3 pos = mk(A.x, A.y, A.z);
-            const f3 nrm = mk(B.x, B.y, B.z);
             const float radius2 = c.ppm_radius2;
             const float radius = c.ppm_radius;
             const float invCellSize = 1.f / g.cell;
             const f3 np = pos - mk(g.ox, g.oy, g.oz);
-            int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
-            int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
-            int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
-            uint32_t x_lo = (uint32_t)(ixl > 0 ? ixl : 0);
-            uint32_t y_lo = (uint32_t)(iyl > 0 ? iyl : 0);
-            uint32_t z_lo = (uint32_t)(izl > 0 ? izl : 0);
-            uint32_t ux = orx_f2u_sat((np.x + radius) * invCellSize);
-            uint32_t uy = orx_f2u_sat((np.y + radius) * invCellSize);
-            uint32_t uz = orx_f2u_sat((np.z + radius) * invCellSize);
-            uint32_t x_hi = (g.gx - 1) < ux ? (g.gx - 1) : ux;
-            uint32_t y_hi = (g.gy - 1) < uy ? (g.gy - 1) : uy;
-            uint32_t z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
+            const int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
+            const int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
+            const int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
+            const uint32_t x_lo = (uint32_t)(ixl > 0 ? ixl : 0);
+            const uint32_t y_lo = (uint32_t)(iyl > 0 ? iyl : 0);
+            const uint32_t z_lo = (uint32_t)(izl > 0 ? izl : 0);
+            const uint32_t ux = orx_f2u_sat((np.x + radius) * invCellSize);
+            const uint32_t uy = orx_f2u_sat((np.y + radius) * invCellSize);
+            const uint32_t uz = orx_f2u_sat((np.z + radius) * invCellSize);
+            const uint32_t x_hi = (g.gx - 1) < ux ? (g.gx - 1) : ux;
+            const uint32_t y_hi = (g.gy - 1) < uy ? (g.gy - 1) : uy;
+            const uint32_t z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
             if (x_lo <= x_hi) {
                 const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
                 const float inv2r2 = 1.0f / (2 * radius2);
                 const float invDen = 1.0f / (1 - expNegativeBeta);
+                const v2f px2 = v2f{pos.x, pos.x}, py2 = v2f{pos.y, pos.y}, pz2 = v2f{pos.z, pos.z};
+                const v2f nx2 = v2f{B.x, B.x}, ny2 = v2f{B.y, B.y}, nz2 = v2f{B.z, B.z};
+                const v2f r2v = v2f{radius2, radius2};
+                const size_t P = pb.splane;
+                const float* __restrict__ SX = pb.sorted;
                 for (uint32_t z = z_lo; z <= z_hi; z++) {
                     for (uint32_t yy = y_lo; yy <= y_hi; yy++) {
-                        uint32_t from = x_lo + yy * g.gx + z * g.gx * g.gy;
-                        uint32_t to = from + (x_hi - x_lo);
-                        uint32_t off = pb.offsets[from];
-                        uint32_t offTo = pb.offsets[to + 1];
+                        const uint32_t from = x_lo + yy * g.gx + z * g.gx * g.gy;
+                        const uint32_t to = from + (x_hi - x_lo);
+                        const uint32_t off = pb.offsets[from];
+                        const uint32_t offTo = pb.offsets[to + 1];
                         dC++;
                         dP += offTo - off;
-                        /* batches of 4: the position loads of a batch are issued
-                         * together (4 L2 round trips in flight per lane), then the
-                         * photons are tested and accumulated in grid order */
-                        for (uint32_t k0 = off; k0 < offTo; k0 += 4) {
-                            const uint32_t last = offTo - 1;
-                            float4 pa[4];
-#pragma unroll
-                            for (int q = 0; q < 4; q++) pa[q] = pb.sortA[min(k0 + q, last)];
-                            float d2[4];
-                            bool in[4];
-#pragma unroll
-                            for (int q = 0; q < 4; q++) {
-                                const f3 diff = pos - mk(pa[q].x, pa[q].y, pa[q].z);
-                                d2[q] = dot(diff, diff);
-                                in[q] = (k0 + q < offTo) && d2[q] <= radius2;
-                            }
-                            if (!(in[0] | in[1] | in[2] | in[3])) continue;
-                            float4 pbv[4];
-                            float pcz[4];
-#pragma unroll
-                            for (int q = 0; q < 4; q++) {
-                                if (in[q]) {
-                                    pbv[q] = pb.sortB[k0 + q];
-                                    pcz[q] = pb.sortC[k0 + q];
-                                }
-                            }
-#pragma unroll
-                            for (int q = 0; q < 4; q++) {
-                                if (in[q] && dot(-mk(pbv[q].x, pbv[q].y, pbv[q].z), nrm) >= 0) {
-                                    float e = orx_expf_core((-beta * d2[q]) * inv2r2);
-                                    float wgt = alpha * (1 - (1 - e) * invDen);
-                                    f3 pw = mk(pa[q].w, pbv[q].w, pcz[q]);
-                                    acc = acc + pw * wgt;
-                                }
-                            }
+                        for (uint32_t kb = off & ~3u; kb < offTo; kb += 4) {
+                            const float4 X = *(const float4*)(SX + kb);
+                            const float4 Y = *(const float4*)(SX + P + kb);
+                            const float4 Z = *(const float4*)(SX + 2 * P + kb);
+                            const v2f dx0 = px2 - lo2(X), dx1 = px2 - hi2(X);
+                            const v2f dy0 = py2 - lo2(Y), dy1 = py2 - hi2(Y);
+                            const v2f dz0 = pz2 - lo2(Z), dz1 = pz2 - hi2(Z);
+                            const v2f d20 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
+                            const v2f d21 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
+                            bool in0 = kb >= off && d20.x <= radius2;
+                            bool in1 = kb + 1 >= off && kb + 1 < offTo && d20.y <= radius2;
+                            bool in2 = kb + 2 >= off && kb + 2 < offTo && d21.x <= radius2;
+                            bool in3 = kb + 3 < offTo && d21.y <= radius2;
+                            if (!(in0 | in1 | in2 | in3)) continue;
+                            const float4 DX = *(const float4*)(SX + 3 * P + kb);
+                            const float4 DY = *(const float4*)(SX + 4 * P + kb);
+                            const float4 DZ = *(const float4*)(SX + 5 * P + kb);
+                            const float4 WX = *(const float4*)(SX + 6 * P + kb);
+                            const float4 WY = *(const float4*)(SX + 7 * P + kb);
+                            const float4 WZ = *(const float4*)(SX + 8 * P + kb);
+                            /* dot(-dir, n) >= 0  <=>  dot(dir, n) <= 0 (negation is exact) */
+                            const v2f nd0 = (lo2(DX) * nx2 + lo2(DY) * ny2) + lo2(DZ) * nz2;
+                            const v2f nd1 = (hi2(DX) * nx2 + hi2(DY) * ny2) + hi2(DZ) * nz2;
+                            in0 = in0 && nd0.x <= 0.f;
+                            in1 = in1 && nd0.y <= 0.f;
+                            in2 = in2 && nd1.x <= 0.f;
+                            in3 = in3 && nd1.y <= 0.f;
+                            /* photonPower: alpha*(1 - (1 - exp(-beta d^2 / 2r^2)) / (1 - e^-beta)) */
+                            const v2f mb = v2f{-beta, -beta}, i2 = v2f{inv2r2, inv2r2};
+                            const v2f x0 = (mb * __builtin_elementwise_min(d20, r2v)) * i2;
+                            const v2f x1 = (mb * __builtin_elementwise_min(d21, r2v)) * i2;
+                            v2f p0 = v2f{ORX_EXPU_C6, ORX_EXPU_C6}, p1 = p0;
+                            p0 = p0 * x0 + ORX_EXPU_C5; p1 = p1 * x1 + ORX_EXPU_C5;
+                            p0 = p0 * x0 + ORX_EXPU_C4; p1 = p1 * x1 + ORX_EXPU_C4;
+                            p0 = p0 * x0 + ORX_EXPU_C3; p1 = p1 * x1 + ORX_EXPU_C3;
+                            p0 = p0 * x0 + ORX_EXPU_C2; p1 = p1 * x1 + ORX_EXPU_C2;
+                            p0 = p0 * x0 + ORX_EXPU_C1; p1 = p1 * x1 + ORX_EXPU_C1;
+                            const v2f e0 = p0 * x0 + 1.0f, e1 = p1 * x1 + 1.0f;
+                            const v2f w0 = alpha * (1.0f - (1.0f - e0) * invDen);
+                            const v2f w1 = alpha * (1.0f - (1.0f - e1) * invDen);
+                            const v2f cx0 = lo2(WX) * w0, cx1 = hi2(WX) * w1;
+                            const v2f cy0 = lo2(WY) * w0, cy1 = hi2(WY) * w1;
+                            const v2f cz0 = lo2(WZ) * w0, cz1 = hi2(WZ) * w1;
+                            if (in0) { ax = ax + cx0.x; ay = ay + cy0.x; az = az + cz0.x; }
+                            if (in1) { ax = ax + cx0.y; ay = ay + cy0.y; az = az + cz0.y; }
+                            if (in2) { ax = ax + cx1.x; ay = ay + cy1.x; az = az + cz1.x; }
+                            if (in3) { ax = ax + cx1.y; ay = ay + cy1.y; az = az + cz1.y; }
                         }
                     }
                 }
             }
         }
         const f3 att = mk(B.w, Cc.x, Cc.y);
-        float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
-        float s2 = 1.0f / c.emitted_f;
-        f3 ind = ((acc * att) * s1) * s2;
+        const float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
+        const float s2 = 1.0f / c.emitted_f;
+        const f3 ind = ((mk(ax, ay, az) * att) * s1) * s2;
         gi.indirect[3 * i + 0] = ind.x;
         gi.indirect[3 * i + 1] = ind.y;
         gi.indirect[3 * i + 2] = ind.z;
@@ -653,147 +699,8 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
             gi.dbg[2 * i + 1] = dP;
         }
     }
-    uint64_t sp = wave_sum_u64(dP), sc = wave_sum_u64(dC);
+    const uint64_t sp = wave_sum_u64(dP), sc = wave_sum_u64(dC);
     if ((threadIdx.x & 63) == 0 && sp) {
-        atomicAdd((unsigned long long*)&pb.grid->photons_visited, (unsigned long long)sp);
-        atomicAdd((unsigned long long*)&pb.grid->cells_visited, (unsigned long long)sc);
-        atomicAdd((unsigned long long*)&pb.grid->photons_visited_total, (unsigned long long)sp);
-        atomicAdd((unsigned long long*)&pb.grid->cells_visited_total, (unsigned long long)sc);
-    }
-}
-/* Wave-per-pixel gather: a 64-lane wave owns an 8x8 pixel tile and walks its
- * 64 pixels one at a time.  For each pixel the lanes split the concatenation
- * of the pixel's (z,y) cell-row photon ranges — exactly the photons the
- * reference loop visits (IndirectRadianceEstimation.cu:95-129) — so every
- * photon load is part of a coalesced 1 KiB run and the loop has no per-lane
- * trip-count divergence; the lanes' partial sums are then combined by a
- * fixed xor-butterfly.  Visit counters are the reference's (rows and photons
- * of the cell window).  Only the fp32 summation order differs from the
- * per-pixel kernel. */
-__device__ __forceinline__ float rl_f(float v, int lane) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
-}
-__device__ __forceinline__ uint32_t rl_u(uint32_t v, int lane) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
-}
-__device__ __forceinline__ float wave_sum_f(float v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__global__ __launch_bounds__(256) void k_ppm_gather_wave(GatherIn gi, PhotonBufs pb, Consts c) {
-    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (l & 7);
-    const uint32_t j = blockIdx.y * 16 + (w >> 1) * 8 + (l >> 3);
-    const GridParams g = *pb.grid;
-    const bool own = x < gi.W && j < gi.segments * gi.seg_rows;
-    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
-    float2 Cc = make_float2(0.f, 0.f);
-    if (own) {
-        const HpRef hr = hp_ref(gi, j, x);
-        A = hr.A[hr.li];
-        B = hr.B[hr.li];
-        Cc = hr.C[hr.li];
-    }
-    const uint32_t ownmask = (uint32_t)own;
-    const float radius2 = c.ppm_radius2;
-    const float radius = c.ppm_radius;
-    const float invCellSize = 1.f / g.cell;
-    const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
-    const float inv2r2 = 1.0f / (2 * radius2);
-    const float invDen = 1.0f / (1 - expNegativeBeta);
-    f3 mine = mk1(0.f);
-    uint32_t my_dC = 0, my_dP = 0;
-    for (int pix = 0; pix < 64; pix++) {
-        if (!rl_u(ownmask, pix)) continue;
-        const uint32_t flags = rl_u(__float_as_uint(A.w), pix);
-        if (!((flags & PRD_HIT_NON_SPECULAR) && g.G)) continue;
-        const f3 pos = mk(rl_f(A.x, pix), rl_f(A.y, pix), rl_f(A.z, pix));
-        const f3 nrm = mk(rl_f(B.x, pix), rl_f(B.y, pix), rl_f(B.z, pix));
-        const f3 np = pos - mk(g.ox, g.oy, g.oz);
-        const int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
-        const int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
-        const int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
-        const uint32_t x_lo = (uint32_t)(ixl > 0 ? ixl : 0);
-        const uint32_t y_lo = (uint32_t)(iyl > 0 ? iyl : 0);
-        const uint32_t z_lo = (uint32_t)(izl > 0 ? izl : 0);
-        const uint32_t ux = orx_f2u_sat((np.x + radius) * invCellSize);
-        const uint32_t uy = orx_f2u_sat((np.y + radius) * invCellSize);
-        const uint32_t uz = orx_f2u_sat((np.z + radius) * invCellSize);
-        const uint32_t x_hi = (g.gx - 1) < ux ? (g.gx - 1) : ux;
-        const uint32_t y_hi = (g.gy - 1) < uy ? (g.gy - 1) : uy;
-        const uint32_t z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
-        if (x_lo > x_hi || y_lo > y_hi || z_lo > z_hi) continue;
-        const uint32_t ny = y_hi - y_lo + 1, nrows = ny * (z_hi - z_lo + 1);
-        f3 acc = mk1(0.0f);
-        uint32_t dP = 0;
-        for (uint32_t r0 = 0; r0 < nrows; r0 += 64) {
-            /* lane r describes row r0 + r (z outer, y inner, as the reference) */
-            const uint32_t r = r0 + l;
-            uint32_t base = 0, len = 0;
-            if (r < nrows) {
-                const uint32_t yy = y_lo + r % ny, z = z_lo + r / ny;
-                const uint32_t from = x_lo + yy * g.gx + z * g.gx * g.gy;
-                base = pb.offsets[from];
-                len = pb.offsets[from + (x_hi - x_lo) + 1] - base;
-            }
-            uint32_t incl = len;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t v = __shfl_up(incl, o, 64);
-                if (l >= (uint32_t)o) incl += v;
-            }
-            const uint32_t excl = incl - len;
-            const uint32_t total = rl_u(incl, 63);
-            const uint32_t nr = nrows - r0 < 64 ? nrows - r0 : 64;
-            dP += total;
-            for (uint32_t g0 = 0; g0 < total; g0 += 64) {
-                const uint32_t gidx = g0 + l;
-                /* last row whose exclusive start is <= gidx */
-                int lo = 0;
-#pragma unroll
-                for (int step = 32; step >= 1; step >>= 1) {
-                    const int mid = lo + step;
-                    const uint32_t v = __shfl(excl, mid & 63, 64);
-                    if ((uint32_t)mid < nr && v <= gidx) lo = mid;
-                }
-                const uint32_t k = __shfl(base, lo, 64) + (gidx - __shfl(excl, lo, 64));
-                if (gidx < total) {
-                    const float4 pa = pb.sortA[k];
-                    const f3 diff = pos - mk(pa.x, pa.y, pa.z);
-                    const float distance2 = dot(diff, diff);
-                    if (distance2 <= radius2) {
-                        const float4 pbv = pb.sortB[k];
-                        if (dot(-mk(pbv.x, pbv.y, pbv.z), nrm) >= 0) {
-                            const float e = orx_expf_core((-beta * distance2) * inv2r2);
-                            const float wgt = alpha * (1 - (1 - e) * invDen);
-                            acc = acc + mk(pa.w, pbv.w, pb.sortC[k]) * wgt;
-                        }
-                    }
-                }
-            }
-        }
-        acc = mk(wave_sum_f(acc.x), wave_sum_f(acc.y), wave_sum_f(acc.z));
-        if (l == (uint32_t)pix) {
-            mine = acc;
-            my_dC = nrows;
-            my_dP = dP;
-        }
-    }
-    if (own) {
-        const size_t i = (size_t)j * gi.W + x;
-        const f3 att = mk(B.w, Cc.x, Cc.y);
-        const float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
-        const float s2 = 1.0f / c.emitted_f;
-        const f3 ind = ((mine * att) * s1) * s2;
-        gi.indirect[3 * i + 0] = ind.x;
-        gi.indirect[3 * i + 1] = ind.y;
-        gi.indirect[3 * i + 2] = ind.z;
-        if (gi.dbg) {
-            gi.dbg[2 * i] = my_dC;
-            gi.dbg[2 * i + 1] = my_dP;
-        }
-    }
-    const uint64_t sp = wave_sum_u64(my_dP), sc = wave_sum_u64(my_dC);
-    if (l == 0 && sp) {
         atomicAdd((unsigned long long*)&pb.grid->photons_visited, (unsigned long long)sp);
         atomicAdd((unsigned long long*)&pb.grid->cells_visited, (unsigned long long)sc);
         atomicAdd((unsigned long long*)&pb.grid->photons_visited_total, (unsigned long long)sp);
@@ -894,9 +801,11 @@ __global__ __launch_bounds__(64) void k_ppm_gather_coop(GatherIn gi, PhotonBufs 
                 for (uint32_t base = rlo; base < rhi; base += 64) {
                     const uint32_t n = min(64u, rhi - base);
                     if (lane < n) {
-                        sA[lane] = pb.sortA[base + lane];
-                        sB[lane] = pb.sortB[base + lane];
-                        sC[lane] = pb.sortC[base + lane];
+                        const float* q = pb.sorted + base + lane;
+                        const size_t P = pb.splane;
+                        sA[lane] = make_float4(q[0], q[P], q[2 * P], q[6 * P]);
+                        sB[lane] = make_float4(q[3 * P], q[4 * P], q[5 * P], q[7 * P]);
+                        sC[lane] = q[8 * P];
                     }
                     __syncthreads();
                     const uint32_t t_lo = lo > base ? lo - base : 0u;
@@ -911,7 +820,7 @@ __global__ __launch_bounds__(64) void k_ppm_gather_coop(GatherIn gi, PhotonBufs 
                         /* predicated, not branched: exp argument stays in [-beta/2, 0] */
                         bool take = t >= t_lo && t < t_hi && distance2 <= radius2 &&
                                     dot(-mk(pbv.x, pbv.y, pbv.z), nrm) >= 0;
-                        float e = orx_expf_core((-beta * fminf(distance2, radius2)) * inv2r2);
+                        float e = orx_expf_unit((-beta * fminf(distance2, radius2)) * inv2r2);
                         float wgt = alpha * (1 - (1 - e) * invDen);
                         f3 pw = mk(pa.w, pbv.w, pc);
                         f3 nacc = acc + pw * wgt;
@@ -950,10 +859,7 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
     const uint32_t rows = gi.segments * gi.seg_rows;
     if (variant != 1) {
         dim3 grid((gi.W + 15) / 16, (rows + 15) / 16);
-        if (variant == 2) hipLaunchKernelGGL(k_ppm_gather<8>, grid, dim3(256), 0, s, gi, pb, c);
-        else if (variant == 3) hipLaunchKernelGGL(k_ppm_gather<2>, grid, dim3(256), 0, s, gi, pb, c);
-        else if (variant == 4) hipLaunchKernelGGL(k_ppm_gather_wave, grid, dim3(256), 0, s, gi, pb, c);
-        else hipLaunchKernelGGL(k_ppm_gather<4>, grid, dim3(256), 0, s, gi, pb, c);
+        hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), 0, s, gi, pb, c);
     } else {
         dim3 grid((gi.W + 7) / 8, (rows + 7) / 8);
         hipLaunchKernelGGL(k_ppm_gather_coop, grid, dim3(64), 0, s, gi, pb, c);

@@ -22,7 +22,7 @@ KERNELS_OF_PASS = {
     "ppm_photon": ["k_ppm_photon"],
     "grid_hash": ["k_grid_setup", "k_grid_hash"],
     "grid_scan": ["k_scan_reduce", "k_scan_partials", "k_scan_apply"],
-    "grid_scatter": ["k_grid_scatter"],
+    "grid_scatter": ["k_grid_scatter", "k_grid_permute"],
     "ppm_gather": ["k_ppm_gather", "k_ppm_gather_coop"],
     "ppm_direct_output": ["k_ppm_direct_output"],
     "pt": ["k_pt"],
@@ -58,8 +58,8 @@ def pass_bytes(method: int, W: int, H: int, photons: int, valid: float = 0.0, ce
             "grid_hash": photons * 1 + valid * (12 + 8 + 4),
             # histogram read + zeroed, offsets written
             "grid_scan": (cells + 2) * 12,
-            # key + rank read, photon 36 B read + written, offset read
-            "grid_scatter": valid * (8 + 36 + 36 + 4),
+            # key + rank read, offset read, permutation written + read, photon 36 B read + written
+            "grid_scatter": valid * (8 + 4 + 4 + 4 + 36 + 36),
             # hitpoint 40 B + indirect 12 B per pixel, each grid photon once, offset table once
             "ppm_gather": N * (40 + 12) + valid * 36 + (cells + 1) * 4,
             # hitpoint, RNG RMW, indirect read, direct written, output read + written

@@ -1192,7 +1192,7 @@ static void ppm_gather_src(orc_renderer* r, const hp_src* src, uint32_t rows_tot
                                     /* photonPower (:59-67); its two divisions compile to div.approx
                                      * under -use_fast_math and are restated as multiplications by
                                      * the IEEE reciprocal of the (loop-invariant) divisor */
-                                    float e = orx_expf((-beta * distance2) * inv2r2);
+                                    float e = orx_expf_unit((-beta * distance2) * inv2r2);
                                     float wgt = alpha * (1 - (1 - e) * invDen);
                                     acc = add(acc, scl(p->power, wgt));
                                 }

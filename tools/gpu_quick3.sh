@@ -1,0 +1,6 @@
+set -o pipefail
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1 || exit 1
+timeout -k 10 300 python tools/trav_stats.py SyntheticHall ppm > gpurun_out/trav_hall.txt 2>&1 || exit 1
+timeout -k 10 300 python bench.py --steps 16 --warmup 2 --no-cpu-baseline > gpurun_out/q_ppm.json 2> gpurun_out/q_ppm.err || exit 1
+timeout -k 10 300 python bench.py --steps 8 --warmup 2 --no-cpu-baseline --method vcm > gpurun_out/q_vcm.json 2> gpurun_out/q_ppm.err || exit 1
+timeout -k 10 300 python bench.py --steps 16 --warmup 2 --no-cpu-baseline --scene Cornell --width 1024 --height 1024 --photon-launch 1024 > gpurun_out/q_cornell.json 2> gpurun_out/q_ppm.err || exit 1
