@@ -189,6 +189,7 @@ struct BvhBuilder {
 struct Bvh4Builder {
     const std::vector<DevBvhNode>* b2 = nullptr;
     std::vector<DevBvh4> out;
+    std::vector<DevBvh4F> outf; /* same topology, fp32 child boxes */
     bool ok = true;
 
     static bool leaf(const DevBvhNode& n) { return (n.count_or_right & 0x80000000u) != 0; }
@@ -259,6 +260,16 @@ struct Bvh4Builder {
         }
         const uint32_t idx = (uint32_t)out.size();
         out.push_back(nd);
+        DevBvh4F nf;
+        std::memset(&nf, 0, sizeof nf);
+        for (int i = 0; i < 4; i++) {
+            const bool has = (size_t)i < ch.size();
+            for (int k = 0; k < 3; k++) {
+                nf.b[2 * k][i] = has ? B[ch[i]].lo[k] : INFINITY;
+                nf.b[2 * k + 1][i] = has ? B[ch[i]].hi[k] : -INFINITY;
+            }
+        }
+        outf.push_back(nf);
         uint32_t sub = 0;
         uint32_t refs[4] = {ORX_EMPTY, ORX_EMPTY, ORX_EMPTY, ORX_EMPTY};
         for (size_t i = 0; i < ch.size(); i++) {
@@ -273,7 +284,7 @@ struct Bvh4Builder {
                 sub = std::max(sub, b);
             }
         }
-        for (int i = 0; i < 4; i++) out[idx].child[i] = refs[i];
+        for (int i = 0; i < 4; i++) out[idx].child[i] = outf[idx].child[i] = refs[i];
         bound = (uint32_t)ch.size() - 1u + sub;
         return idx;
     }
@@ -588,7 +599,11 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     HIPCHK(r, up(r->d_tmat, tmat_leaf.data(), (size_t)nt * 4));
     HIPCHK(r, up(r->d_mats, mats.data(), mats.size() * sizeof(DevMaterial)));
     HIPCHK(r, up(r->d_lights, lights.data(), lights.size() * sizeof(DevLight)));
+#ifdef ORX_BVH_FP32
+    HIPCHK(r, up(r->d_bvh, b4.outf.data(), b4.outf.size() * sizeof(DevBvh4F)));
+#else
     HIPCHK(r, up(r->d_bvh, b4.out.data(), b4.out.size() * sizeof(DevBvh4)));
+#endif
     DevScene& S = r->scene;
     S.nq = nq;
     S.ns = ns;
@@ -603,7 +618,7 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     S.mats = r->d_mats.as<DevMaterial>();
     S.lights = r->d_lights.as<DevLight>();
     S.nl = s->n_lights;
-    S.bvh4 = r->d_bvh.as<DevBvh4>();
+    S.bvh4 = r->d_bvh.as<DevNode4>();
     S.bvh_nodes = (uint32_t)b4.out.size();
     S.stack_entries = nt ? stack_bound + 1 : 0;
 #ifdef ORX_TRAV_STATS

@@ -242,6 +242,18 @@ struct DevBvh4 {
     uint32_t child[4];
     uint32_t pad[2];
 };
+/* fp32 variant (ORX_BVH_FP32): 128 B, child bounds unquantised, SoA by
+ * axis so the near/far bound quadruples are picked by address */
+struct DevBvh4F {
+    float b[6][4];     /* lo_x, hi_x, lo_y, hi_y, lo_z, hi_z; [child] */
+    uint32_t child[4];
+    uint32_t pad[4];
+};
+#ifdef ORX_BVH_FP32
+typedef DevBvh4F DevNode4;
+#else
+typedef DevBvh4 DevNode4;
+#endif
 constexpr uint32_t ORX_LEAF = 0x80000000u;
 constexpr uint32_t ORX_EMPTY = 0xffffffffu;
 constexpr uint32_t ORX_DONE = 0x7fffffffu; /* traversal sentinel: no node */
@@ -263,7 +275,7 @@ struct DevScene {
     /* bounding sphere (AAB::getBoundingSphere with Vector3::length bug) */
     float bs_cx, bs_cy, bs_cz, bs_r;
     /* triangle BVH4 (nt > 0); a traversal pushes at most stack_entries refs */
-    const DevBvh4* bvh4;
+    const DevNode4* bvh4;
     uint32_t bvh_nodes;
     uint32_t stack_entries;
     unsigned long long* trav_stats; /* [8] in ORX_TRAV_STATS builds, else unused */
@@ -357,6 +369,7 @@ __device__ __forceinline__ f3 ld_f3(const float4& v) { return mk(v.x, v.y, v.z);
 struct RayBox {
     f3 o, inv;
     bool nx, ny, nz; /* negative direction: the near slab of that axis is the box's hi bound */
+    f3 oinv;         /* -o * inv (fp32 boxes: t = fma(bound, inv, oinv)) */
 };
 __device__ __forceinline__ RayBox ray_box(f3 o, f3 d) {
     auto safe = [](float v) { return fabsf(v) > 1e-30f ? v : copysignf(1e-30f, v); };
@@ -366,6 +379,7 @@ __device__ __forceinline__ RayBox ray_box(f3 o, f3 d) {
     rb.nx = rb.inv.x < 0.f;
     rb.ny = rb.inv.y < 0.f;
     rb.nz = rb.inv.z < 0.f;
+    rb.oinv = mk(-o.x * rb.inv.x, -o.y * rb.inv.y, -o.z * rb.inv.z);
     return rb;
 }
 /* Test the four quantised child boxes of a node against (tmin, tmax):
@@ -406,6 +420,37 @@ __device__ __forceinline__ void node_test(const DevBvh4* nodes, uint32_t idx, co
         const float t0 = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), tmin);
         const float t1 = fminf(fminf(fminf(tfx, tfy), tfz), tmax);
         t[i] = (t0 <= t1 && c[i] != ORX_EMPTY) ? t0 : INFINITY;
+    }
+}
+typedef float v2t __attribute__((ext_vector_type(2)));
+/* fp32-box node test: t = fma(bound, inv, -o*inv), two children per
+ * v_pk_fma_f32; same conservativeness argument as the quantised form */
+__device__ __forceinline__ void node_test(const DevBvh4F* nodes, uint32_t idx, const RayBox& rb, float tmin, float tmax,
+                                          float t[4], uint32_t c[4]) {
+    const float* base = reinterpret_cast<const float*>(nodes + idx);
+    const float4 NX = *(const float4*)(base + (rb.nx ? 4 : 0)), FX = *(const float4*)(base + (rb.nx ? 0 : 4));
+    const float4 NY = *(const float4*)(base + (rb.ny ? 12 : 8)), FY = *(const float4*)(base + (rb.ny ? 8 : 12));
+    const float4 NZ = *(const float4*)(base + (rb.nz ? 20 : 16)), FZ = *(const float4*)(base + (rb.nz ? 16 : 20));
+    const uint4 CC = *(const uint4*)(base + 24);
+    c[0] = CC.x;
+    c[1] = CC.y;
+    c[2] = CC.z;
+    c[3] = CC.w;
+    const v2t ix = v2t{rb.inv.x, rb.inv.x}, iy = v2t{rb.inv.y, rb.inv.y}, iz = v2t{rb.inv.z, rb.inv.z};
+    const v2t ox = v2t{rb.oinv.x, rb.oinv.x}, oy = v2t{rb.oinv.y, rb.oinv.y}, oz = v2t{rb.oinv.z, rb.oinv.z};
+    const v2t tnx0 = __builtin_elementwise_fma(v2t{NX.x, NX.y}, ix, ox), tnx1 = __builtin_elementwise_fma(v2t{NX.z, NX.w}, ix, ox);
+    const v2t tfx0 = __builtin_elementwise_fma(v2t{FX.x, FX.y}, ix, ox), tfx1 = __builtin_elementwise_fma(v2t{FX.z, FX.w}, ix, ox);
+    const v2t tny0 = __builtin_elementwise_fma(v2t{NY.x, NY.y}, iy, oy), tny1 = __builtin_elementwise_fma(v2t{NY.z, NY.w}, iy, oy);
+    const v2t tfy0 = __builtin_elementwise_fma(v2t{FY.x, FY.y}, iy, oy), tfy1 = __builtin_elementwise_fma(v2t{FY.z, FY.w}, iy, oy);
+    const v2t tnz0 = __builtin_elementwise_fma(v2t{NZ.x, NZ.y}, iz, oz), tnz1 = __builtin_elementwise_fma(v2t{NZ.z, NZ.w}, iz, oz);
+    const v2t tfz0 = __builtin_elementwise_fma(v2t{FZ.x, FZ.y}, iz, oz), tfz1 = __builtin_elementwise_fma(v2t{FZ.z, FZ.w}, iz, oz);
+    const float tn[4][3] = {{tnx0.x, tny0.x, tnz0.x}, {tnx0.y, tny0.y, tnz0.y}, {tnx1.x, tny1.x, tnz1.x}, {tnx1.y, tny1.y, tnz1.y}};
+    const float tf[4][3] = {{tfx0.x, tfy0.x, tfz0.x}, {tfx0.y, tfy0.y, tfz0.y}, {tfx1.x, tfy1.x, tfz1.x}, {tfx1.y, tfy1.y, tfz1.y}};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const float t0 = fmaxf(fmaxf(fmaxf(tn[i][0], tn[i][1]), tn[i][2]), tmin);
+        const float t1 = fminf(fminf(fminf(tf[i][0], tf[i][1]), tf[i][2]), tmax);
+        t[i] = (t0 <= t1 && c[i] != 0xffffffffu) ? t0 : INFINITY;
     }
 }
 __device__ __forceinline__ void cswap(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {

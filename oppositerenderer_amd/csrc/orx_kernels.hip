@@ -407,25 +407,54 @@ void launch_grid_setup(hipStream_t s, const PhotonBufs& pb) {
 /* ------------------------------------------------------------------ */
 /* hash + histogram (atomic rank = position inside the cell)           */
 /* ------------------------------------------------------------------ */
+/* calculateHashCellsKernel + histogram (OptixRenderer_SpatialHash.cu:152-173):
+ * four slots per thread per step, their loads and the rank-returning
+ * histogram atomics issued back to back (memory-level parallelism). */
 __global__ __launch_bounds__(256) void k_grid_hash(PhotonBufs pb) {
     const GridParams g = *pb.grid;
     const uint32_t invalid = g.G + 1;
     const float inv = 1.f / g.cell;
-    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < pb.S; s += gridDim.x * blockDim.x) {
-        uint32_t p = s / pb.D, k = s - p * pb.D;
-        uint32_t key = invalid, rank = 0;
-        if (g.G && ((pb.vmask[p] >> k) & 1u)) {
-            float4 a = pb.slotA[s];
-            f3 pp = (mk(a.x, a.y, a.z) - mk(g.ox, g.oy, g.oz)) * inv;
-            uint32_t cx = orx_f2u_sat(orx_floorf(pp.x));
-            uint32_t cy = orx_f2u_sat(orx_floorf(pp.y));
-            uint32_t cz = orx_f2u_sat(orx_floorf(pp.z));
-            key = cx + cy * g.gx + cz * g.gx * g.gy;
-            if (key > g.G) key = g.G;
-            rank = atomicAdd(&pb.hist[key], 1u);
+    const uint32_t T = gridDim.x * blockDim.x;
+    for (uint32_t s0 = blockIdx.x * blockDim.x + threadIdx.x; s0 < pb.S; s0 += 4 * T) {
+        uint32_t key[4], rank[4];
+        bool v[4];
+        float4 a[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t s = s0 + q * T;
+            key[q] = invalid;
+            rank[q] = 0;
+            v[q] = false;
+            if (s < pb.S && g.G) {
+                const uint32_t p = s / pb.D, k = s - p * pb.D;
+                v[q] = (pb.vmask[p] >> k) & 1u;
+            }
         }
-        pb.keys[s] = key;
-        pb.ranks[s] = rank;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (v[q]) a[q] = pb.slotA[s0 + q * T];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (v[q]) {
+                const f3 pp = (mk(a[q].x, a[q].y, a[q].z) - mk(g.ox, g.oy, g.oz)) * inv;
+                const uint32_t cx = orx_f2u_sat(orx_floorf(pp.x));
+                const uint32_t cy = orx_f2u_sat(orx_floorf(pp.y));
+                const uint32_t cz = orx_f2u_sat(orx_floorf(pp.z));
+                uint32_t kk = cx + cy * g.gx + cz * g.gx * g.gy;
+                key[q] = kk > g.G ? g.G : kk;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (v[q]) rank[q] = atomicAdd(&pb.hist[key[q]], 1u);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t s = s0 + q * T;
+            if (s < pb.S) {
+                pb.keys[s] = key[q];
+                pb.ranks[s] = rank[q];
+            }
+        }
     }
 }
 void launch_grid_hash(hipStream_t s, const PhotonBufs& pb) {
@@ -516,12 +545,26 @@ void launch_grid_scan(hipStream_t s, const PhotonBufs& pb) {
 /* ------------------------------------------------------------------ */
 /* scatter photons into cell order                                     */
 /* ------------------------------------------------------------------ */
+/* sort_by_key as a counting-sort scatter (SpatialHash.cu:193-196): the
+ * destination of slot s is offsets[key] + rank; this writes the permutation,
+ * k_grid_permute then moves the photons destination-major. */
 __global__ __launch_bounds__(256) void k_grid_scatter(PhotonBufs pb) {
     const uint32_t G = pb.grid->G;
-    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < pb.S; s += gridDim.x * blockDim.x) {
-        uint32_t key = pb.keys[s];
-        if (key > G) continue;
-        pb.perm[pb.offsets[key] + pb.ranks[s]] = s;
+    const uint32_t T = gridDim.x * blockDim.x;
+    for (uint32_t s0 = blockIdx.x * blockDim.x + threadIdx.x; s0 < pb.S; s0 += 4 * T) {
+        uint32_t key[4], rank[4], off[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t s = s0 + q * T;
+            key[q] = s < pb.S ? pb.keys[s] : G + 1;
+            rank[q] = s < pb.S ? pb.ranks[s] : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (key[q] <= G) off[q] = pb.offsets[key[q]];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (key[q] <= G) pb.perm[off[q] + rank[q]] = s0 + q * T;
     }
 }
 /* grid order -> SoA planes: destination-major, so the nine plane writes are
@@ -529,20 +572,35 @@ __global__ __launch_bounds__(256) void k_grid_scatter(PhotonBufs pb) {
 __global__ __launch_bounds__(256) void k_grid_permute(PhotonBufs pb) {
     const uint32_t valid = pb.grid->valid;
     const size_t P = pb.splane;
-    for (uint32_t dst = blockIdx.x * blockDim.x + threadIdx.x; dst < valid; dst += gridDim.x * blockDim.x) {
-        const uint32_t s = pb.perm[dst];
-        const float4 a = pb.slotA[s], b = pb.slotB[s];
-        const float cz = pb.slotC[s];
-        float* o = pb.sorted + dst;
-        o[0] = a.x;
-        o[P] = a.y;
-        o[2 * P] = a.z;
-        o[3 * P] = b.x;
-        o[4 * P] = b.y;
-        o[5 * P] = b.z;
-        o[6 * P] = a.w;
-        o[7 * P] = b.w;
-        o[8 * P] = cz;
+    const uint32_t T = gridDim.x * blockDim.x;
+    for (uint32_t d0 = blockIdx.x * blockDim.x + threadIdx.x; d0 < valid; d0 += 4 * T) {
+        uint32_t src[4];
+        float4 a[4], b[4];
+        float cz[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) src[q] = d0 + q * T < valid ? pb.perm[d0 + q * T] : 0xffffffffu;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (src[q] != 0xffffffffu) {
+                a[q] = pb.slotA[src[q]];
+                b[q] = pb.slotB[src[q]];
+                cz[q] = pb.slotC[src[q]];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (src[q] == 0xffffffffu) continue;
+            float* o = pb.sorted + d0 + q * T;
+            o[0] = a[q].x;
+            o[P] = a[q].y;
+            o[2 * P] = a[q].z;
+            o[3 * P] = b[q].x;
+            o[4 * P] = b[q].y;
+            o[5 * P] = b[q].z;
+            o[6 * P] = a[q].w;
+            o[7 * P] = b[q].w;
+            o[8 * P] = cz[q];
+        }
     }
 }
 void launch_grid_scatter(hipStream_t s, const PhotonBufs& pb) {

@@ -18,7 +18,8 @@ from . import _abi
 from .scenes import Camera, Scene
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liborx.so")
+# ORX_LIB selects an alternative in-tree build (e.g. liborx_fp32.so) for A/B measurements
+LIB_PATH = os.environ.get("ORX_LIB") or os.path.join(_HERE, "liborx.so")
 _lib = None
 
 
