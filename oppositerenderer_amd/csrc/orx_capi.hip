@@ -364,7 +364,7 @@ struct orx_renderer {
     hipStream_t ext_stream = nullptr; /* caller-provided stream (orx_set_stream) */
     bool use_ext = false;
     DevBuf d_rng, d_hp, d_ind, d_dir, d_out, d_dbg;
-    DevBuf d_slotA, d_slotB, d_slotC, d_vmask, d_sorted, d_perm, d_keys, d_ranks;
+    DevBuf d_slots, d_vmask, d_sorted, d_perm, d_keys, d_ranks;
     DevBuf d_hist, d_offsets, d_bbox, d_partials, d_grid, d_work;
     PixelBufs px{};
     PhotonBufs pb{};
@@ -666,9 +666,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_dir.ensure(nhp * 12));
     HIPCHK(r, r->d_out.ensure(nhp * 12));
     HIPCHK(r, r->d_dbg.ensure(nhp * 8));
-    HIPCHK(r, r->d_slotA.ensure(S * 16));
-    HIPCHK(r, r->d_slotB.ensure(S * 16));
-    HIPCHK(r, r->d_slotC.ensure(S * 4));
+    HIPCHK(r, r->d_slots.ensure(S * 64));
     HIPCHK(r, r->d_vmask.ensure(nphot));
     const size_t splane = ((S + 4) + 3) & ~(size_t)3;
     HIPCHK(r, r->d_sorted.ensure(9 * splane * 4));
@@ -714,9 +712,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     pb.D = D;
     pb.S = (uint32_t)S;
     pb.gmax = r->cfg.photon_grid_max_size;
-    pb.slotA = r->d_slotA.as<float4>();
-    pb.slotB = r->d_slotB.as<float4>();
-    pb.slotC = r->d_slotC.as<float>();
+    pb.slots = r->d_slots.as<float4>();
     pb.vmask = r->d_vmask.as<uint8_t>();
     pb.sorted = r->d_sorted.as<float>();
     pb.splane = (uint32_t)splane;
@@ -1155,20 +1151,16 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
     }
     case ORX_BUF_PHOTON_SLOTS: {
         const size_t n = (size_t)r->pb.S;
-        std::vector<float4> A(n), B(n);
-        std::vector<float> Cc(n);
+        std::vector<float4> R(4 * n);
         std::vector<uint8_t> vm((size_t)r->prows * r->cfg.photon_launch_width);
-        if (n) {
-            HIPCHK(r, d2h(A.data(), r->d_slotA.p, n * 16));
-            HIPCHK(r, d2h(B.data(), r->d_slotB.p, n * 16));
-            HIPCHK(r, d2h(Cc.data(), r->d_slotC.p, n * 4));
-        }
+        if (n) HIPCHK(r, d2h(R.data(), r->d_slots.p, n * 64));
         if (!vm.empty()) HIPCHK(r, d2h(vm.data(), r->d_vmask.p, vm.size()));
         float* o = (float*)dst;
         const uint32_t D = r->cfg.max_photon_deposits;
         for (size_t i = 0; i < n; i++) {
             const bool valid = (vm[i / D] >> (i % D)) & 1u;
-            float v[9] = {A[i].w, B[i].w, Cc[i], A[i].x, A[i].y, A[i].z, B[i].x, B[i].y, B[i].z};
+            const float4 a = R[4 * i], b = R[4 * i + 1], c = R[4 * i + 2];
+            float v[9] = {a.w, b.w, c.x, a.x, a.y, a.z, b.x, b.y, b.z};
             if (!valid) std::memset(v, 0, sizeof v);
             std::memcpy(o + 9 * i, v, sizeof v);
         }

@@ -59,9 +59,8 @@ struct PhotonBufs {
     uint32_t D;         /* max deposits per emitted photon */
     uint32_t S;         /* local slots = prows*PW*D */
     uint32_t gmax;      /* PHOTON_GRID_MAX_SIZE */
-    float4* slotA;      /* [S] pos.xyz, power.x */
-    float4* slotB;      /* [S] dir.xyz, power.y */
-    float* slotC;       /* [S] power.z */
+    float4* slots;      /* [S][4] 64-B deposit records: pos.xyz|power.x, dir.xyz|power.y, power.z, unused
+                         * (one record per cache-line half: the grid permute reads it in one go) */
     uint8_t* vmask;     /* [S/D] bit k: deposit k stored with fmaxf(power) > 0 */
     float* sorted;      /* grid-ordered photons, nine float planes (SoA): x y z | dir x y z | power x y z */
     uint32_t splane;    /* plane stride in floats (multiple of 4, >= S + 4) */

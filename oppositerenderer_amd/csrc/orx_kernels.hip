@@ -234,9 +234,10 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
                     const f3 N = shading_normal(S, h);
                     if (P.depth >= 1 && P.numStored < pb.D) {
                         const uint32_t si = P.p_local * pb.D + P.numStored;
-                        pb.slotA[si] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, P.power.x);
-                        pb.slotB[si] = make_float4(P.d.x, P.d.y, P.d.z, P.power.y);
-                        pb.slotC[si] = P.power.z;
+                        float4* rec = pb.slots + 4 * (size_t)si;
+                        rec[0] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, P.power.x);
+                        rec[1] = make_float4(P.d.x, P.d.y, P.d.z, P.power.y);
+                        rec[2].x = P.power.z;
                         if (fmax3(P.power) > 0) {
                             P.mask |= 1u << P.numStored;
                             lo_x = fminf(lo_x, hitPoint.x); lo_y = fminf(lo_y, hitPoint.y); lo_z = fminf(lo_z, hitPoint.z);
@@ -432,7 +433,7 @@ __global__ __launch_bounds__(256) void k_grid_hash(PhotonBufs pb) {
         }
 #pragma unroll
         for (int q = 0; q < 4; q++)
-            if (v[q]) a[q] = pb.slotA[s0 + q * T];
+            if (v[q]) a[q] = pb.slots[4 * (size_t)(s0 + q * T)];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             if (v[q]) {
@@ -582,9 +583,10 @@ __global__ __launch_bounds__(256) void k_grid_permute(PhotonBufs pb) {
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             if (src[q] != 0xffffffffu) {
-                a[q] = pb.slotA[src[q]];
-                b[q] = pb.slotB[src[q]];
-                cz[q] = pb.slotC[src[q]];
+                const float4* rec = pb.slots + 4 * (size_t)src[q];
+                a[q] = rec[0];
+                b[q] = rec[1];
+                cz[q] = rec[2].x;
             }
         }
 #pragma unroll
