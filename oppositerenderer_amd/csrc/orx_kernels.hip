@@ -687,14 +687,34 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
                 const v2f r2v = v2f{radius2, radius2};
                 const size_t P = pb.splane;
                 const float* __restrict__ SX = pb.sorted;
+                /* Row culling: a (z,y) row whose cell square (grown by a margin
+                 * m that covers the rounding of the cell assignment) lies
+                 * outside the sphere holds no photon within r; otherwise only
+                 * the cells the chord [p.x - rx, p.x + rx] (+m) touches are
+                 * walked.  The visit counters stay the reference's (whole
+                 * window, IndirectRadianceEstimation.cu:113/:124). */
+                const float m = g.cell * 1e-3f;
                 for (uint32_t z = z_lo; z <= z_hi; z++) {
+                    const float zc0 = g.oz + (float)z * g.cell - m, zc1 = g.oz + (float)(z + 1) * g.cell + m;
+                    const float dz = fmaxf(0.f, fmaxf(zc0 - pos.z, pos.z - zc1));
                     for (uint32_t yy = y_lo; yy <= y_hi; yy++) {
-                        const uint32_t from = x_lo + yy * g.gx + z * g.gx * g.gy;
+                        const uint32_t row = yy * g.gx + z * g.gx * g.gy;
+                        const uint32_t from = x_lo + row;
                         const uint32_t to = from + (x_hi - x_lo);
-                        const uint32_t off = pb.offsets[from];
-                        const uint32_t offTo = pb.offsets[to + 1];
                         dC++;
-                        dP += offTo - off;
+                        dP += pb.offsets[to + 1] - pb.offsets[from];
+                        const float yc0 = g.oy + (float)yy * g.cell - m, yc1 = g.oy + (float)(yy + 1) * g.cell + m;
+                        const float dy = fmaxf(0.f, fmaxf(yc0 - pos.y, pos.y - yc1));
+                        const float rem = radius2 - dy * dy - dz * dz;
+                        if (rem < 0.f) continue;
+                        const float rx = sqrtf(rem) + m;
+                        const int32_t cxl = orx_f2i_sat(orx_floorf((np.x - rx) * invCellSize));
+                        const int32_t cxh = orx_f2i_sat(orx_floorf((np.x + rx) * invCellSize));
+                        const uint32_t xl = cxl > (int32_t)x_lo ? (uint32_t)cxl : x_lo;
+                        const uint32_t xh = cxh < (int32_t)x_hi ? (uint32_t)cxh : x_hi;
+                        if (cxh < 0 || xl > xh) continue;
+                        const uint32_t off = pb.offsets[xl + row];
+                        const uint32_t offTo = pb.offsets[xh + row + 1];
                         for (uint32_t kb = off & ~3u; kb < offTo; kb += 4) {
                             const float4 X = *(const float4*)(SX + kb);
                             const float4 Y = *(const float4*)(SX + P + kb);
