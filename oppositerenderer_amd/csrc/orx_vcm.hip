@@ -233,26 +233,35 @@ struct VBsdf {
         cont = 0.f;
         pick[0] = pick[1] = 0.f;
     }
+    /* (all BxDF slots are addressed with compile-time indices so the BSDF
+     * stays in registers: no scratch) */
     __device__ __forceinline__ void add(const Bxdf& b) {
-        bx[n] = b;
         float rr = 0.f;
         rr += bx_cont(b, fix);
         cont = fminf(1.f, cont + rr);
         float albedo = 0.f;
         albedo += bx_albedo(b, fix);
-        pick[n] = albedo;
+        if (n == 0) {
+            bx[0] = b;
+            pick[0] = albedo;
+        } else {
+            bx[1] = b;
+            pick[1] = albedo;
+        }
         n++;
     }
     __device__ __forceinline__ int count(uint32_t mask) const {
         int c = 0;
-        for (int i = 0; i < n; i++) c += bx_match(bx[i].type, mask) ? 1 : 0;
+#pragma unroll
+        for (int i = 0; i < 2; i++) c += (i < n && bx_match(bx[i].type, mask)) ? 1 : 0;
         return c;
     }
     __device__ __forceinline__ bool is_specular() const { return count(BX_ALL & ~BX_SPECULAR) == 0; }
     __device__ __forceinline__ float sum_pick(uint32_t mask) const {
         float c = 0.f;
-        for (int i = 0; i < n; i++)
-            if (bx_match(bx[i].type, mask)) c += pick[i];
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+            if (i < n && bx_match(bx[i].type, mask)) c += pick[i];
         return c;
     }
     /* VcmBSDF::sampleF via vcmSampleF (BSDF.h:411-485) */
@@ -264,21 +273,24 @@ struct VBsdf {
         if (nMatched) {
             sum = sum_pick(BX_ALL);
             float prev = 0.f;
-            for (int i = 0; i < n; i++) {
-                if (bx_match(bx[i].type, BX_ALL)) {
+            bool found = false;
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                if (!found && i < n && bx_match(bx[i].type, BX_ALL)) {
                     const float cp = pick[i] / sum;
-                    if (sx < prev + cp) { index = i; break; }
-                    prev += cp;
+                    if (sx < prev + cp) { index = i; found = true; }
+                    else prev += cp;
                 }
             }
         }
         if (sum == 0.f) { pdf = 0.0f; return mk1(0.f); }
-        const Bxdf& b = bx[index];
+        const Bxdf b = index ? bx[1] : bx[0];
+        const float pick_index = index ? pick[1] : pick[0];
         const f3 world_wo = dg.to_world(fix);
         const f3 wo = dg.to_local(world_wo);
         f3 wi = mk1(0.f);
         f3 f = bx_sample_f(b, wo, wi, sy, sz, pdf, fix_is_light);
-        const float q = pick[index] / sum;
+        const float q = pick_index / sum;
         pdf *= q;
         if (pdf == 0.0f) { sampled = 0; return mk1(0.f); }
         sampled = b.type;
@@ -286,8 +298,9 @@ struct VBsdf {
         cos_out = fabsf(wi.z);
         if (!(b.type & BX_SPECULAR)) {
             if (nMatched > 1) {
-                for (int i = 0; i < n; i++) {
-                    if (i == index || !bx_match(bx[i].type, BX_ALL)) continue;
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    if (i >= n || i == index || !bx_match(bx[i].type, BX_ALL)) continue;
                     float comp = 0.f;
                     comp += bx_pdf(bx[i], wo, wi, false);
                     pdf += comp * q;
@@ -296,8 +309,9 @@ struct VBsdf {
             uint32_t m2 = BX_ALL;
             if (dot(gn, world_wi) * dot(gn, world_wo) >= 0.0f) m2 &= ~BX_TRANSMISSION;
             else m2 &= ~BX_REFLECTION;
-            for (int i = 0; i < n; i++) {
-                if (i == index || !bx_match(bx[i].type, m2)) continue;
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                if (i >= n || i == index || !bx_match(bx[i].type, m2)) continue;
                 f = f + bx_f(bx[i], wo, wi);
             }
         }
@@ -310,8 +324,9 @@ struct VBsdf {
         const float sum = sum_pick(mask);
         if (sum == 0.f) return 0.f;
         float pdf = 0.f;
-        for (int i = 0; i < n; i++) {
-            if (bx_match(bx[i].type, mask)) {
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            if (i < n && bx_match(bx[i].type, mask)) {
                 float comp = 0.f;
                 comp += bx_pdf(bx[i], fix, wi, true);
                 pdf += comp * pick[i] / sum;
@@ -333,8 +348,9 @@ struct VBsdf {
         const float sum = sum_pick(mask);
         if (sum == 0.f) return mk1(0.f);
         f3 f = mk1(0.f);
-        for (int i = 0; i < n; i++) {
-            if (bx_match(bx[i].type, mask)) {
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            if (i < n && bx_match(bx[i].type, mask)) {
                 float dp = 0.f, rp = 0.f;
                 f = f + bx_vcm_f(bx[i], fix, gen, dp, rp);
                 const float q = pick[i] / sum;
@@ -687,7 +703,7 @@ __device__ inline void connect_light(const DevScene& S, Subpath& C, const VBsdf&
 }
 
 /* cameraPass (VCMCameraPass.cu:48-80), initCameraPayload (:100-135), cameraHit (vcm.h:527-628) */
-__global__ __launch_bounds__(64) void k_vcm_camera(DevScene S, VcmBufs vb, VcmConsts c) {
+__global__ __launch_bounds__(64, 3) void k_vcm_camera(DevScene S, VcmBufs vb, VcmConsts c) {
     ORX_STACK_DECL;
     uint32_t* stk = ORX_STACK_PTR;
     const uint32_t tilesX = (c.W + 7) / 8;
