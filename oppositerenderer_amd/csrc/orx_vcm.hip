@@ -491,7 +491,7 @@ __device__ inline void connect_camera(const DevScene& S, const Subpath& L, const
 
 /* lightPass (VCMLightPass.cu:52-93), initLightPayload (:120-176), lightHit (vcm.h:210-309) */
 template <bool ESTIMATE>
-__global__ __launch_bounds__(64) void k_vcm_light(DevScene S, VcmBufs vb, VcmConsts c) {
+__global__ __launch_bounds__(64, 4) void k_vcm_light(DevScene S, VcmBufs vb, VcmConsts c) {
     ORX_STACK_DECL;
     uint32_t* stk = ORX_STACK_PTR;
     const uint32_t p = blockIdx.x * 64u + threadIdx.x;
@@ -703,7 +703,7 @@ __device__ inline void connect_light(const DevScene& S, Subpath& C, const VBsdf&
 }
 
 /* cameraPass (VCMCameraPass.cu:48-80), initCameraPayload (:100-135), cameraHit (vcm.h:527-628) */
-__global__ __launch_bounds__(64, 3) void k_vcm_camera(DevScene S, VcmBufs vb, VcmConsts c) {
+__global__ __launch_bounds__(64, 4) void k_vcm_camera(DevScene S, VcmBufs vb, VcmConsts c) {
     ORX_STACK_DECL;
     uint32_t* stk = ORX_STACK_PTR;
     const uint32_t tilesX = (c.W + 7) / 8;
