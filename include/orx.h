@@ -265,6 +265,25 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hitpoints_device
 /* indirect_device: max_local_rows * W * 3 floats for the own rows */
 orx_status orx_ppm_finish(orx_renderer* r, const void* indirect_device, size_t indirect_bytes);
 
+/* One VCM iteration of a sharded renderer (OptixRenderer.cpp:675-795 split at
+ * the light-tracing splats).  Light subpath i pairs with camera pixel i
+ * (lightSubpathCount = W*H, VCMLightPass.cu:52), so each rank traces the light
+ * subpaths and camera paths of its own rows; the only cross-rank effect is
+ * connectCameraT1 (vcm.h:311-384), whose splats may land on any row:
+ *   orx_vcm_local_light     light pass over own rows; splats into an owner-block
+ *                           buffer [world][max_local_rows][W][3]
+ *   orx_export_vcm_splats   that buffer -> caller (orx_vcm_splat_bytes)
+ *   (caller reduce-scatters (sum) the buffers, rank-major blocks)
+ *   orx_vcm_finish          camera pass over own rows with the summed own-row splats
+ * The summed splats equal the single-GPU ones up to fp32 atomic order (the
+ * single-GPU pass accumulates them with atomics too). */
+size_t orx_vcm_splat_bytes(const orx_renderer* r); /* world * max_local_rows * W * 12 */
+orx_status orx_vcm_local_light(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
+                               float ppm_radius, const orx_request* details);
+orx_status orx_export_vcm_splats(orx_renderer* r, void* dst_device, size_t dst_bytes);
+/* splat_own_rows_device: local_rows * W * 3 floats (the own block of the sum) */
+orx_status orx_vcm_finish(orx_renderer* r, const void* splat_own_rows_device, size_t bytes);
+
 #ifdef __cplusplus
 }
 #endif

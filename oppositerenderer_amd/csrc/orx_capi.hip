@@ -378,7 +378,11 @@ struct orx_renderer {
     /* VCM: pixelSizeFactor (OptixRenderer.cpp:306, :846), LVC estimate flag (:83, :461, :847) */
     float psf_x = 1.0f, psf_y = 1.0f;
     bool vcm_estimated = false;
-    size_t vcm_npx = 0;
+    size_t vcm_npx = 0;  /* own-row subpaths W*rows the VCM buffers are sized for */
+    size_t vcm_spx = 0;  /* owner-block splat pixels W*max_rows*world */
+    bool vcm_pending = false; /* light pass done, camera pass (orx_vcm_finish) outstanding */
+    VcmBufs vcm_vb{};
+    VcmConsts vcm_c{};
     DevBuf d_vcount, d_vverts, d_vsplat, d_vcam, d_tstats;
     std::vector<DevLight> host_lights;
 };
@@ -653,7 +657,6 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     r->rng_rows = local_rows(r->RH);
     r->prows = local_rows(PH);
     r->max_rows = (H + r->world - 1) / r->world;
-    const size_t npx = (size_t)r->rows * W;
     const size_t nhp = (size_t)r->max_rows * W; /* hitpoint planes padded to max_rows */
     const size_t nslot_rng = (size_t)r->rng_rows * r->RW;
     const size_t nphot = (size_t)r->prows * PW;
@@ -832,30 +835,39 @@ static void ppm_local_passes(orx_renderer* r, const DevCamera& cam, const Consts
 }
 
 /* VCM_BIDIRECTIONAL_PATH_TRACING branch of renderNextIteration (OptixRenderer.cpp:675-795) */
-static orx_status vcm_iteration(orx_renderer* r, const orx_request* det, float ppm_radius) {
-    const size_t npx = (size_t)r->W * r->H;
-    if (r->vcm_npx != npx) {
-        HIPCHK(r, r->d_vcount.ensure(npx * 4));
-        HIPCHK(r, r->d_vverts.ensure(npx * VCM_MAX_VERTS * 64));
-        HIPCHK(r, r->d_vsplat.ensure(npx * 12));
-        HIPCHK(r, r->d_vcam.ensure(npx * 12));
-        HIPCHK(r, hipMemsetAsync(r->d_vcount.p, 0, npx * 4, cur_stream(r)));
-        HIPCHK(r, hipMemsetAsync(r->d_vcam.p, 0, npx * 12, cur_stream(r)));
-        r->vcm_npx = npx;
+/* Row-sharded layout: rank r owns image rows y = rank + j*world (j < rows);
+ * light subpath i pairs with own pixel i, so vertex counts, light vertices,
+ * camera colours and the output hold own rows only.  The light pass's
+ * connectCameraT1 splats land anywhere on the image: they are accumulated in
+ * an owner-block buffer [world][max_rows][W][3] that a sharded run sums
+ * across ranks (reduce-scatter) before the camera pass. */
+static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm_radius) {
+    const size_t lpx = (size_t)r->W * r->rows;
+    const size_t spx = (size_t)r->W * r->max_rows * r->world;
+    if (r->vcm_npx != lpx || r->vcm_spx != spx) {
+        HIPCHK(r, r->d_vcount.ensure(lpx * 4 + 4));
+        HIPCHK(r, r->d_vverts.ensure(lpx * VCM_MAX_VERTS * 64 + 64));
+        HIPCHK(r, r->d_vsplat.ensure(spx * 12 + 12));
+        HIPCHK(r, r->d_vcam.ensure(lpx * 12 + 12));
+        HIPCHK(r, hipMemsetAsync(r->d_vcount.p, 0, lpx * 4, cur_stream(r)));
+        HIPCHK(r, hipMemsetAsync(r->d_vcam.p, 0, lpx * 12, cur_stream(r)));
+        r->vcm_npx = lpx;
+        r->vcm_spx = spx;
     }
-    VcmBufs vb;
+    VcmBufs& vb = r->vcm_vb;
     vb.RW = r->RW;
     vb.rng = r->px.rng;
     vb.vcount = r->d_vcount.as<uint32_t>();
-    const size_t plane = npx * VCM_MAX_VERTS;
+    const size_t plane = lpx * VCM_MAX_VERTS;
     vb.vA = r->d_vverts.as<float4>();
     vb.vB = vb.vA + plane;
     vb.vC = vb.vB + plane;
     vb.vD = vb.vC + plane;
     vb.splat = r->d_vsplat.as<float>();
+    vb.splat_in = vb.splat + (size_t)r->rank * r->max_rows * r->W * 3;
     vb.cam = r->d_vcam.as<float>();
     vb.output = r->d_out.as<float>();
-    VcmConsts c;
+    VcmConsts& c = r->vcm_c;
     float ulen = 0.f, vlen = 0.f;
     DevCamera cam = camera_setup(det->camera, &ulen, &vlen);
     c.eye = cam.eye;
@@ -873,25 +885,52 @@ static orx_status vcm_iteration(orx_renderer* r, const orx_request* det, float p
     c.W = r->W;
     c.H = r->H;
     c.count = r->W * r->H;
+    c.rank = r->rank;
+    c.world = r->world;
+    c.rows = r->rows;
+    c.max_rows = r->max_rows;
+    c.lcount = r->W * r->rows;
     c.maxPathLen = r->cfg.vcm_max_path_length;
     /* etaVCM = (nVM / nVC) * PI * r^2 with nVC = 1, nVM = lightSubPathCount */
     const float ppmRadiusSquared = ppm_radius * ppm_radius;
     const float etaVCM = ((float)c.count / (float)1u) * ORX_PI_F * ppmRadiusSquared;
     c.misVm = 0.f;
     c.misVc = 1.f / etaVCM;
+    return ORX_OK;
+}
+
+static orx_status vcm_light(orx_renderer* r) {
     hipStream_t st = cur_stream(r);
     ev_begin(r, P_VCM_LIGHT);
     if (!r->vcm_estimated) { /* subpath length estimate launch: advances the RNG, stores nothing */
-        launch_vcm_light(st, r->scene, vb, c, true);
+        launch_vcm_light(st, r->scene, r->vcm_vb, r->vcm_c, true);
         r->vcm_estimated = true;
     }
-    HIPCHK(r, hipMemsetAsync(vb.splat, 0, npx * 12, st));
-    launch_vcm_light(st, r->scene, vb, c, false);
+    HIPCHK(r, hipMemsetAsync(r->vcm_vb.splat, 0, r->vcm_spx * 12, st));
+    launch_vcm_light(st, r->scene, r->vcm_vb, r->vcm_c, false);
     ev_end(r, P_VCM_LIGHT);
+    return ORX_OK;
+}
+
+static orx_status vcm_camera(orx_renderer* r) {
     ev_begin(r, P_VCM_CAMERA);
-    launch_vcm_camera(st, r->scene, vb, c);
+    launch_vcm_camera(cur_stream(r), r->scene, r->vcm_vb, r->vcm_c);
     ev_end(r, P_VCM_CAMERA);
     return ORX_OK;
+}
+
+static orx_status vcm_check_lights(orx_renderer* r) {
+    for (const DevLight& l : r->host_lights)
+        if (l.type == LIGHT_SPOT)
+            return set_err(r, ORX_ERR_UNSUPPORTED, "VCM: spot lights are not emitted by lightEmit (helpers/light.h:130)");
+    return ORX_OK;
+}
+
+static orx_status vcm_iteration(orx_renderer* r, const orx_request* det, float ppm_radius) {
+    orx_status s = vcm_prepare(r, det, ppm_radius);
+    if (s != ORX_OK) return s;
+    if ((s = vcm_light(r)) != ORX_OK) return s;
+    return vcm_camera(r);
 }
 
 orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
@@ -903,11 +942,9 @@ orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
         det->method != ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING)
         return set_err(r, ORX_ERR_UNSUPPORTED, "render method not supported by this build");
     if (det->method == ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING && r->world > 1)
-        return set_err(r, ORX_ERR_UNSUPPORTED, "VCM runs on one device");
-    if (det->method == ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING)
-        for (const DevLight& l : r->host_lights)
-            if (l.type == LIGHT_SPOT)
-                return set_err(r, ORX_ERR_UNSUPPORTED, "VCM: spot lights are not emitted by lightEmit (helpers/light.h:130)");
+        return set_err(r, ORX_ERR_STATE, "sharded VCM runs through orx_vcm_local_light/orx_export_vcm_splats/orx_vcm_finish");
+    if (det->method == ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING && vcm_check_lights(r) != ORX_OK)
+        return ORX_ERR_UNSUPPORTED;
     if (det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world > 1)
         return set_err(r, ORX_ERR_STATE, "sharded PPM runs through orx_ppm_local_passes/_gather_external/_finish");
     orx_status s0 = begin_iteration(r, local_iteration_number, det);
@@ -1021,6 +1058,53 @@ orx_status orx_ppm_finish(orx_renderer* r, const void* indirect, size_t bytes) {
     launch_ppm_direct_output(st, r->scene, r->px, r->last_consts);
     ev_end(r, P_DIRECT);
     HIPCHK(r, hipGetLastError());
+    return ORX_OK;
+}
+
+size_t orx_vcm_splat_bytes(const orx_renderer* r) { return r ? (size_t)r->W * r->max_rows * r->world * 12 : 0; }
+
+orx_status orx_vcm_local_light(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
+                               float ppm_radius, const orx_request* det) {
+    (void)iteration_number;
+    if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
+    if (det->method != ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING)
+        return set_err(r, ORX_ERR_INVALID_ARGUMENT, "orx_vcm_local_light needs a VCM request");
+    if (vcm_check_lights(r) != ORX_OK) return ORX_ERR_UNSUPPORTED;
+    orx_status s = begin_iteration(r, local_iteration_number, det);
+    if (s != ORX_OK) return s;
+    if ((s = vcm_prepare(r, det, ppm_radius)) != ORX_OK) return s;
+    if ((s = vcm_light(r)) != ORX_OK) return s;
+    HIPCHK(r, hipGetLastError());
+    r->vcm_pending = true;
+    r->last_method = (uint64_t)det->method;
+    r->last_consts = make_consts(r, ppm_radius, local_iteration_number);
+    return ORX_OK;
+}
+
+orx_status orx_export_vcm_splats(orx_renderer* r, void* dst, size_t bytes) {
+    if (!r || !dst) return ORX_ERR_INVALID_ARGUMENT;
+    if (!r->vcm_pending) return set_err(r, ORX_ERR_STATE, "no VCM light pass to export");
+    const size_t need = orx_vcm_splat_bytes(r);
+    if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "destination too small");
+    HIPCHK(r, hipSetDevice(r->device));
+    HIPCHK(r, hipMemcpyAsync(dst, r->d_vsplat.p, need, hipMemcpyDeviceToDevice, cur_stream(r)));
+    return ORX_OK;
+}
+
+orx_status orx_vcm_finish(orx_renderer* r, const void* splat_own_rows, size_t bytes) {
+    if (!r || !splat_own_rows) return ORX_ERR_INVALID_ARGUMENT;
+    if (!r->vcm_pending) return set_err(r, ORX_ERR_STATE, "orx_vcm_finish without a light pass");
+    const size_t need = (size_t)r->W * r->rows * 12;
+    if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "splat buffer too small");
+    HIPCHK(r, hipSetDevice(r->device));
+    /* the summed own-row splats replace the local ones (readable as ORX_BUF_VCM_SPLAT) */
+    float* own = r->d_vsplat.as<float>() + (size_t)r->rank * r->max_rows * r->W * 3;
+    if ((const void*)own != splat_own_rows)
+        HIPCHK(r, hipMemcpyAsync(own, splat_own_rows, need, hipMemcpyDeviceToDevice, cur_stream(r)));
+    orx_status s = vcm_camera(r);
+    if (s != ORX_OK) return s;
+    HIPCHK(r, hipGetLastError());
+    r->vcm_pending = false;
     return ORX_OK;
 }
 
@@ -1172,7 +1256,9 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
     case ORX_BUF_OUTPUT: HIPCHK(r, d2h(dst, r->d_out.p, need)); break;
     case ORX_BUF_DEBUG_VISITED: HIPCHK(r, d2h(dst, r->d_dbg.p, need)); break;
     case ORX_BUF_VCM_VERTEX_COUNT: HIPCHK(r, d2h(dst, r->d_vcount.p, need)); break;
-    case ORX_BUF_VCM_SPLAT: HIPCHK(r, d2h(dst, r->d_vsplat.p, need)); break;
+    case ORX_BUF_VCM_SPLAT: /* own rows of the owner-block buffer */
+        HIPCHK(r, d2h(dst, r->d_vsplat.as<float>() + (size_t)r->rank * r->max_rows * r->W * 3, need));
+        break;
     case ORX_BUF_VCM_CAMERA: HIPCHK(r, d2h(dst, r->d_vcam.p, need)); break;
     case ORX_BUF_VCM_VERTICES: { /* four float4 planes [9][npx] -> [9][npx][16] */
         const size_t plane = r->vcm_npx * VCM_MAX_VERTS;

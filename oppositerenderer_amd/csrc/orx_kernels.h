@@ -119,7 +119,8 @@ struct VcmBufs {
     float4* vB;         /* [9][W*H] throughput.xyz | dVCM */
     float4* vC;         /* [9][W*H] normal.xyz | dVC */
     float4* vD;         /* [9][W*H] localDirFix.xyz | dVM */
-    float* splat;       /* [W*H*3] connectCameraT1 accumulation of this iteration */
+    float* splat;       /* [world][max_rows][W][3] connectCameraT1 accumulation of this iteration (owner-block layout) */
+    const float* splat_in; /* [rows][W][3] summed splats of the own rows (camera pass) */
     float* cam;         /* [W*H*3] camera subpath colour of this iteration */
     float* output;      /* [W*H*3] running sum */
 };
@@ -129,7 +130,8 @@ struct VcmConsts {
     float lookdirLen, ipsx, ipsy;   /* imagePlaneSize = 2*(ulen, vlen) */
     float psfx, psfy;               /* pixelSizeFactor (OptixRenderer.cpp:846) */
     float misVc, misVm;             /* 1/etaVCM, 0 (vcmUseVM = false) */
-    uint32_t W, H, count;           /* count = lightSubpathCount = W*H */
+    uint32_t W, H, count;           /* count = lightSubpathCount = W*H (global) */
+    uint32_t rank, world, rows, max_rows, lcount; /* own rows y = rank + j*world; lcount = rows*W */
     uint32_t maxPathLen;
 };
 void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c, bool estimate);

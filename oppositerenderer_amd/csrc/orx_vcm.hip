@@ -482,7 +482,8 @@ __device__ inline void connect_camera(const DevScene& S, const Subpath& L, const
     const float conv = 1.f / cameraPdfA;
     const f3 contrib = ((L.throughput * misWeight) * f) / ((float)c.count * conv);
     if (!occluded(S, hit, dirToCamera, distance, stk)) {
-        float* o = splat + 3 * ((size_t)iy * c.W + ix);
+        /* owner-block layout [world][max_rows][W]: row iy belongs to rank iy % world */
+        float* o = splat + 3 * (((size_t)(iy % c.world) * c.max_rows + iy / c.world) * c.W + ix);
         unsafeAtomicAdd(o + 0, contrib.x);
         unsafeAtomicAdd(o + 1, contrib.y);
         unsafeAtomicAdd(o + 2, contrib.z);
@@ -494,10 +495,10 @@ template <bool ESTIMATE>
 __global__ __launch_bounds__(64, 4) void k_vcm_light(DevScene S, VcmBufs vb, VcmConsts c) {
     ORX_STACK_DECL;
     uint32_t* stk = ORX_STACK_PTR;
-    const uint32_t p = blockIdx.x * 64u + threadIdx.x;
-    if (p >= c.count) return;
-    const uint32_t x = p % c.W, y = p / c.W;
-    const size_t slot = (size_t)y * vb.RW + x;
+    const uint32_t p = blockIdx.x * 64u + threadIdx.x; /* own-row subpath: x + j*W */
+    if (p >= c.lcount) return;
+    const uint32_t x = p % c.W, j = p / c.W;
+    const size_t slot = (size_t)j * vb.RW + x; /* RNG planes hold the own rows */
     Rng rs = rng_load(vb.rng, slot);
     uint32_t nverts = 0;
     Subpath L;
@@ -586,7 +587,7 @@ __global__ __launch_bounds__(64, 4) void k_vcm_light(DevScene S, VcmBufs vb, Vcm
         if (!spec) {
             const uint32_t k = nverts++;
             if (!ESTIMATE && k < VCM_MAX_VERTS) {
-                const size_t o = (size_t)k * c.count + p;
+                const size_t o = (size_t)k * c.lcount + p;
                 vb.vA[o] = make_float4(hit.x, hit.y, hit.z, __uint_as_float(mi));
                 vb.vB[o] = make_float4(L.throughput.x, L.throughput.y, L.throughput.z, L.dVCM);
                 vb.vC[o] = make_float4(N.x, N.y, N.z, L.dVC);
@@ -708,10 +709,11 @@ __global__ __launch_bounds__(64, 4) void k_vcm_camera(DevScene S, VcmBufs vb, Vc
     uint32_t* stk = ORX_STACK_PTR;
     const uint32_t tilesX = (c.W + 7) / 8;
     const uint32_t x = (blockIdx.x % tilesX) * 8 + (threadIdx.x & 7);
-    const uint32_t y = (blockIdx.x / tilesX) * 8 + (threadIdx.x >> 3);
-    if (x >= c.W || y >= c.H) return;
-    const uint32_t p = x + y * c.W;
-    const size_t slot = (size_t)y * vb.RW + x;
+    const uint32_t j = (blockIdx.x / tilesX) * 8 + (threadIdx.x >> 3); /* own row j = image row rank + j*world */
+    if (x >= c.W || j >= c.rows) return;
+    const uint32_t y = c.rank + j * c.world;
+    const uint32_t p = x + j * c.W;
+    const size_t slot = (size_t)j * vb.RW + x;
     Rng rs = rng_load(vb.rng, slot);
     Subpath C;
     C.throughput = mk1(1.0f);
@@ -767,7 +769,7 @@ __global__ __launch_bounds__(64, 4) void k_vcm_camera(DevScene S, VcmBufs vb, Vc
         if (!bs.is_specular()) {
             connect_light(S, C, bs, hit, c, rs, stk);
             const uint32_t nv = nverts < VCM_MAX_VERTS ? nverts : VCM_MAX_VERTS;
-            for (uint32_t k = 0; k < nv; ++k) connect_vertex(S, C, bs, hit, vb, (size_t)k * c.count + p, c, stk);
+            for (uint32_t k = 0; k < nv; ++k) connect_vertex(S, C, bs, hit, vb, (size_t)k * c.lcount + p, c, stk);
         }
         if (c.maxPathLen <= C.depth) break;
         sample_scattering(C, hit, bs, c, rs);
@@ -777,9 +779,9 @@ __global__ __launch_bounds__(64, 4) void k_vcm_camera(DevScene S, VcmBufs vb, Vc
     vb.cam[o3 + 0] = C.color.x;
     vb.cam[o3 + 1] = C.color.y;
     vb.cam[o3 + 2] = C.color.z;
-    const float ox = vb.output[o3 + 0] + vb.splat[o3 + 0];
-    const float oy = vb.output[o3 + 1] + vb.splat[o3 + 1];
-    const float oz = vb.output[o3 + 2] + vb.splat[o3 + 2];
+    const float ox = vb.output[o3 + 0] + vb.splat_in[o3 + 0];
+    const float oy = vb.output[o3 + 1] + vb.splat_in[o3 + 1];
+    const float oz = vb.output[o3 + 2] + vb.splat_in[o3 + 2];
     vb.output[o3 + 0] = ox + C.color.x;
     vb.output[o3 + 1] = oy + C.color.y;
     vb.output[o3 + 2] = oz + C.color.z;
@@ -787,12 +789,14 @@ __global__ __launch_bounds__(64, 4) void k_vcm_camera(DevScene S, VcmBufs vb, Vc
 }
 
 void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c, bool estimate) {
-    const uint32_t blocks = (c.count + 63) / 64;
+    const uint32_t blocks = (c.lcount + 63) / 64;
+    if (blocks == 0) return;
     if (estimate) hipLaunchKernelGGL(k_vcm_light<true>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
     else hipLaunchKernelGGL(k_vcm_light<false>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
 }
 void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
-    const uint32_t blocks = ((c.W + 7) / 8) * ((c.H + 7) / 8);
+    const uint32_t blocks = ((c.W + 7) / 8) * ((c.rows + 7) / 8);
+    if (blocks == 0) return;
     hipLaunchKernelGGL(k_vcm_camera, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
 }
 

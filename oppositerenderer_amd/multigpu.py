@@ -94,6 +94,36 @@ class ShardedPPM:
         return assemble_rows(blocks, self.W, self.H, self.world)
 
 
+class ShardedVCM:
+    """Sharded VCM iteration (include/orx.h orx_vcm_*): light + camera subpaths
+    of the own rows; the light pass's connectCameraT1 splats (vcm.h:311-384)
+    are the only cross-rank data, summed with one reduce-scatter of the
+    owner-block splat buffers [world][max_rows][W][3] before the camera pass.
+
+    Backends expose vcm_local_light / export_vcm_splats / vcm_finish / alloc."""
+
+    def __init__(self, backend, dist, world, rank, W, H):
+        self.b, self.dist, self.world, self.rank, self.W, self.H = backend, dist, world, rank, W, H
+        self.max_rows = (H + world - 1) // world
+        self.rows = local_rows(H, rank, world)
+        self.blk = self.max_rows * W * 3
+        self.splat_all = backend.alloc(world * self.blk)
+        self.splat_own = backend.alloc(self.blk)
+        self.gloo = dist.get_backend() == "gloo"
+
+    def iteration(self, it, local_it, radius, request):
+        self.b.vcm_local_light(it, local_it, radius, request)
+        self.b.export_vcm_splats(self.splat_all)
+        if self.gloo:  # gloo has no reduce_scatter: all_reduce + own block
+            self.dist.all_reduce(self.splat_all)
+            self.splat_own.copy_(self.splat_all[self.rank * self.blk:(self.rank + 1) * self.blk])
+        else:
+            self.dist.reduce_scatter_tensor(self.splat_own, self.splat_all)
+        self.b.vcm_finish(self.splat_own)
+
+    image = ShardedPPM.image
+
+
 class DeviceShard:
     """liborx.so backend: buffers are torch device tensors, kernels run on torch's current stream."""
 
@@ -108,6 +138,9 @@ class DeviceShard:
             ("orx_export_hitpoints", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
             ("orx_ppm_gather_external", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t], C.c_int),
             ("orx_ppm_finish", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
+            ("orx_vcm_local_light", [C.c_void_p, C.c_uint64, C.c_uint64, C.c_float, C.c_void_p], C.c_int),
+            ("orx_export_vcm_splats", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
+            ("orx_vcm_finish", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
         ):
             f = getattr(lib, name)
             f.argtypes, f.restype = args, res
@@ -142,6 +175,15 @@ class DeviceShard:
 
     def finish(self, ind_local):
         self.r._check(self.lib.orx_ppm_finish(self.r._h, C.c_void_p(ind_local.data_ptr()), ind_local.numel() * 4))
+
+    def vcm_local_light(self, it, local_it, radius, request):
+        self.r._check(self.lib.orx_vcm_local_light(self.r._h, it, local_it, radius, C.byref(request)))
+
+    def export_vcm_splats(self, t):
+        self.r._check(self.lib.orx_export_vcm_splats(self.r._h, C.c_void_p(t.data_ptr()), t.numel() * 4))
+
+    def vcm_finish(self, splat_own):
+        self.r._check(self.lib.orx_vcm_finish(self.r._h, C.c_void_p(splat_own.data_ptr()), splat_own.numel() * 4))
 
     def output_local_tensor(self, max_rows):
         t = self.alloc(max_rows * self.r.getWidth() * 3)

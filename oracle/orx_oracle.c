@@ -240,9 +240,10 @@ struct orc_renderer {
     uint64_t sum_photons_visited, sum_cells_visited;
     /* VCM: pixelSizeFactor (OptixRenderer.cpp:306, :846), LVC-estimated flag (:83, :461, :847) */
     float psf_x, psf_y;
-    int vcm_estimated;
-    size_t vcm_npx;
+    int vcm_estimated, vcm_pending;
+    size_t vcm_npx, vcm_spx;
     uint32_t* vcount; float* vverts; v3* vsplat; v3* vcam;
+    void* vcm_ctx; /* vcm_ctx_t of the pending sharded light pass */
 };
 
 static orx_status fail(orc_renderer* r, orx_status s, const char* msg) {
@@ -288,10 +289,11 @@ static void free_frame(orc_renderer* r) {
     r->rng = NULL; r->hp = NULL; r->photons = NULL; r->keys = NULL; r->sort_tmp = NULL;
     r->offsets = NULL; r->hist = NULL; r->indirect = NULL; r->direct = NULL; r->output = NULL; r->dbg = NULL;
     free(r->vcount); free(r->vverts); free(r->vsplat); free(r->vcam);
-    r->vcount = NULL; r->vverts = NULL; r->vsplat = NULL; r->vcam = NULL; r->vcm_npx = 0;
+    r->vcount = NULL; r->vverts = NULL; r->vsplat = NULL; r->vcam = NULL; r->vcm_npx = 0; r->vcm_spx = 0;
 }
 void orc_destroy(orc_renderer* r) {
     if (!r) return;
+    free(r->vcm_ctx);
     free_scene(r);
     free_frame(r);
     free(r);
@@ -1341,6 +1343,7 @@ static void pt_pass(orc_renderer* r, const cam_t* cam, uint64_t local) {
     }
 }
 
+static orx_status begin_iteration(orc_renderer* r, uint64_t local, const orx_request* det);
 #include "orx_oracle_vcm.c.inc"
 
 /* ------------------------------------------------------------------ */
@@ -1370,7 +1373,7 @@ orx_status orc_render_next_iteration(orc_renderer* r, uint64_t iter, uint64_t lo
     if (det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world > 1)
         return fail(r, ORX_ERR_STATE, "sharded PPM runs through the phase API");
     if (det->method == ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING && r->world > 1)
-        return fail(r, ORX_ERR_UNSUPPORTED, "VCM is single-device");
+        return fail(r, ORX_ERR_STATE, "sharded VCM runs through the phase API");
     if (det->method != ORX_METHOD_PATH_TRACING && det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING &&
         det->method != ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING)
         return fail(r, ORX_ERR_UNSUPPORTED, "oracle: method not implemented");
@@ -1474,7 +1477,7 @@ orx_status orc_read_buffer(orc_renderer* r, int32_t id, void* dst, size_t bytes,
     case ORX_BUF_DEBUG_VISITED: need = npx * 8; break;
     case ORX_BUF_VCM_VERTEX_COUNT: need = r->vcm_npx * 4; break;
     case ORX_BUF_VCM_VERTICES: need = r->vcm_npx * VCM_MAX_VERTS * 64; break;
-    case ORX_BUF_VCM_SPLAT: case ORX_BUF_VCM_CAMERA: need = r->vcm_npx * 12; break;
+    case ORX_BUF_VCM_SPLAT: case ORX_BUF_VCM_CAMERA: need = r->vcm_npx * 12; break; /* own rows */
     default: return fail(r, ORX_ERR_INVALID_ARGUMENT, "unknown buffer id");
     }
     if (out_bytes) *out_bytes = need;
@@ -1501,7 +1504,7 @@ orx_status orc_read_buffer(orc_renderer* r, int32_t id, void* dst, size_t bytes,
     case ORX_BUF_DEBUG_VISITED: memcpy(dst, r->dbg, need); break;
     case ORX_BUF_VCM_VERTEX_COUNT: memcpy(dst, r->vcount, need); break;
     case ORX_BUF_VCM_VERTICES: memcpy(dst, r->vverts, need); break;
-    case ORX_BUF_VCM_SPLAT: memcpy(dst, r->vsplat, need); break;
+    case ORX_BUF_VCM_SPLAT: memcpy(dst, r->vsplat + (size_t)r->rank * r->max_rows * r->W, need); break;
     case ORX_BUF_VCM_CAMERA: memcpy(dst, r->vcam, need); break;
     }
     return ORX_OK;

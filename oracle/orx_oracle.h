@@ -50,6 +50,13 @@ orx_status orc_ppm_local_passes(orc_renderer* r, uint64_t iter, uint64_t local, 
 orx_status orc_export_hitpoints(orc_renderer* r, void* dst, size_t bytes);
 orx_status orc_ppm_gather_external(orc_renderer* r, const void* hp, uint32_t segments, void* indirect, size_t bytes);
 orx_status orc_ppm_finish(orc_renderer* r, const void* indirect, size_t bytes);
+/* sharded VCM: light pass over own rows; splats in owner-block layout
+ * [world][max_rows][W][3]; the caller sums them across ranks and hands each
+ * rank its own block for the camera pass */
+size_t orc_vcm_splat_bytes(const orc_renderer* r);
+orx_status orc_vcm_local_light(orc_renderer* r, uint64_t iter, uint64_t local, float ppm_radius, const orx_request* det);
+orx_status orc_export_vcm_splats(orc_renderer* r, void* dst, size_t bytes);
+orx_status orc_vcm_finish(orc_renderer* r, const void* splat_own_rows, size_t bytes);
 
 /* building blocks exposed for known-answer tests */
 void orc_xorwow_init(uint64_t seed, uint32_t state[6]);

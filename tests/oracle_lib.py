@@ -108,6 +108,9 @@ class OracleShard:
             ("orc_export_hitpoints", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
             ("orc_ppm_gather_external", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t], C.c_int),
             ("orc_ppm_finish", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
+            ("orc_vcm_local_light", [C.c_void_p, C.c_uint64, C.c_uint64, C.c_float, C.c_void_p], C.c_int),
+            ("orc_export_vcm_splats", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
+            ("orc_vcm_finish", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
         ):
             f = getattr(lib, name)
             f.argtypes, f.restype = args, res
@@ -132,6 +135,16 @@ class OracleShard:
 
     def finish(self, ind_local):
         self.r._check(self.lib.orc_ppm_finish(self.r.h, C.c_void_p(ind_local.data_ptr()), ind_local.numel() * 4))
+
+    def vcm_local_light(self, it, local_it, radius, request):
+        self.r.width, self.r.height = request.width, request.height
+        self.r._check(self.lib.orc_vcm_local_light(self.r.h, it, local_it, radius, C.byref(request)))
+
+    def export_vcm_splats(self, t):
+        self.r._check(self.lib.orc_export_vcm_splats(self.r.h, C.c_void_p(t.data_ptr()), t.numel() * 4))
+
+    def vcm_finish(self, splat_own):
+        self.r._check(self.lib.orc_vcm_finish(self.r.h, C.c_void_p(splat_own.data_ptr()), splat_own.numel() * 4))
 
     def output_local_tensor(self, max_rows):
         t = self.alloc(max_rows * self.r.width * 3)

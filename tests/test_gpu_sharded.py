@@ -63,3 +63,53 @@ def test_sharded_device_path_matches_single(world, W, H, P):
     for b in shards:
         b.r.destroy()
     single.destroy()
+
+
+@pytest.mark.parametrize("world,W,H", [(2, 64, 48), (3, 50, 41)])
+def test_sharded_device_vcm_matches_single(world, W, H):
+    """Device-side sharded VCM (orx_vcm_local_light / _export_vcm_splats /
+    _vcm_finish): own-row subpaths, splat buffers summed by torch ops (the
+    reduce-scatter), must equal the single-device VCM iteration."""
+    dev = torch.device("cuda", 0)
+    scene = scenes.cornell()
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    det = RenderRequestDetails(cam, scene.name, _abi.VCM_BIDIRECTIONAL_PATH_TRACING, W, H)
+    req = det.to_abi()
+    cfg = lambda: _abi.default_config(seed=SEED, photon_launch_width=32, photon_launch_height=32)
+    shards = []
+    for rank in range(world):
+        r = OptixRenderer(cfg())
+        r.initialize(0)
+        r.set_shard(rank, world)
+        r.initScene(scene)
+        shards.append(multigpu.DeviceShard(r, torch, dev))
+    mr = (H + world - 1) // world
+    blk = mr * W * 3
+    radius = scene.initial_ppm_radius()
+    for it in range(3):
+        total = None
+        for b in shards:
+            b.vcm_local_light(it, it, radius, req)
+            t = b.alloc(world * blk)
+            b.export_vcm_splats(t)
+            total = t if total is None else total + t
+        for k, b in enumerate(shards):
+            b.vcm_finish(total[k * blk:(k + 1) * blk].contiguous())
+        radius = next_ppm_radius(radius, it)
+    torch.cuda.synchronize()
+    blocks = [b.output_local_tensor(mr).cpu().numpy().reshape(mr, W, 3) for b in shards]
+    got = multigpu.assemble_rows(blocks, W, H, world)
+    single = OptixRenderer(cfg())
+    single.initialize(0)
+    single.initScene(scene)
+    radius = scene.initial_ppm_radius()
+    for it in range(3):
+        single.renderNextIteration(it, it, radius, True, det)
+        radius = next_ppm_radius(radius, it)
+    ref = single.getOutputBuffer()
+    err = np.sqrt(((got.astype(np.float64) - ref) ** 2).sum() / (ref.astype(np.float64) ** 2).sum())
+    assert err < 1e-5, err
+    assert got.mean() > 0
+    for b in shards:
+        b.r.destroy()
+    single.destroy()

@@ -30,15 +30,15 @@ def free_port():
     return p
 
 
-def request(scene, W, H):
+def request(scene, W, H, method=_abi.PROGRESSIVE_PHOTON_MAPPING):
     req = _abi.OrxRequest()
     req.camera = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H))).to_abi()
-    req.method = _abi.PROGRESSIVE_PHOTON_MAPPING
+    req.method = method
     req.width, req.height, req.ppm_alpha = W, H, 2.0 / 3.0
     return req
 
 
-def worker(rank, world, port, out_path, W, H, P, iters):
+def worker(rank, world, port, out_path, W, H, P, iters, method=_abi.PROGRESSIVE_PHOTON_MAPPING):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -49,8 +49,9 @@ def worker(rank, world, port, out_path, W, H, P, iters):
     r.init_scene(scene)
     b = oracle_lib.OracleShard(r, torch)
     b.set_shard(rank, world)
-    sh = multigpu.ShardedPPM(b, dist, world, rank, W, H)
-    req = request(scene, W, H)
+    cls = multigpu.ShardedVCM if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING else multigpu.ShardedPPM
+    sh = cls(b, dist, world, rank, W, H)
+    req = request(scene, W, H, method)
     radius = scene.initial_ppm_radius()
     for it in range(iters):
         sh.iteration(it, it, radius, req)
@@ -73,6 +74,29 @@ def test_sharded_ppm_matches_single(world, W, H):
     r = oracle_lib.OracleRenderer(cfg)
     r.init_scene(scene)
     req = request(scene, W, H)
+    radius = scene.initial_ppm_radius()
+    for it in range(iters):
+        r.render_next_iteration(it, it, radius, req)
+        radius = next_ppm_radius(radius, it)
+    ref = r.output()
+    err = np.sqrt(((got.astype(np.float64) - ref) ** 2).sum() / (ref.astype(np.float64) ** 2).sum())
+    assert err < 1e-5, err
+    assert got.mean() > 0
+
+
+@pytest.mark.parametrize("world,W,H", [(2, 40, 32), (3, 36, 29)])
+def test_sharded_vcm_matches_single(world, W, H):
+    """VCM row sharding: own-row light + camera subpaths, splats reduce-scattered."""
+    iters = 2
+    out = os.path.join(tempfile.mkdtemp(), "img.npy")
+    vcm = _abi.VCM_BIDIRECTIONAL_PATH_TRACING
+    mp.spawn(worker, args=(world, free_port(), out, W, H, 32, iters, vcm), nprocs=world, join=True)
+    got = np.load(out)
+    scene = scenes.cornell()
+    cfg = _abi.default_config(seed=SEED, photon_launch_width=32, photon_launch_height=32 * world)
+    r = oracle_lib.OracleRenderer(cfg)
+    r.init_scene(scene)
+    req = request(scene, W, H, vcm)
     radius = scene.initial_ppm_radius()
     for it in range(iters):
         r.render_next_iteration(it, it, radius, req)
