@@ -77,7 +77,8 @@ typedef enum {
     ORX_MAT_DIFFUSE_EMITTER = 1, /* DiffuseEmitter(power, Kd)+inverseArea DiffuseEmitter.cpp:17-25 */
     ORX_MAT_MIRROR = 2,          /* Mirror(Kr)                            Mirror.cpp:17-20   */
     ORX_MAT_GLASS = 3,           /* Glass(ior, Kr, Kt)                    Glass.cpp:17-22    */
-    ORX_MAT_GLOSSY = 4           /* Glossy(Kd, Ks, exponent)              Glossy.cpp:16-33   */
+    ORX_MAT_GLOSSY = 4,          /* Glossy(Kd, Ks, exponent)              Glossy.cpp:16-33   */
+    ORX_MAT_TEXTURE = 5          /* Texture(diffuse map [, normal map])   Texture.cpp:18-29  */
 } orx_material_type;
 
 typedef struct {
@@ -90,7 +91,18 @@ typedef struct {
     float exponent;      /* Glossy Phong exponent */
     float power[3];      /* DiffuseEmitter power (scaled by Kd inside the engine, as the ctor does) */
     float inverse_area;  /* DiffuseEmitter 1/area of the emitting quad */
+    int32_t texture;     /* Texture: index into orx_scene.textures */
 } orx_material;
+
+/* Texture images (util/Image.cpp): RGBA8 rows, row 0 first, sampled as
+ * rtTextureSampler<uchar4, 2, cudaReadModeNormalizedFloat> with bilinear
+ * filtering, wrap addressing and normalised coordinates (Texture.cpp:109-122). */
+typedef struct {
+    uint32_t width, height;
+    const uint8_t* rgba;          /* width * height * 4: diffuseSampler */
+    uint32_t normal_width, normal_height;
+    const uint8_t* normal_rgba;   /* normalMapSampler, or NULL (hasNormals = 0) */
+} orx_texture;
 
 /* Light::LightType (renderer/Light.h:14-54). */
 typedef enum { ORX_LIGHT_AREA = 0, ORX_LIGHT_POINT = 1, ORX_LIGHT_SPOT = 2 } orx_light_type;
@@ -128,6 +140,12 @@ typedef struct {
     const orx_light* lights;         /* IScene::getSceneLights */
     float aabb_min[3];               /* IScene::getSceneAABB */
     float aabb_max[3];
+    /* TriangleMesh.cu attribute buffers (Scene.cpp:395-440) */
+    const float* texcoords;          /* n_vertices * 2 or NULL (textureCoordinate = 0) */
+    const float* tangents;           /* n_vertices * 3 or NULL; with bitangents: hasTangentsAndBitangents */
+    const float* bitangents;         /* n_vertices * 3 or NULL */
+    uint32_t n_textures;
+    const orx_texture* textures;
 } orx_scene;
 
 /* Compile-time constants of config.h / OptixRenderer.cpp:38-61 as runtime config. */

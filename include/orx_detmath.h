@@ -24,6 +24,7 @@
 #ifndef ORX_DETMATH_H
 #define ORX_DETMATH_H
 
+#include <stddef.h>
 #include <stdint.h>
 #if !defined(__HIPCC__)
 #include <math.h>
@@ -305,6 +306,41 @@ static inline ORX_HD float orx_powf(float x, float y) {
     if (x < 0.0f) return orx_as_float(0x7fc00000u); /* renderer never raises negatives */
     double l = orx_log_d((double)x);
     return (float)orx_exp_d((double)y * l);
+}
+
+/* tex2D(sampler, u, v) for rtTextureSampler<uchar4, 2, cudaReadModeNormalizedFloat>
+ * with RT_WRAP_REPEAT, RT_FILTER_LINEAR and normalised coordinates
+ * (Texture.cpp:109-122), restating the CUDA programming guide's texture
+ * fetching rules: wrap u -> u - floor(u), x_B = u*W - 0.5, i = floor(x_B),
+ * alpha = frac(x_B) held in 9-bit fixed point with 8 fractional bits (rounded
+ * here), texel indices wrapped, texels read as byte / 255, and
+ *   (1-a)(1-b) T[i,j] + a(1-b) T[i+1,j] + (1-a)b T[i,j+1] + ab T[i+1,j+1].
+ * `rgba` holds w*h RGBA8 texels, row j at rgba + 4*w*j, 4-byte aligned.  Non-finite
+ * coordinates sample texel (0,0).  Parity unpinned (no CUDA here). */
+static inline ORX_HD void orx_tex2d_linear(const uint8_t* rgba, uint32_t w, uint32_t h, float u, float v,
+                                           float out[4]) {
+    if (!(u - u == 0.0f)) u = 0.0f;
+    if (!(v - v == 0.0f)) v = 0.0f;
+    const float uw = u - orx_floorf(u), vw = v - orx_floorf(v);
+    const float xb = uw * (float)w - 0.5f, yb = vw * (float)h - 0.5f;
+    const float fx = orx_floorf(xb), fy = orx_floorf(yb);
+    const float a = orx_floorf((xb - fx) * 256.0f + 0.5f) * (1.0f / 256.0f);
+    const float b = orx_floorf((yb - fy) * 256.0f + 0.5f) * (1.0f / 256.0f);
+    int32_t i0 = (int32_t)fx, j0 = (int32_t)fy;
+    i0 = i0 < 0 ? i0 + (int32_t)w : (i0 >= (int32_t)w ? i0 - (int32_t)w : i0);
+    j0 = j0 < 0 ? j0 + (int32_t)h : (j0 >= (int32_t)h ? j0 - (int32_t)h : j0);
+    const uint32_t i1 = (uint32_t)i0 + 1u == w ? 0u : (uint32_t)i0 + 1u;
+    const uint32_t j1 = (uint32_t)j0 + 1u == h ? 0u : (uint32_t)j0 + 1u;
+    const uint32_t* tx = (const uint32_t*)(const void*)rgba; /* one RGBA8 texel per dword (little endian) */
+    const uint32_t t00 = tx[(size_t)j0 * w + (uint32_t)i0], t10 = tx[(size_t)j0 * w + i1];
+    const uint32_t t01 = tx[(size_t)j1 * w + (uint32_t)i0], t11 = tx[(size_t)j1 * w + i1];
+    const float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+    for (int c = 0; c < 4; c++) {
+        const uint32_t sh = 8u * (uint32_t)c;
+        const float s = w00 * ((float)((t00 >> sh) & 255u) / 255.0f) + w10 * ((float)((t10 >> sh) & 255u) / 255.0f) +
+                        w01 * ((float)((t01 >> sh) & 255u) / 255.0f) + w11 * ((float)((t11 >> sh) & 255u) / 255.0f);
+        out[c] = s;
+    }
 }
 
 #ifdef __cplusplus

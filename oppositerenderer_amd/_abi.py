@@ -25,6 +25,7 @@ MAT_DIFFUSE_EMITTER = 1
 MAT_MIRROR = 2
 MAT_GLASS = 3
 MAT_GLOSSY = 4
+MAT_TEXTURE = 5
 
 LIGHT_AREA = 0
 LIGHT_POINT = 1
@@ -68,7 +69,13 @@ class OrxRequest(C.Structure):
 class OrxMaterial(C.Structure):
     _fields_ = [("type", C.c_int32), ("Kd", F3), ("Ks", F3), ("Kr", F3), ("Kt", F3),
                 ("ior", C.c_float), ("exponent", C.c_float), ("power", F3),
-                ("inverse_area", C.c_float)]
+                ("inverse_area", C.c_float), ("texture", C.c_int32)]
+
+
+class OrxTexture(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("rgba", C.POINTER(C.c_uint8)),
+                ("normal_width", C.c_uint32), ("normal_height", C.c_uint32),
+                ("normal_rgba", C.POINTER(C.c_uint8))]
 
 
 class OrxLight(C.Structure):
@@ -86,6 +93,9 @@ class OrxScene(C.Structure):
         ("n_materials", C.c_uint32), ("materials", C.POINTER(OrxMaterial)),
         ("n_lights", C.c_uint32), ("lights", C.POINTER(OrxLight)),
         ("aabb_min", F3), ("aabb_max", F3),
+        ("texcoords", C.POINTER(C.c_float)), ("tangents", C.POINTER(C.c_float)),
+        ("bitangents", C.POINTER(C.c_float)),
+        ("n_textures", C.c_uint32), ("textures", C.POINTER(OrxTexture)),
     ]
 
 

@@ -355,6 +355,8 @@ struct orx_renderer {
     bool scene_ready = false;
     /* scene */
     DevBuf d_quads, d_qmat, d_spheres, d_smat, d_triv, d_trin, d_tmat, d_mats, d_lights, d_bvh, d_bvhprims;
+    DevBuf d_triuv, d_trit, d_tribt, d_texels, d_texdesc; /* Texture material attributes and images */
+    bool has_tex = false;
     DevScene scene{};
     /* frame */
     uint32_t W = 10, H = 10, RW = 0, RH = 0;
@@ -381,9 +383,10 @@ struct orx_renderer {
     size_t vcm_npx = 0;  /* own-row subpaths W*rows the VCM buffers are sized for */
     size_t vcm_spx = 0;  /* owner-block splat pixels W*max_rows*world */
     bool vcm_pending = false; /* light pass done, camera pass (orx_vcm_finish) outstanding */
+    bool vcm_kd = false;      /* d_vkd sized for the current vcm_npx */
     VcmBufs vcm_vb{};
     VcmConsts vcm_c{};
-    DevBuf d_vcount, d_vverts, d_vsplat, d_vcam, d_tstats;
+    DevBuf d_vcount, d_vverts, d_vsplat, d_vcam, d_vkd, d_tstats;
     std::vector<DevLight> host_lights;
 };
 
@@ -480,6 +483,15 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
         if (s->quad_material[i] >= nm) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "quad material out of range");
     for (uint32_t i = 0; i < ns; i++)
         if (s->sphere_material[i] >= nm) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "sphere material out of range");
+    for (uint32_t i = 0; i < s->n_textures; i++) {
+        const orx_texture& t = s->textures[i];
+        if (!t.rgba || !t.width || !t.height || (t.normal_rgba && (!t.normal_width || !t.normal_height)))
+            return set_err(r, ORX_ERR_INVALID_ARGUMENT, "texture image without texels");
+    }
+    for (uint32_t i = 0; i < nm; i++)
+        if (s->materials[i].type == ORX_MAT_TEXTURE &&
+            (s->materials[i].texture < 0 || (uint32_t)s->materials[i].texture >= s->n_textures))
+            return set_err(r, ORX_ERR_INVALID_ARGUMENT, "Texture material without a texture image");
     for (uint32_t i = 0; i < nt; i++) {
         if (s->triangle_material[i] >= nm) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "triangle material out of range");
         for (int k = 0; k < 3; k++)
@@ -511,6 +523,7 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
         d.Kt = ld3(m.Kt);
         d.ior = m.ior;
         d.exponent = m.exponent;
+        d.tex = m.texture;
         if (m.type == ORX_MAT_DIFFUSE_EMITTER) {
             /* DiffuseEmitter.cpp:17-25, :48-62 */
             f3 power = ld3(m.power) * d.Kd;
@@ -525,7 +538,7 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
                 d.Kd = d.Kd * sumScale;
                 d.Ks = d.Ks * sumScale;
             }
-        } else if (m.type < 0 || m.type > ORX_MAT_GLOSSY) {
+        } else if (m.type < 0 || m.type > ORX_MAT_TEXTURE) {
             return set_err(r, ORX_ERR_INVALID_ARGUMENT, "unknown material type");
         }
         mats[i] = d;
@@ -570,9 +583,13 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
         if (!b4.ok) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "BVH4 quantisation failed");
         if (stack_bound > 96) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "BVH4 traversal stack bound above 96");
     }
-    std::vector<float4> tv((size_t)nt * 3), tn;
+    std::vector<float4> tv((size_t)nt * 3), tn, tt, tbt;
+    std::vector<float2> tuv;
     std::vector<uint32_t> tmat_leaf(nt);
+    const bool has_tb = s->normals && s->tangents && s->bitangents; /* TriangleMesh.cu:56-70 */
     if (s->normals) tn.resize((size_t)nt * 3);
+    if (s->texcoords) tuv.resize((size_t)nt * 3);
+    if (has_tb) tt.resize((size_t)nt * 3), tbt.resize((size_t)nt * 3);
     for (uint32_t k = 0; k < nt; k++) {
         const uint32_t i = bb.prims[k];
         tmat_leaf[k] = s->triangle_material[i];
@@ -585,6 +602,13 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
             if (s->normals) {
                 const float* n = s->normals + 3 * (size_t)vi;
                 tn[3 * (size_t)k + v] = make_float4(n[0], n[1], n[2], 0.f);
+            }
+            if (s->texcoords) tuv[3 * (size_t)k + v] = make_float2(s->texcoords[2 * (size_t)vi], s->texcoords[2 * (size_t)vi + 1]);
+            if (has_tb) {
+                const float* t = s->tangents + 3 * (size_t)vi;
+                const float* b = s->bitangents + 3 * (size_t)vi;
+                tt[3 * (size_t)k + v] = make_float4(t[0], t[1], t[2], 0.f);
+                tbt[3 * (size_t)k + v] = make_float4(b[0], b[1], b[2], 0.f);
             }
         }
     }
@@ -602,6 +626,44 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     HIPCHK(r, up(r->d_trin, tn.data(), tn.size() * sizeof(float4)));
     HIPCHK(r, up(r->d_tmat, tmat_leaf.data(), (size_t)nt * 4));
     HIPCHK(r, up(r->d_mats, mats.data(), mats.size() * sizeof(DevMaterial)));
+    HIPCHK(r, up(r->d_triuv, tuv.data(), tuv.size() * sizeof(float2)));
+    HIPCHK(r, up(r->d_trit, tt.data(), tt.size() * sizeof(float4)));
+    HIPCHK(r, up(r->d_tribt, tbt.data(), tbt.size() * sizeof(float4)));
+    /* texture images back to back (256-B aligned), descriptors with device pointers */
+    std::vector<DevTexture> texd(s->n_textures);
+    {
+        size_t total = 0;
+        auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+        for (uint32_t i = 0; i < s->n_textures; i++) {
+            const orx_texture& t = s->textures[i];
+            total += al((size_t)t.width * t.height * 4);
+            if (t.normal_rgba) total += al((size_t)t.normal_width * t.normal_height * 4);
+        }
+        HIPCHK(r, r->d_texels.ensure(total));
+        size_t off = 0;
+        uint8_t* base = r->d_texels.as<uint8_t>();
+        for (uint32_t i = 0; i < s->n_textures; i++) {
+            const orx_texture& t = s->textures[i];
+            DevTexture& d = texd[i];
+            std::memset(&d, 0, sizeof d);
+            d.w = t.width;
+            d.h = t.height;
+            d.rgba = base + off;
+            HIPCHK(r, hipMemcpy(base + off, t.rgba, (size_t)t.width * t.height * 4, hipMemcpyHostToDevice));
+            off += al((size_t)t.width * t.height * 4);
+            if (t.normal_rgba) {
+                d.nw = t.normal_width;
+                d.nh = t.normal_height;
+                d.nrgba = base + off;
+                HIPCHK(r, hipMemcpy(base + off, t.normal_rgba, (size_t)t.normal_width * t.normal_height * 4,
+                                    hipMemcpyHostToDevice));
+                off += al((size_t)t.normal_width * t.normal_height * 4);
+            }
+        }
+    }
+    HIPCHK(r, up(r->d_texdesc, texd.data(), texd.size() * sizeof(DevTexture)));
+    r->has_tex = false;
+    for (const DevMaterial& m : mats) r->has_tex |= m.type == ORX_MAT_TEXTURE;
     HIPCHK(r, up(r->d_lights, lights.data(), lights.size() * sizeof(DevLight)));
 #ifdef ORX_BVH_FP32
     HIPCHK(r, up(r->d_bvh, b4.outf.data(), b4.outf.size() * sizeof(DevBvh4F)));
@@ -619,6 +681,11 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     S.tri_v = r->d_triv.as<float4>();
     S.tri_n = s->normals ? r->d_trin.as<float4>() : nullptr;
     S.tmat = r->d_tmat.as<uint32_t>();
+    S.tri_uv = s->texcoords && nt ? r->d_triuv.as<float2>() : nullptr;
+    S.tri_t = has_tb && nt ? r->d_trit.as<float4>() : nullptr;
+    S.tri_bt = has_tb && nt ? r->d_tribt.as<float4>() : nullptr;
+    S.tex = r->d_texdesc.as<DevTexture>();
+    S.ntex = s->n_textures;
     S.mats = r->d_mats.as<DevMaterial>();
     S.lights = r->d_lights.as<DevLight>();
     S.nl = s->n_lights;
@@ -852,6 +919,7 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
         HIPCHK(r, hipMemsetAsync(r->d_vcount.p, 0, lpx * 4, cur_stream(r)));
         HIPCHK(r, hipMemsetAsync(r->d_vcam.p, 0, lpx * 12, cur_stream(r)));
         r->vcm_npx = lpx;
+        r->vcm_kd = false;
         r->vcm_spx = spx;
     }
     VcmBufs& vb = r->vcm_vb;
@@ -863,6 +931,11 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
     vb.vB = vb.vA + plane;
     vb.vC = vb.vB + plane;
     vb.vD = vb.vC + plane;
+    if (r->has_tex && !r->vcm_kd) {
+        HIPCHK(r, r->d_vkd.ensure(lpx * VCM_MAX_VERTS * 16 + 16));
+        r->vcm_kd = true;
+    }
+    vb.vE = r->has_tex ? r->d_vkd.as<float4>() : nullptr;
     vb.splat = r->d_vsplat.as<float>();
     vb.splat_in = vb.splat + (size_t)r->rank * r->max_rows * r->W * 3;
     vb.cam = r->d_vcam.as<float>();

@@ -193,7 +193,7 @@ __device__ __forceinline__ f3 sample_disc(float sx, float sy, f3 center, float r
 /* ------------------------------------------------------------------ */
 /* scene                                                               */
 /* ------------------------------------------------------------------ */
-enum : int32_t { MAT_DIFFUSE = 0, MAT_EMITTER = 1, MAT_MIRROR = 2, MAT_GLASS = 3, MAT_GLOSSY = 4 };
+enum : int32_t { MAT_DIFFUSE = 0, MAT_EMITTER = 1, MAT_MIRROR = 2, MAT_GLASS = 3, MAT_GLOSSY = 4, MAT_TEXTURE = 5 };
 enum : int32_t { LIGHT_AREA = 0, LIGHT_POINT = 1, LIGHT_SPOT = 2 };
 
 struct DevMaterial {
@@ -202,6 +202,13 @@ struct DevMaterial {
     float ior, exponent;
     f3 powerPerArea, Lemit;
     float inverseArea;
+    int32_t tex; /* Texture: index into DevScene::tex */
+};
+/* Texture images (material/Texture.cpp:83-107): RGBA8 texels in HBM */
+struct DevTexture {
+    const uint8_t* rgba;
+    const uint8_t* nrgba; /* normal map or NULL */
+    uint32_t w, h, nw, nh;
 };
 struct DevLight {
     int32_t type;
@@ -268,6 +275,11 @@ struct DevScene {
      * tri_v[3k+1] = p1, tri_v[3k+2] = p2 (48 B per triangle, no index indirection) */
     const float4* tri_v;
     const float4* tri_n;       /* [nt][3] vertex normals in leaf order, or NULL */
+    const float2* tri_uv;      /* [nt][3] texcoords in leaf order, or NULL (TriangleMesh.cu:74-84) */
+    const float4* tri_t;       /* [nt][3] tangents, [nt][3] bitangents in leaf order, or NULL */
+    const float4* tri_bt;
+    const DevTexture* tex;
+    uint32_t ntex;
     const uint32_t* tmat;      /* leaf order */
     const DevMaterial* mats;
     const DevLight* lights;
@@ -654,6 +666,43 @@ __device__ __forceinline__ f3 geometric_normal(const DevScene& S, const Hit& h) 
     return normalize(normalize(cross(p0 - p2, p1 - p0)));
 }
 
+/* Texture attributes (TriangleMesh.cu:61-84); parallelograms and spheres
+ * write no textureCoordinate / tangent attributes: (0,0), no normal map. */
+__device__ __forceinline__ void hit_texcoord(const DevScene& S, const Hit& h, float& u, float& v) {
+    u = 0.f;
+    v = 0.f;
+    if ((uint32_t)h.prim < S.nq + S.ns || !S.tri_uv) return;
+    const float2 t0 = S.tri_uv[3 * h.slot], t1 = S.tri_uv[3 * h.slot + 1], t2 = S.tri_uv[3 * h.slot + 2];
+    const float w0 = 1.0f - h.b - h.g;
+    u = (t1.x * h.b + t2.x * h.g) + t0.x * w0;
+    v = (t1.y * h.b + t2.y * h.g) + t0.y * w0;
+}
+/* tex2D(diffuseSampler, textureCoordinate).xyz (Texture.cu:107-109) */
+__device__ inline f3 tex_color(const DevScene& S, const DevMaterial& m, const Hit& h) {
+    const DevTexture& t = S.tex[m.tex];
+    float u, v, c[4];
+    hit_texcoord(S, h, u, v);
+    orx_tex2d_linear(t.rgba, t.w, t.h, u, v, c);
+    return mk(c[0], c[1], c[2]);
+}
+/* getNormalMappedNormal when hasNormals (Texture.cu:69-77, :88-95) */
+__device__ inline f3 tex_normal(const DevScene& S, const DevMaterial& m, const Hit& h, f3 wsn) {
+    const DevTexture& t = S.tex[m.tex];
+    if (!t.nrgba || !S.tri_n || !S.tri_t || (uint32_t)h.prim < S.nq + S.ns) return wsn;
+    const uint32_t k = 3 * h.slot;
+    const float w0 = 1.0f - h.b - h.g;
+    f3 T = normalize(ld_f3(S.tri_t[k + 1]) * h.b + ld_f3(S.tri_t[k + 2]) * h.g + ld_f3(S.tri_t[k]) * w0);
+    f3 B = normalize(ld_f3(S.tri_bt[k + 1]) * h.b + ld_f3(S.tri_bt[k + 2]) * h.g + ld_f3(S.tri_bt[k]) * w0);
+    T = normalize(T);
+    B = normalize(B);
+    float u, v, c[4];
+    hit_texcoord(S, h, u, v);
+    orx_tex2d_linear(t.nrgba, t.nw, t.nh, u, v, c);
+    const float nx = 2.f * c[0] - 1.f, ny = 2.f * c[1] - 1.f, nz = 2.f * c[2] - 1.f;
+    return normalize(mk(nx * T.x + ny * B.x + nz * wsn.x, nx * T.y + ny * B.y + nz * wsn.y,
+                        nx * T.z + ny * B.z + nz * wsn.z));
+}
+
 /* ------------------------------------------------------------------ */
 /* camera (Camera.cpp:333-345 derived on the host; helpers/camera.h)   */
 /* ------------------------------------------------------------------ */
@@ -739,6 +788,17 @@ __device__ inline void trace_radiance(const DevScene& S, uint32_t maxd, f3 o, f3
                 float s1 = rnd(rs);
                 prd.newdir = sample_hemisphere_cos(N, s0, s1);
             }
+            return;
+        } else if (m.type == MAT_TEXTURE) { /* Texture.cu:83-110: mapped normal, no depth++ */
+            prd.flags |= PRD_HIT_NON_SPECULAR;
+            prd.normal = tex_normal(S, m, h, N);
+            prd.position = hitPoint;
+            if (prd.flags & PRD_PATH_TRACING) {
+                float s0 = rnd(rs);
+                float s1 = rnd(rs);
+                prd.newdir = sample_hemisphere_cos(N, s0, s1);
+            }
+            prd.attenuation = prd.attenuation * tex_color(S, m, h);
             return;
         } else if (m.type == MAT_EMITTER) {
             prd.flags |= PRD_HIT_EMITTER;

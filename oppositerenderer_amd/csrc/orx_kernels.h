@@ -119,6 +119,7 @@ struct VcmBufs {
     float4* vB;         /* [9][W*H] throughput.xyz | dVCM */
     float4* vC;         /* [9][W*H] normal.xyz | dVC */
     float4* vD;         /* [9][W*H] localDirFix.xyz | dVM */
+    float4* vE;         /* [9][lcount] texel colour of Texture vertices (NULL without Texture materials) */
     float* splat;       /* [world][max_rows][W][3] connectCameraT1 accumulation of this iteration (owner-block layout) */
     const float* splat_in; /* [rows][W][3] summed splats of the own rows (camera pass) */
     float* cam;         /* [W*H*3] camera subpath colour of this iteration */

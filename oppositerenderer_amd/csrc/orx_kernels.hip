@@ -230,7 +230,10 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
             } else {
                 const DevMaterial& m = S.mats[prim_material(S, h)];
                 const f3 hitPoint = P.o + P.d * h.t;
-                if (m.type == MAT_DIFFUSE || m.type == MAT_GLOSSY) {
+                if (m.type == MAT_DIFFUSE || m.type == MAT_GLOSSY || m.type == MAT_TEXTURE) {
+                    /* Texture.cu:116-175 differs only in Kd = texel colour,
+                     * the weight cutoff (0.01) and the new ray's tmin (0.01) */
+                    const bool tex = m.type == MAT_TEXTURE;
                     const f3 N = shading_normal(S, h);
                     if (P.depth >= 1 && P.numStored < pb.D) {
                         const uint32_t si = P.p_local * pb.D + P.numStored;
@@ -245,24 +248,26 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
                         }
                         P.numStored++;
                     }
-                    P.power = P.power * m.Kd;
-                    P.weight *= fmax3(m.Kd);
+                    const f3 Kd = tex ? tex_color(S, m, h) : m.Kd;
+                    P.power = P.power * Kd;
+                    P.weight *= fmax3(Kd);
                     if (P.depth >= 3) {
-                        float probContinue = favgf(m.Kd);
+                        float probContinue = favgf(Kd);
                         float probSample = rnd(rs);
                         if (probSample >= probContinue) done = true;
                         else P.power = P.power / probContinue;
                     }
                     if (!done) {
                         P.depth++;
-                        if (P.depth >= c.max_photon_depth || (double)P.weight < 0.001 || P.numStored >= pb.D) {
+                        if (P.depth >= c.max_photon_depth || (double)P.weight < (tex ? 0.01 : 0.001) ||
+                            P.numStored >= pb.D) {
                             done = true;
                         } else {
                             float s0 = rnd(rs);
                             float s1 = rnd(rs);
                             P.d = sample_hemisphere_cos(N, s0, s1);
                             P.o = hitPoint;
-                            P.tmin = 0.0001f;
+                            P.tmin = tex ? 0.01f : 0.0001f;
                         }
                     }
                 } else if (m.type == MAT_EMITTER) {

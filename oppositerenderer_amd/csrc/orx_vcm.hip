@@ -365,17 +365,19 @@ struct VBsdf {
 };
 
 /* material vcmClosestHit{Light,Camera}: false = program ends the subpath */
-__device__ inline bool material_bsdf(const DevMaterial& m, f3 gn, f3 dir, bool is_light, VBsdf& s, f3& N) {
+/* kd: m.Kd, or the texel colour for Texture (Texture.cu:215-286) */
+__device__ inline bool material_bsdf(const DevMaterial& m, f3 kd, f3 gn, f3 dir, bool is_light, VBsdf& s, f3& N) {
     switch (m.type) {
     case MAT_DIFFUSE:
+    case MAT_TEXTURE:
         N = gn;
         s.init(gn, -dir, is_light);
-        s.add(mk_bx(T_LAMBERT, m.Kd));
+        s.add(mk_bx(T_LAMBERT, kd));
         return true;
     case MAT_GLOSSY:
         N = gn;
         s.init(gn, -dir, is_light);
-        s.add(mk_bx(T_LAMBERT, m.Kd));
+        s.add(mk_bx(T_LAMBERT, kd));
         s.add(mk_bx(T_PHONG, m.Ks, m.exponent));
         return true;
     case MAT_MIRROR:
@@ -491,7 +493,9 @@ __device__ inline void connect_camera(const DevScene& S, const Subpath& L, const
 }
 
 /* lightPass (VCMLightPass.cu:52-93), initLightPayload (:120-176), lightHit (vcm.h:210-309) */
-template <bool ESTIMATE>
+/* TEX: the scene has Texture materials (vb.vE != NULL); the texel fetch is
+ * compiled out otherwise, it costs the camera kernel ~10% through spills */
+template <bool ESTIMATE, bool TEX>
 __global__ __launch_bounds__(64, 4) void k_vcm_light(DevScene S, VcmBufs vb, VcmConsts c) {
     ORX_STACK_DECL;
     uint32_t* stk = ORX_STACK_PTR;
@@ -578,7 +582,8 @@ __global__ __launch_bounds__(64, 4) void k_vcm_light(DevScene S, VcmBufs vb, Vcm
         if (m.type == MAT_EMITTER) break;
         VBsdf bs;
         f3 N;
-        if (!material_bsdf(m, geometric_normal(S, h), L.direction, true, bs, N)) break;
+        const f3 kd = TEX && m.type == MAT_TEXTURE ? tex_color(S, m, h) : m.Kd;
+        if (!material_bsdf(m, kd, geometric_normal(S, h), L.direction, true, bs, N)) break;
         L.depth++;
         const float cosIn = dot(N, -L.direction);
         if (cosIn < VCM_EPS_COSINE) break;
@@ -592,6 +597,7 @@ __global__ __launch_bounds__(64, 4) void k_vcm_light(DevScene S, VcmBufs vb, Vcm
                 vb.vB[o] = make_float4(L.throughput.x, L.throughput.y, L.throughput.z, L.dVCM);
                 vb.vC[o] = make_float4(N.x, N.y, N.z, L.dVC);
                 vb.vD[o] = make_float4(bs.fix.x, bs.fix.y, bs.fix.z, L.dVM);
+                if (TEX && m.type == MAT_TEXTURE) vb.vE[o] = make_float4(kd.x, kd.y, kd.z, 0.f);
             }
             if (!ESTIMATE) connect_camera(S, L, bs, hit, c, vb.splat, stk);
         }
@@ -604,6 +610,7 @@ __global__ __launch_bounds__(64, 4) void k_vcm_light(DevScene S, VcmBufs vb, Vcm
 }
 
 /* connectVertices (vcm.h:315-400) against light vertex k of this subpath */
+template <bool TEX>
 __device__ inline void connect_vertex(const DevScene& S, Subpath& C, const VBsdf& cb, f3 hit, const VcmBufs& vb,
                                       size_t o, const VcmConsts& c, uint32_t* stk) {
     const float4 A = vb.vA[o];
@@ -627,7 +634,12 @@ __device__ inline void connect_vertex(const DevScene& S, Subpath& C, const VBsdf
     lb.fix = mk(D.x, D.y, D.z);
     lb.n = 0;
     lb.cont = 0.f;
-    lb.add(mk_bx(T_LAMBERT, m.Kd));
+    f3 kd = m.Kd;
+    if (TEX && m.type == MAT_TEXTURE) { /* texel colour kept beside the 64-B record */
+        const float4 E = vb.vE[o];
+        kd = mk(E.x, E.y, E.z);
+    }
+    lb.add(mk_bx(T_LAMBERT, kd));
     if (m.type == MAT_GLOSSY) lb.add(mk_bx(T_PHONG, m.Ks, m.exponent));
     float lightCos = 0.f, lDir, lRev;
     const f3 lightF = lb.vcm_f(-direction, lightCos, lDir, lRev);
@@ -704,6 +716,7 @@ __device__ inline void connect_light(const DevScene& S, Subpath& C, const VBsdf&
 }
 
 /* cameraPass (VCMCameraPass.cu:48-80), initCameraPayload (:100-135), cameraHit (vcm.h:527-628) */
+template <bool TEX>
 __global__ __launch_bounds__(64, 4) void k_vcm_camera(DevScene S, VcmBufs vb, VcmConsts c) {
     ORX_STACK_DECL;
     uint32_t* stk = ORX_STACK_PTR;
@@ -761,7 +774,8 @@ __global__ __launch_bounds__(64, 4) void k_vcm_camera(DevScene S, VcmBufs vb, Vc
         }
         VBsdf bs;
         f3 N;
-        if (!material_bsdf(m, geometric_normal(S, h), C.direction, false, bs, N)) break;
+        const f3 kd = TEX && m.type == MAT_TEXTURE ? tex_color(S, m, h) : m.Kd;
+        if (!material_bsdf(m, kd, geometric_normal(S, h), C.direction, false, bs, N)) break;
         C.depth++;
         const float cosIn = dot(N, -C.direction);
         if (cosIn < VCM_EPS_COSINE) break;
@@ -769,7 +783,7 @@ __global__ __launch_bounds__(64, 4) void k_vcm_camera(DevScene S, VcmBufs vb, Vc
         if (!bs.is_specular()) {
             connect_light(S, C, bs, hit, c, rs, stk);
             const uint32_t nv = nverts < VCM_MAX_VERTS ? nverts : VCM_MAX_VERTS;
-            for (uint32_t k = 0; k < nv; ++k) connect_vertex(S, C, bs, hit, vb, (size_t)k * c.lcount + p, c, stk);
+            for (uint32_t k = 0; k < nv; ++k) connect_vertex<TEX>(S, C, bs, hit, vb, (size_t)k * c.lcount + p, c, stk);
         }
         if (c.maxPathLen <= C.depth) break;
         sample_scattering(C, hit, bs, c, rs);
@@ -791,13 +805,20 @@ __global__ __launch_bounds__(64, 4) void k_vcm_camera(DevScene S, VcmBufs vb, Vc
 void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c, bool estimate) {
     const uint32_t blocks = (c.lcount + 63) / 64;
     if (blocks == 0) return;
-    if (estimate) hipLaunchKernelGGL(k_vcm_light<true>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
-    else hipLaunchKernelGGL(k_vcm_light<false>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
+    const size_t lds = ORX_STACK_BYTES(S);
+    if (vb.vE) {
+        if (estimate) hipLaunchKernelGGL((k_vcm_light<true, true>), dim3(blocks), dim3(64), lds, s, S, vb, c);
+        else hipLaunchKernelGGL((k_vcm_light<false, true>), dim3(blocks), dim3(64), lds, s, S, vb, c);
+    } else {
+        if (estimate) hipLaunchKernelGGL((k_vcm_light<true, false>), dim3(blocks), dim3(64), lds, s, S, vb, c);
+        else hipLaunchKernelGGL((k_vcm_light<false, false>), dim3(blocks), dim3(64), lds, s, S, vb, c);
+    }
 }
 void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
     const uint32_t blocks = ((c.W + 7) / 8) * ((c.rows + 7) / 8);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(k_vcm_camera, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
+    if (vb.vE) hipLaunchKernelGGL(k_vcm_camera<true>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
+    else hipLaunchKernelGGL(k_vcm_camera<false>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
 }
 
 }  // namespace orx

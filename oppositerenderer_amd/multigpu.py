@@ -201,8 +201,10 @@ def bench_main(args, metric):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if getattr(args, "method", "ppm") != "ppm":
-        raise SystemExit("the sharded bench runs PPM (VCM and PT shard trivially by rows; see DESIGN.md)")
+    method = getattr(args, "method", "ppm")
+    if method not in ("ppm", "vcm"):
+        raise SystemExit("the sharded bench runs PPM or VCM (PT has no sharded phase API; see DESIGN.md)")
+    vcm = method == "vcm"
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # RCCL prints its version banner on fd 1: keep stdout for the one JSON line
     json_out = os.fdopen(os.dup(1), "w")
@@ -218,12 +220,13 @@ def bench_main(args, metric):
     r.set_shard(rank, world)
     r.initScene(scene)
     cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
-    det = RenderRequestDetails(cam, scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W, H)
+    mcode = _abi.VCM_BIDIRECTIONAL_PATH_TRACING if vcm else _abi.PROGRESSIVE_PHOTON_MAPPING
+    det = RenderRequestDetails(cam, scene.name, mcode, W, H)
     req = det.to_abi()
     dev = torch.device("cuda", local_rank)
     backend = DeviceShard(r, torch, dev)
     radius = scene.initial_ppm_radius()
-    sharded = ShardedPPM(backend, dist, world, rank, W, H)
+    sharded = (ShardedVCM if vcm else ShardedPPM)(backend, dist, world, rank, W, H)
     it = 0
     for _ in range(max(1, args.warmup)):
         sharded.iteration(it, it, radius, req)
@@ -248,29 +251,41 @@ def bench_main(args, metric):
     st = r.stats()
     if rank == 0:
         from . import roofline
-        paths = W * H + P * P * world
+        # PPM: weak scaling (each rank emits its own P*P photon batch); VCM: the
+        # W*H light + W*H camera subpaths are split over the ranks (strong scaling)
+        paths = 2 * W * H if vcm else W * H + P * P * world
         n_it = max(1, st.timed_iterations)
         per_pass = {name: st.pass_ms[i] / n_it for i, name in enumerate(_abi.PASS_NAMES)}
         per_pass = {k: v for k, v in per_pass.items() if v > 0}
         dominant = max(per_pass, key=per_pass.get)
         valid_avg = st.valid_photons_total / n_it
-        # rank 0's passes: its own photon batch, its pixel rows (eye/direct), all pixels (gather)
-        pb = roofline.pass_bytes(_abi.PROGRESSIVE_PHOTON_MAPPING, W, H, P * P, valid_avg, st.num_cells)
         rows0 = local_rows(H, 0, world)
-        for k in ("ppm_eye", "ppm_direct_output"):
-            pb[k] = pb[k] * rows0 / H
+        if vcm:  # rank 0 traces its own rows' subpaths; light vertices counted in the stats
+            lv = int(np.minimum(r.read_buffer(_abi.BUF_VCM_VERTEX_COUNT, np.uint32), 9).sum())
+            pb = roofline.pass_bytes(mcode, W, rows0, 0, light_vertices=lv)
+        else:
+            # rank 0's passes: its own photon batch, its pixel rows (eye/direct), all pixels (gather)
+            pb = roofline.pass_bytes(mcode, W, H, P * P, valid_avg, st.num_cells)
+            for k in ("ppm_eye", "ppm_direct_output"):
+                pb[k] = pb[k] * rows0 / H
         roof = roofline.roofline(dominant, pb[dominant], per_pass[dominant], None)
         out = {
             "metric": metric, "value": round(paths * args.steps / t_max / 1e6, 3), "unit": "Mpaths/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(t_max * 1e3 / args.steps, 4), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(t_max * 1e3 / args.steps, 4), "higher_is_better": True,
+            "scaling": "strong" if vcm else "weak",
             "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic: seeded procedural scene ({scene.name}), XORWOW streams seeded 1645301512",
-            "config": {"workload": f"{scene.name} {W}x{H} PPM, {P * P} photons/iter per GPU (weak scaling)",
-                       "scene": scene.name, "width": W, "height": H, "photons_per_iteration": P * P * world,
-                       "paths_per_iteration": paths,
-                       "parallelism": f"row-interleaved RNG/pixel/photon ownership x{world}, "
-                                      "RCCL all_gather(hitpoints) + reduce_scatter(indirect)"},
+            "config": ({"workload": f"{scene.name} {W}x{H} VCM, {W * H} light subpaths/iter (strong scaling)",
+                        "scene": scene.name, "width": W, "height": H, "method": "VCM",
+                        "paths_per_iteration": paths,
+                        "parallelism": f"row-interleaved RNG/pixel ownership x{world}, "
+                                       "RCCL reduce_scatter(light-tracing splats)"} if vcm else
+                       {"workload": f"{scene.name} {W}x{H} PPM, {P * P} photons/iter per GPU (weak scaling)",
+                        "scene": scene.name, "width": W, "height": H, "photons_per_iteration": P * P * world,
+                        "paths_per_iteration": paths,
+                        "parallelism": f"row-interleaved RNG/pixel/photon ownership x{world}, "
+                                       "RCCL all_gather(hitpoints) + reduce_scatter(indirect)"}),
             "roofline": roof,
             "passes": {k: round(v, 4) for k, v in per_pass.items()},
             "dominant_pass": dominant,

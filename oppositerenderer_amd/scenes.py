@@ -74,6 +74,7 @@ class Material:
     exponent: float = 1.0
     power: tuple = (0.0, 0.0, 0.0)
     inverse_area: float = 0.0
+    texture: int = -1
 
     def to_abi(self):
         m = _abi.OrxMaterial()
@@ -85,7 +86,16 @@ class Material:
         m.ior, m.exponent = float(self.ior), float(self.exponent)
         m.power[:] = [float(v) for v in self.power]
         m.inverse_area = float(self.inverse_area)
+        m.texture = int(self.texture)
         return m
+
+
+@dataclass
+class TextureImage:
+    """Texture's diffuse map and optional normal map (material/Texture.cpp:18-29,
+    util/Image.cpp): uint8 [h, w, 4] RGBA, row 0 first."""
+    rgba: np.ndarray
+    normal_rgba: np.ndarray | None = None
 
 
 def Diffuse(Kd):
@@ -104,6 +114,11 @@ def Glass(ior, Kr, Kt):
 def Glossy(Kd, Ks, exponent):
     return Material(_abi.MAT_GLOSSY, Kd=tuple(np.broadcast_to(np.float32(Kd), 3)),
                     Ks=tuple(np.broadcast_to(np.float32(Ks), 3)), exponent=float(exponent))
+
+
+def Texture(texture_index):
+    """Texture material: Lambertian with Kd = tex2D(diffuseSampler, uv) (Texture.cu:83-110)."""
+    return Material(_abi.MAT_TEXTURE, texture=int(texture_index))
 
 
 def DiffuseEmitter(power, Kd, inverse_area):
@@ -168,6 +183,10 @@ class Scene:
         self.sphere_mat: list[int] = []
         self.vertices = np.zeros((0, 3), np.float32)
         self.normals = None
+        self.texcoords = None
+        self.tangents = None
+        self.bitangents = None
+        self.textures: list[TextureImage] = []
         self.triangles = np.zeros((0, 3), np.uint32)
         self.triangle_mat = np.zeros((0,), np.uint32)
         self.lights: list[Light] = []
@@ -188,11 +207,22 @@ class Scene:
         self.spheres.append(np.array([*np.float32(center), f32(radius)], dtype=np.float32))
         self.sphere_mat.append(mat)
 
-    def set_mesh(self, vertices, triangles, triangle_mat, normals=None):
-        self.vertices = np.ascontiguousarray(vertices, dtype=np.float32)
+    def set_mesh(self, vertices, triangles, triangle_mat, normals=None, texcoords=None, tangents=None,
+                 bitangents=None):
+        f = lambda a: None if a is None else np.ascontiguousarray(a, dtype=np.float32)
+        self.vertices = f(vertices)
         self.triangles = np.ascontiguousarray(triangles, dtype=np.uint32)
         self.triangle_mat = np.ascontiguousarray(triangle_mat, dtype=np.uint32)
-        self.normals = None if normals is None else np.ascontiguousarray(normals, dtype=np.float32)
+        self.normals = f(normals)
+        self.texcoords = f(texcoords)
+        self.tangents = f(tangents)
+        self.bitangents = f(bitangents)
+
+    def add_texture(self, rgba, normal_rgba=None) -> int:
+        chk = lambda a: None if a is None else np.ascontiguousarray(a, dtype=np.uint8).reshape(
+            np.shape(a)[0], np.shape(a)[1], 4)
+        self.textures.append(TextureImage(chk(rgba), chk(normal_rgba)))
+        return len(self.textures) - 1
 
     @property
     def num_primitives(self):
@@ -239,6 +269,19 @@ class Scene:
         s.lights = C.cast(lights, C.POINTER(_abi.OrxLight))
         s.aabb_min[:] = [float(v) for v in self.aabb_min]
         s.aabb_max[:] = [float(v) for v in self.aabb_max]
+        s.texcoords = arr(self.texcoords, C.c_float) if self.texcoords is not None else None
+        s.tangents = arr(self.tangents, C.c_float) if self.tangents is not None else None
+        s.bitangents = arr(self.bitangents, C.c_float) if self.bitangents is not None else None
+        texs = (_abi.OrxTexture * max(1, len(self.textures)))()
+        for i, t in enumerate(self.textures):
+            texs[i].height, texs[i].width = t.rgba.shape[0], t.rgba.shape[1]
+            texs[i].rgba = arr(t.rgba, C.c_uint8)
+            if t.normal_rgba is not None:
+                texs[i].normal_height, texs[i].normal_width = t.normal_rgba.shape[0], t.normal_rgba.shape[1]
+                texs[i].normal_rgba = arr(t.normal_rgba, C.c_uint8)
+        keep.append(texs)
+        s.n_textures = len(self.textures)
+        s.textures = C.cast(texs, C.POINTER(_abi.OrxTexture))
         self._keep = keep
         return s
 
@@ -390,6 +433,9 @@ def scene_by_name(name: str) -> Scene:
     }
     if name in table:
         return table[name]()
+    if name == "TexturedRoom":
+        from .synthetic import textured_room
+        return textured_room()
     if name.startswith("SyntheticHall"):
         from .synthetic import synthetic_hall
         return synthetic_hall()

@@ -142,3 +142,87 @@ def synthetic_hall(grid_n=64, column_seg=64, column_stack=56, box_n=8, seed=42, 
                                       np.array([L, 450.0 * S, Wd * 0.5], np.float32),
                                       np.array([0.0, 1.0, 0.0], np.float32), 60.0, 45.0, 0.0)
     return sc
+
+
+def _checker(n, cells, c0, c1, seed):
+    """RGBA8 checkerboard with per-texel noise (uint8 [n, n, 4])."""
+    rng = np.random.default_rng(seed)
+    i, j = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+    pick = ((i * cells // n) + (j * cells // n)) % 2
+    rgb = np.where(pick[..., None] == 0, np.float64(c0), np.float64(c1)) * 255.0
+    rgb = np.clip(rgb + rng.uniform(-12, 12, rgb.shape), 0, 255)
+    return np.concatenate([rgb, np.full((n, n, 1), 255.0)], -1).astype(np.uint8)
+
+
+def _bump_normal_map(n, freq):
+    """Tangent-space normal map of a sinusoidal height field, encoded (N+1)/2*255."""
+    y, x = np.meshgrid(np.arange(n) / n, np.arange(n) / n, indexing="ij")
+    dhx = 0.6 * np.cos(2 * np.pi * freq * x) * np.sin(2 * np.pi * freq * y)
+    dhy = 0.6 * np.sin(2 * np.pi * freq * x) * np.cos(2 * np.pi * freq * y)
+    nrm = np.stack([-dhx, -dhy, np.ones_like(x)], -1)
+    nrm /= np.linalg.norm(nrm, axis=-1, keepdims=True)
+    rgb = np.round((nrm + 1.0) * 0.5 * 255.0)
+    return np.concatenate([rgb, np.full((n, n, 1), 255.0)], -1).astype(np.uint8)
+
+
+def textured_room(grid_n=6, tex_n=32, seed=7) -> scenes.Scene:
+    """Small triangle-mesh room whose walls use the Texture material
+    (material/Texture.cu): checker diffuse maps sampled with wrapping
+    texcoords (uv up to 3), vertex normals, tangents/bitangents and a
+    normal map on the floor; a textured parallelogram (no texcoord attribute)
+    and a Diffuse block for contrast; one quad area light.  Procedural and
+    seeded; exercises every Texture code path of the hot passes."""
+    sc = scenes.Scene("TexturedRoom")
+    L, Hh = 10.0, 8.0
+    t_floor = sc.add_texture(_checker(tex_n, 4, (0.85, 0.8, 0.7), (0.25, 0.3, 0.5), seed),
+                             _bump_normal_map(tex_n, 2))
+    t_wall = sc.add_texture(_checker(tex_n, 2, (0.8, 0.2, 0.15), (0.9, 0.85, 0.8), seed + 1))
+    t_back = sc.add_texture(_checker(tex_n // 2, 8, (0.2, 0.7, 0.25), (0.85, 0.85, 0.85), seed + 2))
+    m_floor = sc.add_material(scenes.Texture(t_floor))
+    m_wall = sc.add_material(scenes.Texture(t_wall))
+    m_back = sc.add_material(scenes.Texture(t_back))
+    m_white = sc.add_material(scenes.Diffuse(0.75))
+    verts, norms, uvs, tans, btans, tris, tmat = [], [], [], [], [], [], []
+    base = 0
+
+    def add(origin, du, dv, m, rep):
+        nonlocal base
+        v, n, t = _grid(origin, du, dv, grid_n, grid_n)
+        uu, vv = np.meshgrid(np.linspace(0, rep, grid_n + 1), np.linspace(0, rep, grid_n + 1), indexing="ij")
+        verts.append(v)
+        norms.append(n)
+        uvs.append(np.stack([uu, vv], -1).reshape(-1, 2))
+        tans.append(np.broadcast_to(np.float64(du) / np.linalg.norm(du), v.shape))
+        btans.append(np.broadcast_to(np.float64(dv) / np.linalg.norm(dv), v.shape))
+        tris.append(t + base)
+        tmat.append(np.full(len(t), m, np.uint32))
+        base += len(v)
+
+    add((0, 0, 0), (0, 0, L), (L, 0, 0), m_floor, 3.0)       # floor, +y
+    add((0, Hh, 0), (L, 0, 0), (0, 0, L), m_white, 1.0)      # ceiling, -y
+    add((0, 0, L), (0, Hh, 0), (L, 0, 0), m_back, 2.0)       # back wall, -z
+    add((0, 0, 0), (0, Hh, 0), (0, 0, L), m_wall, 1.5)       # x=0, +x
+    add((L, 0, 0), (0, 0, L), (0, Hh, 0), m_wall, 1.5)       # x=L, -x
+    for p in _box((6.0, 0.0, 5.5), (8.0, 2.5, 7.5), 2):
+        v, n, t = p
+        verts.append(v)
+        norms.append(n)
+        uvs.append(np.zeros((len(v), 2)))
+        tans.append(np.tile([1.0, 0.0, 0.0], (len(v), 1)))
+        btans.append(np.tile([0.0, 1.0, 0.0], (len(v), 1)))
+        tris.append(t + base)
+        tmat.append(np.full(len(t), m_white, np.uint32))
+        base += len(v)
+    cat = lambda a: np.concatenate(a).astype(np.float32)
+    sc.set_mesh(cat(verts), np.concatenate(tris).astype(np.uint32), np.concatenate(tmat), cat(norms),
+                texcoords=cat(uvs), tangents=cat(tans), bitangents=cat(btans))
+    sc.add_parallelogram((1.5, 0.01, 6.0), (0.0, 0.0, 2.5), (2.5, 0.0, 0.0), m_wall)   # textured quad, +y
+    light = scenes.AreaLight((1.2e3, 1.1e3, 0.9e3), (6.0, Hh - 0.01, 4.0), (0.0, 0.0, 2.0), (-2.0, 0.0, 0.0))
+    sc.lights.append(light)
+    em = sc.add_material(scenes.DiffuseEmitter(light.power, 1.0, light.inverse_area))
+    sc.add_parallelogram(light.position, light.v1, light.v2, em)
+    sc.aabb_min = np.array([-0.1, -0.1, -0.1], np.float32)
+    sc.aabb_max = np.array([L + 0.1, Hh + 0.1, L + 0.1], np.float32)
+    sc.default_camera = scenes.Camera(np.array([5.0, 4.0, -6.0], np.float32), np.array([5.0, 3.0, 5.0], np.float32),
+                                      np.array([0.0, 1.0, 0.0], np.float32), 50.0, 50.0, 0.0)
+    return sc

@@ -192,7 +192,11 @@ typedef struct {
     float ior, exponent;
     v3 powerPerArea, Lemit;
     float inverseArea;
+    int tex; /* Texture: index into the scene's textures */
 } mat_t;
+
+/* Texture images (material/Texture.cpp:83-107): diffuse map + optional normal map */
+typedef struct { uint32_t w, h, nw, nh; uint8_t* rgba; uint8_t* nrgba; } tex_t;
 
 typedef struct {
     int type;
@@ -217,6 +221,8 @@ struct orc_renderer {
     sphere_t* sph; uint32_t* smat;
     v3* verts; v3* vnorm; int has_normals;
     uint32_t* tris; uint32_t* tmat;
+    float* uv; v3* tang; v3* btan; /* texCoordBuffer, tangentBuffer, bitangentBuffer (or NULL) */
+    tex_t* tex; uint32_t ntex; int has_tex;
     /* triangle BVH: node i = {lo[3], hi[3], left|first, right|count|leafbit} */
     float* bvh_box; uint32_t* bvh_a; uint32_t* bvh_b; uint32_t* bvh_prims; uint32_t bvh_n;
     mat_t* mats;
@@ -243,6 +249,7 @@ struct orc_renderer {
     int vcm_estimated, vcm_pending;
     size_t vcm_npx, vcm_spx;
     uint32_t* vcount; float* vverts; v3* vsplat; v3* vcam;
+    v3* vkd; /* [9][lpx] texel colour of Texture light vertices */
     void* vcm_ctx; /* vcm_ctx_t of the pending sharded light pass */
 };
 
@@ -280,6 +287,9 @@ static void free_scene(orc_renderer* r) {
     free(r->quads); free(r->qmat); free(r->sph); free(r->smat);
     free(r->verts); free(r->vnorm); free(r->tris); free(r->tmat);
     free(r->mats); free(r->lights);
+    for (uint32_t i = 0; i < r->ntex; i++) { free(r->tex[i].rgba); free(r->tex[i].nrgba); }
+    free(r->tex); free(r->uv); free(r->tang); free(r->btan);
+    r->tex = NULL; r->ntex = 0; r->has_tex = 0; r->uv = NULL; r->tang = NULL; r->btan = NULL;
     r->quads = NULL; r->qmat = NULL; r->sph = NULL; r->smat = NULL; r->verts = NULL;
     r->vnorm = NULL; r->tris = NULL; r->tmat = NULL; r->mats = NULL; r->lights = NULL;
 }
@@ -288,7 +298,8 @@ static void free_frame(orc_renderer* r) {
     free(r->offsets); free(r->hist); free(r->indirect); free(r->direct); free(r->output); free(r->dbg);
     r->rng = NULL; r->hp = NULL; r->photons = NULL; r->keys = NULL; r->sort_tmp = NULL;
     r->offsets = NULL; r->hist = NULL; r->indirect = NULL; r->direct = NULL; r->output = NULL; r->dbg = NULL;
-    free(r->vcount); free(r->vverts); free(r->vsplat); free(r->vcam);
+    free(r->vcount); free(r->vverts); free(r->vsplat); free(r->vcam); free(r->vkd);
+    r->vkd = NULL;
     r->vcount = NULL; r->vverts = NULL; r->vsplat = NULL; r->vcam = NULL; r->vcm_npx = 0; r->vcm_spx = 0;
 }
 void orc_destroy(orc_renderer* r) {
@@ -411,6 +422,15 @@ static void build_tri_bvh(orc_renderer* r) {
 orx_status orc_init_scene(orc_renderer* r, const orx_scene* s) {
     if (!r || !s) return ORX_ERR_INVALID_ARGUMENT;
     if (s->n_lights == 0) return fail(r, ORX_ERR_NO_LIGHTS, "No lights exists in this scene.");
+    for (uint32_t i = 0; i < s->n_textures; i++) {
+        const orx_texture* t = &s->textures[i];
+        if (!t->rgba || !t->width || !t->height || (t->normal_rgba && (!t->normal_width || !t->normal_height)))
+            return fail(r, ORX_ERR_INVALID_ARGUMENT, "texture image without texels");
+    }
+    for (uint32_t i = 0; i < s->n_materials; i++)
+        if (s->materials[i].type == ORX_MAT_TEXTURE &&
+            (s->materials[i].texture < 0 || (uint32_t)s->materials[i].texture >= s->n_textures))
+            return fail(r, ORX_ERR_INVALID_ARGUMENT, "Texture material without a texture image");
     free_scene(r);
     r->nq = s->n_quads; r->ns = s->n_spheres; r->nt = s->n_triangles; r->nv = s->n_vertices;
     r->nm = s->n_materials; r->nl = s->n_lights;
@@ -441,6 +461,32 @@ orx_status orc_init_scene(orc_renderer* r, const orx_scene* s) {
         r->verts[i] = ld3(s->vertices + 3 * i);
         if (s->normals) r->vnorm[i] = ld3(s->normals + 3 * i);
     }
+    if (s->texcoords) {
+        r->uv = (float*)malloc(8 * (size_t)r->nv + 8);
+        memcpy(r->uv, s->texcoords, 8 * (size_t)r->nv);
+    }
+    if (s->tangents && s->bitangents) { /* hasTangentsAndBitangents */
+        r->tang = (v3*)calloc(r->nv + 1, sizeof(v3));
+        r->btan = (v3*)calloc(r->nv + 1, sizeof(v3));
+        for (uint32_t i = 0; i < r->nv; i++) {
+            r->tang[i] = ld3(s->tangents + 3 * i);
+            r->btan[i] = ld3(s->bitangents + 3 * i);
+        }
+    }
+    r->ntex = s->n_textures;
+    r->tex = (tex_t*)calloc(r->ntex + 1, sizeof(tex_t));
+    for (uint32_t i = 0; i < r->ntex; i++) {
+        const orx_texture* t = &s->textures[i];
+        tex_t* d = &r->tex[i];
+        d->w = t->width; d->h = t->height;
+        d->rgba = (uint8_t*)malloc(4 * (size_t)d->w * d->h);
+        memcpy(d->rgba, t->rgba, 4 * (size_t)d->w * d->h);
+        if (t->normal_rgba) {
+            d->nw = t->normal_width; d->nh = t->normal_height;
+            d->nrgba = (uint8_t*)malloc(4 * (size_t)d->nw * d->nh);
+            memcpy(d->nrgba, t->normal_rgba, 4 * (size_t)d->nw * d->nh);
+        }
+    }
     r->tris = (uint32_t*)calloc(3 * (size_t)r->nt + 3, 4);
     r->tmat = (uint32_t*)calloc(r->nt + 1, 4);
     if (r->nt) {
@@ -455,6 +501,8 @@ orx_status orc_init_scene(orc_renderer* r, const orx_scene* s) {
         d->type = m->type;
         d->Kd = ld3(m->Kd); d->Ks = ld3(m->Ks); d->Kr = ld3(m->Kr); d->Kt = ld3(m->Kt);
         d->ior = m->ior; d->exponent = m->exponent;
+        d->tex = m->texture;
+        if (m->type == ORX_MAT_TEXTURE) r->has_tex = 1;
         if (m->type == ORX_MAT_DIFFUSE_EMITTER) {
             /* DiffuseEmitter.cpp:17-25, :48-62 */
             v3 power = mul(ld3(m->power), d->Kd);
@@ -489,6 +537,7 @@ typedef struct {
     float t;
     int32_t prim; /* global id: quads, spheres, triangles */
     v3 gn, sn;    /* geometricNormal / shadingNormal attributes */
+    float b, g;   /* triangle barycentrics (beta, gamma) */
 } hit_t;
 
 /* parallelogram.cu:49-76 */
@@ -606,6 +655,8 @@ static int trace_closest(const orc_renderer* r, v3 o, v3 d, float tmin, float tm
     if (bp < 0) return 0;
     h->t = best;
     h->prim = bp;
+    h->b = tb;
+    h->g = tg;
     if ((uint32_t)bp < r->nq) {
         h->gn = h->sn = r->quads[bp].n;
     } else if ((uint32_t)bp < r->nq + r->ns) {
@@ -628,6 +679,45 @@ static uint32_t prim_material(const orc_renderer* r, int32_t p) {
     if ((uint32_t)p < r->nq + r->ns) return r->smat[p - r->nq];
     return r->tmat[p - r->nq - r->ns];
 }
+/* Texture attributes (TriangleMesh.cu:61-84; quads and spheres write no
+ * textureCoordinate/tangent attributes: (0,0) and no normal mapping here). */
+static void hit_texcoord(const orc_renderer* r, const hit_t* h, float* u, float* v) {
+    *u = 0.f; *v = 0.f;
+    if ((uint32_t)h->prim < r->nq + r->ns || !r->uv) return;
+    const uint32_t* ix = r->tris + 3 * (size_t)((uint32_t)h->prim - r->nq - r->ns);
+    const float w0 = 1.0f - h->b - h->g;
+    *u = (r->uv[2 * ix[1]] * h->b + r->uv[2 * ix[2]] * h->g) + r->uv[2 * ix[0]] * w0;
+    *v = (r->uv[2 * ix[1] + 1] * h->b + r->uv[2 * ix[2] + 1] * h->g) + r->uv[2 * ix[0] + 1] * w0;
+}
+/* tex2D(diffuseSampler, textureCoordinate).xyz (Texture.cu:107-109) */
+static v3 tex_color(const orc_renderer* r, const mat_t* m, const hit_t* h) {
+    const tex_t* t = &r->tex[m->tex];
+    float u, v, c[4];
+    hit_texcoord(r, h, &u, &v);
+    orx_tex2d_linear(t->rgba, t->w, t->h, u, v, c);
+    return mk(c[0], c[1], c[2]);
+}
+/* the radiance program's normal: getNormalMappedNormal when hasNormals
+ * (Texture.cu:69-77, :88-95).  The reference reads the tangent attributes only
+ * a mesh with vertex normals and tangents sets (TriangleMesh.cu:56-70); other
+ * primitives keep the shading normal here. */
+static v3 tex_normal(const orc_renderer* r, const mat_t* m, const hit_t* h, v3 wsn) {
+    const tex_t* t = &r->tex[m->tex];
+    if (!t->nrgba || !r->has_normals || !r->tang || (uint32_t)h->prim < r->nq + r->ns) return wsn;
+    const uint32_t* ix = r->tris + 3 * (size_t)((uint32_t)h->prim - r->nq - r->ns);
+    const float w0 = 1.0f - h->b - h->g;
+    v3 T = normalize(add(add(scl(r->tang[ix[1]], h->b), scl(r->tang[ix[2]], h->g)), scl(r->tang[ix[0]], w0)));
+    v3 B = normalize(add(add(scl(r->btan[ix[1]], h->b), scl(r->btan[ix[2]], h->g)), scl(r->btan[ix[0]], w0)));
+    T = normalize(T);
+    B = normalize(B);
+    float u, v, c[4];
+    hit_texcoord(r, h, &u, &v);
+    orx_tex2d_linear(t->nrgba, t->nw, t->nh, u, v, c);
+    const float nx = 2.f * c[0] - 1.f, ny = 2.f * c[1] - 1.f, nz = 2.f * c[2] - 1.f;
+    v3 N = mk(nx * T.x + ny * B.x + nz * wsn.x, nx * T.y + ny * B.y + nz * wsn.y, nx * T.z + ny * B.z + nz * wsn.z);
+    return normalize(N);
+}
+
 /* shadow ray: any hit in (tmin, tmax) occludes (every material carries
  * gatherAnyHitOnNonEmitter for RayType::SHADOW, Material.cpp:18-26, which
  * DiffuseEmitter.cpp:33 installs last and so overrides gatherAnyHitOnEmitter) */
@@ -703,6 +793,9 @@ static cam_t camera_setup(const orx_camera* c) {
     k.vlen = vlen;
     return k;
 }
+void orc_tex2d(const uint8_t* rgba, uint32_t w, uint32_t h, float u, float v, float out[4]) {
+    orx_tex2d_linear(rgba, w, h, u, v, out);
+}
 void orc_camera_setup(const orx_camera* cam, float lookdir[3], float u[3], float v[3]) {
     cam_t k = camera_setup(cam);
     lookdir[0] = k.lookdir.x; lookdir[1] = k.lookdir.y; lookdir[2] = k.lookdir.z;
@@ -776,6 +869,19 @@ static void trace_radiance(const orc_renderer* r, v3 o, v3 d, float tmin, rprd_t
                 float s1 = orc_uniform(prd->rs);
                 prd->newdir = sample_hemisphere_cos(N, s0, s1);
             }
+            return;
+        } else if (m->type == ORX_MAT_TEXTURE) {
+            /* Texture.cu:83-110: normal-mapped normal, no depth++ */
+            v3 wsn = normalize(h.sn);
+            prd->flags |= PRD_HIT_NON_SPECULAR;
+            prd->normal = tex_normal(r, m, &h, wsn);
+            prd->position = hitPoint;
+            if (prd->flags & PRD_PATH_TRACING) {
+                float s0 = orc_uniform(prd->rs);
+                float s1 = orc_uniform(prd->rs);
+                prd->newdir = sample_hemisphere_cos(wsn, s0, s1);
+            }
+            prd->attenuation = mul(prd->attenuation, tex_color(r, m, &h));
             return;
         } else if (m->type == ORX_MAT_DIFFUSE_EMITTER) {
             /* DiffuseEmitter.cu:40-51 */
@@ -941,6 +1047,33 @@ static void trace_photon(const orc_renderer* r, v3 o, v3 d, v3 power, uint32_t p
             d = sample_hemisphere_cos(N, s0, s1);
             o = hitPoint;
             tmin = 0.0001f;
+        } else if (m->type == ORX_MAT_TEXTURE) {
+            /* Texture.cu:116-175: weight cutoff 0.01, new ray tmin 0.01 */
+            v3 N = normalize(h.sn);
+            if (depth >= 1 && numStored < maxDeposits) {
+                photon_t* p = &r->photons[pm_index + numStored];
+                p->power = power;
+                p->position = hitPoint;
+                p->direction = d;
+                numStored++;
+            }
+            const v3 kd = tex_color(r, m, &h);
+            power = mul(power, kd);
+            weight *= fmax3(kd);
+            if (depth >= 3) {
+                float probContinue = favgf(kd);
+                float probSample = orc_uniform(rs);
+                if (probSample >= probContinue) return;
+                power = divs(power, probContinue);
+            }
+            depth++;
+            if (depth >= maxDepth || (double)weight < 0.01) return;
+            if (numStored >= maxDeposits) return;
+            float s0 = orc_uniform(rs);
+            float s1 = orc_uniform(rs);
+            d = sample_hemisphere_cos(N, s0, s1);
+            o = hitPoint;
+            tmin = 0.01f;
         } else if (m->type == ORX_MAT_DIFFUSE_EMITTER) {
             return; /* depth++ only */
         } else if (m->type == ORX_MAT_MIRROR) {

@@ -68,6 +68,8 @@ int32_t orc_trace_any(orc_renderer* r, const float o[3], const float d[3], float
 void orc_sample_unit_hemisphere_cos(const float n[3], float u1, float u2, float out[3]);
 void orc_sample_unit_hemisphere(const float n[3], float u1, float u2, float out[3]);
 void orc_camera_setup(const orx_camera* cam, float lookdir[3], float u[3], float v[3]);
+/* tex2D of a w x h RGBA8 image (orx_detmath.h orx_tex2d_linear) */
+void orc_tex2d(const uint8_t* rgba, uint32_t w, uint32_t h, float u, float v, float out[4]);
 
 #ifdef __cplusplus
 }

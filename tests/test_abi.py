@@ -49,8 +49,9 @@ def test_struct_layouts_match_c():
 #include <stddef.h>
 #include "orx.h"
 int main(void){
- printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(orx_camera), sizeof(orx_request), sizeof(orx_material),
-        sizeof(orx_light), sizeof(orx_scene), sizeof(orx_config), sizeof(orx_stats), offsetof(orx_stats, pass_ms));
+ printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(orx_camera), sizeof(orx_request), sizeof(orx_material),
+        sizeof(orx_light), sizeof(orx_scene), sizeof(orx_config), sizeof(orx_stats), offsetof(orx_stats, pass_ms),
+        sizeof(orx_texture), offsetof(orx_scene, textures));
  return 0;}
 """
     d = tempfile.mkdtemp()
@@ -60,7 +61,8 @@ int main(void){
     subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
     vals = [int(v) for v in subprocess.check_output([exe]).split()]
     py = [C.sizeof(_abi.OrxCamera), C.sizeof(_abi.OrxRequest), C.sizeof(_abi.OrxMaterial), C.sizeof(_abi.OrxLight),
-          C.sizeof(_abi.OrxScene), C.sizeof(_abi.OrxConfig), C.sizeof(_abi.OrxStats), _abi.OrxStats.pass_ms.offset]
+          C.sizeof(_abi.OrxScene), C.sizeof(_abi.OrxConfig), C.sizeof(_abi.OrxStats), _abi.OrxStats.pass_ms.offset,
+          C.sizeof(_abi.OrxTexture), _abi.OrxScene.textures.offset]
     assert vals == py
 
 

@@ -265,3 +265,34 @@ def test_vcm_resize_reruns_estimate():
     assert rel_l2(gpu.getOutputBuffer(), ora.output()) < 1e-4
     gpu.destroy()
     ora.close()
+
+
+@pytest.mark.parametrize("method", [_abi.PROGRESSIVE_PHOTON_MAPPING, _abi.PATH_TRACING,
+                                    _abi.VCM_BIDIRECTIONAL_PATH_TRACING])
+def test_texture_parity(method):
+    """Texture material (material/Texture.cu): bilinear wrap sampling of the
+    diffuse map, normal mapping with interpolated tangents, the photon program's
+    0.01 cutoffs and VCM Lambertian(texel) vertices, on the TexturedRoom mesh."""
+    from oppositerenderer_amd import synthetic
+    scene = synthetic.textured_room()
+    gpu, ora, det = make_pair(scene, 56, 48, 64, method)
+    radius = scene.initial_ppm_radius()
+    req = det.to_abi()
+    for it in range(3):
+        gpu.renderNextIteration(it, it, radius, True, det)
+        ora.render_next_iteration(it, it, radius, req)
+        if method == _abi.PROGRESSIVE_PHOTON_MAPPING:
+            check_ppm_iteration(gpu, ora)
+        elif method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING:
+            check_vcm_iteration(gpu, ora)
+        else:
+            assert np.array_equal(gpu.read_buffer(_abi.BUF_RNG, np.uint32), ora.read_buffer(_abi.BUF_RNG, np.uint32))
+        radius = next_ppm_radius(radius, it)
+    g, o = gpu.getOutputBuffer(), ora.output()
+    assert np.isfinite(g).all() and g.mean() > 0
+    if method == _abi.PATH_TRACING:
+        assert np.array_equal(g.view(np.uint32), o.view(np.uint32)), rel_l2(g, o)
+    else:
+        assert rel_l2(g, o) < 1e-4, rel_l2(g, o)
+    gpu.destroy()
+    ora.close()
