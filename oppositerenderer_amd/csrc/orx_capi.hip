@@ -368,6 +368,7 @@ struct orx_renderer {
     DevBuf d_rng, d_hp, d_ind, d_dir, d_out, d_dbg;
     DevBuf d_slots, d_vmask, d_sorted, d_perm, d_keys, d_ranks;
     DevBuf d_hist, d_offsets, d_bbox, d_partials, d_grid, d_work;
+    DevBuf d_wray0, d_wray1, d_whit, d_wpath, d_wseg; /* wavefront photon pass queues */
     PixelBufs px{};
     PhotonBufs pb{};
     /* timing: event pairs per pass since the last orx_reset_timing */
@@ -408,8 +409,8 @@ extern "C" {
 /* stats build only: [closest: rays, nodes, leaves, tris, any: rays, nodes, leaves, tris]; reset = 1 zeroes */
 int orx_trav_stats_read(orx_renderer* r, unsigned long long* out, int reset) {
     if (!r || !r->scene.trav_stats || hipDeviceSynchronize() != hipSuccess) return 1;
-    if (hipMemcpy(out, r->scene.trav_stats, 64, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-    if (reset && hipMemset(r->scene.trav_stats, 0, 64) != hipSuccess) return 1;
+    if (hipMemcpy(out, r->scene.trav_stats, 128, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+    if (reset && hipMemset(r->scene.trav_stats, 0, 128) != hipSuccess) return 1;
     return 0;
 }
 #endif
@@ -693,8 +694,8 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     S.bvh_nodes = (uint32_t)b4.out.size();
     S.stack_entries = nt ? stack_bound + 1 : 0;
 #ifdef ORX_TRAV_STATS
-    HIPCHK(r, r->d_tstats.ensure(64));
-    HIPCHK(r, hipMemset(r->d_tstats.p, 0, 64));
+    HIPCHK(r, r->d_tstats.ensure(128));
+    HIPCHK(r, hipMemset(r->d_tstats.p, 0, 128));
     S.trav_stats = r->d_tstats.as<unsigned long long>();
 #else
     S.trav_stats = nullptr;
@@ -750,6 +751,13 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_partials.ensure(nblocks * 4));
     HIPCHK(r, r->d_grid.ensure(sizeof(GridParams)));
     HIPCHK(r, r->d_work.ensure(64));
+    HIPCHK(r, r->d_wray0.ensure(nphot * 32 + 32));
+    HIPCHK(r, r->d_wray1.ensure(nphot * 32 + 32));
+    HIPCHK(r, r->d_whit.ensure(nphot * 32 + 32));
+    HIPCHK(r, r->d_wpath.ensure(nphot * 32 + 32));
+    const size_t wnseg = (nphot + 511) / 512 + 1;
+    HIPCHK(r, r->d_wseg.ensure(2 * wnseg * 4));
+    HIPCHK(r, hipMemsetAsync(r->d_wseg.p, 0, 2 * wnseg * 4, r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_hist.p, 0, G2 * 4, r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_offsets.p, 0, G2 * 4, r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_vmask.p, 0, nphot, r->stream));
@@ -795,6 +803,12 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     pb.scan_partials = r->d_partials.as<uint32_t>();
     pb.grid = r->d_grid.as<GridParams>();
     pb.work = r->d_work.as<uint32_t>();
+    pb.wray[0] = r->d_wray0.as<float4>();
+    pb.wray[1] = r->d_wray1.as<float4>();
+    pb.whit = r->d_whit.as<float4>();
+    pb.wpath = r->d_wpath.as<float4>();
+    pb.wseg = r->d_wseg.as<uint32_t>();
+    pb.wnseg = (uint32_t)wnseg;
 
     /* initializeRandomStates (OptixRenderer_SpatialHash.cu:310-347) */
     uint32_t seed = r->cfg.seed;
@@ -883,7 +897,12 @@ static void ppm_eye(orx_renderer* r, const DevCamera& cam, const Consts& c) {
 static void ppm_photons_grid(orx_renderer* r, const Consts& c) {
     hipStream_t st = cur_stream(r);
     ev_begin(r, P_PHOTON);
-    launch_ppm_photon(st, r->scene, r->px, r->pb, c);
+    static const int wavefront = [] {
+        const char* e = getenv("ORX_PHOTON_WAVEFRONT");
+        return e ? atoi(e) : 0;
+    }();
+    if (wavefront) launch_ppm_photon_wavefront(st, r->scene, r->px, r->pb, c);
+    else launch_ppm_photon(st, r->scene, r->px, r->pb, c);
     ev_end(r, P_PHOTON);
     ev_begin(r, P_SETUP_HASH);
     launch_grid_setup(st, r->pb);

@@ -290,7 +290,7 @@ struct DevScene {
     const DevNode4* bvh4;
     uint32_t bvh_nodes;
     uint32_t stack_entries;
-    unsigned long long* trav_stats; /* [8] in ORX_TRAV_STATS builds, else unused */
+    unsigned long long* trav_stats; /* [16] in ORX_TRAV_STATS builds, else unused */
 };
 
 /* Traversal stack: per-lane column of a dynamic LDS array [stack_entries][64]
@@ -478,18 +478,23 @@ __device__ __forceinline__ void cswap(float& ta, uint32_t& ca, float& tb, uint32
 /* Optional traversal statistics (build with -DORX_TRAV_STATS): rays, inner
  * nodes visited, leaves visited, triangle tests — per ray type (closest/any). */
 #ifdef ORX_TRAV_STATS
-#define ORX_TS_DECL uint32_t ts_nodes = 0, ts_leaves = 0, ts_tris = 0
+#define ORX_TS_DECL uint32_t ts_nodes = 0, ts_leaves = 0, ts_tris = 0, ts_wn = 0, ts_wl = 0
 #define ORX_TS_INC(v, n) (v) += (n)
+/* wave-level loop iterations: counted by the wave's first active lane */
+#define ORX_TS_WAVE(v) (v) += ((uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1) == (threadIdx.x & 63u))
 #define ORX_TS_FLUSH(base)                                                  \
     do {                                                                    \
         atomicAdd(&S.trav_stats[(base) + 0], 1ull);                       \
         atomicAdd(&S.trav_stats[(base) + 1], (unsigned long long)ts_nodes);  \
         atomicAdd(&S.trav_stats[(base) + 2], (unsigned long long)ts_leaves); \
         atomicAdd(&S.trav_stats[(base) + 3], (unsigned long long)ts_tris);   \
+        atomicAdd(&S.trav_stats[8 + (base) / 2], (unsigned long long)ts_wn);  \
+        atomicAdd(&S.trav_stats[9 + (base) / 2], (unsigned long long)ts_wl);  \
     } while (0)
 #else
 #define ORX_TS_DECL
 #define ORX_TS_INC(v, n)
+#define ORX_TS_WAVE(v)
 #define ORX_TS_FLUSH(base)
 #endif
 
@@ -526,15 +531,17 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
         int sp = 0;
         uint32_t ref = 0; /* root */
         ORX_TS_DECL;
-        /* while-while (Aila & Laine 2009): inner nodes until the lane reaches a
-         * leaf, then leaves until the next stack entry is an inner node, so a
-         * wave does not alternate masked node and leaf work every iteration */
+        /* speculative while-while (Aila & Laine 2009): a lane that reaches a
+         * leaf postpones it and keeps descending until every lane of the wave
+         * holds a leaf, then all process theirs together */
+        uint32_t lf = 0; /* postponed leaf, or a non-leaf value for none */
         while (ref != ORX_DONE) {
             while (!(ref & ORX_LEAF) && ref != ORX_DONE) {
                 float ct[4];
                 uint32_t cc[4];
                 node_test(S.bvh4, ref, rb, tmin, best, ct, cc);
                 ORX_TS_INC(ts_nodes, 1);
+                ORX_TS_WAVE(ts_wn);
                 cswap(ct[0], cc[0], ct[1], cc[1]);
                 cswap(ct[2], cc[2], ct[3], cc[3]);
                 cswap(ct[0], cc[0], ct[2], cc[2]);
@@ -548,11 +555,17 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
                 } else {
                     ref = sp ? stk[(--sp) * 64] : ORX_DONE;
                 }
+                if ((ref & ORX_LEAF) && !(lf & ORX_LEAF)) {
+                    lf = ref;
+                    ref = sp ? stk[(--sp) * 64] : ORX_DONE;
+                }
+                if (!__ballot(!(lf & ORX_LEAF))) break;
             }
-            while (ref & ORX_LEAF) {
-                const uint32_t first = (ref & 0x7fffffffu) >> 3, cnt = (ref & 7u) + 1u;
+            while (lf & ORX_LEAF) {
+                const uint32_t first = (lf & 0x7fffffffu) >> 3, cnt = (lf & 7u) + 1u;
                 ORX_TS_INC(ts_leaves, 1);
                 ORX_TS_INC(ts_tris, cnt);
+                ORX_TS_WAVE(ts_wl);
                 for (uint32_t k = first; k < first + cnt; k++) {
                     const float4 v0 = S.tri_v[3 * k], v1 = S.tri_v[3 * k + 1], v2 = S.tri_v[3 * k + 2];
                     const int32_t gid = (int32_t)(base + __float_as_uint(v0.w));
@@ -568,7 +581,8 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
                         bg = g;
                     }
                 }
-                ref = sp ? stk[(--sp) * 64] : ORX_DONE;
+                lf = ref; /* another leaf postponed behind it: process it too */
+                if (ref & ORX_LEAF) ref = sp ? stk[(--sp) * 64] : ORX_DONE;
             }
         }
         ORX_TS_FLUSH(0);
@@ -582,6 +596,105 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
     h.sn = sn;
     return true;
 }
+/* Resumable closest-hit traversal for the wavefront passes: the same
+ * computation as trace_closest, split so that a persistent kernel can run one
+ * while-while round per lane and hand a lane whose ray finished a new ray
+ * (Aila & Laine 2009, "dynamic fetch").  Results are identical to
+ * trace_closest: the hit is fixed by the exact triangle tests and the
+ * (t, primitive id) tie rule, not by the visiting order. */
+struct TraceState {
+    RayBox rb;
+    f3 d;
+    float tmin, best, bb, bg;
+    int32_t bp;
+    uint32_t bslot, ref;
+    int32_t sp;
+    f3 sn;
+};
+__device__ __forceinline__ void trace_begin(const DevScene& S, f3 o, f3 d, float tmin, float tmax, TraceState& T) {
+    float best = tmax, t;
+    int32_t bp = -1;
+    for (uint32_t i = 0; i < S.nq; i++) {
+        if (isect_quad(S.quads[i], o, d, tmin, best, t)) {
+            best = t;
+            bp = (int32_t)i;
+        }
+    }
+    f3 sn = mk1(0);
+    for (uint32_t i = 0; i < S.ns; i++) {
+        f3 n;
+        if (isect_sphere(S.spheres[i], o, d, tmin, best, t, n)) {
+            best = t;
+            bp = (int32_t)(S.nq + i);
+            sn = n;
+        }
+    }
+    T.rb = ray_box(o, d);
+    T.d = d;
+    T.tmin = tmin;
+    T.best = best;
+    T.bp = bp;
+    T.bslot = 0;
+    T.bb = 0.f;
+    T.bg = 0.f;
+    T.sn = sn;
+    T.sp = 0;
+    T.ref = S.nt ? 0u : ORX_DONE;
+}
+/* one round: inner nodes until a leaf (or the end), then leaves until the
+ * next entry is an inner node */
+__device__ __forceinline__ void trace_round(const DevScene& S, TraceState& T, uint32_t* stk) {
+    const uint32_t base = S.nq + S.ns;
+    const f3 o = T.rb.o;
+    uint32_t ref = T.ref;
+    int32_t sp = T.sp;
+    uint32_t lf = 0;
+    while (!(ref & ORX_LEAF) && ref != ORX_DONE) {
+        float ct[4];
+        uint32_t cc[4];
+        node_test(S.bvh4, ref, T.rb, T.tmin, T.best, ct, cc);
+        cswap(ct[0], cc[0], ct[1], cc[1]);
+        cswap(ct[2], cc[2], ct[3], cc[3]);
+        cswap(ct[0], cc[0], ct[2], cc[2]);
+        cswap(ct[1], cc[1], ct[3], cc[3]);
+        cswap(ct[1], cc[1], ct[2], cc[2]);
+        if (ct[0] != INFINITY) {
+            if (ct[3] != INFINITY) stk[(sp++) * 64] = cc[3];
+            if (ct[2] != INFINITY) stk[(sp++) * 64] = cc[2];
+            if (ct[1] != INFINITY) stk[(sp++) * 64] = cc[1];
+            ref = cc[0];
+        } else {
+            ref = sp ? stk[(--sp) * 64] : ORX_DONE;
+        }
+        if ((ref & ORX_LEAF) && !(lf & ORX_LEAF)) {
+            lf = ref;
+            ref = sp ? stk[(--sp) * 64] : ORX_DONE;
+        }
+        if (!__ballot(!(lf & ORX_LEAF))) break;
+    }
+    while (lf & ORX_LEAF) {
+        const uint32_t first = (lf & 0x7fffffffu) >> 3, cnt = (lf & 7u) + 1u;
+        for (uint32_t k = first; k < first + cnt; k++) {
+            const float4 v0 = S.tri_v[3 * k], v1 = S.tri_v[3 * k + 1], v2 = S.tri_v[3 * k + 2];
+            const int32_t gid = (int32_t)(base + __float_as_uint(v0.w));
+            float t, b, g;
+            float lim = T.bp >= 0 ? orx_as_float(orx_as_uint(T.best) + 1u) : T.best;
+            if (isect_tri(ld_f3(v0), ld_f3(v1), ld_f3(v2), o, T.d, T.tmin, lim, t, b, g) &&
+                (t < T.best || gid < T.bp)) {
+                T.best = t;
+                T.bp = gid;
+                T.bslot = k;
+                T.bb = b;
+                T.bg = g;
+            }
+        }
+        lf = ref;
+        if (ref & ORX_LEAF) ref = sp ? stk[(--sp) * 64] : ORX_DONE;
+    }
+    T.ref = ref;
+    T.sp = sp;
+}
+
 /* any hit in (tmin,tmax): every material's RayType::SHADOW any-hit is
  * gatherAnyHitOnNonEmitter (Material.cpp:18-26, DirectRadianceEstimation.cu:79-83) */
 __device__ inline bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, float tmax, uint32_t* stk) {
@@ -597,12 +710,14 @@ __device__ inline bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, floa
         int sp = 0;
         uint32_t ref = 0;
         ORX_TS_DECL;
+        uint32_t lf = 0; /* speculative while-while, as trace_closest */
         while (ref != ORX_DONE) {
             while (!(ref & ORX_LEAF) && ref != ORX_DONE) {
                 float ct[4];
                 uint32_t cc[4];
                 node_test(S.bvh4, ref, rb, tmin, tmax, ct, cc);
                 ORX_TS_INC(ts_nodes, 1);
+                ORX_TS_WAVE(ts_wn);
                 uint32_t next = ORX_DONE;
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
@@ -612,10 +727,16 @@ __device__ inline bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, floa
                     }
                 }
                 ref = next != ORX_DONE ? next : (sp ? stk[(--sp) * 64] : ORX_DONE);
+                if ((ref & ORX_LEAF) && !(lf & ORX_LEAF)) {
+                    lf = ref;
+                    ref = sp ? stk[(--sp) * 64] : ORX_DONE;
+                }
+                if (!__ballot(!(lf & ORX_LEAF))) break;
             }
-            while (ref & ORX_LEAF) {
-                const uint32_t first = (ref & 0x7fffffffu) >> 3, cnt = (ref & 7u) + 1u;
+            while (lf & ORX_LEAF) {
+                const uint32_t first = (lf & 0x7fffffffu) >> 3, cnt = (lf & 7u) + 1u;
                 ORX_TS_INC(ts_leaves, 1);
+                ORX_TS_WAVE(ts_wl);
                 for (uint32_t k = first; k < first + cnt; k++) {
                     float b, g;
                     ORX_TS_INC(ts_tris, 1);
@@ -625,7 +746,8 @@ __device__ inline bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, floa
                         return true;
                     }
                 }
-                ref = sp ? stk[(--sp) * 64] : ORX_DONE;
+                lf = ref;
+                if (ref & ORX_LEAF) ref = sp ? stk[(--sp) * 64] : ORX_DONE;
             }
         }
         ORX_TS_FLUSH(4);

@@ -73,6 +73,12 @@ struct PhotonBufs {
     uint32_t* scan_partials; /* [ceil((gmax+2)/1024)+1] */
     GridParams* grid;
     uint32_t* work;     /* [1] persistent photon pass: next photon index (zeroed before each launch) */
+    /* wavefront photon pass (launch_ppm_photon_wavefront) */
+    float4* wray[2];    /* ping-pong ray queues [n][2]: o.xyz|tmin, d.xyz|photon index */
+    float4* whit;       /* [n][2]: t|prim|slot|b (sphere: sn.x), g|sn.y|sn.z|- */
+    float4* wpath;      /* [P][2]: power.xyz|weight, depth|numStored|mask|- */
+    uint32_t* wseg;     /* [2][wnseg] live entries of each queue segment */
+    uint32_t wnseg;     /* segments per queue */
 };
 
 struct Consts {
@@ -88,6 +94,10 @@ void launch_rng_init(hipStream_t s, RngPlanes rng, uint32_t RW, uint32_t rows, u
                      uint32_t seed);
 void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c);
 void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c);
+/* wavefront form of the photon pass: emit, then per bounce a persistent
+ * trace kernel over the compacted ray queue and a shading kernel */
+void launch_ppm_photon_wavefront(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb,
+                                 const Consts& c);
 void launch_grid_setup(hipStream_t s, const PhotonBufs& pb);
 void launch_grid_hash(hipStream_t s, const PhotonBufs& pb);
 void launch_grid_scan(hipStream_t s, const PhotonBufs& pb);

@@ -342,6 +342,286 @@ void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, co
 }
 
 /* ------------------------------------------------------------------ */
+/* wavefront photon pass                                               */
+/* ------------------------------------------------------------------ */
+/* The single-kernel pass above runs a wave until its longest photon path
+ * has finished, and each bounce until its lane with the most node visits
+ * has: PMC shows it VALU-saturated at ~1/3 useful lanes.  Here every
+ * bounce is a compacted queue: k_wf_trace is a persistent traversal kernel
+ * whose lanes take a new ray from the queue as soon as theirs finishes
+ * (dynamic fetch), k_wf_shade runs the photon closest-hit programs over the
+ * hits and appends the surviving paths to the next bounce's queue.  Every
+ * path evaluates exactly the operations of k_ppm_photon in the same order
+ * (RNG state stays in its slot), so the deposits are bit-identical. */
+__device__ __forceinline__ float4 u4f(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return make_float4(__uint_as_float(a), __uint_as_float(b), __uint_as_float(c), __uint_as_float(d));
+}
+
+/* Queues are kept as WF_SEG-entry segments: segment k of a bounce's queue
+ * holds the surviving paths of segment k of the previous bounce, compacted
+ * in place by the shading block that owns it (an LDS prefix sum), with its
+ * length in wseg[parity][k].  No queue position ever comes from a global
+ * atomic: one counter for all waves serialises at the memory side (~12 ns
+ * per add), which at 19 M rays per pass costs more than the tracing. */
+constexpr uint32_t WF_SEG = 512;
+
+__global__ __launch_bounds__(256) void k_wf_emit(DevScene S, PixelBufs px, PhotonBufs pb) {
+    const uint32_t total = pb.prows * pb.PW;
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < total; p += gridDim.x * blockDim.x) {
+        PhotonPath P;
+        Rng rs;
+        photon_emit(S, px, pb, p, P, rs);
+        rng_store(px.rng, P.slot, rs);
+        pb.wpath[2 * (size_t)p] = make_float4(P.power.x, P.power.y, P.power.z, P.weight);
+        pb.wpath[2 * (size_t)p + 1] = u4f(0u, 0u, 0u, 0u);
+        float4* r = pb.wray[0] + 2 * (size_t)p;
+        r[0] = make_float4(P.o.x, P.o.y, P.o.z, P.tmin);
+        r[1] = make_float4(P.d.x, P.d.y, P.d.z, __uint_as_float(p));
+        if (p % WF_SEG == 0) pb.wseg[p / WF_SEG] = total - p < WF_SEG ? total - p : WF_SEG;
+    }
+}
+
+/* persistent closest-hit traversal over the queue of parity `par`: wave w
+ * walks segments w, w + waves, ...; a lane whose ray is done takes the next
+ * ray of the wave's current segment (dynamic fetch without atomics) */
+__global__ __launch_bounds__(64) void k_wf_trace(DevScene S, PhotonBufs pb, uint32_t par, uint32_t nseg) {
+    ORX_STACK_DECL;
+    uint32_t* stk = ORX_STACK_PTR;
+    const uint32_t lane = threadIdx.x;
+    const float4* rays = pb.wray[par];
+    const uint32_t* cnt = pb.wseg + par * pb.wnseg;
+    TraceState T;
+    uint32_t ri = 0;
+    uint32_t seg = blockIdx.x, next = 0, end = 0;
+    if (seg < nseg) {
+        next = seg * WF_SEG;
+        end = next + cnt[seg];
+    }
+    bool active = false;
+    for (;;) {
+        uint64_t need = __ballot(!active);
+        while (need && next >= end && seg < nseg) { /* wave-uniform: move to the wave's next segment */
+            seg += gridDim.x;
+            if (seg < nseg) {
+                next = seg * WF_SEG;
+                end = next + cnt[seg];
+            }
+        }
+        if (need && next < end) {
+            const uint32_t avail = end - next;
+            const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+            if (!active && rank < avail) {
+                ri = next + rank;
+                const float4 a = rays[2 * (size_t)ri], b = rays[2 * (size_t)ri + 1];
+                trace_begin(S, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), a.w, RT_DEFAULT_MAX, T);
+                active = true;
+            }
+            const uint32_t nn = (uint32_t)__popcll(need);
+            next += nn < avail ? nn : avail;
+        }
+        if (!__ballot(active)) {
+            if (next >= end && seg >= nseg) break;
+            continue;
+        }
+        if (active) {
+            if (T.ref != ORX_DONE) trace_round(S, T, stk);
+            if (T.ref == ORX_DONE) {
+                float4* h = pb.whit + 2 * (size_t)ri;
+                const bool tri = T.bp >= 0 && (uint32_t)T.bp >= S.nq + S.ns;
+                h[0] = make_float4(T.best, __int_as_float(T.bp), __uint_as_float(T.bslot), tri ? T.bb : T.sn.x);
+                h[1] = make_float4(tri ? T.bg : T.sn.y, T.sn.z, 0.f, 0.f);
+                active = false;
+            }
+        }
+    }
+}
+
+/* photon closest-hit programs (as k_ppm_photon) over the queue of parity
+ * `par`; block k owns segment k and compacts its survivors into segment k of
+ * the other queue */
+__global__ __launch_bounds__(256) void k_wf_shade(DevScene S, PixelBufs px, PhotonBufs pb, Consts c, uint32_t par,
+                                                  uint32_t nseg) {
+    __shared__ uint32_t wcount[4];
+    const uint32_t seg = blockIdx.x;
+    if (seg >= nseg) return;
+    const uint32_t n = pb.wseg[par * pb.wnseg + seg];
+    const float4* rays = pb.wray[par];
+    float4* out = pb.wray[par ^ 1];
+    float lo_x = INFINITY, lo_y = INFINITY, lo_z = INFINITY;
+    float hi_x = -INFINITY, hi_y = -INFINITY, hi_z = -INFINITY;
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t written = 0; /* block-uniform */
+    for (uint32_t k0 = 0; k0 < n; k0 += 256) {
+        const uint32_t k = k0 + threadIdx.x;
+        const uint32_t i = seg * WF_SEG + k;
+        bool cont = false;
+        f3 no = mk1(0.f), nd = mk1(0.f);
+        float ntmin = 0.f;
+        uint32_t p = 0;
+        if (k < n) {
+            const float4 a = rays[2 * (size_t)i], b = rays[2 * (size_t)i + 1];
+            const float4 h0 = pb.whit[2 * (size_t)i], h1 = pb.whit[2 * (size_t)i + 1];
+            p = __float_as_uint(b.w);
+            const float4 pa = pb.wpath[2 * (size_t)p], pq = pb.wpath[2 * (size_t)p + 1];
+            PhotonPath P;
+            P.o = mk(a.x, a.y, a.z);
+            P.d = mk(b.x, b.y, b.z);
+            P.tmin = a.w;
+            P.power = mk(pa.x, pa.y, pa.z);
+            P.weight = pa.w;
+            P.depth = __float_as_uint(pq.x);
+            P.numStored = __float_as_uint(pq.y);
+            P.mask = __float_as_uint(pq.z);
+            P.p_local = p;
+            const uint32_t j = p / pb.PW;
+            P.slot = (size_t)j * px.RW + (p - j * pb.PW);
+            bool done = false;
+            Hit h;
+            h.prim = __float_as_int(h0.y);
+            if (h.prim < 0) {
+                done = true;
+            } else {
+                h.t = h0.x;
+                h.slot = __float_as_uint(h0.z);
+                h.b = h0.w;
+                h.g = h1.x;
+                h.sn = mk(h0.w, h1.x, h1.y);
+                Rng rs = rng_load(px.rng, P.slot);
+                const DevMaterial& m = S.mats[prim_material(S, h)];
+                const f3 hitPoint = P.o + P.d * h.t;
+                if (m.type == MAT_DIFFUSE || m.type == MAT_GLOSSY || m.type == MAT_TEXTURE) {
+                    const bool tex = m.type == MAT_TEXTURE;
+                    const f3 N = shading_normal(S, h);
+                    if (P.depth >= 1 && P.numStored < pb.D) {
+                        const uint32_t si = P.p_local * pb.D + P.numStored;
+                        float4* rec = pb.slots + 4 * (size_t)si;
+                        rec[0] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, P.power.x);
+                        rec[1] = make_float4(P.d.x, P.d.y, P.d.z, P.power.y);
+                        rec[2].x = P.power.z;
+                        if (fmax3(P.power) > 0) {
+                            P.mask |= 1u << P.numStored;
+                            lo_x = fminf(lo_x, hitPoint.x); lo_y = fminf(lo_y, hitPoint.y); lo_z = fminf(lo_z, hitPoint.z);
+                            hi_x = fmaxf(hi_x, hitPoint.x); hi_y = fmaxf(hi_y, hitPoint.y); hi_z = fmaxf(hi_z, hitPoint.z);
+                        }
+                        P.numStored++;
+                    }
+                    const f3 Kd = tex ? tex_color(S, m, h) : m.Kd;
+                    P.power = P.power * Kd;
+                    P.weight *= fmax3(Kd);
+                    if (P.depth >= 3) {
+                        float probContinue = favgf(Kd);
+                        float probSample = rnd(rs);
+                        if (probSample >= probContinue) done = true;
+                        else P.power = P.power / probContinue;
+                    }
+                    if (!done) {
+                        P.depth++;
+                        if (P.depth >= c.max_photon_depth || (double)P.weight < (tex ? 0.01 : 0.001) ||
+                            P.numStored >= pb.D) {
+                            done = true;
+                        } else {
+                            float s0 = rnd(rs);
+                            float s1 = rnd(rs);
+                            nd = sample_hemisphere_cos(N, s0, s1);
+                            no = hitPoint;
+                            ntmin = tex ? 0.01f : 0.0001f;
+                        }
+                    }
+                } else if (m.type == MAT_EMITTER) {
+                    done = true;
+                } else if (m.type == MAT_MIRROR) {
+                    const f3 N = shading_normal(S, h);
+                    P.depth++;
+                    if (P.depth <= c.max_photon_depth) {
+                        P.power = P.power * m.Kr;
+                        nd = reflect(P.d, N);
+                        no = hitPoint;
+                        ntmin = 0.0001f;
+                    } else {
+                        done = true;
+                    }
+                } else {
+                    const f3 wsn = shading_normal(S, h);
+                    const bool outside = dot(wsn, P.d) < 0;
+                    const f3 N = outside ? wsn : -wsn;
+                    const float n1 = outside ? 1.0f : m.ior, n2 = outside ? m.ior : 1.0f;
+                    f3 refr;
+                    bool valid;
+                    const float refl = glass_reflect_factor(P.d, N, n1, n2, refr, valid);
+                    const float sample = rnd(rs);
+                    nd = (sample <= refl) ? reflect(P.d, N) : refr;
+                    P.depth++;
+                    if (P.depth <= c.max_photon_depth) {
+                        no = hitPoint;
+                        ntmin = 0.0001f;
+                    } else {
+                        done = true;
+                    }
+                }
+                rng_store(px.rng, P.slot, rs);
+            }
+            if (done) {
+                pb.vmask[p] = (uint8_t)P.mask;
+            } else {
+                cont = true;
+                pb.wpath[2 * (size_t)p] = make_float4(P.power.x, P.power.y, P.power.z, P.weight);
+                pb.wpath[2 * (size_t)p + 1] = u4f(P.depth, P.numStored, P.mask, 0u);
+            }
+        }
+        /* block-local compaction: wave ballots + LDS prefix over the 4 waves */
+        const uint64_t m = __ballot(cont);
+        if (lane == 0) wcount[wid] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+        for (uint32_t w = 0; w < 4; w++) {
+            const uint32_t cw = wcount[w];
+            before += w < wid ? cw : 0u;
+            total += cw;
+        }
+        if (cont) {
+            const uint32_t o = seg * WF_SEG + written + before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            out[2 * (size_t)o] = make_float4(no.x, no.y, no.z, ntmin);
+            out[2 * (size_t)o + 1] = make_float4(nd.x, nd.y, nd.z, __uint_as_float(p));
+        }
+        written += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) pb.wseg[(par ^ 1) * pb.wnseg + seg] = written;
+    lo_x = wave_min(lo_x); lo_y = wave_min(lo_y); lo_z = wave_min(lo_z);
+    hi_x = wave_max(hi_x); hi_y = wave_max(hi_y); hi_z = wave_max(hi_z);
+    const uint32_t rep = (blockIdx.x * 4 + wid) & (BBOX_REPLICAS - 1);
+    if (lane < 6) {
+        float v = lane == 0 ? lo_x : lane == 1 ? lo_y : lane == 2 ? lo_z : lane == 3 ? hi_x : lane == 4 ? hi_y : hi_z;
+        if (lane < 3) {
+            if (v != INFINITY) atomicMin(&pb.bbox[lane * BBOX_REPLICAS + rep], f2ord(v));
+        } else {
+            if (v != -INFINITY) atomicMax(&pb.bbox[lane * BBOX_REPLICAS + rep], f2ord(v));
+        }
+    }
+}
+
+void launch_ppm_photon_wavefront(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb,
+                                 const Consts& c) {
+    const uint32_t total = pb.prows * pb.PW;
+    if (total == 0) return;
+    const uint32_t nseg = (total + WF_SEG - 1) / WF_SEG;
+    const uint32_t eblocks = std::min<uint32_t>((total + 255) / 256, 4096u);
+    hipLaunchKernelGGL(k_wf_emit, dim3(eblocks), dim3(256), 0, s, S, px, pb);
+    /* a path traces at most max_photon_depth + 2 segments (each continuing
+     * bounce raises depth by one and continues only while depth <= max) */
+    const uint32_t rounds = c.max_photon_depth + 2;
+    /* as many one-wave blocks as the LDS stacks of one CU allow (160 KiB),
+     * at most 24 per CU (6 waves/SIMD at the kernel's ~75 VGPRs), 256 CUs */
+    const size_t lds = ORX_STACK_BYTES(S);
+    const uint32_t per_cu = lds ? (uint32_t)std::min<size_t>(24, (160u * 1024u) / lds) : 24u;
+    const uint32_t tblocks = std::min<uint32_t>(256u * per_cu, nseg);
+    for (uint32_t r = 0; r < rounds; r++) {
+        hipLaunchKernelGGL(k_wf_trace, dim3(tblocks), dim3(64), lds, s, S, pb, r & 1u, nseg);
+        hipLaunchKernelGGL(k_wf_shade, dim3(nseg), dim3(256), 0, s, S, px, pb, c, r & 1u, nseg);
+    }
+}
+
+/* ------------------------------------------------------------------ */
 /* grid setup: createUniformGridPhotonMap host math, on one thread     */
 /* ------------------------------------------------------------------ */
 __global__ void k_grid_setup(PhotonBufs pb) {

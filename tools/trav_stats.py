@@ -22,7 +22,7 @@ r = renderer.OptixRenderer(_abi.default_config(seed=1645301512, photon_launch_wi
 r.initialize(0)
 r.initScene(sc)
 det = renderer.RenderRequestDetails(sc.default_camera.set_aspect_ratio(W / H), sc.name, method, W, H)
-buf = (C.c_ulonglong * 8)()
+buf = (C.c_ulonglong * 16)()
 radius = sc.initial_ppm_radius()
 for it in range(3):
     r.renderNextIteration(it, it, radius, False, det)
@@ -31,6 +31,8 @@ for it in range(3):
     v = list(buf)
     for name, b in (("closest", 0), ("any", 4)):
         rays = max(1, v[b])
+        wn, wl = v[8 + b // 2], v[9 + b // 2]
         print(f"it{it} {name:8s} rays {v[b]:12d}  nodes/ray {v[b + 1] / rays:6.2f}  leaves/ray {v[b + 2] / rays:6.2f}"
-              f"  tris/ray {v[b + 3] / rays:6.2f}")
+              f"  tris/ray {v[b + 3] / rays:6.2f}  SIMT node {v[b + 1] / max(1, 64 * wn):5.3f}"
+              f"  leaf {v[b + 2] / max(1, 64 * wl):5.3f}")
 print("bvh stack entries", r.stats().bvh_stack_entries)
