@@ -922,11 +922,12 @@ __device__ __forceinline__ HpRef hp_ref(const GatherIn& gi, uint32_t j, uint32_t
  * 256-thread block, so neighbouring lanes share photons in L1).  The (z,y)
  * cell rows of the window are walked in the reference order
  * (IndirectRadianceEstimation.cu:95-129); within a row the photons go in
- * aligned groups of four: one dwordx4 load per SoA plane, distance tests,
- * normal tests, the kernel weight (photonPower, :59-67) and the
- * contributions evaluated two photons per instruction (v_pk_add_f32 /
- * v_pk_mul_f32 — IEEE per component, so every value is bit-identical to the
- * scalar oracle), then accumulated in photon order. */
+ * aligned groups of four: one dwordx4 load per SoA plane, two photons per
+ * packed instruction.  The acceptance tests (d^2 <= r^2, dot(-w, n) >= 0) use
+ * exactly the oracle's unfused operations, so the accepted photon set is
+ * bit-identical; the kernel weight (photonPower, :59-67) and the sums, which
+ * the device accumulates in a different order anyway, use fused
+ * multiply-adds (v_pk_fma_f32): within ~1e-7 of the oracle per term. */
 typedef float v2f __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ v2f lo2(float4 v) { return v2f{v.x, v.y}; }
 __device__ __forceinline__ v2f hi2(float4 v) { return v2f{v.z, v.w}; }
@@ -967,6 +968,13 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
                 const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
                 const float inv2r2 = 1.0f / (2 * radius2);
                 const float invDen = 1.0f / (1 - expNegativeBeta);
+                const float kx = -beta * inv2r2;
+                const float wB = alpha * invDen, wA = alpha - wB; /* w = A + B*exp(x) */
+                const v2f kx2 = v2f{kx, kx};
+                const v2f wc6 = wB * ORX_EXPU_C6, wc5 = wB * ORX_EXPU_C5, wc4 = wB * ORX_EXPU_C4;
+                const v2f wc3 = wB * ORX_EXPU_C3, wc2 = wB * ORX_EXPU_C2, wc1 = wB * ORX_EXPU_C1;
+                const v2f wc0 = v2f{wA + wB, wA + wB};
+                v2f accx = v2f{0.f, 0.f}, accy = accx, accz = accx;
                 const v2f px2 = v2f{pos.x, pos.x}, py2 = v2f{pos.y, pos.y}, pz2 = v2f{pos.z, pos.z};
                 const v2f nx2 = v2f{B.x, B.x}, ny2 = v2f{B.y, B.y}, nz2 = v2f{B.z, B.z};
                 const v2f r2v = v2f{radius2, radius2};
@@ -1027,29 +1035,35 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
                             in1 = in1 && nd0.y <= 0.f;
                             in2 = in2 && nd1.x <= 0.f;
                             in3 = in3 && nd1.y <= 0.f;
-                            /* photonPower: alpha*(1 - (1 - exp(-beta d^2 / 2r^2)) / (1 - e^-beta)) */
-                            const v2f mb = v2f{-beta, -beta}, i2 = v2f{inv2r2, inv2r2};
-                            const v2f x0 = (mb * __builtin_elementwise_min(d20, r2v)) * i2;
-                            const v2f x1 = (mb * __builtin_elementwise_min(d21, r2v)) * i2;
-                            v2f p0 = v2f{ORX_EXPU_C6, ORX_EXPU_C6}, p1 = p0;
-                            p0 = p0 * x0 + ORX_EXPU_C5; p1 = p1 * x1 + ORX_EXPU_C5;
-                            p0 = p0 * x0 + ORX_EXPU_C4; p1 = p1 * x1 + ORX_EXPU_C4;
-                            p0 = p0 * x0 + ORX_EXPU_C3; p1 = p1 * x1 + ORX_EXPU_C3;
-                            p0 = p0 * x0 + ORX_EXPU_C2; p1 = p1 * x1 + ORX_EXPU_C2;
-                            p0 = p0 * x0 + ORX_EXPU_C1; p1 = p1 * x1 + ORX_EXPU_C1;
-                            const v2f e0 = p0 * x0 + 1.0f, e1 = p1 * x1 + 1.0f;
-                            const v2f w0 = alpha * (1.0f - (1.0f - e0) * invDen);
-                            const v2f w1 = alpha * (1.0f - (1.0f - e1) * invDen);
-                            const v2f cx0 = lo2(WX) * w0, cx1 = hi2(WX) * w1;
-                            const v2f cy0 = lo2(WY) * w0, cy1 = hi2(WY) * w1;
-                            const v2f cz0 = lo2(WZ) * w0, cz1 = hi2(WZ) * w1;
-                            if (in0) { ax = ax + cx0.x; ay = ay + cy0.x; az = az + cz0.x; }
-                            if (in1) { ax = ax + cx0.y; ay = ay + cy0.y; az = az + cz0.y; }
-                            if (in2) { ax = ax + cx1.x; ay = ay + cy1.x; az = az + cz1.x; }
-                            if (in3) { ax = ax + cx1.y; ay = ay + cy1.y; az = az + cz1.y; }
+                            /* photonPower: alpha*(1 - (1 - exp(x)) / (1 - e^-beta)), x = -beta d^2 / 2r^2,
+                             * folded into one Horner chain w = (A + B) + x*B*p(x) with A = alpha*(1 - 1/den),
+                             * B = alpha/den, evaluated with fused multiply-adds, two photons per v_pk_fma_f32;
+                             * rejected photons get weight 0 and everything accumulates by pk_fma */
+                            const v2f x0 = __builtin_elementwise_min(d20, r2v) * kx2;
+                            const v2f x1 = __builtin_elementwise_min(d21, r2v) * kx2;
+                            v2f q0 = wc6, q1 = wc6;
+                            q0 = __builtin_elementwise_fma(q0, x0, wc5); q1 = __builtin_elementwise_fma(q1, x1, wc5);
+                            q0 = __builtin_elementwise_fma(q0, x0, wc4); q1 = __builtin_elementwise_fma(q1, x1, wc4);
+                            q0 = __builtin_elementwise_fma(q0, x0, wc3); q1 = __builtin_elementwise_fma(q1, x1, wc3);
+                            q0 = __builtin_elementwise_fma(q0, x0, wc2); q1 = __builtin_elementwise_fma(q1, x1, wc2);
+                            q0 = __builtin_elementwise_fma(q0, x0, wc1); q1 = __builtin_elementwise_fma(q1, x1, wc1);
+                            v2f w0 = __builtin_elementwise_fma(q0, x0, wc0), w1 = __builtin_elementwise_fma(q1, x1, wc0);
+                            w0.x = in0 ? w0.x : 0.f;
+                            w0.y = in1 ? w0.y : 0.f;
+                            w1.x = in2 ? w1.x : 0.f;
+                            w1.y = in3 ? w1.y : 0.f;
+                            accx = __builtin_elementwise_fma(lo2(WX), w0, accx);
+                            accy = __builtin_elementwise_fma(lo2(WY), w0, accy);
+                            accz = __builtin_elementwise_fma(lo2(WZ), w0, accz);
+                            accx = __builtin_elementwise_fma(hi2(WX), w1, accx);
+                            accy = __builtin_elementwise_fma(hi2(WY), w1, accy);
+                            accz = __builtin_elementwise_fma(hi2(WZ), w1, accz);
                         }
                     }
                 }
+                ax = accx.x + accx.y;
+                ay = accy.x + accy.y;
+                az = accz.x + accz.y;
             }
         }
         const f3 att = mk(B.w, Cc.x, Cc.y);
