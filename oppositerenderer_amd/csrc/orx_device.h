@@ -387,7 +387,8 @@ __device__ __forceinline__ RayBox ray_box(f3 o, f3 d) {
     auto safe = [](float v) { return fabsf(v) > 1e-30f ? v : copysignf(1e-30f, v); };
     RayBox rb;
     rb.o = o;
-    rb.inv = mk(1.0f / safe(d.x), 1.0f / safe(d.y), 1.0f / safe(d.z));
+    /* v_rcp_f32 (1 ulp): the builder's 1e-6 relative box expansion covers it */
+    rb.inv = mk(__builtin_amdgcn_rcpf(safe(d.x)), __builtin_amdgcn_rcpf(safe(d.y)), __builtin_amdgcn_rcpf(safe(d.z)));
     rb.nx = rb.inv.x < 0.f;
     rb.ny = rb.inv.y < 0.f;
     rb.nz = rb.inv.z < 0.f;
@@ -421,17 +422,28 @@ __device__ __forceinline__ void node_test(const DevBvh4* nodes, uint32_t idx, co
     c[1] = __float_as_uint(C.w);
     c[2] = __float_as_uint(D.x);
     c[3] = __float_as_uint(D.y);
+    /* two children per v_pk_fma_f32 */
+    typedef float v2q __attribute__((ext_vector_type(2)));
+    auto q2 = [](uint32_t w, int i) {
+        return v2q{(float)((w >> (8 * i)) & 0xffu), (float)((w >> (8 * i + 8)) & 0xffu)};
+    };
+    const v2q ax2 = v2q{ax, ax}, bx2 = v2q{bx, bx}, ay2 = v2q{ay, ay}, by2 = v2q{by, by};
+    const v2q az2 = v2q{az, az}, bz2 = v2q{bz, bz};
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const float tnx = __builtin_fmaf((float)((nxq >> (8 * i)) & 0xffu), bx, ax);
-        const float tfx = __builtin_fmaf((float)((fxq >> (8 * i)) & 0xffu), bx, ax);
-        const float tny = __builtin_fmaf((float)((nyq >> (8 * i)) & 0xffu), by, ay);
-        const float tfy = __builtin_fmaf((float)((fyq >> (8 * i)) & 0xffu), by, ay);
-        const float tnz = __builtin_fmaf((float)((nzq >> (8 * i)) & 0xffu), bz, az);
-        const float tfz = __builtin_fmaf((float)((fzq >> (8 * i)) & 0xffu), bz, az);
-        const float t0 = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), tmin);
-        const float t1 = fminf(fminf(fminf(tfx, tfy), tfz), tmax);
-        t[i] = (t0 <= t1 && c[i] != ORX_EMPTY) ? t0 : INFINITY;
+    for (int h = 0; h < 2; h++) {
+        const v2q tnx = __builtin_elementwise_fma(q2(nxq, 2 * h), bx2, ax2);
+        const v2q tfx = __builtin_elementwise_fma(q2(fxq, 2 * h), bx2, ax2);
+        const v2q tny = __builtin_elementwise_fma(q2(nyq, 2 * h), by2, ay2);
+        const v2q tfy = __builtin_elementwise_fma(q2(fyq, 2 * h), by2, ay2);
+        const v2q tnz = __builtin_elementwise_fma(q2(nzq, 2 * h), bz2, az2);
+        const v2q tfz = __builtin_elementwise_fma(q2(fzq, 2 * h), bz2, az2);
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const int i = 2 * h + e;
+            const float t0 = fmaxf(fmaxf(fmaxf(tnx[e], tny[e]), tnz[e]), tmin);
+            const float t1 = fminf(fminf(fminf(tfx[e], tfy[e]), tfz[e]), tmax);
+            t[i] = (t0 <= t1 && c[i] != ORX_EMPTY) ? t0 : INFINITY;
+        }
     }
 }
 typedef float v2t __attribute__((ext_vector_type(2)));
