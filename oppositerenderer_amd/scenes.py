@@ -433,6 +433,9 @@ def scene_by_name(name: str) -> Scene:
     }
     if name in table:
         return table[name]()
+    if name.lower().endswith((".obj", ".dae")):  # SceneFactory: any other name is a scene file
+        from .sceneio import load_scene
+        return load_scene(name)
     if name == "TexturedRoom":
         from .synthetic import textured_room
         return textured_room()
