@@ -409,8 +409,15 @@ extern "C" {
 /* stats build only: [closest: rays, nodes, leaves, tris, any: rays, nodes, leaves, tris]; reset = 1 zeroes */
 int orx_trav_stats_read(orx_renderer* r, unsigned long long* out, int reset) {
     if (!r || !r->scene.trav_stats || hipDeviceSynchronize() != hipSuccess) return 1;
-    if (hipMemcpy(out, r->scene.trav_stats, 128, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+    if (hipMemcpy(out, r->scene.trav_stats, 96, hipMemcpyDeviceToHost) != hipSuccess) return 1;
     if (reset && hipMemset(r->scene.trav_stats, 0, 128) != hipSuccess) return 1;
+    /* [12..15]: gather lane batches, wave batches, lane rows, wave rows */
+    if (r->pb.grid) {
+        if (hipMemcpy(out + 12, &r->pb.grid->st_lane_batches, 32, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+        if (reset && hipMemset(&r->pb.grid->st_lane_batches, 0, 32) != hipSuccess) return 1;
+    } else {
+        for (int k = 12; k < 16; k++) out[k] = 0;
+    }
     return 0;
 }
 #endif

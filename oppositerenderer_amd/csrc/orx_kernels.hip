@@ -938,6 +938,7 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
     const uint32_t j = blockIdx.y * 16 + (w >> 1) * 8 + (l >> 3);
     const GridParams g = *pb.grid;
     uint32_t dC = 0, dP = 0;
+    ORX_TS_DECL;
     if (x < gi.W && j < gi.segments * gi.seg_rows) {
         const size_t i = (size_t)j * gi.W + x;
         const HpRef hr = hp_ref(gi, j, x);
@@ -1008,7 +1009,11 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
                         if (cxh < 0 || xl > xh) continue;
                         const uint32_t off = pb.offsets[xl + row];
                         const uint32_t offTo = pb.offsets[xh + row + 1];
+                        ORX_TS_INC(ts_leaves, 1);
+                        ORX_TS_WAVE(ts_wl);
                         for (uint32_t kb = off & ~3u; kb < offTo; kb += 4) {
+                            ORX_TS_INC(ts_nodes, 1);
+                            ORX_TS_WAVE(ts_wn);
                             const float4 X = *(const float4*)(SX + kb);
                             const float4 Y = *(const float4*)(SX + P + kb);
                             const float4 Z = *(const float4*)(SX + 2 * P + kb);
@@ -1078,6 +1083,12 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
             gi.dbg[2 * i + 1] = dP;
         }
     }
+#ifdef ORX_TRAV_STATS
+    atomicAdd((unsigned long long*)&pb.grid->st_lane_batches, (unsigned long long)ts_nodes);
+    atomicAdd((unsigned long long*)&pb.grid->st_wave_batches, (unsigned long long)ts_wn);
+    atomicAdd((unsigned long long*)&pb.grid->st_lane_rows, (unsigned long long)ts_leaves);
+    atomicAdd((unsigned long long*)&pb.grid->st_wave_rows, (unsigned long long)ts_wl);
+#endif
     const uint64_t sp = wave_sum_u64(dP), sc = wave_sum_u64(dC);
     if ((threadIdx.x & 63) == 0 && sp) {
         atomicAdd((unsigned long long*)&pb.grid->photons_visited, (unsigned long long)sp);

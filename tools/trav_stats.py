@@ -35,4 +35,8 @@ for it in range(3):
         print(f"it{it} {name:8s} rays {v[b]:12d}  nodes/ray {v[b + 1] / rays:6.2f}  leaves/ray {v[b + 2] / rays:6.2f}"
               f"  tris/ray {v[b + 3] / rays:6.2f}  SIMT node {v[b + 1] / max(1, 64 * wn):5.3f}"
               f"  leaf {v[b + 2] / max(1, 64 * wl):5.3f}")
+    if method == 2:
+        lb, wb, lr, wr = v[12:16]
+        print(f"it{it} gather   batches/px {lb / (W * H):8.1f}  SIMT batch {lb / max(1, 64 * wb):5.3f}"
+              f"  rows/px {lr / (W * H):6.1f}  SIMT row {lr / max(1, 64 * wr):5.3f}")
 print("bvh stack entries", r.stats().bvh_stack_entries)
