@@ -369,6 +369,7 @@ struct orx_renderer {
     DevBuf d_slots, d_vmask, d_sorted, d_perm, d_keys, d_ranks;
     DevBuf d_hist, d_offsets, d_bbox, d_partials, d_grid, d_work;
     DevBuf d_wray0, d_wray1, d_whit, d_wpath, d_wseg; /* wavefront photon pass queues */
+    DevBuf d_pos4, d_bstable, d_bspartials, d_bspairs;  /* bucket-sort grid build */
     PixelBufs px{};
     PhotonBufs pb{};
     /* timing: event pairs per pass since the last orx_reset_timing */
@@ -762,6 +763,16 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_wray1.ensure(nphot * 32 + 32));
     HIPCHK(r, r->d_whit.ensure(nphot * 32 + 32));
     HIPCHK(r, r->d_wpath.ensure(nphot * 32 + 32));
+    /* bucket-sort grid build: at most 1024 buckets of 2^bshift cells */
+    uint32_t bshift = 10;
+    while ((((size_t)r->cfg.photon_grid_max_size + (1u << bshift) - 1) >> bshift) > 1024) bshift++;
+    const size_t bs_nchunk = (S + 16383) / 16384;
+    const size_t bs_nbmax = ((size_t)r->cfg.photon_grid_max_size + (1u << bshift) - 1) >> bshift;
+    const size_t bs_nscan = (bs_nbmax * bs_nchunk + 1023) / 1024;
+    HIPCHK(r, r->d_pos4.ensure(S * 16 + 16));
+    HIPCHK(r, r->d_bstable.ensure(bs_nbmax * bs_nchunk * 4 + 16));
+    HIPCHK(r, r->d_bspartials.ensure((bs_nscan + 2) * 4));
+    HIPCHK(r, r->d_bspairs.ensure(S * 8 + 16));
     const size_t wnseg = (nphot + 511) / 512 + 1;
     HIPCHK(r, r->d_wseg.ensure(2 * wnseg * 4));
     HIPCHK(r, hipMemsetAsync(r->d_wseg.p, 0, 2 * wnseg * 4, r->stream));
@@ -814,6 +825,12 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     pb.wray[1] = r->d_wray1.as<float4>();
     pb.whit = r->d_whit.as<float4>();
     pb.wpath = r->d_wpath.as<float4>();
+    pb.pos4 = r->d_pos4.as<float4>();
+    pb.bshift = bshift;
+    pb.bs_nchunk = (uint32_t)bs_nchunk;
+    pb.bs_table = r->d_bstable.as<uint32_t>();
+    pb.bs_partials = r->d_bspartials.as<uint32_t>();
+    pb.bs_pairs = r->d_bspairs.as<uint2>();
     pb.wseg = r->d_wseg.as<uint32_t>();
     pb.wnseg = (uint32_t)wnseg;
 
@@ -911,15 +928,24 @@ static void ppm_photons_grid(orx_renderer* r, const Consts& c) {
     if (wavefront) launch_ppm_photon_wavefront(st, r->scene, r->px, r->pb, c);
     else launch_ppm_photon(st, r->scene, r->px, r->pb, c);
     ev_end(r, P_PHOTON);
+    /* grid build: the atomic-free bucket sort (default) or the atomic-rank
+     * counting sort (ORX_GRID_ATOMIC=1, kept for A/B) */
+    static const int atomic_grid = [] {
+        const char* e = getenv("ORX_GRID_ATOMIC");
+        return e ? atoi(e) : 0;
+    }();
     ev_begin(r, P_SETUP_HASH);
     launch_grid_setup(st, r->pb);
-    launch_grid_hash(st, r->pb);
+    if (atomic_grid) launch_grid_hash(st, r->pb);
+    else launch_grid_bucket_count(st, r->pb);
     ev_end(r, P_SETUP_HASH);
     ev_begin(r, P_SCAN);
-    launch_grid_scan(st, r->pb);
+    if (atomic_grid) launch_grid_scan(st, r->pb);
+    else launch_grid_bucket_scan(st, r->pb);
     ev_end(r, P_SCAN);
     ev_begin(r, P_SCATTER);
-    launch_grid_scatter(st, r->pb);
+    if (atomic_grid) launch_grid_scatter(st, r->pb);
+    else launch_grid_bucket_place(st, r->pb);
     ev_end(r, P_SCATTER);
 }
 static void ppm_local_passes(orx_renderer* r, const DevCamera& cam, const Consts& c) {

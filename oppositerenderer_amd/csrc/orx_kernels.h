@@ -78,6 +78,12 @@ struct PhotonBufs {
     float4* wray[2];    /* ping-pong ray queues [n][2]: o.xyz|tmin, d.xyz|photon index */
     float4* whit;       /* [n][2]: t|prim|slot|b (sphere: sn.x), g|sn.y|sn.z|- */
     float4* wpath;      /* [P][2]: power.xyz|weight, depth|numStored|mask|- */
+    float4* pos4;       /* [S] deposit positions (compact copy of the records' first float4) */
+    uint32_t bshift;    /* bucket sort: cells per bucket = 1 << bshift, at most BS_MAXB buckets */
+    uint32_t bs_nchunk; /* slot chunks (ceil(S / BS_CHUNK)) */
+    uint32_t* bs_table; /* [buckets][chunks] counts, then exclusive offsets */
+    uint32_t* bs_partials; /* scan partials + grand total */
+    uint2* bs_pairs;    /* [S] (key, slot) in bucket order */
     uint32_t* wseg;     /* [2][wnseg] live entries of each queue segment */
     uint32_t wnseg;     /* segments per queue */
 };
@@ -103,6 +109,11 @@ void launch_grid_setup(hipStream_t s, const PhotonBufs& pb);
 void launch_grid_hash(hipStream_t s, const PhotonBufs& pb);
 void launch_grid_scan(hipStream_t s, const PhotonBufs& pb);
 void launch_grid_scatter(hipStream_t s, const PhotonBufs& pb);
+/* atomic-free grid build: keys + bucket histogram / scan of the table /
+ * bucket placement + per-bucket cells (offsets, permutation) + permute */
+void launch_grid_bucket_count(hipStream_t s, const PhotonBufs& pb);
+void launch_grid_bucket_scan(hipStream_t s, const PhotonBufs& pb);
+void launch_grid_bucket_place(hipStream_t s, const PhotonBufs& pb);
 /* gathers `rows` pixel rows whose hitpoints are in hp{A,B,C} against the
  * local photon grid; writes indirect (and debug counters) */
 /* Hitpoints to gather: `segments` segments of seg_rows x W pixels, each in the

@@ -239,6 +239,7 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
                         const uint32_t si = P.p_local * pb.D + P.numStored;
                         float4* rec = pb.slots + 4 * (size_t)si;
                         rec[0] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, P.power.x);
+                        pb.pos4[si] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, 0.f);
                         rec[1] = make_float4(P.d.x, P.d.y, P.d.z, P.power.y);
                         rec[2].x = P.power.z;
                         if (fmax3(P.power) > 0) {
@@ -496,6 +497,7 @@ __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, PixelBufs px, Phot
                         const uint32_t si = P.p_local * pb.D + P.numStored;
                         float4* rec = pb.slots + 4 * (size_t)si;
                         rec[0] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, P.power.x);
+                        pb.pos4[si] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, 0.f);
                         rec[1] = make_float4(P.d.x, P.d.y, P.d.z, P.power.y);
                         rec[2].x = P.power.z;
                         if (fmax3(P.power) > 0) {
@@ -890,6 +892,193 @@ __global__ __launch_bounds__(256) void k_grid_permute(PhotonBufs pb) {
         }
     }
 }
+/* ------------------------------------------------------------------ */
+/* photon grid without global atomics: two-level bucket counting sort  */
+/* ------------------------------------------------------------------ */
+/* The atomic-rank counting sort above issues one device-scope atomic per
+ * photon into a 4 MB histogram; across 8 XCDs those resolve at the memory
+ * side (~25 G/s measured), which makes the hash pass the slowest of the grid
+ * build.  Here:
+ *   A  k_bs_count    per chunk of BS_CHUNK slots: keys, LDS histogram of the
+ *                    coarse bucket key >> bshift -> table[bucket][chunk]
+ *   S  scan of the table (bucket-major) -> where each chunk's bucket run starts
+ *   B  k_bs_place    per chunk: LDS cursors from the table, (key, slot) pairs
+ *                    appended to their bucket run
+ *   C  k_bs_cells    one block per bucket: LDS histogram of its cells, LDS
+ *                    scan -> offsets of those cells, permutation by LDS cursors
+ * All counting is in LDS.  Offsets equal the reference's exclusive scan over
+ * the cell histogram (keys >= G are the reference's overflow cell G and, as
+ * there, fall beyond offsets[G] = valid: they are dropped). */
+constexpr uint32_t BS_CHUNK = 16384;
+constexpr uint32_t BS_THREADS = 512;
+constexpr uint32_t BS_MAXB = 1024; /* buckets */
+
+__global__ __launch_bounds__(BS_THREADS) void k_bs_count(PhotonBufs pb) {
+    __shared__ uint32_t hist[BS_MAXB];
+    const GridParams g = *pb.grid;
+    const uint32_t nb = (g.G + (1u << pb.bshift) - 1) >> pb.bshift;
+    for (uint32_t i = threadIdx.x; i < BS_MAXB; i += BS_THREADS) hist[i] = 0;
+    __syncthreads();
+    const float inv = 1.f / g.cell;
+    const uint32_t c0 = blockIdx.x * BS_CHUNK;
+    for (uint32_t k = threadIdx.x; k < BS_CHUNK; k += BS_THREADS) {
+        const uint32_t s = c0 + k;
+        if (s >= pb.S) break;
+        uint32_t key = 0xffffffffu;
+        const uint32_t p = s / pb.D, d = s - p * pb.D;
+        if (g.G && ((pb.vmask[p] >> d) & 1u)) {
+            const float4 a = pb.pos4[s];
+            const f3 pp = (mk(a.x, a.y, a.z) - mk(g.ox, g.oy, g.oz)) * inv;
+            const uint32_t cx = orx_f2u_sat(orx_floorf(pp.x));
+            const uint32_t cy = orx_f2u_sat(orx_floorf(pp.y));
+            const uint32_t cz = orx_f2u_sat(orx_floorf(pp.z));
+            const uint32_t kk = cx + cy * g.gx + cz * g.gx * g.gy;
+            if (kk < g.G) { /* calculateHashCellsKernel clamps to G: the overflow cell, beyond valid */
+                key = kk;
+                atomicAdd(&hist[kk >> pb.bshift], 1u);
+            }
+        }
+        pb.keys[s] = key;
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += BS_THREADS) pb.bs_table[(size_t)b * pb.bs_nchunk + blockIdx.x] = hist[b];
+}
+
+/* exclusive scan of n = nb * nchunk table entries in place (three kernels, as k_scan_*) */
+__global__ __launch_bounds__(256) void k_bs_scan_reduce(PhotonBufs pb) {
+    const uint32_t nb = (pb.grid->G + (1u << pb.bshift) - 1) >> pb.bshift;
+    const uint32_t n = nb * pb.bs_nchunk;
+    const uint32_t base = blockIdx.x * SCAN_BLOCK + threadIdx.x * 4;
+    uint32_t sum = 0;
+    for (int k = 0; k < 4; k++)
+        if (base + k < n) sum += pb.bs_table[base + k];
+    uint32_t total;
+    (void)block_exclusive_scan_256(sum, &total);
+    if (threadIdx.x == 0) pb.bs_partials[blockIdx.x] = total;
+}
+__global__ __launch_bounds__(256) void k_bs_scan_partials(PhotonBufs pb, uint32_t nblocks) {
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nblocks; base += 256) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < nblocks ? pb.bs_partials[i] : 0;
+        uint32_t total;
+        const uint32_t ex = block_exclusive_scan_256(v, &total);
+        if (i < nblocks) pb.bs_partials[i] = carry + ex;
+        carry += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) pb.bs_partials[nblocks] = carry; /* grand total = valid photons */
+}
+__global__ __launch_bounds__(256) void k_bs_scan_apply(PhotonBufs pb) {
+    const uint32_t nb = (pb.grid->G + (1u << pb.bshift) - 1) >> pb.bshift;
+    const uint32_t n = nb * pb.bs_nchunk;
+    if (blockIdx.x * SCAN_BLOCK >= n) return;
+    const uint32_t base = blockIdx.x * SCAN_BLOCK + threadIdx.x * 4;
+    uint32_t v[4], sum = 0;
+    for (int k = 0; k < 4; k++) {
+        v[k] = base + k < n ? pb.bs_table[base + k] : 0;
+        sum += v[k];
+    }
+    uint32_t total;
+    uint32_t ex = block_exclusive_scan_256(sum, &total) + pb.bs_partials[blockIdx.x];
+    for (int k = 0; k < 4; k++) {
+        if (base + k < n) pb.bs_table[base + k] = ex;
+        ex += v[k];
+    }
+}
+
+__global__ __launch_bounds__(BS_THREADS) void k_bs_place(PhotonBufs pb) {
+    __shared__ uint32_t cur[BS_MAXB];
+    const uint32_t G = pb.grid->G;
+    const uint32_t nb = (G + (1u << pb.bshift) - 1) >> pb.bshift;
+    for (uint32_t b = threadIdx.x; b < nb; b += BS_THREADS) cur[b] = pb.bs_table[(size_t)b * pb.bs_nchunk + blockIdx.x];
+    __syncthreads();
+    const uint32_t c0 = blockIdx.x * BS_CHUNK;
+    for (uint32_t k = threadIdx.x; k < BS_CHUNK; k += BS_THREADS) {
+        const uint32_t s = c0 + k;
+        if (s >= pb.S) break;
+        const uint32_t key = pb.keys[s];
+        if (key != 0xffffffffu) {
+            const uint32_t pos = atomicAdd(&cur[key >> pb.bshift], 1u);
+            pb.bs_pairs[pos] = make_uint2(key, s);
+        }
+    }
+}
+
+/* one block per bucket: cell histogram, offsets, permutation */
+__global__ __launch_bounds__(1024) void k_bs_cells(PhotonBufs pb, uint32_t cb, uint32_t nscan) {
+    extern __shared__ uint32_t lds[]; /* [cb] histogram / cursors */
+    const uint32_t G = pb.grid->G;
+    const uint32_t nb = (G + cb - 1) / cb;
+    const uint32_t b = blockIdx.x;
+    const uint32_t total = pb.bs_partials[nscan]; /* grand total written by k_bs_scan_partials */
+    if (b > nb) return;
+    /* bucket nb (one past the last) only writes offsets[G] = valid when G is a multiple of cb */
+    const uint32_t start = b < nb ? pb.bs_table[(size_t)b * pb.bs_nchunk] : total;
+    const uint32_t end = b + 1 < nb ? pb.bs_table[(size_t)(b + 1) * pb.bs_nchunk] : total;
+    for (uint32_t i = threadIdx.x; i < cb; i += blockDim.x) lds[i] = 0;
+    __syncthreads();
+    for (uint32_t i = start + threadIdx.x; i < end; i += blockDim.x) atomicAdd(&lds[pb.bs_pairs[i].x - b * cb], 1u);
+    __syncthreads();
+    /* exclusive scan of lds[0..cb) by 1024 threads, cb/1024 entries each */
+    __shared__ uint32_t wsum[16];
+    const uint32_t per = cb / blockDim.x;
+    const uint32_t t0 = threadIdx.x * per;
+    uint32_t run = 0;
+    for (uint32_t k = 0; k < per; k++) run += lds[t0 + k];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = run;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (uint32_t q = 0; q < w; q++) pre += wsum[q];
+    uint32_t ex = start + pre + x - run;
+    for (uint32_t k = 0; k < per; k++) {
+        const uint32_t c = b * cb + t0 + k;
+        const uint32_t v = lds[t0 + k];
+        if (c <= G) pb.offsets[c] = ex;
+        lds[t0 + k] = ex; /* becomes the cell's cursor */
+        ex += v;
+    }
+    if (threadIdx.x == 0 && b == 0) {
+        pb.grid->valid = total;
+        pb.grid->valid_total += total;
+    }
+    __syncthreads();
+    for (uint32_t i = start + threadIdx.x; i < end; i += blockDim.x) {
+        const uint2 kp = pb.bs_pairs[i];
+        const uint32_t pos = atomicAdd(&lds[kp.x - b * cb], 1u);
+        pb.perm[pos] = kp.y;
+    }
+}
+
+static uint32_t bs_nscan(const PhotonBufs& pb) {
+    const uint32_t nbmax = (pb.gmax + (1u << pb.bshift) - 1) >> pb.bshift;
+    return (nbmax * pb.bs_nchunk + SCAN_BLOCK - 1) / SCAN_BLOCK;
+}
+void launch_grid_bucket_count(hipStream_t s, const PhotonBufs& pb) {
+    hipLaunchKernelGGL(k_bs_count, dim3(pb.bs_nchunk), dim3(BS_THREADS), 0, s, pb);
+}
+void launch_grid_bucket_scan(hipStream_t s, const PhotonBufs& pb) {
+    const uint32_t nscan = bs_nscan(pb);
+    hipLaunchKernelGGL(k_bs_scan_reduce, dim3(nscan), dim3(256), 0, s, pb);
+    hipLaunchKernelGGL(k_bs_scan_partials, dim3(1), dim3(256), 0, s, pb, nscan);
+    hipLaunchKernelGGL(k_bs_scan_apply, dim3(nscan), dim3(256), 0, s, pb);
+}
+void launch_grid_bucket_place(hipStream_t s, const PhotonBufs& pb) {
+    hipLaunchKernelGGL(k_bs_place, dim3(pb.bs_nchunk), dim3(BS_THREADS), 0, s, pb);
+    const uint32_t cb = 1u << pb.bshift;
+    const uint32_t nbmax = (pb.gmax + cb - 1) / cb;
+    hipLaunchKernelGGL(k_bs_cells, dim3(nbmax + 1), dim3(1024), cb * 4, s, pb, cb, bs_nscan(pb));
+    unsigned blocks = (pb.S + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_grid_permute, dim3(blocks), dim3(256), 0, s, pb);
+}
+
 void launch_grid_scatter(hipStream_t s, const PhotonBufs& pb) {
     unsigned blocks = (pb.S + 255) / 256;
     if (blocks > 8192) blocks = 8192;
