@@ -20,9 +20,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 KERNELS_OF_PASS = {
     "ppm_eye": ["k_ppm_eye"],
     "ppm_photon": ["k_ppm_photon"],
-    "grid_hash": ["k_grid_setup", "k_grid_hash"],
-    "grid_scan": ["k_scan_reduce", "k_scan_partials", "k_scan_apply"],
-    "grid_scatter": ["k_grid_scatter", "k_grid_permute"],
+    # default bucket-sort grid build; the atomic path (ORX_GRID_ATOMIC=1) is
+    # k_grid_hash / k_scan_* / k_grid_scatter with the same pass split
+    "grid_hash": ["k_grid_setup", "k_bs_count"],
+    "grid_scan": ["k_bs_scan_reduce", "k_bs_scan_partials", "k_bs_scan_apply"],
+    "grid_scatter": ["k_bs_place", "k_bs_cells", "k_grid_permute"],
     "ppm_gather": ["k_ppm_gather", "k_ppm_gather_coop"],
     "ppm_direct_output": ["k_ppm_direct_output"],
     "pt": ["k_pt"],
@@ -41,25 +43,30 @@ def paths_per_iteration(method: int, W: int, H: int, photons: int) -> int:
 
 
 def pass_bytes(method: int, W: int, H: int, photons: int, valid: float = 0.0, cells: int = 0,
-               light_vertices: float = 0.0) -> dict:
+               light_vertices: float = 0.0, deposits_max: int = 4, grid_max: int = 1000000) -> dict:
     """Bytes per launch of each pass.
 
     valid: grid-resident photons (deposits with power > 0); cells: grid cells G;
-    light_vertices: stored VCM light vertices per iteration."""
+    light_vertices: stored VCM light vertices per iteration; deposits_max: D
+    slots per emitted photon; grid_max: PHOTON_GRID_MAX_SIZE (bucket table size)."""
     N = W * H
+    slots = photons * deposits_max
+    table = ((cells + 1023) // 1024) * ((slots + 16383) // 16384)
     R2 = 2 * R_RNG
     if method == _abi.PROGRESSIVE_PHOTON_MAPPING:
         return {
             # RNG RMW + one 40 B hitpoint (pos|flags 16, normal-or-radiance|atten.x 16, atten.yz 8)
             "ppm_eye": N * (R2 + 40),
             # RNG RMW + 1 B deposit mask per emitted photon + 36 B per stored deposit
-            "ppm_photon": photons * (R2 + 1) + valid * 36,
-            # mask per emitted photon, position 12 B read, key + rank 8 B written, histogram 4 B per photon
-            "grid_hash": photons * 1 + valid * (12 + 8 + 4),
-            # histogram read + zeroed, offsets written
-            "grid_scan": (cells + 2) * 12,
-            # key + rank read, offset read, permutation written + read, photon 36 B read + written
-            "grid_scatter": valid * (8 + 4 + 4 + 4 + 36 + 36),
+            # + its 12 B compact position copy (the grid build's key input)
+            "ppm_photon": photons * (R2 + 1) + valid * (36 + 12),
+            # mask per emitted photon, position 12 B per deposit, key 4 B per slot
+            "grid_hash": photons * 1 + valid * 12 + slots * 4,
+            # bucket x chunk table read + written (counts -> offsets)
+            "grid_scan": table * 8,
+            # keys read, (key, slot) pairs written + read twice, permutation written + read,
+            # offsets written, photon 36 B read + written
+            "grid_scatter": slots * 4 + valid * (8 + 16 + 4 + 4 + 36 + 36) + (cells + 1) * 4,
             # hitpoint 40 B + indirect 12 B per pixel, each grid photon once, offset table once
             "ppm_gather": N * (40 + 12) + valid * 36 + (cells + 1) * 4,
             # hitpoint, RNG RMW, indirect read, direct written, output read + written
