@@ -411,11 +411,13 @@ extern "C" {
 int orx_trav_stats_read(orx_renderer* r, unsigned long long* out, int reset) {
     if (!r || !r->scene.trav_stats || hipDeviceSynchronize() != hipSuccess) return 1;
     if (hipMemcpy(out, r->scene.trav_stats, 96, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+    /* [16]: gather photons accepted (out must hold 17 values) */
+    if (r->pb.grid && hipMemcpy(out + 16, &r->pb.grid->st_accepted, 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
     if (reset && hipMemset(r->scene.trav_stats, 0, 128) != hipSuccess) return 1;
     /* [12..15]: gather lane batches, wave batches, lane rows, wave rows */
     if (r->pb.grid) {
         if (hipMemcpy(out + 12, &r->pb.grid->st_lane_batches, 32, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-        if (reset && hipMemset(&r->pb.grid->st_lane_batches, 0, 32) != hipSuccess) return 1;
+        if (reset && hipMemset(&r->pb.grid->st_lane_batches, 0, 40) != hipSuccess) return 1;
     } else {
         for (int k = 12; k < 16; k++) out[k] = 0;
     }

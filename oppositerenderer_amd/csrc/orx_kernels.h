@@ -29,6 +29,7 @@ struct GridParams {
     uint64_t valid_total;
     uint64_t union_photons_total; /* coop gather: photons staged per wave, summed */
     uint64_t st_lane_batches, st_wave_batches, st_lane_rows, st_wave_rows; /* ORX_TRAV_STATS builds: gather SIMT */
+    uint64_t st_accepted;   /* ORX_TRAV_STATS builds: gather photons within r and facing the normal */
 };
 
 /* Per-frame pixel state. Pixel (x,y) of rank r is stored at local row

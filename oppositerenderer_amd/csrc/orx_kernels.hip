@@ -1242,6 +1242,7 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
                             q0 = __builtin_elementwise_fma(q0, x0, wc2); q1 = __builtin_elementwise_fma(q1, x1, wc2);
                             q0 = __builtin_elementwise_fma(q0, x0, wc1); q1 = __builtin_elementwise_fma(q1, x1, wc1);
                             v2f w0 = __builtin_elementwise_fma(q0, x0, wc0), w1 = __builtin_elementwise_fma(q1, x1, wc0);
+                            ORX_TS_INC(ts_tris, (uint32_t)in0 + (uint32_t)in1 + (uint32_t)in2 + (uint32_t)in3);
                             w0.x = in0 ? w0.x : 0.f;
                             w0.y = in1 ? w0.y : 0.f;
                             w1.x = in2 ? w1.x : 0.f;
@@ -1277,6 +1278,7 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
     atomicAdd((unsigned long long*)&pb.grid->st_wave_batches, (unsigned long long)ts_wn);
     atomicAdd((unsigned long long*)&pb.grid->st_lane_rows, (unsigned long long)ts_leaves);
     atomicAdd((unsigned long long*)&pb.grid->st_wave_rows, (unsigned long long)ts_wl);
+    atomicAdd((unsigned long long*)&pb.grid->st_accepted, (unsigned long long)ts_tris);
 #endif
     const uint64_t sp = wave_sum_u64(dP), sc = wave_sum_u64(dC);
     if ((threadIdx.x & 63) == 0 && sp) {

@@ -22,7 +22,7 @@ r = renderer.OptixRenderer(_abi.default_config(seed=1645301512, photon_launch_wi
 r.initialize(0)
 r.initScene(sc)
 det = renderer.RenderRequestDetails(sc.default_camera.set_aspect_ratio(W / H), sc.name, method, W, H)
-buf = (C.c_ulonglong * 16)()
+buf = (C.c_ulonglong * 17)()
 radius = sc.initial_ppm_radius()
 for it in range(3):
     r.renderNextIteration(it, it, radius, False, det)
@@ -38,5 +38,6 @@ for it in range(3):
     if method == 2:
         lb, wb, lr, wr = v[12:16]
         print(f"it{it} gather   batches/px {lb / (W * H):8.1f}  SIMT batch {lb / max(1, 64 * wb):5.3f}"
-              f"  rows/px {lr / (W * H):6.1f}  SIMT row {lr / max(1, 64 * wr):5.3f}")
+              f"  rows/px {lr / (W * H):6.1f}  SIMT row {lr / max(1, 64 * wr):5.3f}"
+              f"  accepted/px {v[16] / (W * H):7.1f} ({v[16] / max(1, 4 * lb):5.3f} of slots)")
 print("bvh stack entries", r.stats().bvh_stack_entries)
