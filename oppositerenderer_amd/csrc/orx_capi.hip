@@ -369,7 +369,7 @@ struct orx_renderer {
     DevBuf d_slots, d_vmask, d_sorted, d_perm, d_keys, d_ranks;
     DevBuf d_hist, d_offsets, d_bbox, d_partials, d_grid, d_work;
     DevBuf d_wray0, d_wray1, d_whit, d_wpath, d_wseg; /* wavefront photon pass queues */
-    DevBuf d_pos4, d_bstable, d_bspartials, d_bspairs;  /* bucket-sort grid build */
+    DevBuf d_pos4, d_bstable, d_bspartials, d_bspairs, d_subofs;  /* bucket-sort grid build */
     PixelBufs px{};
     PhotonBufs pb{};
     /* timing: event pairs per pass since the last orx_reset_timing */
@@ -775,6 +775,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_bstable.ensure(bs_nbmax * bs_nchunk * 4 + 16));
     HIPCHK(r, r->d_bspartials.ensure((bs_nscan + 2) * 4));
     HIPCHK(r, r->d_bspairs.ensure(S * 8 + 16));
+    HIPCHK(r, r->d_subofs.ensure(G2 * 16 + 16));
     const size_t wnseg = (nphot + 511) / 512 + 1;
     HIPCHK(r, r->d_wseg.ensure(2 * wnseg * 4));
     HIPCHK(r, hipMemsetAsync(r->d_wseg.p, 0, 2 * wnseg * 4, r->stream));
@@ -833,6 +834,13 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     pb.bs_table = r->d_bstable.as<uint32_t>();
     pb.bs_partials = r->d_bspartials.as<uint32_t>();
     pb.bs_pairs = r->d_bspairs.as<uint2>();
+    {
+        static const int atomic_grid_env = [] {
+            const char* e = getenv("ORX_GRID_ATOMIC");
+            return e ? atoi(e) : 0;
+        }();
+        pb.subofs = atomic_grid_env ? nullptr : r->d_subofs.as<uint32_t>();
+    }
     pb.wseg = r->d_wseg.as<uint32_t>();
     pb.wnseg = (uint32_t)wnseg;
 

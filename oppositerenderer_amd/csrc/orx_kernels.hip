@@ -934,7 +934,11 @@ __global__ __launch_bounds__(BS_THREADS) void k_bs_count(PhotonBufs pb) {
             const uint32_t cz = orx_f2u_sat(orx_floorf(pp.z));
             const uint32_t kk = cx + cy * g.gx + cz * g.gx * g.gy;
             if (kk < g.G) { /* calculateHashCellsKernel clamps to G: the overflow cell, beyond valid */
-                key = kk;
+                /* sub-cell key: the x quarter of the cell, so that the gather can
+                 * trim a row to the chord at quarter-cell granularity */
+                int32_t q = (int32_t)orx_floorf(pp.x * 4.f) - 4 * (int32_t)cx;
+                q = q < 0 ? 0 : (q > 3 ? 3 : q);
+                key = kk * 4u + (uint32_t)q;
                 atomicAdd(&hist[kk >> pb.bshift], 1u);
             }
         }
@@ -999,15 +1003,17 @@ __global__ __launch_bounds__(BS_THREADS) void k_bs_place(PhotonBufs pb) {
         if (s >= pb.S) break;
         const uint32_t key = pb.keys[s];
         if (key != 0xffffffffu) {
-            const uint32_t pos = atomicAdd(&cur[key >> pb.bshift], 1u);
+            const uint32_t pos = atomicAdd(&cur[(key >> 2) >> pb.bshift], 1u);
             pb.bs_pairs[pos] = make_uint2(key, s);
         }
     }
 }
 
-/* one block per bucket: cell histogram, offsets, permutation */
+/* one block per bucket: histogram of its sub-cells (cell x quarter), LDS
+ * scan -> cell offsets (the reference's) and sub-cell offsets (the gather's
+ * chord trimming), permutation by LDS cursors */
 __global__ __launch_bounds__(1024) void k_bs_cells(PhotonBufs pb, uint32_t cb, uint32_t nscan) {
-    extern __shared__ uint32_t lds[]; /* [cb] histogram / cursors */
+    extern __shared__ uint32_t lds[]; /* [4 * cb] histogram / cursors */
     const uint32_t G = pb.grid->G;
     const uint32_t nb = (G + cb - 1) / cb;
     const uint32_t b = blockIdx.x;
@@ -1016,13 +1022,14 @@ __global__ __launch_bounds__(1024) void k_bs_cells(PhotonBufs pb, uint32_t cb, u
     /* bucket nb (one past the last) only writes offsets[G] = valid when G is a multiple of cb */
     const uint32_t start = b < nb ? pb.bs_table[(size_t)b * pb.bs_nchunk] : total;
     const uint32_t end = b + 1 < nb ? pb.bs_table[(size_t)(b + 1) * pb.bs_nchunk] : total;
-    for (uint32_t i = threadIdx.x; i < cb; i += blockDim.x) lds[i] = 0;
+    const uint32_t nf = 4 * cb, f0 = b * nf;
+    for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) lds[i] = 0;
     __syncthreads();
-    for (uint32_t i = start + threadIdx.x; i < end; i += blockDim.x) atomicAdd(&lds[pb.bs_pairs[i].x - b * cb], 1u);
+    for (uint32_t i = start + threadIdx.x; i < end; i += blockDim.x) atomicAdd(&lds[pb.bs_pairs[i].x - f0], 1u);
     __syncthreads();
-    /* exclusive scan of lds[0..cb) by 1024 threads, cb/1024 entries each */
+    /* exclusive scan of lds[0..nf) by 1024 threads, nf/1024 entries each */
     __shared__ uint32_t wsum[16];
-    const uint32_t per = cb / blockDim.x;
+    const uint32_t per = nf / blockDim.x;
     const uint32_t t0 = threadIdx.x * per;
     uint32_t run = 0;
     for (uint32_t k = 0; k < per; k++) run += lds[t0 + k];
@@ -1038,10 +1045,13 @@ __global__ __launch_bounds__(1024) void k_bs_cells(PhotonBufs pb, uint32_t cb, u
     for (uint32_t q = 0; q < w; q++) pre += wsum[q];
     uint32_t ex = start + pre + x - run;
     for (uint32_t k = 0; k < per; k++) {
-        const uint32_t c = b * cb + t0 + k;
+        const uint32_t f = f0 + t0 + k, c = f >> 2;
         const uint32_t v = lds[t0 + k];
-        if (c <= G) pb.offsets[c] = ex;
-        lds[t0 + k] = ex; /* becomes the cell's cursor */
+        if (c <= G) {
+            if ((f & 3u) == 0) pb.offsets[c] = ex;
+            if (c < G || (f & 3u) == 0) pb.subofs[f] = ex;
+        }
+        lds[t0 + k] = ex; /* becomes the sub-cell's cursor */
         ex += v;
     }
     if (threadIdx.x == 0 && b == 0) {
@@ -1051,7 +1061,7 @@ __global__ __launch_bounds__(1024) void k_bs_cells(PhotonBufs pb, uint32_t cb, u
     __syncthreads();
     for (uint32_t i = start + threadIdx.x; i < end; i += blockDim.x) {
         const uint2 kp = pb.bs_pairs[i];
-        const uint32_t pos = atomicAdd(&lds[kp.x - b * cb], 1u);
+        const uint32_t pos = atomicAdd(&lds[kp.x - f0], 1u);
         pb.perm[pos] = kp.y;
     }
 }
@@ -1073,7 +1083,7 @@ void launch_grid_bucket_place(hipStream_t s, const PhotonBufs& pb) {
     hipLaunchKernelGGL(k_bs_place, dim3(pb.bs_nchunk), dim3(BS_THREADS), 0, s, pb);
     const uint32_t cb = 1u << pb.bshift;
     const uint32_t nbmax = (pb.gmax + cb - 1) / cb;
-    hipLaunchKernelGGL(k_bs_cells, dim3(nbmax + 1), dim3(1024), cb * 4, s, pb, cb, bs_nscan(pb));
+    hipLaunchKernelGGL(k_bs_cells, dim3(nbmax + 1), dim3(1024), 4 * cb * 4, s, pb, cb, bs_nscan(pb));
     unsigned blocks = (pb.S + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(k_grid_permute, dim3(blocks), dim3(256), 0, s, pb);
@@ -1196,8 +1206,19 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
                         const uint32_t xl = cxl > (int32_t)x_lo ? (uint32_t)cxl : x_lo;
                         const uint32_t xh = cxh < (int32_t)x_hi ? (uint32_t)cxh : x_hi;
                         if (cxh < 0 || xl > xh) continue;
-                        const uint32_t off = pb.offsets[xl + row];
-                        const uint32_t offTo = pb.offsets[xh + row + 1];
+                        uint32_t off, offTo;
+                        if (pb.subofs) { /* quarter-cell trimming of the chord's end cells */
+                            const int32_t q0 = orx_f2i_sat(orx_floorf((np.x - rx) * invCellSize * 4.f));
+                            const int32_t q1 = orx_f2i_sat(orx_floorf((np.x + rx) * invCellSize * 4.f));
+                            const uint32_t a0 = q0 > (int32_t)(4 * xl) ? (uint32_t)q0 : 4 * xl;
+                            const uint32_t a1 = q1 < (int32_t)(4 * xh + 3) ? (uint32_t)q1 : 4 * xh + 3;
+                            if (q1 < 0 || a0 > a1) continue;
+                            off = pb.subofs[4 * row + a0];
+                            offTo = pb.subofs[4 * row + a1 + 1];
+                        } else {
+                            off = pb.offsets[xl + row];
+                            offTo = pb.offsets[xh + row + 1];
+                        }
                         ORX_TS_INC(ts_leaves, 1);
                         ORX_TS_WAVE(ts_wl);
                         for (uint32_t kb = off & ~3u; kb < offTo; kb += 4) {
