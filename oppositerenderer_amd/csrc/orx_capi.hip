@@ -775,7 +775,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_bstable.ensure(bs_nbmax * bs_nchunk * 4 + 16));
     HIPCHK(r, r->d_bspartials.ensure((bs_nscan + 2) * 4));
     HIPCHK(r, r->d_bspairs.ensure(S * 8 + 16));
-    HIPCHK(r, r->d_subofs.ensure(G2 * 16 + 16));
+    HIPCHK(r, r->d_subofs.ensure(G2 * 4 * SUBX + 16));
     const size_t wnseg = (nphot + 511) / 512 + 1;
     HIPCHK(r, r->d_wseg.ensure(2 * wnseg * 4));
     HIPCHK(r, hipMemsetAsync(r->d_wseg.p, 0, 2 * wnseg * 4, r->stream));

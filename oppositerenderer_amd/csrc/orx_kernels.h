@@ -54,6 +54,7 @@ struct PixelBufs {
 };
 
 constexpr uint32_t BBOX_REPLICAS = 64;
+constexpr uint32_t SUBX = 4; /* sub-cells per grid cell along x (bucket-sort grid, gather chord trimming) */
 
 struct PhotonBufs {
     uint32_t PW, PH;    /* photon launch (full) */
@@ -84,8 +85,8 @@ struct PhotonBufs {
     uint32_t bs_nchunk; /* slot chunks (ceil(S / BS_CHUNK)) */
     uint32_t* bs_table; /* [buckets][chunks] counts, then exclusive offsets */
     uint32_t* bs_partials; /* scan partials + grand total */
-    uint2* bs_pairs;    /* [S] (sub-cell key, slot) in bucket order; sub-cell key = cell * 4 + x quarter */
-    uint32_t* subofs;   /* [4 G + 1] first photon of each sub-cell (NULL: atomic grid path, cell offsets only) */
+    uint2* bs_pairs;    /* [S] (sub-cell key, slot) in bucket order; sub-cell key = cell * SUBX + x slice */
+    uint32_t* subofs;   /* [SUBX G + 1] first photon of each sub-cell (NULL: atomic grid path, cell offsets only) */
     uint32_t* wseg;     /* [2][wnseg] live entries of each queue segment */
     uint32_t wnseg;     /* segments per queue */
 };

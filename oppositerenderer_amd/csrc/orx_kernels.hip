@@ -936,9 +936,9 @@ __global__ __launch_bounds__(BS_THREADS) void k_bs_count(PhotonBufs pb) {
             if (kk < g.G) { /* calculateHashCellsKernel clamps to G: the overflow cell, beyond valid */
                 /* sub-cell key: the x quarter of the cell, so that the gather can
                  * trim a row to the chord at quarter-cell granularity */
-                int32_t q = (int32_t)orx_floorf(pp.x * 4.f) - 4 * (int32_t)cx;
-                q = q < 0 ? 0 : (q > 3 ? 3 : q);
-                key = kk * 4u + (uint32_t)q;
+                int32_t q = (int32_t)orx_floorf(pp.x * (float)SUBX) - (int32_t)SUBX * (int32_t)cx;
+                q = q < 0 ? 0 : (q > (int32_t)SUBX - 1 ? (int32_t)SUBX - 1 : q);
+                key = kk * SUBX + (uint32_t)q;
                 atomicAdd(&hist[kk >> pb.bshift], 1u);
             }
         }
@@ -1003,7 +1003,7 @@ __global__ __launch_bounds__(BS_THREADS) void k_bs_place(PhotonBufs pb) {
         if (s >= pb.S) break;
         const uint32_t key = pb.keys[s];
         if (key != 0xffffffffu) {
-            const uint32_t pos = atomicAdd(&cur[(key >> 2) >> pb.bshift], 1u);
+            const uint32_t pos = atomicAdd(&cur[(key / SUBX) >> pb.bshift], 1u);
             pb.bs_pairs[pos] = make_uint2(key, s);
         }
     }
@@ -1013,7 +1013,7 @@ __global__ __launch_bounds__(BS_THREADS) void k_bs_place(PhotonBufs pb) {
  * scan -> cell offsets (the reference's) and sub-cell offsets (the gather's
  * chord trimming), permutation by LDS cursors */
 __global__ __launch_bounds__(1024) void k_bs_cells(PhotonBufs pb, uint32_t cb, uint32_t nscan) {
-    extern __shared__ uint32_t lds[]; /* [4 * cb] histogram / cursors */
+    extern __shared__ uint32_t lds[]; /* [SUBX * cb] histogram / cursors */
     const uint32_t G = pb.grid->G;
     const uint32_t nb = (G + cb - 1) / cb;
     const uint32_t b = blockIdx.x;
@@ -1022,7 +1022,7 @@ __global__ __launch_bounds__(1024) void k_bs_cells(PhotonBufs pb, uint32_t cb, u
     /* bucket nb (one past the last) only writes offsets[G] = valid when G is a multiple of cb */
     const uint32_t start = b < nb ? pb.bs_table[(size_t)b * pb.bs_nchunk] : total;
     const uint32_t end = b + 1 < nb ? pb.bs_table[(size_t)(b + 1) * pb.bs_nchunk] : total;
-    const uint32_t nf = 4 * cb, f0 = b * nf;
+    const uint32_t nf = SUBX * cb, f0 = b * nf;
     for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) lds[i] = 0;
     __syncthreads();
     for (uint32_t i = start + threadIdx.x; i < end; i += blockDim.x) atomicAdd(&lds[pb.bs_pairs[i].x - f0], 1u);
@@ -1045,11 +1045,11 @@ __global__ __launch_bounds__(1024) void k_bs_cells(PhotonBufs pb, uint32_t cb, u
     for (uint32_t q = 0; q < w; q++) pre += wsum[q];
     uint32_t ex = start + pre + x - run;
     for (uint32_t k = 0; k < per; k++) {
-        const uint32_t f = f0 + t0 + k, c = f >> 2;
+        const uint32_t f = f0 + t0 + k, c = f / SUBX;
         const uint32_t v = lds[t0 + k];
         if (c <= G) {
-            if ((f & 3u) == 0) pb.offsets[c] = ex;
-            if (c < G || (f & 3u) == 0) pb.subofs[f] = ex;
+            if (f % SUBX == 0) pb.offsets[c] = ex;
+            if (c < G || f % SUBX == 0) pb.subofs[f] = ex;
         }
         lds[t0 + k] = ex; /* becomes the sub-cell's cursor */
         ex += v;
@@ -1083,7 +1083,7 @@ void launch_grid_bucket_place(hipStream_t s, const PhotonBufs& pb) {
     hipLaunchKernelGGL(k_bs_place, dim3(pb.bs_nchunk), dim3(BS_THREADS), 0, s, pb);
     const uint32_t cb = 1u << pb.bshift;
     const uint32_t nbmax = (pb.gmax + cb - 1) / cb;
-    hipLaunchKernelGGL(k_bs_cells, dim3(nbmax + 1), dim3(1024), 4 * cb * 4, s, pb, cb, bs_nscan(pb));
+    hipLaunchKernelGGL(k_bs_cells, dim3(nbmax + 1), dim3(1024), SUBX * cb * 4, s, pb, cb, bs_nscan(pb));
     unsigned blocks = (pb.S + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(k_grid_permute, dim3(blocks), dim3(256), 0, s, pb);
@@ -1207,14 +1207,15 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
                         const uint32_t xh = cxh < (int32_t)x_hi ? (uint32_t)cxh : x_hi;
                         if (cxh < 0 || xl > xh) continue;
                         uint32_t off, offTo;
-                        if (pb.subofs) { /* quarter-cell trimming of the chord's end cells */
-                            const int32_t q0 = orx_f2i_sat(orx_floorf((np.x - rx) * invCellSize * 4.f));
-                            const int32_t q1 = orx_f2i_sat(orx_floorf((np.x + rx) * invCellSize * 4.f));
-                            const uint32_t a0 = q0 > (int32_t)(4 * xl) ? (uint32_t)q0 : 4 * xl;
-                            const uint32_t a1 = q1 < (int32_t)(4 * xh + 3) ? (uint32_t)q1 : 4 * xh + 3;
+                        if (pb.subofs) { /* sub-cell trimming of the chord's end cells */
+                            const float sx = invCellSize * (float)SUBX;
+                            const int32_t q0 = orx_f2i_sat(orx_floorf((np.x - rx) * sx));
+                            const int32_t q1 = orx_f2i_sat(orx_floorf((np.x + rx) * sx));
+                            const uint32_t a0 = q0 > (int32_t)(SUBX * xl) ? (uint32_t)q0 : SUBX * xl;
+                            const uint32_t a1 = q1 < (int32_t)(SUBX * xh + SUBX - 1) ? (uint32_t)q1 : SUBX * xh + SUBX - 1;
                             if (q1 < 0 || a0 > a1) continue;
-                            off = pb.subofs[4 * row + a0];
-                            offTo = pb.subofs[4 * row + a1 + 1];
+                            off = pb.subofs[SUBX * row + a0];
+                            offTo = pb.subofs[SUBX * row + a1 + 1];
                         } else {
                             off = pb.offsets[xl + row];
                             offTo = pb.offsets[xh + row + 1];
