@@ -124,6 +124,22 @@ class ShardedVCM:
     image = ShardedPPM.image
 
 
+class ShardedPT:
+    """Path tracing shards by pixel rows with no per-iteration exchange
+    (SURVEY 8(e)): each rank runs RayGeneratorPT over its own rows
+    (orx_render_next_iteration on a sharded renderer); only the image is
+    gathered, on request."""
+
+    def __init__(self, backend, dist, world, rank, W, H):
+        self.b, self.dist, self.world, self.rank, self.W, self.H = backend, dist, world, rank, W, H
+        self.max_rows = (H + world - 1) // world
+
+    def iteration(self, it, local_it, radius, request):
+        self.b.render_next(it, local_it, radius, request)
+
+    image = ShardedPPM.image
+
+
 class DeviceShard:
     """liborx.so backend: buffers are torch device tensors, kernels run on torch's current stream."""
 
@@ -176,6 +192,9 @@ class DeviceShard:
     def finish(self, ind_local):
         self.r._check(self.lib.orx_ppm_finish(self.r._h, C.c_void_p(ind_local.data_ptr()), ind_local.numel() * 4))
 
+    def render_next(self, it, local_it, radius, request):
+        self.r._check(self.lib.orx_render_next_iteration(self.r._h, it, local_it, radius, 1, C.byref(request)))
+
     def vcm_local_light(self, it, local_it, radius, request):
         self.r._check(self.lib.orx_vcm_local_light(self.r._h, it, local_it, radius, C.byref(request)))
 
@@ -202,9 +221,10 @@ def bench_main(args, metric):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     method = getattr(args, "method", "ppm")
-    if method not in ("ppm", "vcm"):
-        raise SystemExit("the sharded bench runs PPM or VCM (PT has no sharded phase API; see DESIGN.md)")
+    if method not in ("ppm", "vcm", "pt"):
+        raise SystemExit("the sharded bench runs ppm, vcm or pt")
     vcm = method == "vcm"
+    pt = method == "pt"
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # RCCL prints its version banner on fd 1: keep stdout for the one JSON line
     json_out = os.fdopen(os.dup(1), "w")
@@ -220,13 +240,14 @@ def bench_main(args, metric):
     r.set_shard(rank, world)
     r.initScene(scene)
     cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
-    mcode = _abi.VCM_BIDIRECTIONAL_PATH_TRACING if vcm else _abi.PROGRESSIVE_PHOTON_MAPPING
+    mcode = (_abi.VCM_BIDIRECTIONAL_PATH_TRACING if vcm else _abi.PATH_TRACING if pt
+             else _abi.PROGRESSIVE_PHOTON_MAPPING)
     det = RenderRequestDetails(cam, scene.name, mcode, W, H)
     req = det.to_abi()
     dev = torch.device("cuda", local_rank)
     backend = DeviceShard(r, torch, dev)
     radius = scene.initial_ppm_radius()
-    sharded = (ShardedVCM if vcm else ShardedPPM)(backend, dist, world, rank, W, H)
+    sharded = (ShardedVCM if vcm else ShardedPT if pt else ShardedPPM)(backend, dist, world, rank, W, H)
     it = 0
     for _ in range(max(1, args.warmup)):
         sharded.iteration(it, it, radius, req)
@@ -253,14 +274,16 @@ def bench_main(args, metric):
         from . import roofline
         # PPM: weak scaling (each rank emits its own P*P photon batch); VCM: the
         # W*H light + W*H camera subpaths are split over the ranks (strong scaling)
-        paths = 2 * W * H if vcm else W * H + P * P * world
+        paths = 2 * W * H if vcm else W * H if pt else W * H + P * P * world
         n_it = max(1, st.timed_iterations)
         per_pass = {name: st.pass_ms[i] / n_it for i, name in enumerate(_abi.PASS_NAMES)}
         per_pass = {k: v for k, v in per_pass.items() if v > 0}
         dominant = max(per_pass, key=per_pass.get)
         valid_avg = st.valid_photons_total / n_it
         rows0 = local_rows(H, 0, world)
-        if vcm:  # rank 0 traces its own rows' subpaths; light vertices counted in the stats
+        if pt:
+            pb = roofline.pass_bytes(mcode, W, rows0, 0)
+        elif vcm:  # rank 0 traces its own rows' subpaths; light vertices counted in the stats
             lv = int(np.minimum(r.read_buffer(_abi.BUF_VCM_VERTEX_COUNT, np.uint32), 9).sum())
             pb = roofline.pass_bytes(mcode, W, rows0, 0, light_vertices=lv)
         else:
@@ -273,10 +296,15 @@ def bench_main(args, metric):
             "metric": metric, "value": round(paths * args.steps / t_max / 1e6, 3), "unit": "Mpaths/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t_max * 1e3 / args.steps, 4), "higher_is_better": True,
-            "scaling": "strong" if vcm else "weak",
+            "scaling": "strong" if (vcm or pt) else "weak",
             "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic: seeded procedural scene ({scene.name}), XORWOW streams seeded 1645301512",
-            "config": ({"workload": f"{scene.name} {W}x{H} VCM, {W * H} light subpaths/iter (strong scaling)",
+            "config": ({"workload": f"{scene.name} {W}x{H} PT, 1 spp/iter (strong scaling)",
+                        "scene": scene.name, "width": W, "height": H, "method": "PT",
+                        "paths_per_iteration": paths,
+                        "parallelism": f"row-interleaved RNG/pixel ownership x{world}, no per-iteration exchange"}
+                       if pt else
+                       {"workload": f"{scene.name} {W}x{H} VCM, {W * H} light subpaths/iter (strong scaling)",
                         "scene": scene.name, "width": W, "height": H, "method": "VCM",
                         "paths_per_iteration": paths,
                         "parallelism": f"row-interleaved RNG/pixel ownership x{world}, "

@@ -136,6 +136,10 @@ class OracleShard:
     def finish(self, ind_local):
         self.r._check(self.lib.orc_ppm_finish(self.r.h, C.c_void_p(ind_local.data_ptr()), ind_local.numel() * 4))
 
+    def render_next(self, it, local_it, radius, request):
+        self.r.width, self.r.height = request.width, request.height
+        self.r._check(self.lib.orc_render_next_iteration(self.r.h, it, local_it, radius, 1, C.byref(request)))
+
     def vcm_local_light(self, it, local_it, radius, request):
         self.r.width, self.r.height = request.width, request.height
         self.r._check(self.lib.orc_vcm_local_light(self.r.h, it, local_it, radius, C.byref(request)))

@@ -113,3 +113,37 @@ def test_sharded_device_vcm_matches_single(world, W, H):
     for b in shards:
         b.r.destroy()
     single.destroy()
+
+
+@pytest.mark.parametrize("world,W,H", [(2, 64, 48), (3, 50, 41)])
+def test_sharded_device_pt_matches_single(world, W, H):
+    """Device-side PT row shards (no exchange): bit-identical to one device."""
+    dev = torch.device("cuda", 0)
+    scene = scenes.scene_by_name("CornellSmallSmallSpheres")
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    det = RenderRequestDetails(cam, scene.name, _abi.PATH_TRACING, W, H)
+    req = det.to_abi()
+    cfg = lambda: _abi.default_config(seed=SEED, photon_launch_width=32, photon_launch_height=32)
+    shards = []
+    for rank in range(world):
+        r = OptixRenderer(cfg())
+        r.initialize(0)
+        r.set_shard(rank, world)
+        r.initScene(scene)
+        shards.append(multigpu.DeviceShard(r, torch, dev))
+    for it in range(3):
+        for b in shards:
+            b.render_next(it, it, 1.0, req)
+    torch.cuda.synchronize()
+    mr = (H + world - 1) // world
+    got = multigpu.assemble_rows([b.output_local_tensor(mr).cpu().numpy().reshape(mr, W, 3) for b in shards], W, H, world)
+    single = OptixRenderer(cfg())
+    single.initialize(0)
+    single.initScene(scene)
+    for it in range(3):
+        single.renderNextIteration(it, it, 1.0, True, det)
+    ref = single.getOutputBuffer()
+    assert np.array_equal(got.reshape(-1).view(np.uint32), ref.reshape(-1).view(np.uint32))
+    for b in shards:
+        b.r.destroy()
+    single.destroy()

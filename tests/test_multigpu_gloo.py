@@ -49,7 +49,8 @@ def worker(rank, world, port, out_path, W, H, P, iters, method=_abi.PROGRESSIVE_
     r.init_scene(scene)
     b = oracle_lib.OracleShard(r, torch)
     b.set_shard(rank, world)
-    cls = multigpu.ShardedVCM if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING else multigpu.ShardedPPM
+    cls = {_abi.VCM_BIDIRECTIONAL_PATH_TRACING: multigpu.ShardedVCM,
+           _abi.PATH_TRACING: multigpu.ShardedPT}.get(method, multigpu.ShardedPPM)
     sh = cls(b, dist, world, rank, W, H)
     req = request(scene, W, H, method)
     radius = scene.initial_ppm_radius()
@@ -104,6 +105,24 @@ def test_sharded_vcm_matches_single(world, W, H):
     ref = r.output()
     err = np.sqrt(((got.astype(np.float64) - ref) ** 2).sum() / (ref.astype(np.float64) ** 2).sum())
     assert err < 1e-5, err
+    assert got.mean() > 0
+
+
+@pytest.mark.parametrize("world,W,H", [(2, 40, 32), (3, 36, 29)])
+def test_sharded_pt_matches_single_bitexact(world, W, H):
+    """PT row sharding: no exchange; every pixel's path is the single-renderer one."""
+    out = os.path.join(tempfile.mkdtemp(), "img.npy")
+    pt = _abi.PATH_TRACING
+    mp.spawn(worker, args=(world, free_port(), out, W, H, 32, 2, pt), nprocs=world, join=True)
+    got = np.load(out)
+    scene = scenes.cornell()
+    cfg = _abi.default_config(seed=SEED, photon_launch_width=32, photon_launch_height=32 * world)
+    r = oracle_lib.OracleRenderer(cfg)
+    r.init_scene(scene)
+    req = request(scene, W, H, pt)
+    for it in range(2):
+        r.render_next_iteration(it, it, 1.0, req)
+    assert np.array_equal(got.view(np.uint32), r.output().view(np.uint32))
     assert got.mean() > 0
 
 
