@@ -572,28 +572,61 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
         }
         for (int k = 0; k < 3; k++) b.c[k] = 0.5f * (b.lo[k] + b.hi[k]);
     }
+    /* BVH: built on the device (orx_bvh.hip) by default; the host builder
+     * below is the reference implementation (ORX_BVH_HOST=1) and the only
+     * one for the fp32-box variant */
+    int bins = 32;
+    uint32_t leaf_max = 8;
+    float leaf_sah = 0.6f;
+    if (const char* e = getenv("ORX_BVH_BINS")) bins = std::max(2, std::min(32, atoi(e)));
+    if (const char* e = getenv("ORX_BVH_LEAF_MAX")) leaf_max = (uint32_t)std::max(1, std::min(8, atoi(e)));
+    if (const char* e = getenv("ORX_BVH_LEAF_SAH")) leaf_sah = (float)atof(e);
+#ifdef ORX_BVH_FP32
+    const bool device_bvh = false;
+#else
+    const char* host_env = getenv("ORX_BVH_HOST");
+    const bool device_bvh = !(host_env && atoi(host_env));
+#endif
+    std::vector<uint32_t> leaf_order;
+    uint32_t stack_bound = 0, nodes4 = 0;
     BvhBuilder bb;
-    if (nt) {
+    Bvh4Builder b4;
+    if (nt && device_bvh) {
+        DevBuf dV, dI;
+        HIPCHK(r, dV.ensure((size_t)s->n_vertices * 12));
+        HIPCHK(r, dI.ensure((size_t)nt * 12));
+        HIPCHK(r, hipMemcpy(dV.p, s->vertices, (size_t)s->n_vertices * 12, hipMemcpyHostToDevice));
+        HIPCHK(r, hipMemcpy(dI.p, s->triangles, (size_t)nt * 12, hipMemcpyHostToDevice));
+        HIPCHK(r, r->d_bvh.ensure((size_t)nt * sizeof(DevBvh4) + 64));
+        HIPCHK(r, r->d_bvhprims.ensure((size_t)nt * 4));
+        uint32_t depth = 0;
+        bool ok = false;
+        HIPCHK(r, device_build_bvh4(r->stream, dV.as<float>(), dI.as<uint32_t>(), nt, bins, leaf_max, leaf_sah,
+                                    r->d_bvh.as<DevBvh4>(), nt, r->d_bvhprims.as<uint32_t>(), &nodes4, &stack_bound,
+                                    &depth, &ok));
+        if (!ok) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "device BVH build failed (quantisation or capacity)");
+        if (depth >= ORX_BVH_STACK) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "BVH deeper than the traversal stack");
+        leaf_order.resize(nt);
+        HIPCHK(r, hipMemcpy(leaf_order.data(), r->d_bvhprims.p, (size_t)nt * 4, hipMemcpyDeviceToHost));
+    } else if (nt) {
         bb.tris = &bt;
-        if (const char* e = getenv("ORX_BVH_BINS")) bb.bins = std::max(2, std::min(64, atoi(e)));
-        if (const char* e = getenv("ORX_BVH_LEAF_MAX")) bb.leaf_max = (uint32_t)std::max(1, std::min(8, atoi(e)));
-        if (const char* e = getenv("ORX_BVH_LEAF_SAH")) bb.leaf_sah = (float)atof(e);
+        bb.bins = bins;
+        bb.leaf_max = leaf_max;
+        bb.leaf_sah = leaf_sah;
         bb.prims.resize(nt);
         for (uint32_t i = 0; i < nt; i++) bb.prims[i] = i;
         bb.nodes.reserve(2 * (size_t)nt / 2 + 1);
         bb.build(0, nt);
         if (bb.max_depth >= ORX_BVH_STACK)
             return set_err(r, ORX_ERR_INVALID_ARGUMENT, "BVH deeper than the traversal stack");
-    }
-    Bvh4Builder b4;
-    uint32_t stack_bound = 0;
-    if (nt) {
         b4.b2 = &bb.nodes;
         b4.out.reserve(bb.nodes.size() / 2 + 1);
         b4.build(0, stack_bound);
         if (!b4.ok) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "BVH4 quantisation failed");
-        if (stack_bound > 96) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "BVH4 traversal stack bound above 96");
+        leaf_order = bb.prims;
+        nodes4 = (uint32_t)b4.out.size();
     }
+    if (stack_bound > 96) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "BVH4 traversal stack bound above 96");
     std::vector<float4> tv((size_t)nt * 3), tn, tt, tbt;
     std::vector<float2> tuv;
     std::vector<uint32_t> tmat_leaf(nt);
@@ -602,7 +635,7 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     if (s->texcoords) tuv.resize((size_t)nt * 3);
     if (has_tb) tt.resize((size_t)nt * 3), tbt.resize((size_t)nt * 3);
     for (uint32_t k = 0; k < nt; k++) {
-        const uint32_t i = bb.prims[k];
+        const uint32_t i = leaf_order[k];
         tmat_leaf[k] = s->triangle_material[i];
         for (int v = 0; v < 3; v++) {
             uint32_t vi = s->triangles[3 * (size_t)i + v];
@@ -679,7 +712,7 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
 #ifdef ORX_BVH_FP32
     HIPCHK(r, up(r->d_bvh, b4.outf.data(), b4.outf.size() * sizeof(DevBvh4F)));
 #else
-    HIPCHK(r, up(r->d_bvh, b4.out.data(), b4.out.size() * sizeof(DevBvh4)));
+    if (!device_bvh) HIPCHK(r, up(r->d_bvh, b4.out.data(), b4.out.size() * sizeof(DevBvh4)));
 #endif
     DevScene& S = r->scene;
     S.nq = nq;
@@ -701,7 +734,7 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     S.lights = r->d_lights.as<DevLight>();
     S.nl = s->n_lights;
     S.bvh4 = r->d_bvh.as<DevNode4>();
-    S.bvh_nodes = (uint32_t)b4.out.size();
+    S.bvh_nodes = nodes4;
     S.stack_entries = nt ? stack_bound + 1 : 0;
 #ifdef ORX_TRAV_STATS
     HIPCHK(r, r->d_tstats.ensure(128));
