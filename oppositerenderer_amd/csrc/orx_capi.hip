@@ -388,7 +388,7 @@ struct orx_renderer {
     bool vcm_kd = false;      /* d_vkd sized for the current vcm_npx */
     VcmBufs vcm_vb{};
     VcmConsts vcm_c{};
-    DevBuf d_vcount, d_vverts, d_vsplat, d_vcam, d_vkd, d_tstats;
+    DevBuf d_vcount, d_vverts, d_vsplat, d_vcam, d_vkd, d_vshq, d_tstats;
     std::vector<DevLight> host_lights;
 };
 
@@ -1033,6 +1033,11 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
     vb.vE = r->has_tex ? r->d_vkd.as<float4>() : nullptr;
     vb.splat = r->d_vsplat.as<float>();
     vb.splat_in = vb.splat + (size_t)r->rank * r->max_rows * r->W * 3;
+    {
+        const size_t waves = (size_t)((r->W + 7) / 8) * ((r->rows + 7) / 8);
+        HIPCHK(r, r->d_vshq.ensure(waves * VCM_SHQ_PER_WAVE * 16 + 16));
+        vb.shq = r->d_vshq.as<float4>();
+    }
     vb.cam = r->d_vcam.as<float>();
     vb.output = r->d_out.as<float>();
     VcmConsts& c = r->vcm_c;

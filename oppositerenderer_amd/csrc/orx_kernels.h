@@ -140,6 +140,8 @@ void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const Pix
 
 /* ---- VCM (orx_vcm.hip) ---- */
 constexpr uint32_t VCM_MAX_VERTS = 9; /* VCM_MAX_PATH_LENGTH - 1 (OptixRenderer.cpp:343-344) */
+/* camera pass shadow-ray queue per wave, in float4: [64 lanes x (1 + 9) tests][2] + [64] points */
+constexpr uint32_t VCM_SHQ_PER_WAVE = 2 * 64 * (VCM_MAX_VERTS + 1) + 64;
 /* light subpath p = x + y*W pairs with pixel p; RNG slot y*RW + x serves both */
 struct VcmBufs {
     uint32_t RW;
@@ -150,6 +152,7 @@ struct VcmBufs {
     float4* vC;         /* [9][W*H] normal.xyz | dVC */
     float4* vD;         /* [9][W*H] localDirFix.xyz | dVM */
     float4* vE;         /* [9][lcount] texel colour of Texture vertices (NULL without Texture materials) */
+    float4* shq;        /* [camera-pass waves][VCM_SHQ_PER_WAVE] deferred shadow-ray queues */
     float* splat;       /* [world][max_rows][W][3] connectCameraT1 accumulation of this iteration (owner-block layout) */
     const float* splat_in; /* [rows][W][3] summed splats of the own rows (camera pass) */
     float* cam;         /* [W*H*3] camera subpath colour of this iteration */

@@ -611,8 +611,8 @@ __global__ __launch_bounds__(64, 4) void k_vcm_light(DevScene S, VcmBufs vb, Vcm
 
 /* connectVertices (vcm.h:315-400) against light vertex k of this subpath */
 template <bool TEX>
-__device__ inline void connect_vertex(const DevScene& S, Subpath& C, const VBsdf& cb, f3 hit, const VcmBufs& vb,
-                                      size_t o, const VcmConsts& c, uint32_t* stk) {
+__device__ inline bool connect_vertex(const DevScene& S, const Subpath& C, const VBsdf& cb, f3 hit, const VcmBufs& vb,
+                                      size_t o, const VcmConsts& c, f3& sdir, float& sdist, f3& add) {
     const float4 A = vb.vA[o];
     f3 direction = mk(A.x, A.y, A.z) - hit;
     const float dist2 = dot(direction, direction);
@@ -620,7 +620,7 @@ __device__ inline void connect_vertex(const DevScene& S, Subpath& C, const VBsdf
     direction = direction / distance;
     float camCos = 0.f, cDir, cRev;
     const f3 camF = cb.vcm_f(direction, camCos, cDir, cRev);
-    if (iszero(camF)) return;
+    if (iszero(camF)) return false;
     cDir *= cb.cont;
     cRev *= cb.cont;
     const float4 Cn = vb.vC[o];
@@ -643,11 +643,11 @@ __device__ inline void connect_vertex(const DevScene& S, Subpath& C, const VBsdf
     if (m.type == MAT_GLOSSY) lb.add(mk_bx(T_PHONG, m.Ks, m.exponent));
     float lightCos = 0.f, lDir, lRev;
     const f3 lightF = lb.vcm_f(-direction, lightCos, lDir, lRev);
-    if (iszero(lightF)) return;
+    if (iszero(lightF)) return false;
     lDir *= lb.cont;
     lRev *= lb.cont;
     const float geometryTerm = lightCos * camCos / dist2;
-    if (geometryTerm < 0.f) return;
+    if (geometryTerm < 0.f) return false;
     const float camDirPdfA = cDir * fabsf(camCos) / (distance * distance);
     const float lightDirPdfA = lDir * fabsf(lightCos) / (distance * distance);
     const float4 B = vb.vB[o];
@@ -656,13 +656,15 @@ __device__ inline void connect_vertex(const DevScene& S, Subpath& C, const VBsdf
     const float misWeight = 1.f / (wLight + 1.f + wCamera);
     f3 contrib = ((camF * geometryTerm) * lightF) * 1.f;
     contrib = contrib * ((C.throughput * misWeight) * mk(B.x, B.y, B.z));
-    if (occluded(S, hit, direction, distance, stk)) return;
-    C.color = C.color + contrib;
+    sdir = direction; /* the caller traces occluded(hit, sdir, sdist) and adds `add` if clear */
+    sdist = distance;
+    add = contrib;
+    return true;
 }
 
 /* connectLightSourceS1 (vcm.h:406-488) + lightIlluminate (helpers/light.h:141-203) */
-__device__ inline void connect_light(const DevScene& S, Subpath& C, const VBsdf& cb, f3 hit, const VcmConsts& c,
-                                     Rng& rs, uint32_t* stk) {
+__device__ inline bool connect_light(const DevScene& S, const Subpath& C, const VBsdf& cb, f3 hit, const VcmConsts& c,
+                                     Rng& rs, f3& sdir, float& sdist, f3& add) {
     int li = 0;
     if (1 < S.nl) {
         const float s = rnd(rs);
@@ -680,7 +682,7 @@ __device__ inline void connect_light(const DevScene& S, Subpath& C, const VBsdf&
         distance = length(dirToLight);
         dirToLight = dirToLight / distance;
         const float cosThetaLight = dot(light.normal, -dirToLight);
-        if (cosThetaLight < VCM_EPS_COSINE) return;
+        if (cosThetaLight < VCM_EPS_COSINE) return false;
         directPdfW = light.inverseArea * (distance * distance) / cosThetaLight;
         cosAtLight = cosThetaLight;
         emissionPdfW = light.inverseArea * cosThetaLight * ORX_1_PI_F;
@@ -700,19 +702,21 @@ __device__ inline void connect_light(const DevScene& S, Subpath& C, const VBsdf&
         cosAtLight = 1.f;
     }
     const f3 radiance = light.Lemit;
-    if (iszero(radiance)) return;
+    if (iszero(radiance)) return false;
     float cosToLight = 0.f, bDir, bRev;
     const f3 f = cb.vcm_f(dirToLight, cosToLight, bDir, bRev);
-    if (iszero(f)) return;
+    if (iszero(f)) return false;
     bDir *= light.type != LIGHT_AREA ? 0.f : cb.cont;
     bRev *= cb.cont;
     const float wLight = bDir / (lightPickProb * directPdfW);
     const float wCamera = (emissionPdfW * cosToLight / (directPdfW * cosAtLight)) * (c.misVm + C.dVCM + C.dVC * bRev);
     const float misWeight = 1.f / (wLight + 1.f + wCamera);
     const f3 contrib = (radiance * f) * (misWeight * cosToLight / (lightPickProb * directPdfW));
-    if (iszero(contrib)) return;
-    if (occluded(S, hit, dirToLight, distance, stk)) return;
-    C.color = C.color + contrib * C.throughput;
+    if (iszero(contrib)) return false;
+    sdir = dirToLight;
+    sdist = distance;
+    add = contrib * C.throughput;
+    return true;
 }
 
 /* cameraPass (VCMCameraPass.cu:48-80), initCameraPayload (:100-135), cameraHit (vcm.h:527-628) */
@@ -723,10 +727,11 @@ __global__ __launch_bounds__(64, 4) void k_vcm_camera(DevScene S, VcmBufs vb, Vc
     const uint32_t tilesX = (c.W + 7) / 8;
     const uint32_t x = (blockIdx.x % tilesX) * 8 + (threadIdx.x & 7);
     const uint32_t j = (blockIdx.x / tilesX) * 8 + (threadIdx.x >> 3); /* own row j = image row rank + j*world */
-    if (x >= c.W || j >= c.rows) return;
+    /* lanes outside the image stay in the wave (they take part in the shadow-ray flushes) */
+    const bool inimg = x < c.W && j < c.rows;
     const uint32_t y = c.rank + j * c.world;
-    const uint32_t p = x + j * c.W;
-    const size_t slot = (size_t)j * vb.RW + x;
+    const uint32_t p = inimg ? x + j * c.W : 0u;
+    const size_t slot = inimg ? (size_t)j * vb.RW + x : 0;
     Rng rs = rng_load(vb.rng, slot);
     Subpath C;
     C.throughput = mk1(1.0f);
@@ -747,48 +752,127 @@ __global__ __launch_bounds__(64, 4) void k_vcm_camera(DevScene S, VcmBufs vb, Vc
     const float areaSamplePdf = 1.f / pixelArea;
     const float cameraPdfW = areaSamplePdf * i2s;
     C.dVCM = (float)c.count / cameraPdfW;
-    const uint32_t nverts = vb.vcount[p];
+    const uint32_t nverts = inimg ? vb.vcount[p] : 0u;
+    /* The connections' shadow rays are deferred to a per-wave queue and traced
+     * by all 64 lanes together (lanes whose subpath has ended help too): traced
+     * in place, inside the divergent per-vertex loop, they ran at ~8 % lane
+     * utilisation.  Every subpath still adds its unoccluded contributions in
+     * the reference order (light sample, then light vertices 0..n-1), so the
+     * colour is unchanged bit for bit. */
+    const uint32_t lane = threadIdx.x & 63;
+    float4* q = vb.shq + (size_t)blockIdx.x * VCM_SHQ_PER_WAVE;   /* [64 * 10][2] entries */
+    float4* qhit = q + 2 * 64 * (VCM_MAX_VERTS + 1);              /* [64] connection points */
+    bool alive = inimg;
     for (;;) {
-        Hit h;
-        if (!trace_closest(S, C.origin, C.direction, VCM_RAY_LEN_MIN, RT_DEFAULT_MAX, h, stk)) break;
-        const DevMaterial& m = S.mats[prim_material(S, h)];
-        const f3 hit = C.origin + C.direction * h.t;
-        if (m.type == MAT_EMITTER) { /* DiffuseEmitter.cu:95-120 + connectLightSourceS0 (vcm.h:493-522) */
-            C.depth++;
-            if (iszero(m.Lemit)) break;
-            const f3 N = geometric_normal(S, h);
-            if (dot(N, -C.direction) < 0.f) break;
-            const float lightPickProb = 1.f / (float)S.nl;
-            float directPdfA = m.inverseArea;
-            float emissionPdfW = maxf(0.f, dot(N, -C.direction)) * ORX_1_PI_F * m.inverseArea;
-            if (C.depth == 1) {
-                C.color = C.color + C.throughput * m.Lemit;
-                break;
-            }
-            directPdfA *= lightPickProb;
-            emissionPdfW *= lightPickProb;
-            const float wCamera = directPdfA * C.dVCM + emissionPdfW * C.dVC;
-            const float misWeight = 1.f / (1.f + wCamera);
-            C.color = C.color + (C.throughput * misWeight) * m.Lemit;
-            break;
-        }
+        if (!__ballot(alive)) break;
+        uint32_t npend = 0;
+        bool spec = true, last = false;
         VBsdf bs;
-        f3 N;
-        const f3 kd = TEX && m.type == MAT_TEXTURE ? tex_color(S, m, h) : m.Kd;
-        if (!material_bsdf(m, kd, geometric_normal(S, h), C.direction, false, bs, N)) break;
-        C.depth++;
-        const float cosIn = dot(N, -C.direction);
-        if (cosIn < VCM_EPS_COSINE) break;
-        mis_on_hit(C, cosIn, h.t);
-        if (!bs.is_specular()) {
-            connect_light(S, C, bs, hit, c, rs, stk);
-            const uint32_t nv = nverts < VCM_MAX_VERTS ? nverts : VCM_MAX_VERTS;
-            for (uint32_t k = 0; k < nv; ++k) connect_vertex<TEX>(S, C, bs, hit, vb, (size_t)k * c.lcount + p, c, stk);
+        f3 hit = mk1(0.f);
+        if (alive) {
+            Hit h;
+            if (!trace_closest(S, C.origin, C.direction, VCM_RAY_LEN_MIN, RT_DEFAULT_MAX, h, stk)) {
+                alive = false;
+            } else {
+                const DevMaterial& m = S.mats[prim_material(S, h)];
+                hit = C.origin + C.direction * h.t;
+                if (m.type == MAT_EMITTER) { /* DiffuseEmitter.cu:95-120 + connectLightSourceS0 (vcm.h:493-522) */
+                    alive = false;
+                    C.depth++;
+                    const f3 N = geometric_normal(S, h);
+                    if (!iszero(m.Lemit) && !(dot(N, -C.direction) < 0.f)) {
+                        const float lightPickProb = 1.f / (float)S.nl;
+                        float directPdfA = m.inverseArea;
+                        float emissionPdfW = maxf(0.f, dot(N, -C.direction)) * ORX_1_PI_F * m.inverseArea;
+                        if (C.depth == 1) {
+                            C.color = C.color + C.throughput * m.Lemit;
+                        } else {
+                            directPdfA *= lightPickProb;
+                            emissionPdfW *= lightPickProb;
+                            const float wCamera = directPdfA * C.dVCM + emissionPdfW * C.dVC;
+                            const float misWeight = 1.f / (1.f + wCamera);
+                            C.color = C.color + (C.throughput * misWeight) * m.Lemit;
+                        }
+                    }
+                } else {
+                    f3 N;
+                    const f3 kd = TEX && m.type == MAT_TEXTURE ? tex_color(S, m, h) : m.Kd;
+                    if (!material_bsdf(m, kd, geometric_normal(S, h), C.direction, false, bs, N)) {
+                        alive = false;
+                    } else {
+                        C.depth++;
+                        const float cosIn = dot(N, -C.direction);
+                        if (cosIn < VCM_EPS_COSINE) {
+                            alive = false;
+                        } else {
+                            mis_on_hit(C, cosIn, h.t);
+                            spec = bs.is_specular();
+                            last = c.maxPathLen <= C.depth;
+                        }
+                    }
+                }
+            }
         }
-        if (c.maxPathLen <= C.depth) break;
-        sample_scattering(C, hit, bs, c, rs);
-        if (C.done) break;
+        /* connections of this vertex: pending shadow tests in the lane's rows */
+        const bool conn = alive && !spec;
+        uint32_t qbase = 0;
+        {
+            /* upper bound first (1 + n vertices), real count after building */
+            const uint32_t nv = nverts < VCM_MAX_VERTS ? nverts : VCM_MAX_VERTS;
+            const uint32_t want = conn ? 1u + nv : 0u;
+            uint32_t incl = want;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (lane >= (uint32_t)o) incl += y;
+            }
+            qbase = incl - want;
+            if (conn) {
+                qhit[lane] = make_float4(hit.x, hit.y, hit.z, 0.f);
+                f3 sd, ad;
+                float sl;
+                if (connect_light(S, C, bs, hit, c, rs, sd, sl, ad)) {
+                    q[2 * (qbase + npend)] = make_float4(sd.x, sd.y, sd.z, sl);
+                    q[2 * (qbase + npend) + 1] = make_float4(ad.x, ad.y, ad.z, __uint_as_float(lane));
+                    npend++;
+                }
+                for (uint32_t k = 0; k < nv; ++k) {
+                    if (connect_vertex<TEX>(S, C, bs, hit, vb, (size_t)k * c.lcount + p, c, sd, sl, ad)) {
+                        q[2 * (qbase + npend)] = make_float4(sd.x, sd.y, sd.z, sl);
+                        q[2 * (qbase + npend) + 1] = make_float4(ad.x, ad.y, ad.z, __uint_as_float(lane));
+                        npend++;
+                    }
+                }
+                /* unused reserved rows: no test */
+                for (uint32_t k = npend; k < want; ++k) q[2 * (qbase + k)] = make_float4(0.f, 0.f, 0.f, -1.f);
+            }
+            const uint32_t total = __shfl(incl, 63, 64);
+            __threadfence_block();
+            /* all lanes trace the wave's shadow rays; the result goes into .w of the contribution row */
+            for (uint32_t e = lane; e < total; e += 64) {
+                const float4 r0 = q[2 * e];
+                if (r0.w < 0.f) continue;
+                const float4 r1 = q[2 * e + 1];
+                const float4 hp = qhit[__float_as_uint(r1.w)];
+                const bool occ = occluded(S, mk(hp.x, hp.y, hp.z), mk(r0.x, r0.y, r0.z), r0.w, stk);
+                q[2 * e] = make_float4(r0.x, r0.y, r0.z, occ ? -2.f : -3.f);
+            }
+            __threadfence_block();
+            for (uint32_t k = 0; k < npend; ++k) {
+                const float4 r0 = q[2 * (qbase + k)];
+                const float4 r1 = q[2 * (qbase + k) + 1];
+                if (r0.w == -3.f) C.color = C.color + mk(r1.x, r1.y, r1.z);
+            }
+        }
+        if (alive) {
+            if (last) {
+                alive = false;
+            } else {
+                sample_scattering(C, hit, bs, c, rs);
+                if (C.done) alive = false;
+            }
+        }
     }
+    if (!inimg) return;
     const size_t o3 = 3 * (size_t)p;
     vb.cam[o3 + 0] = C.color.x;
     vb.cam[o3 + 1] = C.color.y;
