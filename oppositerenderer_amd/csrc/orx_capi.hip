@@ -351,6 +351,9 @@ struct orx_renderer {
     int device = 0;
     orx_config cfg{};
     hipStream_t stream = nullptr;
+    hipStream_t aux = nullptr;   /* PPM direct pass, overlapped with the grid build and gather */
+    hipEvent_t ev_photon_done = nullptr, ev_direct_done = nullptr;
+    bool overlap_direct = false;
     std::string err;
     bool scene_ready = false;
     /* scene */
@@ -454,7 +457,10 @@ orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out)
         delete r;
         return ORX_ERR_INVALID_ARGUMENT;
     }
-    if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&r->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&r->ev_photon_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&r->ev_direct_done, hipEventDisableTiming) != hipSuccess) {
         delete r;
         return ORX_ERR_DEVICE;
     }
@@ -468,6 +474,10 @@ void orx_destroy(orx_renderer* r) {
     if (r->stream) hipStreamSynchronize(r->stream);
     for (int p = 0; p < P_COUNT; p++)
         for (hipEvent_t e : r->ev[p]) hipEventDestroy(e);
+    if (r->aux) hipStreamSynchronize(r->aux);
+    if (r->ev_photon_done) hipEventDestroy(r->ev_photon_done);
+    if (r->ev_direct_done) hipEventDestroy(r->ev_direct_done);
+    if (r->aux) hipStreamDestroy(r->aux);
     if (r->stream) hipStreamDestroy(r->stream);
     delete r;
 }
@@ -902,6 +912,22 @@ static inline void ev_end(orx_renderer* r, int p) {
     hipEventRecord(r->ev[p][2 * r->ev_n[p] + 1], r->use_ext ? r->ext_stream : r->stream);
     r->ev_n[p]++;
 }
+/* the same on an explicit stream (the overlapped direct pass) */
+static inline void ev_begin_on(orx_renderer* r, int p, hipStream_t st) {
+    if (!r->timing || r->ev_n[p] >= EV_POOL) return;
+    auto& v = r->ev[p];
+    while (v.size() < 2 * (size_t)r->ev_n[p] + 2) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        v.push_back(e);
+    }
+    hipEventRecord(v[2 * r->ev_n[p]], st);
+}
+static inline void ev_end_on(orx_renderer* r, int p, hipStream_t st) {
+    if (!r->timing || r->ev_n[p] >= EV_POOL || r->ev[p].size() < 2 * (size_t)r->ev_n[p] + 2) return;
+    hipEventRecord(r->ev[p][2 * r->ev_n[p] + 1], st);
+    r->ev_n[p]++;
+}
 
 static orx_status sync_all(orx_renderer* r) {
     HIPCHK(r, hipStreamSynchronize(r->stream));
@@ -971,6 +997,18 @@ static void ppm_photons_grid(orx_renderer* r, const Consts& c) {
     if (wavefront) launch_ppm_photon_wavefront(st, r->scene, r->px, r->pb, c);
     else launch_ppm_photon(st, r->scene, r->px, r->pb, c);
     ev_end(r, P_PHOTON);
+    if (r->overlap_direct) {
+        /* the direct pass needs the hitpoints and the RNG states the photon pass
+         * left (slot (x,y) is shared, Appendix A.2); nothing after it reads
+         * either until the output pass, so it runs beside the grid build and
+         * the gather */
+        hipEventRecord(r->ev_photon_done, st);
+        hipStreamWaitEvent(r->aux, r->ev_photon_done, 0);
+        ev_begin_on(r, P_DIRECT, r->aux);
+        launch_ppm_direct_output(r->aux, r->scene, r->px, c, 1);
+        ev_end_on(r, P_DIRECT, r->aux);
+        hipEventRecord(r->ev_direct_done, r->aux);
+    }
     /* grid build: the atomic-free bucket sort (default) or the atomic-rank
      * counting sort (ORX_GRID_ATOMIC=1, kept for A/B) */
     static const int atomic_grid = [] {
@@ -1133,13 +1171,24 @@ orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
         orx_status sv = vcm_iteration(r, det, ppm_radius);
         if (sv != ORX_OK) return sv;
     } else {
+        static const int overlap = [] {
+            const char* e = getenv("ORX_OVERLAP_DIRECT");
+            return e ? atoi(e) : 1;
+        }();
+        r->overlap_direct = overlap != 0;
         ppm_local_passes(r, cam, c);
         ev_begin(r, P_GATHER);
         launch_ppm_gather(st, local_gather_in(r), r->pb, c, (int)r->cfg.gather_variant);
         ev_end(r, P_GATHER);
         ev_begin(r, P_DIRECT);
-        launch_ppm_direct_output(st, r->scene, r->px, c);
+        if (r->overlap_direct) {
+            HIPCHK(r, hipStreamWaitEvent(st, r->ev_direct_done, 0));
+            launch_ppm_direct_output(st, r->scene, r->px, c, 2);
+        } else {
+            launch_ppm_direct_output(st, r->scene, r->px, c, 0);
+        }
         ev_end(r, P_DIRECT);
+        r->overlap_direct = false;
     }
     HIPCHK(r, hipGetLastError());
     r->last_method = (uint64_t)det->method;

@@ -135,7 +135,8 @@ struct GatherIn {
 };
 /* variant 0: one thread per pixel, 8x8 wave tiles (default); 1: wave-cooperative LDS staging */
 void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, int variant);
-void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c);
+/* mode 0: direct + output; 1: direct only; 2: output only */
+void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c, int mode = 0);
 void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c);
 
 /* ---- VCM (orx_vcm.hip) ---- */

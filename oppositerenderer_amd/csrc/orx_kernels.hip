@@ -1472,12 +1472,26 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
 /* ------------------------------------------------------------------ */
 /* direct radiance (4 shadow samples) + output accumulation            */
 /* ------------------------------------------------------------------ */
+/* MODE 0: direct + output fused; 1: direct only (overlapping the grid build
+ * and gather on a second stream); 2: output only (out = [out +] direct + indirect) */
+template <int MODE>
 __global__ __launch_bounds__(64) void k_ppm_direct_output(DevScene S, PixelBufs px, Consts c) {
     ORX_STACK_DECL;
     const uint32_t x = blockIdx.x * 8 + (threadIdx.x & 7);
     const uint32_t j = blockIdx.y * 8 + (threadIdx.x >> 3);
     if (x >= px.W || j >= px.rows) return;
     const size_t i = (size_t)j * px.W + x;
+    if (MODE == 2) {
+        const f3 d = mk(px.direct[3 * i], px.direct[3 * i + 1], px.direct[3 * i + 2]);
+        const f3 ind = mk(px.indirect[3 * i], px.indirect[3 * i + 1], px.indirect[3 * i + 2]);
+        const f3 fin = d + ind;
+        f3 out = fin;
+        if (c.local_iteration != 0) out = mk(px.output[3 * i], px.output[3 * i + 1], px.output[3 * i + 2]) + fin;
+        px.output[3 * i + 0] = out.x;
+        px.output[3 * i + 1] = out.y;
+        px.output[3 * i + 2] = out.z;
+        return;
+    }
     const float4 A = px.hpA[i];
     const float4 B = px.hpB[i];
     const float2 Cc = px.hpC[i];
@@ -1509,6 +1523,7 @@ __global__ __launch_bounds__(64) void k_ppm_direct_output(DevScene S, PixelBufs 
     px.direct[3 * i + 0] = direct.x;
     px.direct[3 * i + 1] = direct.y;
     px.direct[3 * i + 2] = direct.z;
+    if (MODE == 1) return;
     f3 ind = mk(px.indirect[3 * i], px.indirect[3 * i + 1], px.indirect[3 * i + 2]);
     f3 fin = direct + ind;
     f3 out = fin;
@@ -1517,9 +1532,11 @@ __global__ __launch_bounds__(64) void k_ppm_direct_output(DevScene S, PixelBufs 
     px.output[3 * i + 1] = out.y;
     px.output[3 * i + 2] = out.z;
 }
-void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c) {
+void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c, int mode) {
     dim3 grid((px.W + 7) / 8, (px.rows + 7) / 8);
-    hipLaunchKernelGGL(k_ppm_direct_output, grid, dim3(64), ORX_STACK_BYTES(S), s, S, px, c);
+    if (mode == 1) hipLaunchKernelGGL(k_ppm_direct_output<1>, grid, dim3(64), ORX_STACK_BYTES(S), s, S, px, c);
+    else if (mode == 2) hipLaunchKernelGGL(k_ppm_direct_output<2>, grid, dim3(64), 0, s, S, px, c);
+    else hipLaunchKernelGGL(k_ppm_direct_output<0>, grid, dim3(64), ORX_STACK_BYTES(S), s, S, px, c);
 }
 
 /* ------------------------------------------------------------------ */
