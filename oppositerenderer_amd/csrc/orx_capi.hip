@@ -793,6 +793,8 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_slots.ensure(S * 64));
     HIPCHK(r, r->d_vmask.ensure(nphot));
     const size_t splane = ((S + 4) + 3) & ~(size_t)3;
+    if (9 * splane * 4 > 0xffffff00ull) /* the gather addresses the nine planes with 32-bit buffer offsets */
+        return set_err(r, ORX_ERR_UNSUPPORTED, "photon slots per device exceed the 4 GiB sorted-photon window");
     HIPCHK(r, r->d_sorted.ensure(9 * splane * 4));
     HIPCHK(r, r->d_perm.ensure(S * 4 + 16));
     HIPCHK(r, hipMemsetAsync(r->d_sorted.p, 0, 9 * splane * 4, r->stream)); /* tail reads stay finite */

@@ -1128,8 +1128,19 @@ __device__ __forceinline__ HpRef hp_ref(const GatherIn& gi, uint32_t j, uint32_t
  * the device accumulates in a different order anyway, use fused
  * multiply-adds (v_pk_fma_f32): within ~1e-7 of the oracle per term. */
 typedef float v2f __attribute__((ext_vector_type(2)));
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4))); /* dword-aligned float4 */
 __device__ __forceinline__ v2f lo2(float4 v) { return v2f{v.x, v.y}; }
 __device__ __forceinline__ v2f hi2(float4 v) { return v2f{v.z, v.w}; }
+__device__ __forceinline__ v2f lo2(f4u v) { return v2f{v.x, v.y}; }
+__device__ __forceinline__ v2f hi2(f4u v) { return v2f{v.z, v.w}; }
+/* sorted-photon plane load: one buffer resource over the nine planes, the
+ * plane's byte offset in an SGPR (soffset) and the photon's byte offset in a
+ * VGPR, so the nine loads of a batch share one address register */
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4u ldp(__amdgpu_buffer_rsrc_t rs, uint32_t so, uint32_t bo) {
+    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)bo, (int)so, 0);
+    return f4u{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+}
 
 __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, Consts c) {
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -1179,7 +1190,10 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
                 const v2f nx2 = v2f{B.x, B.x}, ny2 = v2f{B.y, B.y}, nz2 = v2f{B.z, B.z};
                 const v2f r2v = v2f{radius2, radius2};
                 const size_t P = pb.splane;
-                const float* __restrict__ SX = pb.sorted;
+                /* 9 * P * 4 < 4 GiB: checked on the host (resize) */
+                const __amdgpu_buffer_rsrc_t SR =
+                    __builtin_amdgcn_make_buffer_rsrc((void*)pb.sorted, 0, 0xffffffff, 0x00020000);
+                const uint32_t PB = (uint32_t)P * 4u;
                 /* Row culling: a (z,y) row whose cell square (grown by a margin
                  * m that covers the rounding of the cell assignment) lies
                  * outside the sphere holds no photon within r; otherwise only
@@ -1222,28 +1236,27 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
                         }
                         ORX_TS_INC(ts_leaves, 1);
                         ORX_TS_WAVE(ts_wl);
-                        for (uint32_t kb = off & ~3u; kb < offTo; kb += 4) {
+                        /* batches start at `off` itself (dword-aligned dwordx4 loads), so only
+                         * the last batch of a range can hold photons past its end; the loads
+                         * address nine uniform plane bases with one 32-bit byte offset */
+                        const uint32_t e1 = offTo - 1, e2 = offTo - 2, e3 = offTo - 3;
+                        for (uint32_t kb = off; kb < offTo; kb += 4) {
                             ORX_TS_INC(ts_nodes, 1);
                             ORX_TS_WAVE(ts_wn);
-                            const float4 X = *(const float4*)(SX + kb);
-                            const float4 Y = *(const float4*)(SX + P + kb);
-                            const float4 Z = *(const float4*)(SX + 2 * P + kb);
+                            const uint32_t bo = kb << 2;
+                            const f4u X = ldp(SR, 0u, bo), Y = ldp(SR, PB, bo), Z = ldp(SR, 2u * PB, bo);
                             const v2f dx0 = px2 - lo2(X), dx1 = px2 - hi2(X);
                             const v2f dy0 = py2 - lo2(Y), dy1 = py2 - hi2(Y);
                             const v2f dz0 = pz2 - lo2(Z), dz1 = pz2 - hi2(Z);
                             const v2f d20 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
                             const v2f d21 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
-                            bool in0 = kb >= off && d20.x <= radius2;
-                            bool in1 = kb + 1 >= off && kb + 1 < offTo && d20.y <= radius2;
-                            bool in2 = kb + 2 >= off && kb + 2 < offTo && d21.x <= radius2;
-                            bool in3 = kb + 3 < offTo && d21.y <= radius2;
+                            bool in0 = d20.x <= radius2;
+                            bool in1 = kb < e1 && d20.y <= radius2;
+                            bool in2 = kb < e2 && d21.x <= radius2;
+                            bool in3 = kb < e3 && d21.y <= radius2;
                             if (!(in0 | in1 | in2 | in3)) continue;
-                            const float4 DX = *(const float4*)(SX + 3 * P + kb);
-                            const float4 DY = *(const float4*)(SX + 4 * P + kb);
-                            const float4 DZ = *(const float4*)(SX + 5 * P + kb);
-                            const float4 WX = *(const float4*)(SX + 6 * P + kb);
-                            const float4 WY = *(const float4*)(SX + 7 * P + kb);
-                            const float4 WZ = *(const float4*)(SX + 8 * P + kb);
+                            const f4u DX = ldp(SR, 3u * PB, bo), DY = ldp(SR, 4u * PB, bo), DZ = ldp(SR, 5u * PB, bo);
+                            const f4u WX = ldp(SR, 6u * PB, bo), WY = ldp(SR, 7u * PB, bo), WZ = ldp(SR, 8u * PB, bo);
                             /* dot(-dir, n) >= 0  <=>  dot(dir, n) <= 0 (negation is exact) */
                             const v2f nd0 = (lo2(DX) * nx2 + lo2(DY) * ny2) + lo2(DZ) * nz2;
                             const v2f nd1 = (hi2(DX) * nx2 + hi2(DY) * ny2) + hi2(DZ) * nz2;
@@ -1253,10 +1266,12 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
                             in3 = in3 && nd1.y <= 0.f;
                             /* photonPower: alpha*(1 - (1 - exp(x)) / (1 - e^-beta)), x = -beta d^2 / 2r^2,
                              * folded into one Horner chain w = (A + B) + x*B*p(x) with A = alpha*(1 - 1/den),
-                             * B = alpha/den, evaluated with fused multiply-adds, two photons per v_pk_fma_f32;
-                             * rejected photons get weight 0 and everything accumulates by pk_fma */
-                            const v2f x0 = __builtin_elementwise_min(d20, r2v) * kx2;
-                            const v2f x1 = __builtin_elementwise_min(d21, r2v) * kx2;
+                             * B = alpha/den, evaluated with fused multiply-adds, two photons per v_pk_fma_f32.
+                             * Rejected photons (whose x may lie outside [-beta/2, 0]) get weight 0 by
+                             * select, so their polynomial value is never used; everything accumulates
+                             * by pk_fma */
+                            const v2f x0 = d20 * kx2;
+                            const v2f x1 = d21 * kx2;
                             v2f q0 = wc6, q1 = wc6;
                             q0 = __builtin_elementwise_fma(q0, x0, wc5); q1 = __builtin_elementwise_fma(q1, x1, wc5);
                             q0 = __builtin_elementwise_fma(q0, x0, wc4); q1 = __builtin_elementwise_fma(q1, x1, wc4);
@@ -1458,9 +1473,207 @@ __global__ __launch_bounds__(64) void k_ppm_gather_coop(GatherIn gi, PhotonBufs 
         atomicAdd((unsigned long long*)&pb.grid->cells_visited_total, (unsigned long long)sc);
     }
 }
+/* Wave-broadcast gather (variant 2): one wave per 8x8 pixel tile walks, row by
+ * row, the union of its lanes' chord-trimmed photon ranges; four photons at a
+ * time come in through scalar loads (SGPRs: no per-lane vector-memory traffic,
+ * which is what bounds the per-pixel kernel -- its texture-address unit is
+ * busy for the whole launch) and every lane tests them against its own range,
+ * radius and normal with the per-pixel kernel's packed arithmetic.  Each
+ * pixel sees exactly the photons of k_ppm_gather in the same row order; only
+ * the pairing of photons into the two accumulator halves differs (rounding). */
+__global__ __launch_bounds__(256) void k_ppm_gather_wave(GatherIn gi, PhotonBufs pb, Consts c) {
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (l & 7);
+    const uint32_t j = blockIdx.y * 16 + (w >> 1) * 8 + (l >> 3);
+    const GridParams g = *pb.grid;
+    const bool inimg = x < gi.W && j < gi.segments * gi.seg_rows;
+    const size_t i = (size_t)j * gi.W + x;
+    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+    float2 Cc = make_float2(0.f, 0.f);
+    if (inimg) {
+        const HpRef hr = hp_ref(gi, j, x);
+        A = hr.A[hr.li];
+        B = hr.B[hr.li];
+        Cc = hr.C[hr.li];
+    }
+    const uint32_t flags = __float_as_uint(A.w);
+    const f3 pos = mk(A.x, A.y, A.z);
+    const float radius2 = c.ppm_radius2;
+    const float radius = c.ppm_radius;
+    const float invCellSize = 1.f / g.cell;
+    const f3 np = pos - mk(g.ox, g.oy, g.oz);
+    uint32_t x_lo = 1, x_hi = 0, y_lo = 1, y_hi = 0, z_lo = 1, z_hi = 0;
+    bool active = false;
+    if (inimg && (flags & PRD_HIT_NON_SPECULAR) && g.G) {
+        const int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
+        const int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
+        const int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
+        x_lo = (uint32_t)(ixl > 0 ? ixl : 0);
+        y_lo = (uint32_t)(iyl > 0 ? iyl : 0);
+        z_lo = (uint32_t)(izl > 0 ? izl : 0);
+        const uint32_t ux = orx_f2u_sat((np.x + radius) * invCellSize);
+        const uint32_t uy = orx_f2u_sat((np.y + radius) * invCellSize);
+        const uint32_t uz = orx_f2u_sat((np.z + radius) * invCellSize);
+        x_hi = (g.gx - 1) < ux ? (g.gx - 1) : ux;
+        y_hi = (g.gy - 1) < uy ? (g.gy - 1) : uy;
+        z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
+        active = x_lo <= x_hi;
+    }
+    uint32_t uz_lo = active ? z_lo : 0xffffffffu, uz_hi = active ? z_hi : 0u;
+    uint32_t uy_lo = active ? y_lo : 0xffffffffu, uy_hi = active ? y_hi : 0u;
+    for (int o = 32; o > 0; o >>= 1) {
+        uz_lo = min(uz_lo, (uint32_t)__shfl_xor((int)uz_lo, o, 64));
+        uz_hi = max(uz_hi, (uint32_t)__shfl_xor((int)uz_hi, o, 64));
+        uy_lo = min(uy_lo, (uint32_t)__shfl_xor((int)uy_lo, o, 64));
+        uy_hi = max(uy_hi, (uint32_t)__shfl_xor((int)uy_hi, o, 64));
+    }
+    uz_lo = __builtin_amdgcn_readfirstlane(uz_lo);
+    uz_hi = __builtin_amdgcn_readfirstlane(uz_hi);
+    uy_lo = __builtin_amdgcn_readfirstlane(uy_lo);
+    uy_hi = __builtin_amdgcn_readfirstlane(uy_hi);
+    uint32_t dC = 0, dP = 0, dU = 0;
+    const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
+    const float inv2r2 = 1.0f / (2 * radius2);
+    const float invDen = 1.0f / (1 - expNegativeBeta);
+    const float kx = -beta * inv2r2;
+    const float wB = alpha * invDen, wA = alpha - wB;
+    const v2f kx2 = v2f{kx, kx};
+    const v2f wc6 = wB * ORX_EXPU_C6, wc5 = wB * ORX_EXPU_C5, wc4 = wB * ORX_EXPU_C4;
+    const v2f wc3 = wB * ORX_EXPU_C3, wc2 = wB * ORX_EXPU_C2, wc1 = wB * ORX_EXPU_C1;
+    const v2f wc0 = v2f{wA + wB, wA + wB};
+    v2f accx = v2f{0.f, 0.f}, accy = accx, accz = accx;
+    const v2f px2 = v2f{pos.x, pos.x}, py2 = v2f{pos.y, pos.y}, pz2 = v2f{pos.z, pos.z};
+    const v2f nx2 = v2f{B.x, B.x}, ny2 = v2f{B.y, B.y}, nz2 = v2f{B.z, B.z};
+    const size_t P = pb.splane;
+    const float* __restrict__ S0 = pb.sorted;
+    const float m = g.cell * 1e-3f;
+    for (uint32_t z = uz_lo; z <= uz_hi && uz_lo <= uz_hi; z++) {
+        const float zc0 = g.oz + (float)z * g.cell - m, zc1 = g.oz + (float)(z + 1) * g.cell + m;
+        const float dz = fmaxf(0.f, fmaxf(zc0 - pos.z, pos.z - zc1));
+        for (uint32_t yy = uy_lo; yy <= uy_hi; yy++) {
+            const uint32_t row = yy * g.gx + z * g.gx * g.gy;
+            uint32_t off = 0xffffffffu, offTo = 0u;
+            if (active && z >= z_lo && z <= z_hi && yy >= y_lo && yy <= y_hi) {
+                const uint32_t from = x_lo + row;
+                const uint32_t to = from + (x_hi - x_lo);
+                dC++;
+                dP += pb.offsets[to + 1] - pb.offsets[from];
+                const float yc0 = g.oy + (float)yy * g.cell - m, yc1 = g.oy + (float)(yy + 1) * g.cell + m;
+                const float dy = fmaxf(0.f, fmaxf(yc0 - pos.y, pos.y - yc1));
+                const float rem = radius2 - dy * dy - dz * dz;
+                if (rem >= 0.f) {
+                    const float rx = sqrtf(rem) + m;
+                    const int32_t cxl = orx_f2i_sat(orx_floorf((np.x - rx) * invCellSize));
+                    const int32_t cxh = orx_f2i_sat(orx_floorf((np.x + rx) * invCellSize));
+                    const uint32_t xl = cxl > (int32_t)x_lo ? (uint32_t)cxl : x_lo;
+                    const uint32_t xh = cxh < (int32_t)x_hi ? (uint32_t)cxh : x_hi;
+                    if (cxh >= 0 && xl <= xh) {
+                        if (pb.subofs) {
+                            const float sx = invCellSize * (float)SUBX;
+                            const int32_t q0 = orx_f2i_sat(orx_floorf((np.x - rx) * sx));
+                            const int32_t q1 = orx_f2i_sat(orx_floorf((np.x + rx) * sx));
+                            const uint32_t a0 = q0 > (int32_t)(SUBX * xl) ? (uint32_t)q0 : SUBX * xl;
+                            const uint32_t a1 = q1 < (int32_t)(SUBX * xh + SUBX - 1) ? (uint32_t)q1 : SUBX * xh + SUBX - 1;
+                            if (q1 >= 0 && a0 <= a1) {
+                                off = pb.subofs[SUBX * row + a0];
+                                offTo = pb.subofs[SUBX * row + a1 + 1];
+                            }
+                        } else {
+                            off = pb.offsets[xl + row];
+                            offTo = pb.offsets[xh + row + 1];
+                        }
+                    }
+                }
+            }
+            if (off >= offTo) { off = 0xffffffffu; offTo = 0u; }
+            uint32_t rlo = off, rhi = offTo;
+            for (int o = 32; o > 0; o >>= 1) {
+                rlo = min(rlo, (uint32_t)__shfl_xor((int)rlo, o, 64));
+                rhi = max(rhi, (uint32_t)__shfl_xor((int)rhi, o, 64));
+            }
+            rlo = __builtin_amdgcn_readfirstlane(rlo);
+            rhi = __builtin_amdgcn_readfirstlane(rhi);
+            if (rlo >= rhi) continue;
+            dU += rhi - rlo;
+            const uint32_t len = offTo - off; /* 0 for lanes without photons in this row (offTo = 0 < off) */
+            for (uint32_t k = rlo; k < rhi; k += 4) {
+                const uint32_t ku = __builtin_amdgcn_readfirstlane(k);
+                const f4u X = *(const f4u*)(S0 + ku);
+                const f4u Y = *(const f4u*)(S0 + P + ku);
+                const f4u Z = *(const f4u*)(S0 + 2 * P + ku);
+                const f4u DX = *(const f4u*)(S0 + 3 * P + ku);
+                const f4u DY = *(const f4u*)(S0 + 4 * P + ku);
+                const f4u DZ = *(const f4u*)(S0 + 5 * P + ku);
+                const f4u WX = *(const f4u*)(S0 + 6 * P + ku);
+                const f4u WY = *(const f4u*)(S0 + 7 * P + ku);
+                const f4u WZ = *(const f4u*)(S0 + 8 * P + ku);
+                const uint32_t t = ku - off;
+                const v2f dx0 = px2 - lo2(X), dx1 = px2 - hi2(X);
+                const v2f dy0 = py2 - lo2(Y), dy1 = py2 - hi2(Y);
+                const v2f dz0 = pz2 - lo2(Z), dz1 = pz2 - hi2(Z);
+                const v2f d20 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
+                const v2f d21 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
+                bool in0 = t < len && d20.x <= radius2;
+                bool in1 = t + 1 < len && d20.y <= radius2;
+                bool in2 = t + 2 < len && d21.x <= radius2;
+                bool in3 = t + 3 < len && d21.y <= radius2;
+                const v2f nd0 = (lo2(DX) * nx2 + lo2(DY) * ny2) + lo2(DZ) * nz2;
+                const v2f nd1 = (hi2(DX) * nx2 + hi2(DY) * ny2) + hi2(DZ) * nz2;
+                in0 = in0 && nd0.x <= 0.f;
+                in1 = in1 && nd0.y <= 0.f;
+                in2 = in2 && nd1.x <= 0.f;
+                in3 = in3 && nd1.y <= 0.f;
+                const v2f x0 = d20 * kx2;
+                const v2f x1 = d21 * kx2;
+                v2f q0 = wc6, q1 = wc6;
+                q0 = __builtin_elementwise_fma(q0, x0, wc5); q1 = __builtin_elementwise_fma(q1, x1, wc5);
+                q0 = __builtin_elementwise_fma(q0, x0, wc4); q1 = __builtin_elementwise_fma(q1, x1, wc4);
+                q0 = __builtin_elementwise_fma(q0, x0, wc3); q1 = __builtin_elementwise_fma(q1, x1, wc3);
+                q0 = __builtin_elementwise_fma(q0, x0, wc2); q1 = __builtin_elementwise_fma(q1, x1, wc2);
+                q0 = __builtin_elementwise_fma(q0, x0, wc1); q1 = __builtin_elementwise_fma(q1, x1, wc1);
+                v2f w0 = __builtin_elementwise_fma(q0, x0, wc0), w1 = __builtin_elementwise_fma(q1, x1, wc0);
+                w0.x = in0 ? w0.x : 0.f;
+                w0.y = in1 ? w0.y : 0.f;
+                w1.x = in2 ? w1.x : 0.f;
+                w1.y = in3 ? w1.y : 0.f;
+                accx = __builtin_elementwise_fma(lo2(WX), w0, accx);
+                accy = __builtin_elementwise_fma(lo2(WY), w0, accy);
+                accz = __builtin_elementwise_fma(lo2(WZ), w0, accz);
+                accx = __builtin_elementwise_fma(hi2(WX), w1, accx);
+                accy = __builtin_elementwise_fma(hi2(WY), w1, accy);
+                accz = __builtin_elementwise_fma(hi2(WZ), w1, accz);
+            }
+        }
+    }
+    if (inimg) {
+        const float ax = accx.x + accx.y, ay = accy.x + accy.y, az = accz.x + accz.y;
+        const f3 att = mk(B.w, Cc.x, Cc.y);
+        const float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
+        const float s2 = 1.0f / c.emitted_f;
+        const f3 ind = ((mk(ax, ay, az) * att) * s1) * s2;
+        gi.indirect[3 * i + 0] = ind.x;
+        gi.indirect[3 * i + 1] = ind.y;
+        gi.indirect[3 * i + 2] = ind.z;
+        if (gi.dbg) {
+            gi.dbg[2 * i] = dC;
+            gi.dbg[2 * i + 1] = dP;
+        }
+    }
+    const uint64_t sp = wave_sum_u64(dP), sc = wave_sum_u64(dC);
+    if (l == 0 && sp) {
+        atomicAdd((unsigned long long*)&pb.grid->union_photons_total, (unsigned long long)dU);
+        atomicAdd((unsigned long long*)&pb.grid->photons_visited, (unsigned long long)sp);
+        atomicAdd((unsigned long long*)&pb.grid->cells_visited, (unsigned long long)sc);
+        atomicAdd((unsigned long long*)&pb.grid->photons_visited_total, (unsigned long long)sp);
+        atomicAdd((unsigned long long*)&pb.grid->cells_visited_total, (unsigned long long)sc);
+    }
+}
 void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, int variant) {
     const uint32_t rows = gi.segments * gi.seg_rows;
-    if (variant != 1) {
+    if (variant == 2) {
+        dim3 grid((gi.W + 15) / 16, (rows + 15) / 16);
+        hipLaunchKernelGGL(k_ppm_gather_wave, grid, dim3(256), 0, s, gi, pb, c);
+    } else if (variant != 1) {
         dim3 grid((gi.W + 15) / 16, (rows + 15) / 16);
         hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), 0, s, gi, pb, c);
     } else {
