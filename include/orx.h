@@ -159,7 +159,9 @@ typedef struct {
     uint32_t vcm_max_path_length;     /* VCM_MAX_PATH_LENGTH = 10 */
     uint32_t seed;                    /* 0: 574133*clock()+47844152748*time() like SpatialHash.cu:322; else DEBUG_RANDOM_SEED */
     uint32_t debug_counters;          /* 1: keep per-pixel cells/photons visited (OptixRenderer.cpp:872-953) */
-    uint32_t gather_variant;          /* 0: one thread per pixel in 8x8 wave tiles (default), 1: wave-cooperative LDS staging */
+    uint32_t gather_variant;          /* photon-grid layout for the gather: 0 (default) photons ordered by
+                                         cell-row quarter sub-rows (y and z halves) and x quarters; 1 photons in
+                                         cell order with x quarters only.  Any other value: ORX_ERR_INVALID_ARGUMENT */
     uint32_t reserved[6];
 } orx_config;
 
@@ -230,7 +232,7 @@ typedef struct {
     uint64_t photons_visited_total; /* summed since orx_reset_timing */
     uint64_t cells_visited_total;
     uint64_t valid_photons_total;
-    uint64_t gather_staged_total;   /* cooperative gather: photons staged through LDS, summed over waves */
+    uint64_t gather_staged_total;   /* reserved: 0 */
     uint32_t timed_iterations;   /* iterations since orx_reset_timing */
     uint32_t bvh_stack_entries;  /* LDS traversal stack depth bound of the scene's BVH4 */
     float pass_ms[16];           /* device time per orx_pass summed since orx_reset_timing */

@@ -453,7 +453,8 @@ orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out)
     if (cfg) r->cfg = *cfg;
     else orx_default_config(&r->cfg);
     if (r->cfg.max_photon_deposits == 0 || r->cfg.max_photon_deposits > 8 || r->cfg.photon_launch_width == 0 ||
-        r->cfg.photon_launch_height == 0 || r->cfg.photon_grid_max_size == 0) {
+        r->cfg.photon_launch_height == 0 || r->cfg.photon_grid_max_size == 0 ||
+        r->cfg.photon_grid_max_size > (1u << 26) || r->cfg.gather_variant > 1) {
         delete r;
         return ORX_ERR_INVALID_ARGUMENT;
     }
@@ -810,17 +811,20 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_wray1.ensure(nphot * 32 + 32));
     HIPCHK(r, r->d_whit.ensure(nphot * 32 + 32));
     HIPCHK(r, r->d_wpath.ensure(nphot * 32 + 32));
-    /* bucket-sort grid build: at most 1024 buckets of 2^bshift cells */
+    /* bucket-sort grid build: at most 2048 buckets of 2^bshift virtual cells
+     * (nsub sub-rows per cell row, k_bs_count) */
+    const uint32_t nsub = r->cfg.gather_variant == 1 ? 1u : SUBR * SUBR;
+    const size_t vmax = (size_t)r->cfg.photon_grid_max_size * nsub;
     uint32_t bshift = 10;
-    while ((((size_t)r->cfg.photon_grid_max_size + (1u << bshift) - 1) >> bshift) > 1024) bshift++;
+    while (((vmax + (1u << bshift) - 1) >> bshift) > 2048) bshift++;
     const size_t bs_nchunk = (S + 16383) / 16384;
-    const size_t bs_nbmax = ((size_t)r->cfg.photon_grid_max_size + (1u << bshift) - 1) >> bshift;
+    const size_t bs_nbmax = (vmax + (1u << bshift) - 1) >> bshift;
     const size_t bs_nscan = (bs_nbmax * bs_nchunk + 1023) / 1024;
     HIPCHK(r, r->d_pos4.ensure(S * 16 + 16));
     HIPCHK(r, r->d_bstable.ensure(bs_nbmax * bs_nchunk * 4 + 16));
     HIPCHK(r, r->d_bspartials.ensure((bs_nscan + 2) * 4));
     HIPCHK(r, r->d_bspairs.ensure(S * 8 + 16));
-    HIPCHK(r, r->d_subofs.ensure(G2 * 4 * SUBX + 16));
+    HIPCHK(r, r->d_subofs.ensure(G2 * 4 * SUBX * nsub + 16));
     const size_t wnseg = (nphot + 511) / 512 + 1;
     HIPCHK(r, r->d_wseg.ensure(2 * wnseg * 4));
     HIPCHK(r, hipMemsetAsync(r->d_wseg.p, 0, 2 * wnseg * 4, r->stream));
@@ -875,6 +879,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     pb.wpath = r->d_wpath.as<float4>();
     pb.pos4 = r->d_pos4.as<float4>();
     pb.bshift = bshift;
+    pb.nsub = nsub;
     pb.bs_nchunk = (uint32_t)bs_nchunk;
     pb.bs_table = r->d_bstable.as<uint32_t>();
     pb.bs_partials = r->d_bspartials.as<uint32_t>();
@@ -885,6 +890,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
             return e ? atoi(e) : 0;
         }();
         pb.subofs = atomic_grid_env ? nullptr : r->d_subofs.as<uint32_t>();
+        if (atomic_grid_env) pb.nsub = 1; /* the atomic path sorts by cell only */
     }
     pb.wseg = r->d_wseg.as<uint32_t>();
     pb.wnseg = (uint32_t)wnseg;
@@ -1180,7 +1186,7 @@ orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
         r->overlap_direct = overlap != 0;
         ppm_local_passes(r, cam, c);
         ev_begin(r, P_GATHER);
-        launch_ppm_gather(st, local_gather_in(r), r->pb, c, (int)r->cfg.gather_variant);
+        launch_ppm_gather(st, local_gather_in(r), r->pb, c);
         ev_end(r, P_GATHER);
         ev_begin(r, P_DIRECT);
         if (r->overlap_direct) {
@@ -1265,7 +1271,7 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hp, uint32_t seg
     gi.indirect = (float*)indirect;
     gi.dbg = nullptr;
     ev_begin(r, P_GATHER);
-    launch_ppm_gather(cur_stream(r), gi, r->pb, r->last_consts, (int)r->cfg.gather_variant);
+    launch_ppm_gather(cur_stream(r), gi, r->pb, r->last_consts);
     ev_end(r, P_GATHER);
     HIPCHK(r, hipGetLastError());
     return ORX_OK;
@@ -1452,9 +1458,28 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
         std::vector<float> pl(9 * n);
         for (int q = 0; q < 9 && n; q++) HIPCHK(r, d2h(pl.data() + q * n, r->d_sorted.as<float>() + q * P, n * 4));
         static const int order[9] = {6, 7, 8, 0, 1, 2, 3, 4, 5};
+        /* sub-row layout: present the reference's cell order (each cell = its
+         * nsub sub-row pieces, k_bs_count); within a cell the order is free */
+        std::vector<uint32_t> idx;
+        if (r->pb.subofs && r->pb.nsub > 1 && n) {
+            const size_t rowlen = (size_t)g.gx * SUBX, nso = (size_t)g.G * r->pb.nsub * SUBX + 1;
+            std::vector<uint32_t> so(nso);
+            HIPCHK(r, d2h(so.data(), r->pb.subofs, nso * 4));
+            idx.reserve(n);
+            for (size_t c = 0; c < g.G; c++) {
+                const size_t row = c / g.gx, x = c % g.gx;
+                for (uint32_t sr = 0; sr < r->pb.nsub; sr++) {
+                    const size_t b = (row * r->pb.nsub + sr) * rowlen + x * SUBX;
+                    for (uint32_t k = so[b]; k < so[b + SUBX]; k++) idx.push_back(k);
+                }
+            }
+            if (idx.size() != n) return set_err(r, ORX_ERR_STATE, "sub-row offsets do not cover the valid photons");
+        }
         float* o = (float*)dst;
-        for (size_t i = 0; i < n; i++)
-            for (int k = 0; k < 9; k++) o[9 * i + k] = pl[order[k] * n + i];
+        for (size_t i = 0; i < n; i++) {
+            const size_t src = idx.empty() ? i : idx[i];
+            for (int k = 0; k < 9; k++) o[9 * i + k] = pl[order[k] * n + src];
+        }
         break;
     }
     case ORX_BUF_PHOTON_SLOTS: {

@@ -27,7 +27,7 @@ struct GridParams {
     uint64_t photons_visited_total; /* since orx_reset_timing */
     uint64_t cells_visited_total;
     uint64_t valid_total;
-    uint64_t union_photons_total; /* coop gather: photons staged per wave, summed */
+    uint64_t union_photons_total; /* reserved (stats ABI: gather_staged_total, always 0) */
     uint64_t st_lane_batches, st_wave_batches, st_lane_rows, st_wave_rows; /* ORX_TRAV_STATS builds: gather SIMT */
     uint64_t st_accepted;   /* ORX_TRAV_STATS builds: gather photons within r and facing the normal */
 };
@@ -55,6 +55,7 @@ struct PixelBufs {
 
 constexpr uint32_t BBOX_REPLICAS = 64;
 constexpr uint32_t SUBX = 4; /* sub-cells per grid cell along x (bucket-sort grid, gather chord trimming) */
+constexpr uint32_t SUBR = 2; /* sub-rows per grid cell along y and along z (bucket-sort grid, nsub = SUBR^2) */
 
 struct PhotonBufs {
     uint32_t PW, PH;    /* photon launch (full) */
@@ -86,7 +87,8 @@ struct PhotonBufs {
     uint32_t* bs_table; /* [buckets][chunks] counts, then exclusive offsets */
     uint32_t* bs_partials; /* scan partials + grand total */
     uint2* bs_pairs;    /* [S] (sub-cell key, slot) in bucket order; sub-cell key = cell * SUBX + x slice */
-    uint32_t* subofs;   /* [SUBX G + 1] first photon of each sub-cell (NULL: atomic grid path, cell offsets only) */
+    uint32_t* subofs;   /* [SUBX nsub G + 1] first photon of each sub-cell (NULL: atomic grid path, cell offsets only) */
+    uint32_t nsub;      /* sub-rows per cell row: 1 (photons in cell order) or SUBR^2 (see k_bs_count) */
     uint32_t* wseg;     /* [2][wnseg] live entries of each queue segment */
     uint32_t wnseg;     /* segments per queue */
 };
@@ -134,7 +136,7 @@ struct GatherIn {
     uint32_t* dbg;      /* [segments*seg_rows*W*2] or NULL */
 };
 /* variant 0: one thread per pixel, 8x8 wave tiles (default); 1: wave-cooperative LDS staging */
-void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, int variant);
+void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c);
 /* mode 0: direct + output; 1: direct only; 2: output only */
 void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c, int mode = 0);
 void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c);

@@ -906,17 +906,28 @@ __global__ __launch_bounds__(256) void k_grid_permute(PhotonBufs pb) {
  *                    appended to their bucket run
  *   C  k_bs_cells    one block per bucket: LDS histogram of its cells, LDS
  *                    scan -> offsets of those cells, permutation by LDS cursors
+ *   D  k_grid_coarse_offsets (nsub > 1) the reference's cell offsets
  * All counting is in LDS.  Offsets equal the reference's exclusive scan over
  * the cell histogram (keys >= G are the reference's overflow cell G and, as
- * there, fall beyond offsets[G] = valid: they are dropped). */
+ * there, fall beyond offsets[G] = valid: they are dropped).
+ *
+ * Sub-row layout (nsub = SUBR^2 = 4).  Photons are ordered by a virtual cell
+ *   vc = ((y + z gy) nsub + s) gx + x,   s = 2 (z half) + (y half),
+ * then by the x quarter: every cell row (y,z) is stored as four sub-rows, each
+ * holding the photons of one (y,z) quarter of the row's cells in x order.  A
+ * gather chord on a sub-row is one contiguous range of subofs, and the
+ * quarter-height sub-rows hug the sphere (fewer photons tested per pixel);
+ * the photons of a reference cell are the union of its four sub-row pieces,
+ * so the reference offsets (the visit counters, the exported grid) come from
+ * the sub-row offsets by k_grid_coarse_offsets. */
 constexpr uint32_t BS_CHUNK = 16384;
 constexpr uint32_t BS_THREADS = 512;
-constexpr uint32_t BS_MAXB = 1024; /* buckets */
+constexpr uint32_t BS_MAXB = 2048; /* buckets */
 
 __global__ __launch_bounds__(BS_THREADS) void k_bs_count(PhotonBufs pb) {
     __shared__ uint32_t hist[BS_MAXB];
     const GridParams g = *pb.grid;
-    const uint32_t nb = (g.G + (1u << pb.bshift) - 1) >> pb.bshift;
+    const uint32_t nb = (g.G * pb.nsub + (1u << pb.bshift) - 1) >> pb.bshift;
     for (uint32_t i = threadIdx.x; i < BS_MAXB; i += BS_THREADS) hist[i] = 0;
     __syncthreads();
     const float inv = 1.f / g.cell;
@@ -938,8 +949,17 @@ __global__ __launch_bounds__(BS_THREADS) void k_bs_count(PhotonBufs pb) {
                  * trim a row to the chord at quarter-cell granularity */
                 int32_t q = (int32_t)orx_floorf(pp.x * (float)SUBX) - (int32_t)SUBX * (int32_t)cx;
                 q = q < 0 ? 0 : (q > (int32_t)SUBX - 1 ? (int32_t)SUBX - 1 : q);
-                key = kk * SUBX + (uint32_t)q;
-                atomicAdd(&hist[kk >> pb.bshift], 1u);
+                uint32_t vc = kk;
+                if (pb.nsub > 1) { /* sub-row: y and z halves (x2 is exact, so the halves nest in the cells) */
+                    int32_t hy = (int32_t)orx_floorf(pp.y * (float)SUBR) - (int32_t)SUBR * (int32_t)cy;
+                    int32_t hz = (int32_t)orx_floorf(pp.z * (float)SUBR) - (int32_t)SUBR * (int32_t)cz;
+                    hy = hy < 0 ? 0 : (hy > (int32_t)SUBR - 1 ? (int32_t)SUBR - 1 : hy);
+                    hz = hz < 0 ? 0 : (hz > (int32_t)SUBR - 1 ? (int32_t)SUBR - 1 : hz);
+                    const uint32_t row = cy + cz * g.gy;
+                    vc = (row * pb.nsub + (uint32_t)hz * SUBR + (uint32_t)hy) * g.gx + cx;
+                }
+                key = vc * SUBX + (uint32_t)q;
+                atomicAdd(&hist[vc >> pb.bshift], 1u);
             }
         }
         pb.keys[s] = key;
@@ -950,7 +970,7 @@ __global__ __launch_bounds__(BS_THREADS) void k_bs_count(PhotonBufs pb) {
 
 /* exclusive scan of n = nb * nchunk table entries in place (three kernels, as k_scan_*) */
 __global__ __launch_bounds__(256) void k_bs_scan_reduce(PhotonBufs pb) {
-    const uint32_t nb = (pb.grid->G + (1u << pb.bshift) - 1) >> pb.bshift;
+    const uint32_t nb = (pb.grid->G * pb.nsub + (1u << pb.bshift) - 1) >> pb.bshift;
     const uint32_t n = nb * pb.bs_nchunk;
     const uint32_t base = blockIdx.x * SCAN_BLOCK + threadIdx.x * 4;
     uint32_t sum = 0;
@@ -974,7 +994,7 @@ __global__ __launch_bounds__(256) void k_bs_scan_partials(PhotonBufs pb, uint32_
     if (threadIdx.x == 0) pb.bs_partials[nblocks] = carry; /* grand total = valid photons */
 }
 __global__ __launch_bounds__(256) void k_bs_scan_apply(PhotonBufs pb) {
-    const uint32_t nb = (pb.grid->G + (1u << pb.bshift) - 1) >> pb.bshift;
+    const uint32_t nb = (pb.grid->G * pb.nsub + (1u << pb.bshift) - 1) >> pb.bshift;
     const uint32_t n = nb * pb.bs_nchunk;
     if (blockIdx.x * SCAN_BLOCK >= n) return;
     const uint32_t base = blockIdx.x * SCAN_BLOCK + threadIdx.x * 4;
@@ -993,7 +1013,7 @@ __global__ __launch_bounds__(256) void k_bs_scan_apply(PhotonBufs pb) {
 
 __global__ __launch_bounds__(BS_THREADS) void k_bs_place(PhotonBufs pb) {
     __shared__ uint32_t cur[BS_MAXB];
-    const uint32_t G = pb.grid->G;
+    const uint32_t G = pb.grid->G * pb.nsub;
     const uint32_t nb = (G + (1u << pb.bshift) - 1) >> pb.bshift;
     for (uint32_t b = threadIdx.x; b < nb; b += BS_THREADS) cur[b] = pb.bs_table[(size_t)b * pb.bs_nchunk + blockIdx.x];
     __syncthreads();
@@ -1009,12 +1029,12 @@ __global__ __launch_bounds__(BS_THREADS) void k_bs_place(PhotonBufs pb) {
     }
 }
 
-/* one block per bucket: histogram of its sub-cells (cell x quarter), LDS
- * scan -> cell offsets (the reference's) and sub-cell offsets (the gather's
- * chord trimming), permutation by LDS cursors */
+/* one block per bucket: histogram of its sub-cells (virtual cell x quarter),
+ * LDS scan -> sub-cell offsets (the gather's chord trimming) and, for nsub = 1,
+ * the cell offsets (the reference's), permutation by LDS cursors */
 __global__ __launch_bounds__(1024) void k_bs_cells(PhotonBufs pb, uint32_t cb, uint32_t nscan) {
     extern __shared__ uint32_t lds[]; /* [SUBX * cb] histogram / cursors */
-    const uint32_t G = pb.grid->G;
+    const uint32_t G = pb.grid->G * pb.nsub; /* virtual cells */
     const uint32_t nb = (G + cb - 1) / cb;
     const uint32_t b = blockIdx.x;
     const uint32_t total = pb.bs_partials[nscan]; /* grand total written by k_bs_scan_partials */
@@ -1048,7 +1068,7 @@ __global__ __launch_bounds__(1024) void k_bs_cells(PhotonBufs pb, uint32_t cb, u
         const uint32_t f = f0 + t0 + k, c = f / SUBX;
         const uint32_t v = lds[t0 + k];
         if (c <= G) {
-            if (f % SUBX == 0) pb.offsets[c] = ex;
+            if (f % SUBX == 0 && pb.nsub == 1) pb.offsets[c] = ex;
             if (c < G || f % SUBX == 0) pb.subofs[f] = ex;
         }
         lds[t0 + k] = ex; /* becomes the sub-cell's cursor */
@@ -1066,8 +1086,27 @@ __global__ __launch_bounds__(1024) void k_bs_cells(PhotonBufs pb, uint32_t cb, u
     }
 }
 
+/* the reference's cell offsets from the sub-row offsets: cell (x, row) starts
+ * after all photons of the earlier rows and, in each of the row's nsub
+ * sub-rows, after the photons of cells x' < x */
+__global__ __launch_bounds__(256) void k_grid_coarse_offsets(PhotonBufs pb) {
+    const GridParams g = *pb.grid;
+    const uint32_t rowlen = g.gx * SUBX;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c <= g.G; c += gridDim.x * blockDim.x) {
+        const uint32_t row = c / g.gx, x = c - row * g.gx;
+        const size_t r0 = (size_t)row * pb.nsub * rowlen;
+        uint32_t o = pb.subofs[r0];
+        if (c < g.G)
+            for (uint32_t s = 0; s < pb.nsub; s++) {
+                const size_t b = r0 + (size_t)s * rowlen;
+                o += pb.subofs[b + x * SUBX] - pb.subofs[b];
+            }
+        pb.offsets[c] = o;
+    }
+}
+
 static uint32_t bs_nscan(const PhotonBufs& pb) {
-    const uint32_t nbmax = (pb.gmax + (1u << pb.bshift) - 1) >> pb.bshift;
+    const uint32_t nbmax = (pb.gmax * pb.nsub + (1u << pb.bshift) - 1) >> pb.bshift;
     return (nbmax * pb.bs_nchunk + SCAN_BLOCK - 1) / SCAN_BLOCK;
 }
 void launch_grid_bucket_count(hipStream_t s, const PhotonBufs& pb) {
@@ -1082,8 +1121,13 @@ void launch_grid_bucket_scan(hipStream_t s, const PhotonBufs& pb) {
 void launch_grid_bucket_place(hipStream_t s, const PhotonBufs& pb) {
     hipLaunchKernelGGL(k_bs_place, dim3(pb.bs_nchunk), dim3(BS_THREADS), 0, s, pb);
     const uint32_t cb = 1u << pb.bshift;
-    const uint32_t nbmax = (pb.gmax + cb - 1) / cb;
+    const uint32_t nbmax = (pb.gmax * pb.nsub + cb - 1) / cb;
     hipLaunchKernelGGL(k_bs_cells, dim3(nbmax + 1), dim3(1024), SUBX * cb * 4, s, pb, cb, bs_nscan(pb));
+    if (pb.nsub > 1) {
+        unsigned cblocks = (pb.gmax + 1 + 255) / 256;
+        if (cblocks > 4096) cblocks = 4096;
+        hipLaunchKernelGGL(k_grid_coarse_offsets, dim3(cblocks), dim3(256), 0, s, pb);
+    }
     unsigned blocks = (pb.S + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(k_grid_permute, dim3(blocks), dim3(256), 0, s, pb);
@@ -1188,29 +1232,33 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
                 v2f accx = v2f{0.f, 0.f}, accy = accx, accz = accx;
                 const v2f px2 = v2f{pos.x, pos.x}, py2 = v2f{pos.y, pos.y}, pz2 = v2f{pos.z, pos.z};
                 const v2f nx2 = v2f{B.x, B.x}, ny2 = v2f{B.y, B.y}, nz2 = v2f{B.z, B.z};
-                const v2f r2v = v2f{radius2, radius2};
                 const size_t P = pb.splane;
                 /* 9 * P * 4 < 4 GiB: checked on the host (resize) */
                 const __amdgpu_buffer_rsrc_t SR =
                     __builtin_amdgcn_make_buffer_rsrc((void*)pb.sorted, 0, 0xffffffff, 0x00020000);
                 const uint32_t PB = (uint32_t)P * 4u;
-                /* Row culling: a (z,y) row whose cell square (grown by a margin
-                 * m that covers the rounding of the cell assignment) lies
-                 * outside the sphere holds no photon within r; otherwise only
-                 * the cells the chord [p.x - rx, p.x + rx] (+m) touches are
-                 * walked.  The visit counters stay the reference's (whole
-                 * window, IndirectRadianceEstimation.cu:113/:124). */
+                /* Row culling: a (z,y) sub-row whose box (grown by a margin m
+                 * that covers the rounding of the cell / half-cell assignment)
+                 * lies outside the sphere holds no photon within r; otherwise
+                 * only the x quarters the chord [p.x - rx, p.x + rx] (+m)
+                 * touches are walked.  The visit counters stay the reference's
+                 * (whole window, IndirectRadianceEstimation.cu:113/:124). */
                 const float m = g.cell * 1e-3f;
+                const uint32_t nsub = pb.subofs ? pb.nsub : 1u;
+                const uint32_t hs = nsub > 1 ? SUBR : 1u;
+                const float hc = g.cell / (float)hs; /* exact: hs is 1 or 2 */
                 for (uint32_t z = z_lo; z <= z_hi; z++) {
-                    const float zc0 = g.oz + (float)z * g.cell - m, zc1 = g.oz + (float)(z + 1) * g.cell + m;
-                    const float dz = fmaxf(0.f, fmaxf(zc0 - pos.z, pos.z - zc1));
                     for (uint32_t yy = y_lo; yy <= y_hi; yy++) {
                         const uint32_t row = yy * g.gx + z * g.gx * g.gy;
                         const uint32_t from = x_lo + row;
                         const uint32_t to = from + (x_hi - x_lo);
                         dC++;
                         dP += pb.offsets[to + 1] - pb.offsets[from];
-                        const float yc0 = g.oy + (float)yy * g.cell - m, yc1 = g.oy + (float)(yy + 1) * g.cell + m;
+                      for (uint32_t sr = 0; sr < nsub; sr++) {
+                        const uint32_t hz = z * hs + sr / hs, hy = yy * hs + sr % hs;
+                        const float zc0 = g.oz + (float)hz * hc - m, zc1 = g.oz + (float)(hz + 1) * hc + m;
+                        const float dz = fmaxf(0.f, fmaxf(zc0 - pos.z, pos.z - zc1));
+                        const float yc0 = g.oy + (float)hy * hc - m, yc1 = g.oy + (float)(hy + 1) * hc + m;
                         const float dy = fmaxf(0.f, fmaxf(yc0 - pos.y, pos.y - yc1));
                         const float rem = radius2 - dy * dy - dz * dz;
                         if (rem < 0.f) continue;
@@ -1221,15 +1269,16 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
                         const uint32_t xh = cxh < (int32_t)x_hi ? (uint32_t)cxh : x_hi;
                         if (cxh < 0 || xl > xh) continue;
                         uint32_t off, offTo;
-                        if (pb.subofs) { /* sub-cell trimming of the chord's end cells */
+                        if (pb.subofs) { /* x-quarter trimming of the chord's end cells */
                             const float sx = invCellSize * (float)SUBX;
                             const int32_t q0 = orx_f2i_sat(orx_floorf((np.x - rx) * sx));
                             const int32_t q1 = orx_f2i_sat(orx_floorf((np.x + rx) * sx));
                             const uint32_t a0 = q0 > (int32_t)(SUBX * xl) ? (uint32_t)q0 : SUBX * xl;
                             const uint32_t a1 = q1 < (int32_t)(SUBX * xh + SUBX - 1) ? (uint32_t)q1 : SUBX * xh + SUBX - 1;
                             if (q1 < 0 || a0 > a1) continue;
-                            off = pb.subofs[SUBX * row + a0];
-                            offTo = pb.subofs[SUBX * row + a1 + 1];
+                            const uint32_t* so = pb.subofs + ((size_t)(yy + z * g.gy) * nsub + sr) * g.gx * SUBX;
+                            off = so[a0];
+                            offTo = so[a1 + 1];
                         } else {
                             off = pb.offsets[xl + row];
                             offTo = pb.offsets[xh + row + 1];
@@ -1291,6 +1340,7 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
                             accy = __builtin_elementwise_fma(hi2(WY), w1, accy);
                             accz = __builtin_elementwise_fma(hi2(WZ), w1, accz);
                         }
+                      }
                     }
                 }
                 ax = accx.x + accx.y;
@@ -1326,360 +1376,10 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
     }
 }
 
-/* Wave-cooperative gather: one 64-lane wave owns an 8x8 pixel tile.  For
- * every (z,y) cell row that any lane's window touches, the wave stages the
- * row's photons (the union of the lanes' contiguous sub-ranges) through LDS
- * in chunks of 64 with one coalesced load per lane, then every lane tests
- * every staged photon against its own [offset[from], offset[to+1]) range
- * and radius.  Each pixel therefore visits exactly the photons of the
- * per-pixel loop above, in the same order (rows in z,y order, photons in
- * grid order), so the sums are bit-identical to k_ppm_gather; only the
- * photon loads are shared and the inner loop is divergence-free. */
-__global__ __launch_bounds__(64) void k_ppm_gather_coop(GatherIn gi, PhotonBufs pb, Consts c) {
-    __shared__ float4 sA[64];
-    __shared__ float4 sB[64];
-    __shared__ float sC[64];
-    const uint32_t lane = threadIdx.x;
-    const uint32_t x = blockIdx.x * 8 + (lane & 7);
-    const uint32_t j = blockIdx.y * 8 + (lane >> 3);
-    const GridParams g = *pb.grid;
-    const bool inimg = x < gi.W && j < gi.segments * gi.seg_rows;
-    const size_t i = (size_t)j * gi.W + x;
-    float4 A = make_float4(0, 0, 0, 0), B = A;
-    float2 Cc = make_float2(0, 0);
-    if (inimg) {
-        const HpRef hr = hp_ref(gi, j, x);
-        A = hr.A[hr.li];
-        B = hr.B[hr.li];
-        Cc = hr.C[hr.li];
-    }
-    const uint32_t flags = __float_as_uint(A.w);
-    const f3 pos = mk(A.x, A.y, A.z);
-    const f3 nrm = mk(B.x, B.y, B.z);
-    const float radius2 = c.ppm_radius2;
-    const float radius = c.ppm_radius;
-    uint32_t x_lo = 1, x_hi = 0, y_lo = 1, y_hi = 0, z_lo = 1, z_hi = 0;
-    bool active = false;
-    if (inimg && (flags & PRD_HIT_NON_SPECULAR) && g.G) {
-        const float invCellSize = 1.f / g.cell;
-        const f3 np = pos - mk(g.ox, g.oy, g.oz);
-        int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
-        int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
-        int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
-        x_lo = (uint32_t)(ixl > 0 ? ixl : 0);
-        y_lo = (uint32_t)(iyl > 0 ? iyl : 0);
-        z_lo = (uint32_t)(izl > 0 ? izl : 0);
-        uint32_t ux = orx_f2u_sat((np.x + radius) * invCellSize);
-        uint32_t uy = orx_f2u_sat((np.y + radius) * invCellSize);
-        uint32_t uz = orx_f2u_sat((np.z + radius) * invCellSize);
-        x_hi = (g.gx - 1) < ux ? (g.gx - 1) : ux;
-        y_hi = (g.gy - 1) < uy ? (g.gy - 1) : uy;
-        z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
-        active = x_lo <= x_hi && y_lo <= y_hi && z_lo <= z_hi;
-    }
-    /* union of the lanes' (z,y) row windows */
-    uint32_t uz_lo = active ? z_lo : 0xffffffffu, uz_hi = active ? z_hi : 0u;
-    uint32_t uy_lo = active ? y_lo : 0xffffffffu, uy_hi = active ? y_hi : 0u;
-    for (int o = 32; o > 0; o >>= 1) {
-        uz_lo = min(uz_lo, (uint32_t)__shfl_xor((int)uz_lo, o, 64));
-        uz_hi = max(uz_hi, (uint32_t)__shfl_xor((int)uz_hi, o, 64));
-        uy_lo = min(uy_lo, (uint32_t)__shfl_xor((int)uy_lo, o, 64));
-        uy_hi = max(uy_hi, (uint32_t)__shfl_xor((int)uy_hi, o, 64));
-    }
-    /* wave-uniform by construction: make it visible to the compiler (scalar loop control) */
-    uz_lo = __builtin_amdgcn_readfirstlane(uz_lo);
-    uz_hi = __builtin_amdgcn_readfirstlane(uz_hi);
-    uy_lo = __builtin_amdgcn_readfirstlane(uy_lo);
-    uy_hi = __builtin_amdgcn_readfirstlane(uy_hi);
-    f3 acc = mk1(0.0f);
-    uint32_t dC = 0, dP = 0, dU = 0;
-    const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
-    const float inv2r2 = 1.0f / (2 * radius2);
-    const float invDen = 1.0f / (1 - expNegativeBeta);
-    if (uz_lo <= uz_hi) {
-        for (uint32_t z = uz_lo; z <= uz_hi; z++) {
-            for (uint32_t yy = uy_lo; yy <= uy_hi; yy++) {
-                const bool row_in = active && z >= z_lo && z <= z_hi && yy >= y_lo && yy <= y_hi;
-                uint32_t lo = 0xffffffffu, hi = 0u;
-                if (row_in) {
-                    uint32_t from = x_lo + yy * g.gx + z * g.gx * g.gy;
-                    uint32_t to = from + (x_hi - x_lo);
-                    lo = pb.offsets[from];
-                    hi = pb.offsets[to + 1];
-                    dC++;
-                    dP += hi - lo;
-                }
-                uint32_t rlo = lo, rhi = row_in ? hi : 0u;
-                for (int o = 32; o > 0; o >>= 1) {
-                    rlo = min(rlo, (uint32_t)__shfl_xor((int)rlo, o, 64));
-                    rhi = max(rhi, (uint32_t)__shfl_xor((int)rhi, o, 64));
-                }
-                rlo = __builtin_amdgcn_readfirstlane(rlo);
-                rhi = __builtin_amdgcn_readfirstlane(rhi);
-                for (uint32_t base = rlo; base < rhi; base += 64) {
-                    const uint32_t n = min(64u, rhi - base);
-                    if (lane < n) {
-                        const float* q = pb.sorted + base + lane;
-                        const size_t P = pb.splane;
-                        sA[lane] = make_float4(q[0], q[P], q[2 * P], q[6 * P]);
-                        sB[lane] = make_float4(q[3 * P], q[4 * P], q[5 * P], q[7 * P]);
-                        sC[lane] = q[8 * P];
-                    }
-                    __syncthreads();
-                    const uint32_t t_lo = lo > base ? lo - base : 0u;
-                    const uint32_t t_hi = hi > base ? min(hi - base, n) : 0u;
-                    dU += n;
-                    for (uint32_t t = 0; t < n; t++) {
-                        const float4 pa = sA[t];
-                        const float4 pbv = sB[t];
-                        const float pc = sC[t];
-                        f3 diff = pos - mk(pa.x, pa.y, pa.z);
-                        float distance2 = dot(diff, diff);
-                        /* predicated, not branched: exp argument stays in [-beta/2, 0] */
-                        bool take = t >= t_lo && t < t_hi && distance2 <= radius2 &&
-                                    dot(-mk(pbv.x, pbv.y, pbv.z), nrm) >= 0;
-                        float e = orx_expf_unit((-beta * fminf(distance2, radius2)) * inv2r2);
-                        float wgt = alpha * (1 - (1 - e) * invDen);
-                        f3 pw = mk(pa.w, pbv.w, pc);
-                        f3 nacc = acc + pw * wgt;
-                        acc.x = take ? nacc.x : acc.x;
-                        acc.y = take ? nacc.y : acc.y;
-                        acc.z = take ? nacc.z : acc.z;
-                    }
-                    __syncthreads();
-                }
-            }
-        }
-    }
-    if (inimg) {
-        const f3 att = mk(B.w, Cc.x, Cc.y);
-        float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
-        float s2 = 1.0f / c.emitted_f;
-        f3 ind = ((acc * att) * s1) * s2;
-        gi.indirect[3 * i + 0] = ind.x;
-        gi.indirect[3 * i + 1] = ind.y;
-        gi.indirect[3 * i + 2] = ind.z;
-        if (gi.dbg) {
-            gi.dbg[2 * i] = dC;
-            gi.dbg[2 * i + 1] = dP;
-        }
-    }
-    uint64_t sp = wave_sum_u64(dP), sc = wave_sum_u64(dC);
-    if (lane == 0 && sp) {
-        atomicAdd((unsigned long long*)&pb.grid->union_photons_total, (unsigned long long)dU);
-        atomicAdd((unsigned long long*)&pb.grid->photons_visited, (unsigned long long)sp);
-        atomicAdd((unsigned long long*)&pb.grid->cells_visited, (unsigned long long)sc);
-        atomicAdd((unsigned long long*)&pb.grid->photons_visited_total, (unsigned long long)sp);
-        atomicAdd((unsigned long long*)&pb.grid->cells_visited_total, (unsigned long long)sc);
-    }
-}
-/* Wave-broadcast gather (variant 2): one wave per 8x8 pixel tile walks, row by
- * row, the union of its lanes' chord-trimmed photon ranges; four photons at a
- * time come in through scalar loads (SGPRs: no per-lane vector-memory traffic,
- * which is what bounds the per-pixel kernel -- its texture-address unit is
- * busy for the whole launch) and every lane tests them against its own range,
- * radius and normal with the per-pixel kernel's packed arithmetic.  Each
- * pixel sees exactly the photons of k_ppm_gather in the same row order; only
- * the pairing of photons into the two accumulator halves differs (rounding). */
-__global__ __launch_bounds__(256) void k_ppm_gather_wave(GatherIn gi, PhotonBufs pb, Consts c) {
-    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (l & 7);
-    const uint32_t j = blockIdx.y * 16 + (w >> 1) * 8 + (l >> 3);
-    const GridParams g = *pb.grid;
-    const bool inimg = x < gi.W && j < gi.segments * gi.seg_rows;
-    const size_t i = (size_t)j * gi.W + x;
-    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
-    float2 Cc = make_float2(0.f, 0.f);
-    if (inimg) {
-        const HpRef hr = hp_ref(gi, j, x);
-        A = hr.A[hr.li];
-        B = hr.B[hr.li];
-        Cc = hr.C[hr.li];
-    }
-    const uint32_t flags = __float_as_uint(A.w);
-    const f3 pos = mk(A.x, A.y, A.z);
-    const float radius2 = c.ppm_radius2;
-    const float radius = c.ppm_radius;
-    const float invCellSize = 1.f / g.cell;
-    const f3 np = pos - mk(g.ox, g.oy, g.oz);
-    uint32_t x_lo = 1, x_hi = 0, y_lo = 1, y_hi = 0, z_lo = 1, z_hi = 0;
-    bool active = false;
-    if (inimg && (flags & PRD_HIT_NON_SPECULAR) && g.G) {
-        const int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
-        const int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
-        const int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
-        x_lo = (uint32_t)(ixl > 0 ? ixl : 0);
-        y_lo = (uint32_t)(iyl > 0 ? iyl : 0);
-        z_lo = (uint32_t)(izl > 0 ? izl : 0);
-        const uint32_t ux = orx_f2u_sat((np.x + radius) * invCellSize);
-        const uint32_t uy = orx_f2u_sat((np.y + radius) * invCellSize);
-        const uint32_t uz = orx_f2u_sat((np.z + radius) * invCellSize);
-        x_hi = (g.gx - 1) < ux ? (g.gx - 1) : ux;
-        y_hi = (g.gy - 1) < uy ? (g.gy - 1) : uy;
-        z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
-        active = x_lo <= x_hi;
-    }
-    uint32_t uz_lo = active ? z_lo : 0xffffffffu, uz_hi = active ? z_hi : 0u;
-    uint32_t uy_lo = active ? y_lo : 0xffffffffu, uy_hi = active ? y_hi : 0u;
-    for (int o = 32; o > 0; o >>= 1) {
-        uz_lo = min(uz_lo, (uint32_t)__shfl_xor((int)uz_lo, o, 64));
-        uz_hi = max(uz_hi, (uint32_t)__shfl_xor((int)uz_hi, o, 64));
-        uy_lo = min(uy_lo, (uint32_t)__shfl_xor((int)uy_lo, o, 64));
-        uy_hi = max(uy_hi, (uint32_t)__shfl_xor((int)uy_hi, o, 64));
-    }
-    uz_lo = __builtin_amdgcn_readfirstlane(uz_lo);
-    uz_hi = __builtin_amdgcn_readfirstlane(uz_hi);
-    uy_lo = __builtin_amdgcn_readfirstlane(uy_lo);
-    uy_hi = __builtin_amdgcn_readfirstlane(uy_hi);
-    uint32_t dC = 0, dP = 0, dU = 0;
-    const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
-    const float inv2r2 = 1.0f / (2 * radius2);
-    const float invDen = 1.0f / (1 - expNegativeBeta);
-    const float kx = -beta * inv2r2;
-    const float wB = alpha * invDen, wA = alpha - wB;
-    const v2f kx2 = v2f{kx, kx};
-    const v2f wc6 = wB * ORX_EXPU_C6, wc5 = wB * ORX_EXPU_C5, wc4 = wB * ORX_EXPU_C4;
-    const v2f wc3 = wB * ORX_EXPU_C3, wc2 = wB * ORX_EXPU_C2, wc1 = wB * ORX_EXPU_C1;
-    const v2f wc0 = v2f{wA + wB, wA + wB};
-    v2f accx = v2f{0.f, 0.f}, accy = accx, accz = accx;
-    const v2f px2 = v2f{pos.x, pos.x}, py2 = v2f{pos.y, pos.y}, pz2 = v2f{pos.z, pos.z};
-    const v2f nx2 = v2f{B.x, B.x}, ny2 = v2f{B.y, B.y}, nz2 = v2f{B.z, B.z};
-    const size_t P = pb.splane;
-    const float* __restrict__ S0 = pb.sorted;
-    const float m = g.cell * 1e-3f;
-    for (uint32_t z = uz_lo; z <= uz_hi && uz_lo <= uz_hi; z++) {
-        const float zc0 = g.oz + (float)z * g.cell - m, zc1 = g.oz + (float)(z + 1) * g.cell + m;
-        const float dz = fmaxf(0.f, fmaxf(zc0 - pos.z, pos.z - zc1));
-        for (uint32_t yy = uy_lo; yy <= uy_hi; yy++) {
-            const uint32_t row = yy * g.gx + z * g.gx * g.gy;
-            uint32_t off = 0xffffffffu, offTo = 0u;
-            if (active && z >= z_lo && z <= z_hi && yy >= y_lo && yy <= y_hi) {
-                const uint32_t from = x_lo + row;
-                const uint32_t to = from + (x_hi - x_lo);
-                dC++;
-                dP += pb.offsets[to + 1] - pb.offsets[from];
-                const float yc0 = g.oy + (float)yy * g.cell - m, yc1 = g.oy + (float)(yy + 1) * g.cell + m;
-                const float dy = fmaxf(0.f, fmaxf(yc0 - pos.y, pos.y - yc1));
-                const float rem = radius2 - dy * dy - dz * dz;
-                if (rem >= 0.f) {
-                    const float rx = sqrtf(rem) + m;
-                    const int32_t cxl = orx_f2i_sat(orx_floorf((np.x - rx) * invCellSize));
-                    const int32_t cxh = orx_f2i_sat(orx_floorf((np.x + rx) * invCellSize));
-                    const uint32_t xl = cxl > (int32_t)x_lo ? (uint32_t)cxl : x_lo;
-                    const uint32_t xh = cxh < (int32_t)x_hi ? (uint32_t)cxh : x_hi;
-                    if (cxh >= 0 && xl <= xh) {
-                        if (pb.subofs) {
-                            const float sx = invCellSize * (float)SUBX;
-                            const int32_t q0 = orx_f2i_sat(orx_floorf((np.x - rx) * sx));
-                            const int32_t q1 = orx_f2i_sat(orx_floorf((np.x + rx) * sx));
-                            const uint32_t a0 = q0 > (int32_t)(SUBX * xl) ? (uint32_t)q0 : SUBX * xl;
-                            const uint32_t a1 = q1 < (int32_t)(SUBX * xh + SUBX - 1) ? (uint32_t)q1 : SUBX * xh + SUBX - 1;
-                            if (q1 >= 0 && a0 <= a1) {
-                                off = pb.subofs[SUBX * row + a0];
-                                offTo = pb.subofs[SUBX * row + a1 + 1];
-                            }
-                        } else {
-                            off = pb.offsets[xl + row];
-                            offTo = pb.offsets[xh + row + 1];
-                        }
-                    }
-                }
-            }
-            if (off >= offTo) { off = 0xffffffffu; offTo = 0u; }
-            uint32_t rlo = off, rhi = offTo;
-            for (int o = 32; o > 0; o >>= 1) {
-                rlo = min(rlo, (uint32_t)__shfl_xor((int)rlo, o, 64));
-                rhi = max(rhi, (uint32_t)__shfl_xor((int)rhi, o, 64));
-            }
-            rlo = __builtin_amdgcn_readfirstlane(rlo);
-            rhi = __builtin_amdgcn_readfirstlane(rhi);
-            if (rlo >= rhi) continue;
-            dU += rhi - rlo;
-            const uint32_t len = offTo - off; /* 0 for lanes without photons in this row (offTo = 0 < off) */
-            for (uint32_t k = rlo; k < rhi; k += 4) {
-                const uint32_t ku = __builtin_amdgcn_readfirstlane(k);
-                const f4u X = *(const f4u*)(S0 + ku);
-                const f4u Y = *(const f4u*)(S0 + P + ku);
-                const f4u Z = *(const f4u*)(S0 + 2 * P + ku);
-                const f4u DX = *(const f4u*)(S0 + 3 * P + ku);
-                const f4u DY = *(const f4u*)(S0 + 4 * P + ku);
-                const f4u DZ = *(const f4u*)(S0 + 5 * P + ku);
-                const f4u WX = *(const f4u*)(S0 + 6 * P + ku);
-                const f4u WY = *(const f4u*)(S0 + 7 * P + ku);
-                const f4u WZ = *(const f4u*)(S0 + 8 * P + ku);
-                const uint32_t t = ku - off;
-                const v2f dx0 = px2 - lo2(X), dx1 = px2 - hi2(X);
-                const v2f dy0 = py2 - lo2(Y), dy1 = py2 - hi2(Y);
-                const v2f dz0 = pz2 - lo2(Z), dz1 = pz2 - hi2(Z);
-                const v2f d20 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
-                const v2f d21 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
-                bool in0 = t < len && d20.x <= radius2;
-                bool in1 = t + 1 < len && d20.y <= radius2;
-                bool in2 = t + 2 < len && d21.x <= radius2;
-                bool in3 = t + 3 < len && d21.y <= radius2;
-                const v2f nd0 = (lo2(DX) * nx2 + lo2(DY) * ny2) + lo2(DZ) * nz2;
-                const v2f nd1 = (hi2(DX) * nx2 + hi2(DY) * ny2) + hi2(DZ) * nz2;
-                in0 = in0 && nd0.x <= 0.f;
-                in1 = in1 && nd0.y <= 0.f;
-                in2 = in2 && nd1.x <= 0.f;
-                in3 = in3 && nd1.y <= 0.f;
-                const v2f x0 = d20 * kx2;
-                const v2f x1 = d21 * kx2;
-                v2f q0 = wc6, q1 = wc6;
-                q0 = __builtin_elementwise_fma(q0, x0, wc5); q1 = __builtin_elementwise_fma(q1, x1, wc5);
-                q0 = __builtin_elementwise_fma(q0, x0, wc4); q1 = __builtin_elementwise_fma(q1, x1, wc4);
-                q0 = __builtin_elementwise_fma(q0, x0, wc3); q1 = __builtin_elementwise_fma(q1, x1, wc3);
-                q0 = __builtin_elementwise_fma(q0, x0, wc2); q1 = __builtin_elementwise_fma(q1, x1, wc2);
-                q0 = __builtin_elementwise_fma(q0, x0, wc1); q1 = __builtin_elementwise_fma(q1, x1, wc1);
-                v2f w0 = __builtin_elementwise_fma(q0, x0, wc0), w1 = __builtin_elementwise_fma(q1, x1, wc0);
-                w0.x = in0 ? w0.x : 0.f;
-                w0.y = in1 ? w0.y : 0.f;
-                w1.x = in2 ? w1.x : 0.f;
-                w1.y = in3 ? w1.y : 0.f;
-                accx = __builtin_elementwise_fma(lo2(WX), w0, accx);
-                accy = __builtin_elementwise_fma(lo2(WY), w0, accy);
-                accz = __builtin_elementwise_fma(lo2(WZ), w0, accz);
-                accx = __builtin_elementwise_fma(hi2(WX), w1, accx);
-                accy = __builtin_elementwise_fma(hi2(WY), w1, accy);
-                accz = __builtin_elementwise_fma(hi2(WZ), w1, accz);
-            }
-        }
-    }
-    if (inimg) {
-        const float ax = accx.x + accx.y, ay = accy.x + accy.y, az = accz.x + accz.y;
-        const f3 att = mk(B.w, Cc.x, Cc.y);
-        const float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
-        const float s2 = 1.0f / c.emitted_f;
-        const f3 ind = ((mk(ax, ay, az) * att) * s1) * s2;
-        gi.indirect[3 * i + 0] = ind.x;
-        gi.indirect[3 * i + 1] = ind.y;
-        gi.indirect[3 * i + 2] = ind.z;
-        if (gi.dbg) {
-            gi.dbg[2 * i] = dC;
-            gi.dbg[2 * i + 1] = dP;
-        }
-    }
-    const uint64_t sp = wave_sum_u64(dP), sc = wave_sum_u64(dC);
-    if (l == 0 && sp) {
-        atomicAdd((unsigned long long*)&pb.grid->union_photons_total, (unsigned long long)dU);
-        atomicAdd((unsigned long long*)&pb.grid->photons_visited, (unsigned long long)sp);
-        atomicAdd((unsigned long long*)&pb.grid->cells_visited, (unsigned long long)sc);
-        atomicAdd((unsigned long long*)&pb.grid->photons_visited_total, (unsigned long long)sp);
-        atomicAdd((unsigned long long*)&pb.grid->cells_visited_total, (unsigned long long)sc);
-    }
-}
-void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, int variant) {
+void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c) {
     const uint32_t rows = gi.segments * gi.seg_rows;
-    if (variant == 2) {
-        dim3 grid((gi.W + 15) / 16, (rows + 15) / 16);
-        hipLaunchKernelGGL(k_ppm_gather_wave, grid, dim3(256), 0, s, gi, pb, c);
-    } else if (variant != 1) {
-        dim3 grid((gi.W + 15) / 16, (rows + 15) / 16);
-        hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), 0, s, gi, pb, c);
-    } else {
-        dim3 grid((gi.W + 7) / 8, (rows + 7) / 8);
-        hipLaunchKernelGGL(k_ppm_gather_coop, grid, dim3(64), 0, s, gi, pb, c);
-    }
+    dim3 grid((gi.W + 15) / 16, (rows + 15) / 16);
+    hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), 0, s, gi, pb, c);
 }
 
 /* ------------------------------------------------------------------ */

@@ -25,7 +25,7 @@ KERNELS_OF_PASS = {
     "grid_hash": ["k_grid_setup", "k_bs_count"],
     "grid_scan": ["k_bs_scan_reduce", "k_bs_scan_partials", "k_bs_scan_apply"],
     "grid_scatter": ["k_bs_place", "k_bs_cells", "k_grid_permute"],
-    "ppm_gather": ["k_ppm_gather", "k_ppm_gather_coop"],
+    "ppm_gather": ["k_ppm_gather"],
     "ppm_direct_output": ["k_ppm_direct_output"],
     "pt": ["k_pt"],
     "vcm_light": ["k_vcm_light"],
