@@ -15,8 +15,8 @@ from oppositerenderer_amd import _abi, renderer, scenes
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_symbols():
-    src = open(os.path.join(ROOT, "include", "orx.h")).read()
+def declared_symbols(header="orx.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     return sorted(set(re.findall(r"\b(orx_[a-z_]+)\s*\(", src)))
 
 
@@ -27,6 +27,37 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(renderer.EXPORTED_SYMBOLS) <= set(syms)
+
+
+def test_library_exports_every_wire_symbol():
+    from oppositerenderer_amd import wire
+    lib = renderer.load_library()
+    syms = declared_symbols("orx_wire.h")
+    assert len(syms) >= 19
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(wire.WIRE_SYMBOLS) == set(syms)
+
+
+def test_wire_struct_layouts_match_c():
+    from oppositerenderer_amd import wire
+    probe = r"""
+#include <stdio.h>
+#include "orx_wire.h"
+int main(void){
+ printf("%zu %zu %zu %zu %zu %zu\n", sizeof(orx_wire_request), sizeof(orx_wire_request_info), sizeof(orx_wire_result),
+        sizeof(orx_wire_result_info), offsetof(orx_wire_request, ppm_alpha), offsetof(orx_wire_result, output_bytes));
+ return 0;}
+"""
+    d = tempfile.mkdtemp()
+    c = os.path.join(d, "w.c")
+    exe = os.path.join(d, "w")
+    open(c, "w").write(probe)
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
+    vals = [int(v) for v in subprocess.check_output([exe]).split()]
+    py = [C.sizeof(wire.OrxWireRequest), C.sizeof(wire.OrxWireRequestInfo), C.sizeof(wire.OrxWireResult),
+          C.sizeof(wire.OrxWireResultInfo), wire.OrxWireRequest.ppm_alpha.offset, wire.OrxWireResult.output_bytes.offset]
+    assert vals == py
 
 
 def test_no_gpu_create_fails_cleanly():

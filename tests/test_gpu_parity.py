@@ -332,3 +332,29 @@ def test_device_bvh_matches_host_bvh(method, monkeypatch):
     else:
         assert rel_l2(g0, g1) < 1e-5
     assert 0 < stats[0] <= 96
+
+
+@pytest.mark.gpu
+def test_wire_server_packet_matches_oracle():
+    """A render server's packet (wire.render_request on the HIP renderer: a run of iterations with
+    the client's radii, local iteration numbers 0..n-1, output = sum over the run) equals the
+    oracle's for the same request, and survives the reference framing bit for bit."""
+    from oppositerenderer_amd import wire
+    scene = scenes.scene_by_name("Cornell")
+    W, H, P = 48, 40, 64
+    gpu, ora, det = make_pair(scene, W, H, P, _abi.PROGRESSIVE_PHOTON_MAPPING)
+    d = wire.RenderServerRenderRequestDetails.from_camera(det.camera, scene.name, det.render_method, W, H)
+    gen = wire.RequestGenerator(scene.initial_ppm_radius(), d)
+    gen.next_request(2)  # this server's run starts at iteration 2
+    req = wire.RenderServerRenderRequest.decode(gen.next_request(3).encode())
+    pkt = wire.RenderResultPacket.decode(wire.render_request(gpu, req, det).encode())
+    for i, (it, r) in enumerate(zip(req.iteration_numbers, req.ppm_radii)):
+        ora.render_next_iteration(it, i, r, det.to_abi())
+    ref = ora.output().reshape(-1)
+    assert pkt.iteration_numbers == [2, 3, 4] and pkt.output.shape == ref.shape
+    assert rel_l2(pkt.output, ref) < 1e-4
+    rx = wire.RenderResultPacketReceiver(_abi.PROGRESSIVE_PHOTON_MAPPING)
+    assert rx.onRenderResultPacketReceived(pkt, gen.sequence_number)
+    assert rx.next_expected_iteration() == 0 and rx.getBackBufferNumIterations() == 3  # waits for 0..1
+    gpu.destroy()
+    ora.close()
