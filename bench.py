@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=20.0)
     p.add_argument("--gather-variant", type=int, default=0)
+    p.add_argument("--photon-map", choices=["grid", "hash"], default="grid",
+                   help="uniform grid (the reference's shipped configuration) or stochastic hash (single GPU)")
     p.add_argument("--force-sharded", action="store_true",
                    help="run the torch.distributed/RCCL sharded path even with one rank (tests the N>1 code)")
     return p.parse_args()
@@ -65,7 +67,7 @@ def traffic_lookup(key, kernels):
     return int(sum(vals)) if vals else None
 
 
-def cpu_baseline(scene, method, W, H, P, seconds):
+def cpu_baseline(scene, method, W, H, P, seconds, photon_map=0):
     """Oracle (oracle/liborx_oracle.so: the C/OpenMP restatement of the
     reference passes) on the host cores, same scene, resolution, photon count
     and seed as the GPU line: one untimed warm-up iteration (allocation, RNG
@@ -84,7 +86,7 @@ def cpu_baseline(scene, method, W, H, P, seconds):
     req.camera = cam.to_abi()
     req.method = method
     req.width, req.height, req.ppm_alpha = W, H, 2.0 / 3.0
-    cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P)
+    cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P, photon_map=photon_map)
     r = oracle_lib.OracleRenderer(cfg)
     r.init_scene(scene)
     radius = scene.initial_ppm_radius()
@@ -127,7 +129,8 @@ def main():
     W, H, P = args.width, args.height, args.photon_launch
     scene = scenes.scene_by_name(args.scene)
     cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P,
-                              gather_variant=args.gather_variant)
+                              gather_variant=args.gather_variant,
+                              photon_map=_abi.PHOTON_MAP_STOCHASTIC_HASH if args.photon_map == "hash" else 0)
     r = OptixRenderer(cfg)
     r.initialize(local_rank)
     r.initScene(scene)
@@ -181,6 +184,7 @@ def main():
                                + (f", {P * P} photons/iter" if method == 2 else ""),
                    "scene": scene.name, "width": W, "height": H, "method": _METHOD_NAME[method],
                    "photons_per_iteration": P * P if method == 2 else 0, "paths_per_iteration": paths,
+                   "photon_map": "stochastic hash" if args.photon_map == "hash" else "uniform grid",
                    "parallelism": "single GPU"},
         "roofline": roof,
         "passes": passes,
@@ -188,7 +192,8 @@ def main():
     }
     if not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(scene, method, W, H, P, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(scene, method, W, H, P, args.cpu_seconds,
+                                               photon_map=1 if args.photon_map == "hash" else 0)
         except Exception as e:  # the baseline must never hide the GPU line
             out["cpu_baseline"] = {"error": repr(e)}
     r.destroy()

@@ -162,7 +162,11 @@ typedef struct {
     uint32_t gather_variant;          /* photon-grid layout for the gather: 0 (default) photons ordered by
                                          cell-row quarter sub-rows (y and z halves) and x quarters; 1 photons in
                                          cell order with x quarters only.  Any other value: ORX_ERR_INVALID_ARGUMENT */
-    uint32_t reserved[6];
+    uint32_t photon_map;              /* ACCELERATION_STRUCTURE (config.h): 0 uniform grid (the shipped
+                                         configuration), 1 stochastic hash (OptixRenderer_SpatialHash.cu:286-302,
+                                         store_photon.h, IndirectRadianceEstimation.cu:131-162; needs
+                                         PW*PH*max deposits a power of two, one rank, trace depth <= 9) */
+    uint32_t reserved[5];
 } orx_config;
 
 void orx_default_config(orx_config* cfg);
@@ -188,8 +192,9 @@ void orx_destroy(orx_renderer* r);
 typedef enum {
     ORX_BUF_RNG = 0,        /* uint32 [slots][6]: xorwow v0..v4, d */
     ORX_BUF_HITPOINTS = 1,  /* float  [W*H][13]: pos3 normal3 atten3 radiance3 flags(bits) */
-    ORX_BUF_PHOTONS = 2,    /* float  [S][9] grid-sorted photons: power3 position3 direction3 (valid prefix) */
-    ORX_BUF_GRID_OFFSETS = 3,/* uint32 [G+1] */
+    ORX_BUF_PHOTONS = 2,    /* float  [S][9] grid-sorted photons: power3 position3 direction3 (valid prefix);
+                               stochastic hash: [photonsSize][9] the photon each table entry holds (0 if empty) */
+    ORX_BUF_GRID_OFFSETS = 3,/* uint32 [G+1]; stochastic hash: [photonsSize] photonsHashTableCount */
     ORX_BUF_INDIRECT = 4,   /* float  [W*H][3] */
     ORX_BUF_DIRECT = 5,     /* float  [W*H][3] */
     ORX_BUF_OUTPUT = 6,     /* float  [W*H][3] */

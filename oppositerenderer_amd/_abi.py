@@ -20,6 +20,10 @@ PATH_TRACING = 0
 VCM_BIDIRECTIONAL_PATH_TRACING = 1
 PROGRESSIVE_PHOTON_MAPPING = 2
 
+# orx_config.photon_map (config.h ACCELERATION_STRUCTURE)
+PHOTON_MAP_UNIFORM_GRID = 0
+PHOTON_MAP_STOCHASTIC_HASH = 1
+
 MAT_DIFFUSE = 0
 MAT_DIFFUSE_EMITTER = 1
 MAT_MIRROR = 2
@@ -104,7 +108,8 @@ class OrxConfig(C.Structure):
                 ("max_photon_deposits", C.c_uint32), ("photon_grid_max_size", C.c_uint32),
                 ("max_photon_trace_depth", C.c_uint32), ("max_radiance_trace_depth", C.c_uint32),
                 ("vcm_max_path_length", C.c_uint32), ("seed", C.c_uint32),
-                ("debug_counters", C.c_uint32), ("gather_variant", C.c_uint32), ("reserved", C.c_uint32 * 6)]
+                ("debug_counters", C.c_uint32), ("gather_variant", C.c_uint32), ("photon_map", C.c_uint32),
+                ("reserved", C.c_uint32 * 5)]
 
 
 class OrxStats(C.Structure):

@@ -373,6 +373,8 @@ struct orx_renderer {
     DevBuf d_hist, d_offsets, d_bbox, d_partials, d_grid, d_work;
     DevBuf d_wray0, d_wray1, d_whit, d_wpath, d_wseg; /* wavefront photon pass queues */
     DevBuf d_pos4, d_bstable, d_bspartials, d_bspairs, d_subofs;  /* bucket-sort grid build */
+    DevBuf d_hcount, d_hwin;  /* stochastic hash table */
+    f3 aabb_lo{}, aabb_hi{};  /* IScene::getSceneAABB (the stochastic hash grid's bounds) */
     PixelBufs px{};
     PhotonBufs pb{};
     /* timing: event pairs per pass since the last orx_reset_timing */
@@ -441,23 +443,31 @@ void orx_default_config(orx_config* c) {
     c->debug_counters = 1;
 }
 
+/* stochastic hash: photonsSize = NUM_PHOTONS must be a power of two (getHashValue masks with
+ * photonsSize - 1; OptixRenderer.cpp:46 "Ensure that NUM PHOTONS are a power of 2"), and a path's
+ * deposits (one per non-specular hit at depth >= 1, never capped) fit the 8-bit deposit mask */
+static bool hash_config_ok(const orx_config& c) {
+    const uint64_t n = (uint64_t)c.photon_launch_width * c.photon_launch_height * c.max_photon_deposits;
+    return n && n <= (1ull << 31) && (n & (n - 1)) == 0 && c.max_photon_trace_depth <= 9;
+}
+
 orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out) {
     if (!out) return ORX_ERR_INVALID_ARGUMENT;
     *out = nullptr;
+    orx_config c;
+    if (cfg) c = *cfg;
+    else orx_default_config(&c);
+    if (c.max_photon_deposits == 0 || c.max_photon_deposits > 8 || c.photon_launch_width == 0 ||
+        c.photon_launch_height == 0 || c.photon_grid_max_size == 0 || c.photon_grid_max_size > (1u << 26) ||
+        c.gather_variant > 1 || c.photon_map > 1 || (c.photon_map == 1 && !hash_config_ok(c)))
+        return ORX_ERR_INVALID_ARGUMENT;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ORX_ERR_DEVICE;
     if (hip_device < 0 || hip_device >= n) return ORX_ERR_INVALID_ARGUMENT;
     orx_renderer* r = new (std::nothrow) orx_renderer();
     if (!r) return ORX_ERR_OUT_OF_MEMORY;
     r->device = hip_device;
-    if (cfg) r->cfg = *cfg;
-    else orx_default_config(&r->cfg);
-    if (r->cfg.max_photon_deposits == 0 || r->cfg.max_photon_deposits > 8 || r->cfg.photon_launch_width == 0 ||
-        r->cfg.photon_launch_height == 0 || r->cfg.photon_grid_max_size == 0 ||
-        r->cfg.photon_grid_max_size > (1u << 26) || r->cfg.gather_variant > 1) {
-        delete r;
-        return ORX_ERR_INVALID_ARGUMENT;
-    }
+    r->cfg = c;
     if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&r->aux, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_photon_done, hipEventDisableTiming) != hipSuccess ||
@@ -488,6 +498,8 @@ void* orx_stream(orx_renderer* r) { return r ? (void*)r->stream : nullptr; }
 
 orx_status orx_set_shard(orx_renderer* r, uint32_t rank, uint32_t world) {
     if (!r || world == 0 || rank >= world) return ORX_ERR_INVALID_ARGUMENT;
+    if (world > 1 && r->cfg.photon_map == 1)
+        return set_err(r, ORX_ERR_UNSUPPORTED, "the stochastic hash photon map is single-device (one table per iteration)");
     r->rank = rank;
     r->world = world;
     r->rng_ready = false; /* force re-allocation of the local rows */
@@ -757,6 +769,8 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     /* AAB::getBoundingSphere (math/AAB.cpp:26-33) with Vector3::length's
      * dot bug a.z*b.x (math/Vector3.cpp:27-30) */
     f3 lo = ld3(s->aabb_min), hi = ld3(s->aabb_max);
+    r->aabb_lo = lo;
+    r->aabb_hi = hi;
     f3 center = (lo + hi) * 0.5f;
     f3 e = hi - center;
     S.bs_cx = center.x;
@@ -769,7 +783,11 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
 }
 
 static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
-    const uint32_t PW = r->cfg.photon_launch_width, PH = r->cfg.photon_launch_height, D = r->cfg.max_photon_deposits;
+    const uint32_t PW = r->cfg.photon_launch_width, PH = r->cfg.photon_launch_height;
+    const bool hash = r->cfg.photon_map == 1;
+    /* slots per emitted photon: the deposit limit (uniform grid), or room for every non-specular
+     * hit at depth 1..max depth - 1 (stochastic hash: store_photon.h never counts deposits) */
+    const uint32_t D = hash ? std::min(r->cfg.max_photon_trace_depth, 8u) : r->cfg.max_photon_deposits;
     r->W = W;
     r->H = H;
     r->RW = std::max(PW, W);
@@ -859,6 +877,18 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     pb.prows = r->prows;
     pb.D = D;
     pb.S = (uint32_t)S;
+    pb.hash = hash ? 1u : 0u;
+    pb.Dlim = hash ? 0xffffffffu : D;
+    pb.hnum = 0;
+    pb.hcount = pb.hwin = nullptr;
+    if (hash) {
+        const size_t hnum = (size_t)PW * PH * r->cfg.max_photon_deposits; /* NUM_PHOTONS */
+        HIPCHK(r, r->d_hcount.ensure(hnum * 4));
+        HIPCHK(r, r->d_hwin.ensure(hnum * 4));
+        pb.hnum = (uint32_t)hnum;
+        pb.hcount = r->d_hcount.as<uint32_t>();
+        pb.hwin = r->d_hwin.as<uint32_t>();
+    }
     pb.gmax = r->cfg.photon_grid_max_size;
     pb.slots = r->d_slots.as<float4>();
     pb.vmask = r->d_vmask.as<uint8_t>();
@@ -995,6 +1025,24 @@ static void ppm_eye(orx_renderer* r, const DevCamera& cam, const Consts& c) {
     launch_ppm_eye(cur_stream(r), r->scene, cam, r->px, c);
     ev_end(r, P_EYE);
 }
+/* initializeStochasticHashPhotonMap (OptixRenderer_SpatialHash.cu:286-302): the scene AABB padded
+ * by r + 0.0001 (AAB::addPadding, the sum in double as written), cell = r, grid = max(1, ceil(extent/r))
+ * with OptiX's float3/float (multiplication by the reciprocal, calculateGridSize :42-50) */
+static HashParams hash_params(const orx_renderer* r, float ppm_radius) {
+    const float a = (float)((double)ppm_radius + 0.0001);
+    const f3 lo = r->aabb_lo - mk1(a), hi = r->aabb_hi + mk1(a);
+    const f3 f = (hi - lo) * (1.0f / ppm_radius);
+    HashParams hp;
+    hp.ox = lo.x;
+    hp.oy = lo.y;
+    hp.oz = lo.z;
+    hp.cell = ppm_radius;
+    hp.gx = std::max(1u, orx_f2u_sat(orx_ceilf(f.x)));
+    hp.gy = std::max(1u, orx_f2u_sat(orx_ceilf(f.y)));
+    hp.gz = std::max(1u, orx_f2u_sat(orx_ceilf(f.z)));
+    hp.mask = r->pb.hnum - 1u;
+    return hp;
+}
 static void ppm_photons_grid(orx_renderer* r, const Consts& c) {
     hipStream_t st = cur_stream(r);
     ev_begin(r, P_PHOTON);
@@ -1002,7 +1050,7 @@ static void ppm_photons_grid(orx_renderer* r, const Consts& c) {
         const char* e = getenv("ORX_PHOTON_WAVEFRONT");
         return e ? atoi(e) : 0;
     }();
-    if (wavefront) launch_ppm_photon_wavefront(st, r->scene, r->px, r->pb, c);
+    if (wavefront && !r->pb.hash) launch_ppm_photon_wavefront(st, r->scene, r->px, r->pb, c);
     else launch_ppm_photon(st, r->scene, r->px, r->pb, c);
     ev_end(r, P_PHOTON);
     if (r->overlap_direct) {
@@ -1016,6 +1064,12 @@ static void ppm_photons_grid(orx_renderer* r, const Consts& c) {
         launch_ppm_direct_output(r->aux, r->scene, r->px, c, 1);
         ev_end_on(r, P_DIRECT, r->aux);
         hipEventRecord(r->ev_direct_done, r->aux);
+    }
+    if (r->pb.hash) {
+        ev_begin(r, P_SETUP_HASH);
+        launch_hash_build(st, r->pb, hash_params(r, c.ppm_radius));
+        ev_end(r, P_SETUP_HASH);
+        return;
     }
     /* grid build: the atomic-free bucket sort (default) or the atomic-rank
      * counting sort (ORX_GRID_ATOMIC=1, kept for A/B) */
@@ -1186,7 +1240,8 @@ orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
         r->overlap_direct = overlap != 0;
         ppm_local_passes(r, cam, c);
         ev_begin(r, P_GATHER);
-        launch_ppm_gather(st, local_gather_in(r), r->pb, c);
+        if (r->pb.hash) launch_ppm_gather_hash(st, local_gather_in(r), r->pb, hash_params(r, c.ppm_radius), c);
+        else launch_ppm_gather(st, local_gather_in(r), r->pb, c);
         ev_end(r, P_GATHER);
         ev_begin(r, P_DIRECT);
         if (r->overlap_direct) {
@@ -1259,6 +1314,7 @@ orx_status orx_export_hitpoints(orx_renderer* r, void* dst, size_t bytes) {
 orx_status orx_ppm_gather_external(orx_renderer* r, const void* hp, uint32_t segments, void* indirect, size_t bytes) {
     if (!r || !hp || !indirect || segments == 0) return ORX_ERR_INVALID_ARGUMENT;
     if (!r->rng_ready) return set_err(r, ORX_ERR_STATE, "no local passes yet");
+    if (r->pb.hash) return set_err(r, ORX_ERR_UNSUPPORTED, "the stochastic hash photon map is single-device");
     size_t need = (size_t)segments * r->max_rows * r->W * 12;
     if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "indirect buffer too small");
     HIPCHK(r, hipSetDevice(r->device));
@@ -1409,8 +1465,8 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
     switch (id) {
     case ORX_BUF_RNG: need = nslot * 24; break;
     case ORX_BUF_HITPOINTS: need = npx * 13 * 4; break;
-    case ORX_BUF_PHOTONS: need = (size_t)g.valid * 36; break;
-    case ORX_BUF_GRID_OFFSETS: need = ((size_t)g.G + 1) * 4; break;
+    case ORX_BUF_PHOTONS: need = (r->pb.hash ? (size_t)r->pb.hnum : (size_t)g.valid) * 36; break;
+    case ORX_BUF_GRID_OFFSETS: need = (r->pb.hash ? (size_t)r->pb.hnum : (size_t)g.G + 1) * 4; break;
     case ORX_BUF_INDIRECT: case ORX_BUF_DIRECT: case ORX_BUF_OUTPUT: need = npx * 12; break;
     case ORX_BUF_PHOTON_SLOTS: need = (size_t)r->pb.S * 36; break;
     case ORX_BUF_DEBUG_VISITED: need = npx * 8; break;
@@ -1453,6 +1509,25 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
         break;
     }
     case ORX_BUF_PHOTONS: {
+        if (r->pb.hash) { /* the table: each entry's photon (its winning slot), zeros when empty */
+            const size_t hn = r->pb.hnum, ns = (size_t)r->pb.S;
+            std::vector<uint32_t> cnt(hn), win(hn);
+            std::vector<float4> R(4 * ns);
+            HIPCHK(r, d2h(cnt.data(), r->pb.hcount, hn * 4));
+            HIPCHK(r, d2h(win.data(), r->pb.hwin, hn * 4));
+            if (ns) HIPCHK(r, d2h(R.data(), r->d_slots.p, ns * 64));
+            float* o = (float*)dst;
+            for (size_t h = 0; h < hn; h++) {
+                float v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+                if (cnt[h] && win[h] && win[h] <= ns) {
+                    const float4 a = R[4 * (win[h] - 1)], b = R[4 * (win[h] - 1) + 1], c = R[4 * (win[h] - 1) + 2];
+                    const float t[9] = {a.w, b.w, c.x, a.x, a.y, a.z, b.x, b.y, b.z};
+                    std::memcpy(v, t, sizeof v);
+                }
+                std::memcpy(o + 9 * h, v, sizeof v);
+            }
+            break;
+        }
         /* nine SoA planes -> [n][power3 position3 direction3] (Photon.h:10-33 order) */
         const size_t n = g.valid, P = r->pb.splane;
         std::vector<float> pl(9 * n);
@@ -1489,7 +1564,7 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
         if (n) HIPCHK(r, d2h(R.data(), r->d_slots.p, n * 64));
         if (!vm.empty()) HIPCHK(r, d2h(vm.data(), r->d_vmask.p, vm.size()));
         float* o = (float*)dst;
-        const uint32_t D = r->cfg.max_photon_deposits;
+        const uint32_t D = r->pb.D; /* slots per emitted photon */
         for (size_t i = 0; i < n; i++) {
             const bool valid = (vm[i / D] >> (i % D)) & 1u;
             const float4 a = R[4 * i], b = R[4 * i + 1], c = R[4 * i + 2];
@@ -1499,7 +1574,7 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
         }
         break;
     }
-    case ORX_BUF_GRID_OFFSETS: HIPCHK(r, d2h(dst, r->d_offsets.p, need)); break;
+    case ORX_BUF_GRID_OFFSETS: HIPCHK(r, d2h(dst, r->pb.hash ? r->d_hcount.p : r->d_offsets.p, need)); break;
     case ORX_BUF_INDIRECT: HIPCHK(r, d2h(dst, r->d_ind.p, need)); break;
     case ORX_BUF_DIRECT: HIPCHK(r, d2h(dst, r->d_dir.p, need)); break;
     case ORX_BUF_OUTPUT: HIPCHK(r, d2h(dst, r->d_out.p, need)); break;

@@ -91,6 +91,21 @@ struct PhotonBufs {
     uint32_t nsub;      /* sub-rows per cell row: 1 (photons in cell order) or SUBR^2 (see k_bs_count) */
     uint32_t* wseg;     /* [2][wnseg] live entries of each queue segment */
     uint32_t wnseg;     /* segments per queue */
+    /* stochastic-hash photon map (orx_config.photon_map = 1) */
+    uint32_t hash;      /* 1: deposits go to the hash table, D = slot capacity per photon */
+    uint32_t Dlim;      /* deposits that end a photon path: D (uniform grid), none (hash: store_photon.h never counts) */
+    uint32_t hnum;      /* photonsSize = NUM_PHOTONS = PW * PH * max deposits (OptixRenderer.cpp:50) */
+    uint32_t* hcount;   /* [hnum] photonsHashTableCount */
+    uint32_t* hwin;     /* [hnum] slot + 1 of the photon the cell keeps (0: empty) */
+};
+
+/* Stochastic-hash grid of one iteration: initializeStochasticHashPhotonMap
+ * (OptixRenderer_SpatialHash.cu:286-302), computed on the host */
+struct HashParams {
+    float ox, oy, oz;   /* photonsWorldOrigo = scene AABB min - (r + 0.0001) */
+    float cell;         /* photonsGridCellSize = r */
+    uint32_t gx, gy, gz;
+    uint32_t mask;      /* photonsSize - 1 (getHashValue, PhotonGrid.h:30-33) */
 };
 
 struct Consts {
@@ -137,6 +152,9 @@ struct GatherIn {
 };
 /* variant 0: one thread per pixel, 8x8 wave tiles (default); 1: wave-cooperative LDS staging */
 void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c);
+void launch_hash_build(hipStream_t s, const PhotonBufs& pb, const HashParams& hp);
+void launch_ppm_gather_hash(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const HashParams& hp,
+                            const Consts& c);
 /* mode 0: direct + output; 1: direct only; 2: output only */
 void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c, int mode = 0);
 void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c);

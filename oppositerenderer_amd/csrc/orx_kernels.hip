@@ -242,7 +242,8 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
                         pb.pos4[si] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, 0.f);
                         rec[1] = make_float4(P.d.x, P.d.y, P.d.z, P.power.y);
                         rec[2].x = P.power.z;
-                        if (fmax3(P.power) > 0) {
+                        /* the hash's STORE_PHOTON (store_photon.h:19-25) counts every deposit */
+                        if (fmax3(P.power) > 0 || pb.hash) {
                             P.mask |= 1u << P.numStored;
                             lo_x = fminf(lo_x, hitPoint.x); lo_y = fminf(lo_y, hitPoint.y); lo_z = fminf(lo_z, hitPoint.z);
                             hi_x = fmaxf(hi_x, hitPoint.x); hi_y = fmaxf(hi_y, hitPoint.y); hi_z = fmaxf(hi_z, hitPoint.z);
@@ -261,7 +262,7 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
                     if (!done) {
                         P.depth++;
                         if (P.depth >= c.max_photon_depth || (double)P.weight < (tex ? 0.01 : 0.001) ||
-                            P.numStored >= pb.D) {
+                            P.numStored >= pb.Dlim) {
                             done = true;
                         } else {
                             float s0 = rnd(rs);
@@ -500,7 +501,8 @@ __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, PixelBufs px, Phot
                         pb.pos4[si] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, 0.f);
                         rec[1] = make_float4(P.d.x, P.d.y, P.d.z, P.power.y);
                         rec[2].x = P.power.z;
-                        if (fmax3(P.power) > 0) {
+                        /* the hash's STORE_PHOTON (store_photon.h:19-25) counts every deposit */
+                        if (fmax3(P.power) > 0 || pb.hash) {
                             P.mask |= 1u << P.numStored;
                             lo_x = fminf(lo_x, hitPoint.x); lo_y = fminf(lo_y, hitPoint.y); lo_z = fminf(lo_z, hitPoint.z);
                             hi_x = fmaxf(hi_x, hitPoint.x); hi_y = fmaxf(hi_y, hitPoint.y); hi_z = fmaxf(hi_z, hitPoint.z);
@@ -519,7 +521,7 @@ __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, PixelBufs px, Phot
                     if (!done) {
                         P.depth++;
                         if (P.depth >= c.max_photon_depth || (double)P.weight < (tex ? 0.01 : 0.001) ||
-                            P.numStored >= pb.D) {
+                            P.numStored >= pb.Dlim) {
                             done = true;
                         } else {
                             float s0 = rnd(rs);
@@ -1380,6 +1382,148 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
     const uint32_t rows = gi.segments * gi.seg_rows;
     dim3 grid((gi.W + 15) / 16, (rows + 15) / 16);
     hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), 0, s, gi, pb, c);
+}
+
+/* ------------------------------------------------------------------ */
+/* stochastic-hash photon map (ACCELERATION_STRUCTURE_STOCHASTIC_HASH)  */
+/* ------------------------------------------------------------------ */
+/* STORE_PHOTON of the hash configuration (helpers/store_photon.h:19-25):
+ * every deposit lands in table entry getHashValue(cell) and bumps its
+ * count.  The reference lets the racing stores pick the entry's photon; here
+ * the entry keeps the deposit with the highest slot index (atomicMax), so the
+ * table is reproducible and equals the oracle's.  Deposits come from the
+ * slots the photon pass wrote (vmask), positions from the compact plane. */
+__global__ __launch_bounds__(256) void k_hash_build(PhotonBufs pb, HashParams hp) {
+    const uint32_t np = pb.prows * pb.PW;
+    const float inv = 1.f / hp.cell;
+    uint32_t deposits = 0;
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < np; p += gridDim.x * blockDim.x) {
+        uint32_t m = pb.vmask[p];
+        deposits += (uint32_t)__builtin_popcount(m);
+        while (m) {
+            const uint32_t k = (uint32_t)__builtin_ctz(m);
+            m &= m - 1;
+            const uint32_t si = p * pb.D + k;
+            const float4 a = pb.pos4[si];
+            /* getPhotonGridIndex (PhotonGrid.h:19-23) */
+            const f3 pp = (mk(a.x, a.y, a.z) - mk(hp.ox, hp.oy, hp.oz)) * inv;
+            const uint32_t cx = orx_f2u_sat(orx_floorf(pp.x)), cy = orx_f2u_sat(orx_floorf(pp.y)),
+                           cz = orx_f2u_sat(orx_floorf(pp.z));
+            const uint32_t h = (cx + cy * hp.gx + cz * hp.gx * hp.gy) & hp.mask;
+            atomicAdd(&pb.hcount[h], 1u);
+            atomicMax(&pb.hwin[h], si + 1u);
+        }
+    }
+    const uint64_t t = wave_sum_u64(deposits);
+    if ((threadIdx.x & 63) == 0 && t) {
+        atomicAdd(&pb.grid->valid, (uint32_t)t);
+        atomicAdd((unsigned long long*)&pb.grid->valid_total, (unsigned long long)t);
+    }
+}
+/* the grid record the stats and exports read: the hash grid, the table size as
+ * the cell count, zeroed per-iteration counters (k_hash_build adds the deposits) */
+__global__ void k_hash_setup(PhotonBufs pb, HashParams hp) {
+    GridParams* g = pb.grid;
+    g->ox = hp.ox;
+    g->oy = hp.oy;
+    g->oz = hp.oz;
+    g->cell = hp.cell;
+    g->gx = hp.gx;
+    g->gy = hp.gy;
+    g->gz = hp.gz;
+    g->G = pb.hnum;
+    g->valid = 0;
+    g->error = 0;
+    g->any_valid = 1;
+    g->photons_visited = 0;
+    g->cells_visited = 0;
+}
+void launch_hash_build(hipStream_t s, const PhotonBufs& pb, const HashParams& hp) {
+    hipMemsetAsync(pb.hcount, 0, (size_t)pb.hnum * 4, s); /* UniformGridPhotonInitialize.cu:20-23 */
+    hipMemsetAsync(pb.hwin, 0, (size_t)pb.hnum * 4, s);
+    hipLaunchKernelGGL(k_hash_setup, dim3(1), dim3(1), 0, s, pb, hp);
+    const uint32_t np = pb.prows * pb.PW;
+    unsigned blocks = (np + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks) hipLaunchKernelGGL(k_hash_build, dim3(blocks), dim3(256), 0, s, pb, hp);
+}
+
+/* IndirectRadianceEstimation.cu:131-162: the 27 cells around the hit point's
+ * cell, one photon per cell weighted by the cell's count; the visit counters
+ * count 27 cells and 27 photons (:150-151).  Cells in a fixed order and
+ * unfused arithmetic, so the sum is the oracle's bit for bit. */
+__global__ __launch_bounds__(64) void k_ppm_gather_hash(GatherIn gi, PhotonBufs pb, HashParams hp, Consts c) {
+    const uint32_t x = blockIdx.x * 8 + (threadIdx.x & 7);
+    const uint32_t j = blockIdx.y * 8 + (threadIdx.x >> 3);
+    const bool inimg = x < gi.W && j < gi.segments * gi.seg_rows;
+    const size_t i = (size_t)j * gi.W + x;
+    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+    float2 Cc = make_float2(0.f, 0.f);
+    if (inimg) {
+        const HpRef hr = hp_ref(gi, j, x);
+        A = hr.A[hr.li];
+        B = hr.B[hr.li];
+        Cc = hr.C[hr.li];
+    }
+    const uint32_t flags = __float_as_uint(A.w);
+    f3 acc = mk1(0.0f);
+    uint32_t dC = 0, dP = 0;
+    if (inimg && (flags & PRD_HIT_NON_SPECULAR)) {
+        const f3 pos = mk(A.x, A.y, A.z), nrm = mk(B.x, B.y, B.z);
+        const float radius2 = c.ppm_radius2;
+        const f3 pp = (pos - mk(hp.ox, hp.oy, hp.oz)) * (1.f / hp.cell);
+        const uint32_t hx = orx_f2u_sat(orx_floorf(pp.x)), hy = orx_f2u_sat(orx_floorf(pp.y)),
+                       hz = orx_f2u_sat(orx_floorf(pp.z));
+        const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
+        const float inv2r2 = 1.0f / (2 * radius2);
+        const float invDen = 1.0f / (1 - expNegativeBeta);
+        for (int dz = -1; dz <= 1; dz++)
+            for (int dy = -1; dy <= 1; dy++)
+                for (int dx = -1; dx <= 1; dx++) {
+                    const uint32_t cx = hx + (uint32_t)dx, cy = hy + (uint32_t)dy, cz = hz + (uint32_t)dz;
+                    dC++;
+                    dP++;
+                    const uint32_t h = (cx + cy * hp.gx + cz * hp.gx * hp.gy) & hp.mask;
+                    const uint32_t n = pb.hcount[h];
+                    if (!n) continue; /* an empty entry contributes power * 0 */
+                    const float4* rec = pb.slots + 4 * (size_t)(pb.hwin[h] - 1u);
+                    const float4 a = rec[0], b = rec[1];
+                    const float pz = rec[2].x;
+                    const f3 diff = pos - mk(a.x, a.y, a.z);
+                    const float distance2 = dot(diff, diff);
+                    if (distance2 <= radius2 && dot(-mk(b.x, b.y, b.z), nrm) >= 0) {
+                        const float e = orx_expf_unit((-beta * distance2) * inv2r2);
+                        const float wgt = alpha * (1 - (1 - e) * invDen);
+                        acc = acc + (mk(a.w, b.w, pz) * wgt) * (float)n;
+                    }
+                }
+    }
+    if (inimg) {
+        const f3 att = mk(B.w, Cc.x, Cc.y);
+        const float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
+        const float s2 = 1.0f / c.emitted_f;
+        const f3 ind = ((acc * att) * s1) * s2;
+        gi.indirect[3 * i + 0] = ind.x;
+        gi.indirect[3 * i + 1] = ind.y;
+        gi.indirect[3 * i + 2] = ind.z;
+        if (gi.dbg) {
+            gi.dbg[2 * i] = dC;
+            gi.dbg[2 * i + 1] = dP;
+        }
+    }
+    const uint64_t sp = wave_sum_u64(dP), sc = wave_sum_u64(dC);
+    if ((threadIdx.x & 63) == 0 && sp) {
+        atomicAdd((unsigned long long*)&pb.grid->photons_visited, (unsigned long long)sp);
+        atomicAdd((unsigned long long*)&pb.grid->cells_visited, (unsigned long long)sc);
+        atomicAdd((unsigned long long*)&pb.grid->photons_visited_total, (unsigned long long)sp);
+        atomicAdd((unsigned long long*)&pb.grid->cells_visited_total, (unsigned long long)sc);
+    }
+}
+void launch_ppm_gather_hash(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const HashParams& hp,
+                            const Consts& c) {
+    const uint32_t rows = gi.segments * gi.seg_rows;
+    dim3 grid((gi.W + 7) / 8, (rows + 7) / 8);
+    hipLaunchKernelGGL(k_ppm_gather_hash, grid, dim3(64), 0, s, gi, pb, hp, c);
 }
 
 /* ------------------------------------------------------------------ */

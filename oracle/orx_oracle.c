@@ -243,6 +243,9 @@ struct orc_renderer {
     uint32_t* dbg; /* [W*H][2] */
     /* grid state */
     uint32_t gsize[3]; float cell; v3 origo; uint32_t ncells; uint32_t valid;
+    /* stochastic hash (cfg.photon_map == 1): dslot slots per emitted photon, deposits per photon,
+     * photonsHashTableCount and the slot + 1 each entry keeps */
+    uint32_t dslot; uint8_t* ndep; uint32_t* hcount; uint32_t* hwin; size_t hnum;
     uint64_t sum_photons_visited, sum_cells_visited;
     /* VCM: pixelSizeFactor (OptixRenderer.cpp:306, :846), LVC-estimated flag (:83, :461, :847) */
     float psf_x, psf_y;
@@ -301,6 +304,8 @@ static void free_frame(orc_renderer* r) {
     free(r->vcount); free(r->vverts); free(r->vsplat); free(r->vcam); free(r->vkd);
     r->vkd = NULL;
     r->vcount = NULL; r->vverts = NULL; r->vsplat = NULL; r->vcam = NULL; r->vcm_npx = 0; r->vcm_spx = 0;
+    free(r->ndep); free(r->hcount); free(r->hwin);
+    r->ndep = NULL; r->hcount = NULL; r->hwin = NULL;
 }
 void orc_destroy(orc_renderer* r) {
     if (!r) return;
@@ -952,7 +957,18 @@ static orx_status resize(orc_renderer* r, uint32_t W, uint32_t H) {
     r->max_rows = (H + r->world - 1) / r->world;
     r->prows = PH > r->rank ? (PH - r->rank + r->world - 1) / r->world : 0;
     size_t npx = (size_t)r->max_rows * W;
-    size_t S = (size_t)PW * r->prows * r->cfg.max_photon_deposits;
+    const int hash = r->cfg.photon_map == 1;
+    /* stochastic hash: store_photon.h never counts deposits, so a path deposits at every
+     * non-specular hit at depth 1..max depth - 1 */
+    r->dslot = hash ? (r->cfg.max_photon_trace_depth < 8 ? r->cfg.max_photon_trace_depth : 8) : r->cfg.max_photon_deposits;
+    size_t S = (size_t)PW * r->prows * r->dslot;
+    if (hash) {
+        r->hnum = (size_t)PW * PH * r->cfg.max_photon_deposits; /* NUM_PHOTONS (OptixRenderer.cpp:50) */
+        r->ndep = (uint8_t*)calloc((size_t)PW * r->prows + 1, 1);
+        r->hcount = (uint32_t*)calloc(r->hnum, 4);
+        r->hwin = (uint32_t*)calloc(r->hnum, 4);
+        if (!r->ndep || !r->hcount || !r->hwin) return fail(r, ORX_ERR_OUT_OF_MEMORY, "oracle: out of memory");
+    }
     size_t G = r->cfg.photon_grid_max_size;
     r->rng = (uint32_t*)malloc((size_t)r->RW * r->RH * 6 * 4);
     r->hp = (hitpoint_t*)calloc(npx, sizeof(hitpoint_t));
@@ -1011,8 +1027,13 @@ static void ppm_eye_pass(orc_renderer* r, const cam_t* cam) {
 
 /* Photon closest-hit chain (Diffuse.cu:92-135, Mirror.cu:65-77, Glass.cu:164-205,
  * DiffuseEmitter.cu:56-59) in iterative form. */
-static void trace_photon(const orc_renderer* r, v3 o, v3 d, v3 power, uint32_t pm_index, uint32_t* rs) {
-    const uint32_t maxDeposits = r->cfg.max_photon_deposits;
+static void trace_photon(const orc_renderer* r, v3 o, v3 d, v3 power, uint32_t pm_index, uint32_t* rs,
+                         uint8_t* ndep) {
+    /* uniform grid: at most maxDeposits, then the path ends (Diffuse.cu:97, :128-131); stochastic
+     * hash: STORE_PHOTON never counts (store_photon.h:19-25), every hit at depth >= 1 deposits */
+    const int hash = r->cfg.photon_map == 1;
+    const uint32_t maxDeposits = hash ? r->dslot : r->cfg.max_photon_deposits;
+    const uint32_t depositLimit = hash ? 0xffffffffu : maxDeposits;
     const uint32_t maxDepth = r->cfg.max_photon_trace_depth;
     uint32_t numStored = 0, depth = 0;
     float weight = 1.0f;
@@ -1030,6 +1051,7 @@ static void trace_photon(const orc_renderer* r, v3 o, v3 d, v3 power, uint32_t p
                 p->position = hitPoint;
                 p->direction = d;
                 numStored++;
+                if (ndep) *ndep = (uint8_t)numStored;
             }
             power = mul(power, m->Kd);
             weight *= fmax3(m->Kd);
@@ -1041,7 +1063,7 @@ static void trace_photon(const orc_renderer* r, v3 o, v3 d, v3 power, uint32_t p
             }
             depth++;
             if (depth >= maxDepth || (double)weight < 0.001) return;
-            if (numStored >= maxDeposits) return;
+            if (numStored >= depositLimit) return;
             float s0 = orc_uniform(rs);
             float s1 = orc_uniform(rs);
             d = sample_hemisphere_cos(N, s0, s1);
@@ -1056,6 +1078,7 @@ static void trace_photon(const orc_renderer* r, v3 o, v3 d, v3 power, uint32_t p
                 p->position = hitPoint;
                 p->direction = d;
                 numStored++;
+                if (ndep) *ndep = (uint8_t)numStored;
             }
             const v3 kd = tex_color(r, m, &h);
             power = mul(power, kd);
@@ -1068,7 +1091,7 @@ static void trace_photon(const orc_renderer* r, v3 o, v3 d, v3 power, uint32_t p
             }
             depth++;
             if (depth >= maxDepth || (double)weight < 0.01) return;
-            if (numStored >= maxDeposits) return;
+            if (numStored >= depositLimit) return;
             float s0 = orc_uniform(rs);
             float s1 = orc_uniform(rs);
             d = sample_hemisphere_cos(N, s0, s1);
@@ -1117,7 +1140,7 @@ static void trace_photon(const orc_renderer* r, v3 o, v3 d, v3 power, uint32_t p
 /* PhotonGenerator.cu:40-79 + :81-128 */
 static void ppm_photon_pass(orc_renderer* r) {
     const uint32_t PW = r->cfg.photon_launch_width, PH = r->cfg.photon_launch_height;
-    const uint32_t maxDeposits = r->cfg.max_photon_deposits;
+    const uint32_t maxDeposits = r->dslot;
     const uint32_t nl = r->nl;
     (void)PH;
 #pragma omp parallel for schedule(dynamic, 4)
@@ -1166,7 +1189,9 @@ static void ppm_photon_pass(orc_renderer* r) {
                 r->photons[pm_index + i].position = mk1(0.0f);
                 r->photons[pm_index + i].power = mk1(0.0f);
             }
-            trace_photon(r, origin, dir, power, pm_index, rs);
+            uint8_t* nd = r->ndep ? &r->ndep[(size_t)j * PW + x] : NULL;
+            if (nd) *nd = 0;
+            trace_photon(r, origin, dir, power, pm_index, rs, nd);
             memcpy(g, rs, 24);
         }
     }
@@ -1247,6 +1272,102 @@ static orx_status ppm_build_grid(orc_renderer* r) {
     free(pos);
     photon_t* t = r->photons; r->photons = r->sort_tmp; r->sort_tmp = t;
     return ORX_OK;
+}
+
+/* Stochastic hash (ACCELERATION_STRUCTURE_STOCHASTIC_HASH).
+ * initializeStochasticHashPhotonMap (OptixRenderer_SpatialHash.cu:286-302): scene AABB padded
+ * by r + 0.0001 (the sum in double, as written), cell = r, grid = calculateGridSize (:42-50);
+ * the table counts are cleared (UniformGridPhotonInitialize.cu:20-23).  STORE_PHOTON
+ * (store_photon.h:19-25) puts every deposit at getHashValue(getPhotonGridIndex(pos))
+ * (PhotonGrid.h:19-33) and bumps the count; the reference's racing stores leave an arbitrary
+ * deposit in the entry, here the one with the highest slot index (the device's atomicMax). */
+static void ppm_build_hash(orc_renderer* r, float ppmRadius) {
+    const float a = (float)((double)ppmRadius + 0.0001);
+    const v3 lo = sub_s(r->aabb_min, a), hi = mk(r->aabb_max.x + a, r->aabb_max.y + a, r->aabb_max.z + a);
+    const v3 f = divs(sub(hi, lo), ppmRadius);
+    uint32_t g[3] = {orx_f2u_sat(orx_ceilf(f.x)), orx_f2u_sat(orx_ceilf(f.y)), orx_f2u_sat(orx_ceilf(f.z))};
+    for (int k = 0; k < 3; k++) if (g[k] < 1) g[k] = 1;
+    r->gsize[0] = g[0]; r->gsize[1] = g[1]; r->gsize[2] = g[2];
+    r->cell = ppmRadius;
+    r->origo = lo;
+    r->ncells = (uint32_t)r->hnum;
+    const uint32_t mask = (uint32_t)r->hnum - 1u;
+    memset(r->hcount, 0, r->hnum * 4);
+    memset(r->hwin, 0, r->hnum * 4);
+    const size_t np = (size_t)r->cfg.photon_launch_width * r->prows;
+    const float inv = 1.f / ppmRadius;
+    uint32_t total = 0;
+    for (size_t p = 0; p < np; p++) {
+        for (uint32_t k = 0; k < r->ndep[p]; k++) {
+            const uint32_t slot = (uint32_t)(p * r->dslot + k);
+            const v3 pp = scl(sub(r->photons[slot].position, lo), inv);
+            const uint32_t cx = orx_f2u_sat(orx_floorf(pp.x)), cy = orx_f2u_sat(orx_floorf(pp.y)),
+                           cz = orx_f2u_sat(orx_floorf(pp.z));
+            const uint32_t h = (cx + cy * g[0] + cz * g[0] * g[1]) & mask;
+            r->hcount[h]++;
+            if (slot + 1u > r->hwin[h]) r->hwin[h] = slot + 1u;
+            total++;
+        }
+    }
+    r->valid = total;
+}
+
+/* IndirectRadianceEstimation.cu:131-162: the 27 cells around the hit point's cell, one photon
+ * per cell weighted by the cell's count; 27 cells and 27 photons counted as visited. */
+static void ppm_gather_hash(orc_renderer* r, float ppmRadiusSquared, float emittedF) {
+    const uint32_t W = r->W, H = r->rows;
+    const uint32_t gx = r->gsize[0], gy = r->gsize[1];
+    const uint32_t mask = (uint32_t)r->hnum - 1u;
+    const v3 origo = r->origo;
+    const float inv = 1.f / r->cell;
+    uint64_t sumP = 0, sumC = 0;
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : sumP, sumC)
+    for (long long y = 0; y < (long long)H; y++) {
+        for (uint32_t x = 0; x < W; x++) {
+            const size_t px = (size_t)y * W + x;
+            const hitpoint_t rec = r->hp[px];
+            v3 acc = mk1(0.0f);
+            uint32_t dP = 0, dC = 0;
+            if (rec.flags & PRD_HIT_NON_SPECULAR) {
+                const float radius2 = ppmRadiusSquared;
+                const v3 pp = scl(sub(rec.position, origo), inv);
+                const uint32_t hx = orx_f2u_sat(orx_floorf(pp.x)), hy = orx_f2u_sat(orx_floorf(pp.y)),
+                               hz = orx_f2u_sat(orx_floorf(pp.z));
+                const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
+                const float inv2r2 = 1.0f / (2 * radius2);
+                const float invDen = 1.0f / (1 - expNegativeBeta);
+                for (int dz = -1; dz <= 1; dz++)
+                    for (int dy = -1; dy <= 1; dy++)
+                        for (int dx = -1; dx <= 1; dx++) {
+                            const uint32_t cx = hx + (uint32_t)dx, cy = hy + (uint32_t)dy, cz = hz + (uint32_t)dz;
+                            dC++;
+                            dP++;
+                            const uint32_t h = (cx + cy * gx + cz * gx * gy) & mask;
+                            const uint32_t n = r->hcount[h];
+                            if (!n) continue; /* an empty entry contributes power * 0 */
+                            const photon_t* p = &r->photons[r->hwin[h] - 1u];
+                            const v3 diff = sub(rec.position, p->position);
+                            const float distance2 = dot(diff, diff);
+                            if (distance2 <= radius2 && dot(neg(p->direction), rec.normal) >= 0) {
+                                const float e = orx_expf_unit((-beta * distance2) * inv2r2);
+                                const float wgt = alpha * (1 - (1 - e) * invDen);
+                                acc = add(acc, scl(scl(p->power, wgt), (float)n));
+                            }
+                        }
+            }
+            const float s1 = 1.0f / (ORX_PI_F * ppmRadiusSquared);
+            const float s2 = 1.0f / emittedF;
+            r->indirect[px] = scl(scl(mul(acc, rec.attenuation), s1), s2);
+            if (r->dbg) {
+                r->dbg[2 * px] = dC;
+                r->dbg[2 * px + 1] = dP;
+            }
+            sumP += dP;
+            sumC += dC;
+        }
+    }
+    r->sum_photons_visited = sumP;
+    r->sum_cells_visited = sumC;
 }
 
 /* hitpoint source for the gather: the own rows, or `segments` export buffers
@@ -1521,10 +1642,15 @@ orx_status orc_render_next_iteration(orc_renderer* r, uint64_t iter, uint64_t lo
         ppm_eye_pass(r, &cam);
         const float ppmRadiusSquared = ppmRadius * ppmRadius;
         ppm_photon_pass(r);
-        orx_status s = ppm_build_grid(r);
-        if (s != ORX_OK) return s;
         float emittedF = (float)(r->cfg.photon_launch_width * r->cfg.photon_launch_height);
-        ppm_gather(r, ppmRadius, ppmRadiusSquared, emittedF);
+        if (r->cfg.photon_map == 1) {
+            ppm_build_hash(r, ppmRadius);
+            ppm_gather_hash(r, ppmRadiusSquared, emittedF);
+        } else {
+            orx_status s = ppm_build_grid(r);
+            if (s != ORX_OK) return s;
+            ppm_gather(r, ppmRadius, ppmRadiusSquared, emittedF);
+        }
         ppm_direct(r);
         ppm_output(r, local);
     }
@@ -1534,6 +1660,8 @@ orx_status orc_render_next_iteration(orc_renderer* r, uint64_t iter, uint64_t lo
 /* ---- sharded phase API (mirrors orx_ppm_* in include/orx.h) ---- */
 orx_status orc_set_shard(orc_renderer* r, uint32_t rank, uint32_t world) {
     if (!r || world == 0 || rank >= world) return ORX_ERR_INVALID_ARGUMENT;
+    if (world > 1 && r->cfg.photon_map == 1)
+        return fail(r, ORX_ERR_UNSUPPORTED, "the stochastic hash photon map is single-device");
     r->rank = rank;
     r->world = world;
     r->rng_ready = 0;
@@ -1604,8 +1732,8 @@ orx_status orc_read_buffer(orc_renderer* r, int32_t id, void* dst, size_t bytes,
     switch (id) {
     case ORX_BUF_RNG: need = (size_t)r->RW * r->RH * 24; break;
     case ORX_BUF_HITPOINTS: need = npx * 13 * 4; break;
-    case ORX_BUF_PHOTONS: need = (size_t)r->valid * 36; break;
-    case ORX_BUF_GRID_OFFSETS: need = ((size_t)r->ncells + 1) * 4; break;
+    case ORX_BUF_PHOTONS: need = (r->hcount ? r->hnum : (size_t)r->valid) * 36; break;
+    case ORX_BUF_GRID_OFFSETS: need = (r->hcount ? r->hnum : (size_t)r->ncells + 1) * 4; break;
     case ORX_BUF_INDIRECT: case ORX_BUF_DIRECT: case ORX_BUF_OUTPUT: need = npx * 12; break;
     case ORX_BUF_DEBUG_VISITED: need = npx * 8; break;
     case ORX_BUF_VCM_VERTEX_COUNT: need = r->vcm_npx * 4; break;
@@ -1629,8 +1757,19 @@ orx_status orc_read_buffer(orc_renderer* r, int32_t id, void* dst, size_t bytes,
         }
         break;
     }
-    case ORX_BUF_PHOTONS: memcpy(dst, r->photons, need); break;
-    case ORX_BUF_GRID_OFFSETS: memcpy(dst, r->offsets, need); break;
+    case ORX_BUF_PHOTONS:
+        if (r->hcount) { /* the table: each entry's photon, zeros when empty */
+            float* f = (float*)dst;
+            for (size_t h = 0; h < r->hnum; h++) {
+                float v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+                if (r->hcount[h]) memcpy(v, &r->photons[r->hwin[h] - 1u], sizeof v);
+                memcpy(f + 9 * h, v, sizeof v);
+            }
+        } else {
+            memcpy(dst, r->photons, need);
+        }
+        break;
+    case ORX_BUF_GRID_OFFSETS: memcpy(dst, r->hcount ? r->hcount : r->offsets, need); break;
     case ORX_BUF_INDIRECT: memcpy(dst, r->indirect, need); break;
     case ORX_BUF_DIRECT: memcpy(dst, r->direct, need); break;
     case ORX_BUF_OUTPUT: memcpy(dst, r->output, need); break;

@@ -358,3 +358,33 @@ def test_wire_server_packet_matches_oracle():
     assert rx.next_expected_iteration() == 0 and rx.getBackBufferNumIterations() == 3  # waits for 0..1
     gpu.destroy()
     ora.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene_name,W,H,P", [("Cornell", 64, 48, 64), ("CornellSmall", 48, 48, 32)])
+def test_stochastic_hash_parity(scene_name, W, H, P):
+    """photon_map = 1 (ACCELERATION_STRUCTURE_STOCHASTIC_HASH): uncapped deposits, the hash table
+    (counts and the photon each entry keeps), the 27-cell gather and the output are bit-exact."""
+    scene = scenes.scene_by_name(scene_name)
+    gpu, ora, det = make_pair(scene, W, H, P, _abi.PROGRESSIVE_PHOTON_MAPPING,
+                              photon_map=_abi.PHOTON_MAP_STOCHASTIC_HASH)
+    radius = scene.initial_ppm_radius()
+    for it in range(3):
+        gpu.renderNextIteration(it, it, radius, True, det)
+        ora.render_next_iteration(it, it, radius, det.to_abi())
+        for buf, dt in ((_abi.BUF_RNG, np.uint32), (_abi.BUF_HITPOINTS, np.uint32), (_abi.BUF_GRID_OFFSETS, np.uint32),
+                        (_abi.BUF_PHOTONS, np.uint32), (_abi.BUF_INDIRECT, np.uint32), (_abi.BUF_DIRECT, np.uint32),
+                        (_abi.BUF_DEBUG_VISITED, np.uint32)):
+            g, o = gpu.read_buffer(buf, dt), ora.read_buffer(buf, dt)
+            assert g.shape == o.shape, buf
+            assert np.count_nonzero(g != o) == 0, f"buffer {buf} differs (iteration {it})"
+        gs, os_ = gpu.stats(), ora.stats()
+        assert list(gs.grid_size) == list(os_.grid_size) and gs.cell_size == os_.cell_size
+        assert gs.valid_photons == os_.valid_photons == ora.read_buffer(_abi.BUF_GRID_OFFSETS, np.uint32).sum()
+        assert gs.num_cells == P * P * 4
+        radius = next_ppm_radius(radius, it)
+    g, o = gpu.getOutputBuffer(), ora.output()
+    assert np.array_equal(g.view(np.uint32), o.view(np.uint32))
+    assert g.mean() > 0
+    gpu.destroy()
+    ora.close()
