@@ -44,8 +44,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=20.0)
     p.add_argument("--gather-variant", type=int, default=0)
-    p.add_argument("--photon-map", choices=["grid", "hash"], default="grid",
-                   help="uniform grid (the reference's shipped configuration) or stochastic hash (single GPU)")
+    p.add_argument("--photon-map", choices=["grid", "hash", "kd"], default="grid",
+                   help="uniform grid (the reference's shipped configuration), stochastic hash (single GPU) "
+                        "or kd-tree (ACCELERATION_STRUCTURE_KD_TREE_CPU, built on the device)")
     p.add_argument("--force-sharded", action="store_true",
                    help="run the torch.distributed/RCCL sharded path even with one rank (tests the N>1 code)")
     return p.parse_args()
@@ -65,6 +66,9 @@ def traffic_lookup(key, kernels):
         return None
     vals = [table[k]["bytes_per_launch"] for k in kernels if k in table]
     return int(sum(vals)) if vals else None
+
+
+PHOTON_MAPS = {"grid": 0, "hash": 1, "kd": 2}  # orx_config.photon_map
 
 
 def cpu_baseline(scene, method, W, H, P, seconds, photon_map=0):
@@ -130,7 +134,7 @@ def main():
     scene = scenes.scene_by_name(args.scene)
     cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P,
                               gather_variant=args.gather_variant,
-                              photon_map=_abi.PHOTON_MAP_STOCHASTIC_HASH if args.photon_map == "hash" else 0)
+                              photon_map=PHOTON_MAPS[args.photon_map])
     r = OptixRenderer(cfg)
     r.initialize(local_rank)
     r.initScene(scene)
@@ -184,7 +188,7 @@ def main():
                                + (f", {P * P} photons/iter" if method == 2 else ""),
                    "scene": scene.name, "width": W, "height": H, "method": _METHOD_NAME[method],
                    "photons_per_iteration": P * P if method == 2 else 0, "paths_per_iteration": paths,
-                   "photon_map": "stochastic hash" if args.photon_map == "hash" else "uniform grid",
+                   "photon_map": {"grid": "uniform grid", "hash": "stochastic hash", "kd": "kd-tree"}[args.photon_map],
                    "parallelism": "single GPU"},
         "roofline": roof,
         "passes": passes,
@@ -193,7 +197,7 @@ def main():
     if not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(scene, method, W, H, P, args.cpu_seconds,
-                                               photon_map=1 if args.photon_map == "hash" else 0)
+                                               photon_map=PHOTON_MAPS[args.photon_map])
         except Exception as e:  # the baseline must never hide the GPU line
             out["cpu_baseline"] = {"error": repr(e)}
     r.destroy()

@@ -165,7 +165,10 @@ typedef struct {
     uint32_t photon_map;              /* ACCELERATION_STRUCTURE (config.h): 0 uniform grid (the shipped
                                          configuration), 1 stochastic hash (OptixRenderer_SpatialHash.cu:286-302,
                                          store_photon.h, IndirectRadianceEstimation.cu:131-162; needs
-                                         PW*PH*max deposits a power of two, one rank, trace depth <= 9) */
+                                         PW*PH*max deposits a power of two, one rank, trace depth <= 9),
+                                         2 kd-tree (ACCELERATION_STRUCTURE_KD_TREE_CPU:
+                                         OptixRenderer_CPUKdTree.cpp, IndirectRadianceEstimation.cu:164-209;
+                                         built on the device here) */
     uint32_t reserved[5];
 } orx_config;
 
@@ -205,7 +208,12 @@ typedef enum {
     ORX_BUF_VCM_VERTICES = 10,    /* float [9][W*H][16]: per vertex slot k, subpath p: pos3 mat(bits) throughput3 dVCM
                                      normal3 dVC dirFix3 dVM; entries k >= count[p] are stale */
     ORX_BUF_VCM_SPLAT = 11,       /* float [W*H][3]: this iteration's light-tracing splats (connectCameraT1) */
-    ORX_BUF_VCM_CAMERA = 12       /* float [W*H][3]: this iteration's camera subpath colour (cameraPrd.color) */
+    ORX_BUF_VCM_CAMERA = 12,      /* float [W*H][3]: this iteration's camera subpath colour (cameraPrd.color) */
+    /* kd-tree photon map (photon_map = 2): the implicit tree m_photonKdTree of pow2roundup(S + 1) - 1 nodes,
+       node i's children at 2i+1, 2i+2; per node power3 position3 direction3 axis(uint32 bits: PPM_X 1, PPM_Y 2,
+       PPM_Z 4, PPM_LEAF 8, PPM_NULL 16, config.h:12-16).  Only nodes reachable from the root are defined (the
+       reference never clears the buffer; a NULL node defines axis and power only). */
+    ORX_BUF_KD_TREE = 13
 } orx_buffer_id;
 /* Copies buffer `id` to host; returns the byte size through *out_bytes
  * (call with dst=NULL to query). */

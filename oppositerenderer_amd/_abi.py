@@ -23,6 +23,7 @@ PROGRESSIVE_PHOTON_MAPPING = 2
 # orx_config.photon_map (config.h ACCELERATION_STRUCTURE)
 PHOTON_MAP_UNIFORM_GRID = 0
 PHOTON_MAP_STOCHASTIC_HASH = 1
+PHOTON_MAP_KD_TREE = 2
 
 MAT_DIFFUSE = 0
 MAT_DIFFUSE_EMITTER = 1
@@ -48,6 +49,7 @@ BUF_VCM_VERTEX_COUNT = 9
 BUF_VCM_VERTICES = 10
 BUF_VCM_SPLAT = 11
 BUF_VCM_CAMERA = 12
+BUF_KD_TREE = 13
 
 # RadiancePRD.h:30-35 flag bits
 PRD_HIT_EMITTER = 1 << 31

@@ -374,6 +374,10 @@ struct orx_renderer {
     DevBuf d_wray0, d_wray1, d_whit, d_wpath, d_wseg; /* wavefront photon pass queues */
     DevBuf d_pos4, d_bstable, d_bspartials, d_bspairs, d_subofs;  /* bucket-sort grid build */
     DevBuf d_hcount, d_hwin;  /* stochastic hash table */
+    /* kd-tree photon map (photon_map = 2, orx_kdtree.hip) */
+    DevBuf d_kdtree, d_kdids, d_kdkeys, d_kdnodepos, d_kdside, d_kdseg, d_kdbox, d_kdninfo, d_kdP, d_kdppart,
+        d_kdtable, d_kdtpart, d_kdvpart, d_kdcount;
+    KdBufs kd{};
     f3 aabb_lo{}, aabb_hi{};  /* IScene::getSceneAABB (the stochastic hash grid's bounds) */
     PixelBufs px{};
     PhotonBufs pb{};
@@ -459,7 +463,9 @@ orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out)
     else orx_default_config(&c);
     if (c.max_photon_deposits == 0 || c.max_photon_deposits > 8 || c.photon_launch_width == 0 ||
         c.photon_launch_height == 0 || c.photon_grid_max_size == 0 || c.photon_grid_max_size > (1u << 26) ||
-        c.gather_variant > 1 || c.photon_map > 1 || (c.photon_map == 1 && !hash_config_ok(c)))
+        c.gather_variant > 1 || c.photon_map > 2 || (c.photon_map == 1 && !hash_config_ok(c)) ||
+        (c.photon_map == 2 && (uint64_t)c.photon_launch_width * c.photon_launch_height * c.max_photon_deposits >
+                                  (1ull << 28)))
         return ORX_ERR_INVALID_ARGUMENT;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ORX_ERR_DEVICE;
@@ -889,6 +895,58 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
         pb.hcount = r->d_hcount.as<uint32_t>();
         pb.hwin = r->d_hwin.as<uint32_t>();
     }
+    if (r->cfg.photon_map == 2) {
+        /* m_photonKdTreeSize = pow2roundup(NUM_PHOTONS + 1) - 1 (OptixRenderer.cpp:65-74, :207) */
+        uint32_t t = (uint32_t)S;
+        t |= t >> 1;
+        t |= t >> 2;
+        t |= t >> 4;
+        t |= t >> 8;
+        t |= t >> 16;
+        const size_t tree = (size_t)t; /* pow2roundup(S + 1) - 1 */
+        uint32_t levels = 0;
+        while (((size_t)1 << levels) - 1 < tree) levels++;
+        const size_t nblk = (S + 1023) / 1024;
+        const size_t ntiles = (S + 4095) / 4096;
+        const size_t tp = std::max((256 * ntiles + 1023) / 1024, (6 * nblk + 1023) / 1024) + 16;
+        HIPCHK(r, r->d_kdtree.ensure(tree * 48 + 48));
+        HIPCHK(r, r->d_kdids.ensure(6 * S * 4 + 64));
+        HIPCHK(r, r->d_kdkeys.ensure(2 * S * 4 + 64));
+        HIPCHK(r, r->d_kdnodepos.ensure(S * 4 + 16));
+        HIPCHK(r, r->d_kdside.ensure(S + 16));
+        HIPCHK(r, r->d_kdseg.ensure(tree * 8 + 16));
+        HIPCHK(r, r->d_kdbox.ensure(tree * 24 + 24));
+        HIPCHK(r, r->d_kdninfo.ensure(tree * 4 + 16));
+        HIPCHK(r, r->d_kdP.ensure(6 * S * 4 + 64));
+        HIPCHK(r, r->d_kdppart.ensure(6 * nblk * 4 + 64));
+        HIPCHK(r, r->d_kdtable.ensure(256 * ntiles * 4 + 64));
+        HIPCHK(r, r->d_kdtpart.ensure(tp * 4));
+        HIPCHK(r, r->d_kdvpart.ensure(nblk * 4 + 64));
+        HIPCHK(r, r->d_kdcount.ensure(64));
+        HIPCHK(r, hipMemsetAsync(r->d_kdtree.p, 0, tree * 48 + 48, r->stream));
+        KdBufs& kd = r->kd;
+        kd.S = (uint32_t)S;
+        kd.tree_size = (uint32_t)tree;
+        kd.levels = levels;
+        kd.ntiles = (uint32_t)ntiles;
+        kd.tree = r->d_kdtree.as<float4>();
+        for (int q = 0; q < 2; q++)
+            for (int a = 0; a < 3; a++) kd.ids[q][a] = r->d_kdids.as<uint32_t>() + (size_t)(3 * q + a) * S;
+        kd.keys[0] = r->d_kdkeys.as<uint32_t>();
+        kd.keys[1] = kd.keys[0] + S;
+        kd.nodepos = r->d_kdnodepos.as<uint32_t>();
+        kd.side = r->d_kdside.as<uint8_t>();
+        kd.seg = r->d_kdseg.as<uint2>();
+        kd.box = r->d_kdbox.as<float>();
+        kd.ninfo = r->d_kdninfo.as<uint32_t>();
+        kd.P = r->d_kdP.as<uint32_t>();
+        kd.ppart = r->d_kdppart.as<uint32_t>();
+        kd.table = r->d_kdtable.as<uint32_t>();
+        kd.tpart = r->d_kdtpart.as<uint32_t>();
+        kd.vpart = r->d_kdvpart.as<uint32_t>();
+        kd.count = r->d_kdcount.as<uint32_t>();
+        HIPCHK(r, hipMemsetAsync(r->d_kdcount.p, 0, 64, r->stream));
+    }
     pb.gmax = r->cfg.photon_grid_max_size;
     pb.slots = r->d_slots.as<float4>();
     pb.vmask = r->d_vmask.as<uint8_t>();
@@ -1071,6 +1129,12 @@ static void ppm_photons_grid(orx_renderer* r, const Consts& c) {
         ev_end(r, P_SETUP_HASH);
         return;
     }
+    if (r->cfg.photon_map == 2) { /* createPhotonKdTreeOnCPU, on the device */
+        ev_begin(r, P_SETUP_HASH);
+        launch_kd_build(st, r->pb, r->kd);
+        ev_end(r, P_SETUP_HASH);
+        return;
+    }
     /* grid build: the atomic-free bucket sort (default) or the atomic-rank
      * counting sort (ORX_GRID_ATOMIC=1, kept for A/B) */
     static const int atomic_grid = [] {
@@ -1241,6 +1305,7 @@ orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
         ppm_local_passes(r, cam, c);
         ev_begin(r, P_GATHER);
         if (r->pb.hash) launch_ppm_gather_hash(st, local_gather_in(r), r->pb, hash_params(r, c.ppm_radius), c);
+        else if (r->cfg.photon_map == 2) launch_ppm_gather_kd(st, local_gather_in(r), r->pb, r->kd, c);
         else launch_ppm_gather(st, local_gather_in(r), r->pb, c);
         ev_end(r, P_GATHER);
         ev_begin(r, P_DIRECT);
@@ -1327,7 +1392,8 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hp, uint32_t seg
     gi.indirect = (float*)indirect;
     gi.dbg = nullptr;
     ev_begin(r, P_GATHER);
-    launch_ppm_gather(cur_stream(r), gi, r->pb, r->last_consts);
+    if (r->cfg.photon_map == 2) launch_ppm_gather_kd(cur_stream(r), gi, r->pb, r->kd, r->last_consts);
+    else launch_ppm_gather(cur_stream(r), gi, r->pb, r->last_consts);
     ev_end(r, P_GATHER);
     HIPCHK(r, hipGetLastError());
     return ORX_OK;
@@ -1469,6 +1535,7 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
     case ORX_BUF_GRID_OFFSETS: need = (r->pb.hash ? (size_t)r->pb.hnum : (size_t)g.G + 1) * 4; break;
     case ORX_BUF_INDIRECT: case ORX_BUF_DIRECT: case ORX_BUF_OUTPUT: need = npx * 12; break;
     case ORX_BUF_PHOTON_SLOTS: need = (size_t)r->pb.S * 36; break;
+    case ORX_BUF_KD_TREE: need = r->cfg.photon_map == 2 ? (size_t)r->kd.tree_size * 40 : 0; break;
     case ORX_BUF_DEBUG_VISITED: need = npx * 8; break;
     case ORX_BUF_VCM_VERTEX_COUNT: need = r->vcm_npx * 4; break;
     case ORX_BUF_VCM_VERTICES: need = r->vcm_npx * VCM_MAX_VERTS * 64; break;
@@ -1571,6 +1638,18 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
             float v[9] = {a.w, b.w, c.x, a.x, a.y, a.z, b.x, b.y, b.z};
             if (!valid) std::memset(v, 0, sizeof v);
             std::memcpy(o + 9 * i, v, sizeof v);
+        }
+        break;
+    }
+    case ORX_BUF_KD_TREE: { /* [tree_size][power3 position3 direction3 axis] */
+        const size_t n = r->kd.tree_size;
+        std::vector<float4> T(3 * n);
+        if (n) HIPCHK(r, d2h(T.data(), r->kd.tree, n * 48));
+        float* o = (float*)dst;
+        for (size_t i = 0; i < n; i++) {
+            const float4 a = T[3 * i], b = T[3 * i + 1], c = T[3 * i + 2];
+            const float v[10] = {b.x, b.y, b.z, a.x, a.y, a.z, b.w, c.x, c.y, a.w};
+            std::memcpy(o + 10 * i, v, sizeof v);
         }
         break;
     }

@@ -1,0 +1,577 @@
+/*
+ * orx_kdtree.hip — kd-tree photon map (orx_config.photon_map = 2), gfx950.
+ *
+ * The reference's ACCELERATION_STRUCTURE_KD_TREE_CPU maps the photon buffer to
+ * the host every iteration and builds a balanced kd-tree there
+ * (createPhotonKdTreeOnCPU / buildKDTree, OptixRenderer_CPUKdTree.cpp:27-127,
+ * quickselect from the OptiX SDK's select.h), then the gather walks it
+ * (IndirectRadianceEstimation.cu:164-209).  Here the same tree is built on the
+ * device, level by level, with no host round trip:
+ *
+ *   k_kd_vcount / k_kd_vwrite   valid slots (vmask) in slot order        -> ids
+ *   k_kd_keys, k_rs_count, k_rs_scatter (x4 digits)  stable LSD radix sort of
+ *                               the ids by each axis' coordinate         -> one list per axis
+ *   k_kd_root                   root box = photon AABB (the photon pass's
+ *                               fused bbox replicas), root segment [0, n)
+ *   per level l:
+ *     k_kd_nodes                node = its segment's median along the
+ *                               box's longest axis (max_component), children
+ *                               segments and boxes; NULL / LEAF nodes
+ *     k_kd_side                 every element of a split segment: left,
+ *                               median or right, from its rank in the
+ *                               split axis' list
+ *     k_kd_pcount, scan, k_kd_pprefix, k_kd_pmove   stable partition of all
+ *                               three lists into [left | median | right]
+ *
+ * Each segment of every list stays sorted by its axis (ties by slot order), so
+ * the median of a segment is read directly at (start+end)/2.  The tree's shape,
+ * axes and split coordinates depend only on the photon multiset, so they equal
+ * the reference's; which of several photons with the same split coordinate
+ * becomes the node is the one freedom (select.h breaks such ties by its
+ * partition order), and it only permutes the gather's summation.
+ *
+ * Node record: three float4 — A pos.xyz | axis bits, B power.xyz | dir.x,
+ * C dir.yz — so the traversal loads 16 B per node and the rest only for
+ * photons inside the radius.
+ */
+#include <cfloat>
+
+#include "orx_kernels.h"
+
+namespace orx {
+
+constexpr uint32_t KD_NONE = 0xffffffffu;
+constexpr uint32_t KD_PPM_X = 1u, KD_PPM_Y = 2u, KD_PPM_Z = 4u, KD_PPM_LEAF = 8u, KD_PPM_NULL = 16u; /* config.h:12-16 */
+static_assert(KD_PPM_Z == KD_PPM_X << 2, "split flags are PPM_X << axis");
+
+__device__ __forceinline__ uint32_t kd_f2ord(float f) {
+    uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float kd_ord2f(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+__device__ __forceinline__ float kd_comp(const float4& p, uint32_t a) { return a == 0 ? p.x : a == 1 ? p.y : p.z; }
+
+/* exclusive scan of one uint32 per thread over a 256-thread block (4 waves) */
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* lds4, uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)inc, o, 64);
+        if (lane >= (uint32_t)o) inc += t;
+    }
+    if (lane == 63) lds4[w] = inc;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t t = lds4[k];
+        if (k < w) base += t;
+        tot += t;
+    }
+    __syncthreads();
+    if (total) *total = tot;
+    return base + inc - v;
+}
+
+/* ------------------------------------------------------------------ */
+/* generic exclusive scan of m uint32 (in place): block sums, one-block */
+/* scan of the sums, apply                                              */
+/* ------------------------------------------------------------------ */
+__global__ __launch_bounds__(256) void k_kd_scan_reduce(const uint32_t* a, uint32_t m, uint32_t* part) {
+    __shared__ uint32_t l4[4];
+    const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x * 4;
+    uint32_t s = 0;
+    for (int k = 0; k < 4; k++)
+        if (base + k < m) s += a[base + k];
+    uint32_t tot;
+    block_excl_scan256(s, l4, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(1024) void k_kd_scan_top(uint32_t* part, uint32_t np, uint32_t* grand) {
+    __shared__ uint32_t wsum[16];
+    const uint32_t chunk = (np + 1023) / 1024;
+    const uint32_t b = threadIdx.x * chunk;
+    uint32_t s = 0;
+    for (uint32_t k = 0; k < chunk; k++)
+        if (b + k < np) s += part[b + k];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)inc, o, 64);
+        if (lane >= (uint32_t)o) inc += t;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (uint32_t k = 0; k < 16; k++) {
+        if (k < w) base += wsum[k];
+        tot += wsum[k];
+    }
+    uint32_t run = base + inc - s;
+    for (uint32_t k = 0; k < chunk; k++)
+        if (b + k < np) {
+            const uint32_t t = part[b + k];
+            part[b + k] = run;
+            run += t;
+        }
+    if (threadIdx.x == 0 && grand) *grand = tot;
+}
+__global__ __launch_bounds__(256) void k_kd_scan_apply(uint32_t* a, uint32_t m, const uint32_t* part) {
+    __shared__ uint32_t l4[4];
+    const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x * 4;
+    uint32_t v[4], s = 0;
+    for (int k = 0; k < 4; k++) {
+        v[k] = base + k < m ? a[base + k] : 0u;
+        s += v[k];
+    }
+    uint32_t run = part[blockIdx.x] + block_excl_scan256(s, l4, nullptr);
+    for (int k = 0; k < 4; k++)
+        if (base + k < m) {
+            a[base + k] = run;
+            run += v[k];
+        }
+}
+static void kd_scan(hipStream_t st, uint32_t* a, uint32_t m, uint32_t* part, uint32_t* grand) {
+    const uint32_t nb = (m + 1023) / 1024;
+    hipLaunchKernelGGL(k_kd_scan_reduce, dim3(nb), dim3(256), 0, st, a, m, part);
+    hipLaunchKernelGGL(k_kd_scan_top, dim3(1), dim3(1024), 0, st, part, nb, grand);
+    hipLaunchKernelGGL(k_kd_scan_apply, dim3(nb), dim3(256), 0, st, a, m, part);
+}
+
+/* ------------------------------------------------------------------ */
+/* valid photons in slot order (the reference's numValidPhotons loop,  */
+/* OptixRenderer_CPUKdTree.cpp:98-110, keeps the same set)             */
+/* ------------------------------------------------------------------ */
+__device__ __forceinline__ bool kd_slot_valid(const PhotonBufs& pb, uint32_t s) {
+    return s < pb.S && ((pb.vmask[s / pb.D] >> (s % pb.D)) & 1u);
+}
+__global__ __launch_bounds__(256) void k_kd_vcount(PhotonBufs pb, KdBufs kd) {
+    __shared__ uint32_t l4[4];
+    const uint32_t base = blockIdx.x * 1024 + threadIdx.x * 4;
+    uint32_t s = 0;
+    for (int k = 0; k < 4; k++) s += kd_slot_valid(pb, base + k) ? 1u : 0u;
+    uint32_t tot;
+    block_excl_scan256(s, l4, &tot);
+    if (threadIdx.x == 0) kd.vpart[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(256) void k_kd_vwrite(PhotonBufs pb, KdBufs kd) {
+    __shared__ uint32_t l4[4];
+    const uint32_t base = blockIdx.x * 1024 + threadIdx.x * 4;
+    bool v[4];
+    uint32_t s = 0;
+    for (int k = 0; k < 4; k++) {
+        v[k] = kd_slot_valid(pb, base + k);
+        s += v[k] ? 1u : 0u;
+    }
+    uint32_t run = kd.vpart[blockIdx.x] + block_excl_scan256(s, l4, nullptr);
+    for (int k = 0; k < 4; k++)
+        if (v[k]) kd.ids[1][0][run++] = base + k;
+}
+
+/* ------------------------------------------------------------------ */
+/* stable LSD radix sort of (key, slot) by 8-bit digits                */
+/* ------------------------------------------------------------------ */
+constexpr uint32_t RS_ITEMS = 16, RS_TILE = 256 * RS_ITEMS;
+
+__global__ __launch_bounds__(256) void k_kd_keys(PhotonBufs pb, KdBufs kd, uint32_t axis) {
+    const uint32_t n = kd.count[0];
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = kd.ids[1][0][i];
+    kd.keys[0][i] = kd_f2ord(kd_comp(pb.pos4[s], axis));
+    kd.ids[0][axis][i] = s;
+}
+/* histogram of one digit per tile -> table[digit][tile] */
+__global__ __launch_bounds__(256) void k_rs_count(const uint32_t* keys, const uint32_t* count, uint32_t shift,
+                                                  uint32_t* table, uint32_t ntiles) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t n = *count;
+    const uint32_t t0 = blockIdx.x * RS_TILE;
+    for (uint32_t j = 0; j < RS_ITEMS; j++) {
+        const uint32_t i = t0 + j * 256 + threadIdx.x;
+        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    table[threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+/* stable scatter: within a tile, element order = (round j, thread); ranks of equal
+ * digits inside a wave from eight ballots, across waves from LDS counts */
+__global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t* keys, const uint32_t* vals, const uint32_t* count,
+                                                    uint32_t shift, const uint32_t* table, uint32_t ntiles,
+                                                    uint32_t* okeys, uint32_t* ovals) {
+    __shared__ uint32_t run[256];
+    __shared__ uint32_t wc[4][256];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    run[tid] = table[tid * ntiles + blockIdx.x];
+    const uint32_t n = *count;
+    const uint32_t t0 = blockIdx.x * RS_TILE;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t j = 0; j < RS_ITEMS; j++) {
+        if (t0 + j * 256 >= n) break; /* uniform across the block */
+        wc[0][tid] = 0;
+        wc[1][tid] = 0;
+        wc[2][tid] = 0;
+        wc[3][tid] = 0;
+        const uint32_t i = t0 + j * 256 + tid;
+        const bool ok = i < n;
+        const uint32_t key = ok ? keys[i] : 0u;
+        const uint32_t val = ok ? vals[i] : 0u;
+        const uint32_t d = (key >> shift) & 255u;
+        uint64_t peers = __ballot(ok);
+        for (int b = 0; b < 8; b++) {
+            const uint64_t m = __ballot((d >> b) & 1u);
+            peers &= ((d >> b) & 1u) ? m : ~m;
+        }
+        __syncthreads(); /* wc zeroed */
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
+        if (ok && rank == 0) wc[w][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (ok) {
+            uint32_t off = run[d] + rank;
+            for (uint32_t k = 0; k < w; k++) off += wc[k][d];
+            okeys[off] = key;
+            ovals[off] = val;
+        }
+        __syncthreads();
+        run[tid] += wc[0][tid] + wc[1][tid] + wc[2][tid] + wc[3][tid];
+        __syncthreads();
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* root: the photon AABB (fminf/fmaxf over valid positions,            */
+/* OptixRenderer_CPUKdTree.cpp:112-124) from the photon pass's fused   */
+/* replicas, which are reset for the next iteration                    */
+/* ------------------------------------------------------------------ */
+__global__ void k_kd_root(PhotonBufs pb, KdBufs kd) {
+    __shared__ uint32_t red[6];
+    const uint32_t lane = threadIdx.x;
+    for (int k = 0; k < 6; k++) {
+        uint32_t v = pb.bbox[k * BBOX_REPLICAS + lane];
+        for (int o = 32; o > 0; o >>= 1) {
+            uint32_t w = (uint32_t)__shfl_xor((int)v, o, 64);
+            v = k < 3 ? min(v, w) : max(v, w);
+        }
+        if (lane == 0) red[k] = v;
+        pb.bbox[k * BBOX_REPLICAS + lane] = k < 3 ? 0xffffffffu : 0u;
+    }
+    __syncthreads();
+    if (lane != 0) return;
+    const uint32_t n = kd.count[0];
+    for (int k = 0; k < 3; k++) {
+        kd.box[k] = n ? kd_ord2f(red[k]) : FLT_MAX;
+        kd.box[3 + k] = n ? kd_ord2f(red[3 + k]) : -FLT_MAX;
+    }
+    kd.seg[0] = make_uint2(0u, n);
+    GridParams* g = pb.grid;
+    g->ox = g->oy = g->oz = 0.f;
+    g->cell = 0.f;
+    g->gx = g->gy = g->gz = 0;
+    g->G = kd.tree_size;
+    g->valid = n;
+    g->error = 0;
+    g->any_valid = n ? 1u : 0u;
+    g->photons_visited = 0;
+    g->cells_visited = 0;
+    g->valid_total += n;
+}
+
+/* ------------------------------------------------------------------ */
+/* levels                                                              */
+/* ------------------------------------------------------------------ */
+/* one thread per node of level l: buildKDTree's body (OptixRenderer_CPUKdTree.cpp:27-88) */
+__global__ __launch_bounds__(256) void k_kd_nodes(PhotonBufs pb, KdBufs kd, uint32_t level, uint32_t src) {
+    const uint32_t first = (1u << level) - 1u;
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= (1u << level)) return;
+    const uint32_t node = first + k;
+    const uint2 se = kd.seg[node];
+    const uint32_t c0 = 2 * node + 1;
+    const bool has_children = c0 + 1 < kd.tree_size;
+    uint32_t info = KD_NONE;
+    if (se.x != KD_NONE) {
+        float4* rec = kd.tree + 3 * (size_t)node;
+        const uint32_t size = se.y - se.x;
+        if (size == 0) { /* NULL node: axis and power */
+            const float4 b = rec[1];
+            rec[0].w = __uint_as_float(KD_PPM_NULL);
+            rec[1] = make_float4(0.f, 0.f, 0.f, b.w);
+        } else {
+            uint32_t axis = 0, med = se.x;
+            if (size > 1) {
+                const float* bx = kd.box + 6 * (size_t)node;
+                const float dx = bx[3] - bx[0], dy = bx[4] - bx[1], dz = bx[5] - bx[2];
+                axis = (dx > dy && dx > dz) ? 0u : (dy > dz ? 1u : 2u); /* max_component :14-25 */
+                med = (se.x + se.y) / 2;
+            }
+            const uint32_t s = kd.ids[src][axis][med];
+            const float4* sl = pb.slots + 4 * (size_t)s;
+            const float4 a = sl[0], b = sl[1], c = sl[2];
+            const uint32_t flag = size == 1 ? KD_PPM_LEAF : (KD_PPM_X << axis);
+            rec[0] = make_float4(a.x, a.y, a.z, __uint_as_float(flag));
+            rec[1] = make_float4(a.w, b.w, c.x, b.x);
+            rec[2] = make_float4(b.y, b.z, 0.f, 0.f);
+            if (size > 1) {
+                info = (med << 2) | axis;
+                if (has_children) {
+                    const float* bx = kd.box + 6 * (size_t)node;
+                    const float split = kd_comp(make_float4(a.x, a.y, a.z, 0.f), axis);
+                    float* lb = kd.box + 6 * (size_t)c0;
+                    float* rb = lb + 6;
+                    for (int q = 0; q < 6; q++) {
+                        lb[q] = bx[q];
+                        rb[q] = bx[q];
+                    }
+                    lb[3 + axis] = split; /* leftMax */
+                    rb[axis] = split;     /* rightMin */
+                    kd.seg[c0] = make_uint2(se.x, med);
+                    kd.seg[c0 + 1] = make_uint2(med + 1, se.y);
+                }
+            }
+        }
+    }
+    kd.ninfo[node] = info;
+    if (info == KD_NONE && has_children) {
+        kd.seg[c0] = make_uint2(KD_NONE, KD_NONE);
+        kd.seg[c0 + 1] = make_uint2(KD_NONE, KD_NONE);
+    }
+}
+
+/* every element of a split segment learns its side from its rank in the split axis' list */
+__global__ __launch_bounds__(256) void k_kd_side(KdBufs kd, uint32_t src) {
+    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= kd.count[0]) return;
+    const uint32_t node = kd.nodepos[p];
+    if (node == KD_NONE) return;
+    const uint32_t info = kd.ninfo[node];
+    if (info == KD_NONE) return;
+    const uint32_t m = info >> 2, axis = info & 3u;
+    kd.side[kd.ids[src][axis][p]] = p < m ? 0 : (p == m ? 2 : 1);
+}
+
+/* per position: (left, median) indicators of the three lists, packed left | median << 16 */
+__device__ __forceinline__ void kd_pos_bits(const KdBufs& kd, uint32_t src, uint32_t p, uint32_t n, uint32_t v[3]) {
+    v[0] = v[1] = v[2] = 0;
+    if (p >= n) return;
+    const uint32_t node = kd.nodepos[p];
+    if (node == KD_NONE || kd.ninfo[node] == KD_NONE) return;
+    for (int b = 0; b < 3; b++) {
+        const uint32_t sd = kd.side[kd.ids[src][b][p]];
+        v[b] = sd == 0 ? 1u : (sd == 2 ? 0x10000u : 0u);
+    }
+}
+__global__ __launch_bounds__(256) void k_kd_pcount(KdBufs kd, uint32_t src, uint32_t nblk) {
+    __shared__ uint32_t l4[4];
+    const uint32_t n = kd.count[0];
+    const uint32_t base = blockIdx.x * 1024 + threadIdx.x * 4;
+    uint32_t s[3] = {0, 0, 0};
+    for (int k = 0; k < 4; k++) {
+        uint32_t v[3];
+        kd_pos_bits(kd, src, base + k, n, v);
+        for (int b = 0; b < 3; b++) s[b] += v[b];
+    }
+    for (int b = 0; b < 3; b++) {
+        uint32_t tot;
+        block_excl_scan256(s[b], l4, &tot);
+        if (threadIdx.x == 0) {
+            kd.ppart[(2 * b) * nblk + blockIdx.x] = tot & 0xffffu;
+            kd.ppart[(2 * b + 1) * nblk + blockIdx.x] = tot >> 16;
+        }
+    }
+}
+/* global exclusive (left, median) prefix of every position, per list, into P planes */
+__global__ __launch_bounds__(256) void k_kd_pprefix(KdBufs kd, uint32_t src, uint32_t nblk) {
+    __shared__ uint32_t l4[4];
+    const uint32_t n = kd.count[0];
+    const uint32_t base = blockIdx.x * 1024 + threadIdx.x * 4;
+    uint32_t v[4][3];
+    uint32_t s[3] = {0, 0, 0};
+    for (int k = 0; k < 4; k++) {
+        kd_pos_bits(kd, src, base + k, n, v[k]);
+        for (int b = 0; b < 3; b++) s[b] += v[k][b];
+    }
+    const size_t S = kd.S;
+    for (int b = 0; b < 3; b++) {
+        const uint32_t ex = block_excl_scan256(s[b], l4, nullptr);
+        uint32_t rl = kd.ppart[(2 * b) * nblk + blockIdx.x] + (ex & 0xffffu);
+        uint32_t rm = kd.ppart[(2 * b + 1) * nblk + blockIdx.x] + (ex >> 16);
+        for (int k = 0; k < 4; k++) {
+            const uint32_t p = base + k;
+            if (p < n) {
+                kd.P[(2 * b) * S + p] = rl;
+                kd.P[(2 * b + 1) * S + p] = rm;
+            }
+            rl += v[k][b] & 0xffffu;
+            rm += v[k][b] >> 16;
+        }
+    }
+}
+/* stable partition of the three lists of every split segment into [left | median | right]
+ * (the median leaves the lists: it is the node), and the positions' next-level nodes */
+__global__ __launch_bounds__(256) void k_kd_pmove(KdBufs kd, uint32_t src) {
+    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= kd.count[0]) return;
+    const uint32_t node = kd.nodepos[p];
+    if (node == KD_NONE) return;
+    const uint32_t info = kd.ninfo[node];
+    if (info == KD_NONE) { /* a leaf: its element is the node */
+        kd.nodepos[p] = KD_NONE;
+        return;
+    }
+    const uint32_t m = info >> 2;
+    const uint32_t s = kd.seg[node].x;
+    const size_t S = kd.S;
+    for (int b = 0; b < 3; b++) {
+        const uint32_t id = kd.ids[src][b][p];
+        const uint32_t sd = kd.side[id];
+        if (sd == 2) continue;
+        const uint32_t L = kd.P[(2 * b) * S + p] - kd.P[(2 * b) * S + s];
+        const uint32_t M = kd.P[(2 * b + 1) * S + p] - kd.P[(2 * b + 1) * S + s];
+        const uint32_t dst = sd == 0 ? s + L : m + 1 + (p - s) - L - M;
+        kd.ids[src ^ 1][b][dst] = id;
+    }
+    kd.nodepos[p] = p < m ? 2 * node + 1 : (p > m ? 2 * node + 2 : KD_NONE);
+}
+__global__ __launch_bounds__(256) void k_kd_pos_init(KdBufs kd) {
+    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+    if (p < kd.S) kd.nodepos[p] = p < kd.count[0] ? 0u : KD_NONE;
+}
+
+void launch_kd_build(hipStream_t st, const PhotonBufs& pb, const KdBufs& kd) {
+    const uint32_t S = kd.S;
+    const uint32_t nb1024 = (S + 1023) / 1024;
+    const uint32_t nb256 = (S + 255) / 256;
+    /* valid slots in slot order -> ids[1][0], count[0] = n */
+    hipLaunchKernelGGL(k_kd_vcount, dim3(nb1024), dim3(256), 0, st, pb, kd);
+    hipLaunchKernelGGL(k_kd_scan_top, dim3(1), dim3(1024), 0, st, kd.vpart, nb1024, kd.count);
+    hipLaunchKernelGGL(k_kd_vwrite, dim3(nb1024), dim3(256), 0, st, pb, kd);
+    /* one stably sorted list per axis -> ids[0][axis] */
+    for (uint32_t axis = 0; axis < 3; axis++) {
+        hipLaunchKernelGGL(k_kd_keys, dim3(nb256), dim3(256), 0, st, pb, kd, axis);
+        uint32_t* k0 = kd.keys[0];
+        uint32_t* k1 = kd.keys[1];
+        uint32_t* v0 = kd.ids[0][axis];
+        uint32_t* v1 = kd.ids[1][1]; /* scratch list during the sorts */
+        for (uint32_t pass = 0; pass < 4; pass++) {
+            hipLaunchKernelGGL(k_rs_count, dim3(kd.ntiles), dim3(256), 0, st, k0, kd.count, 8 * pass, kd.table,
+                               kd.ntiles);
+            kd_scan(st, kd.table, 256 * kd.ntiles, kd.tpart, nullptr);
+            hipLaunchKernelGGL(k_rs_scatter, dim3(kd.ntiles), dim3(256), 0, st, k0, v0, kd.count, 8 * pass, kd.table,
+                               kd.ntiles, k1, v1);
+            std::swap(k0, k1);
+            std::swap(v0, v1);
+        }
+        /* four passes: the result is back in (keys[0], ids[0][axis]) */
+    }
+    hipLaunchKernelGGL(k_kd_root, dim3(1), dim3(64), 0, st, pb, kd);
+    hipLaunchKernelGGL(k_kd_pos_init, dim3(nb256), dim3(256), 0, st, kd);
+    const uint32_t nblk = nb1024;
+    uint32_t src = 0;
+    for (uint32_t level = 0; level < kd.levels; level++) {
+        const uint32_t nodes = 1u << level;
+        hipLaunchKernelGGL(k_kd_nodes, dim3((nodes + 255) / 256), dim3(256), 0, st, pb, kd, level, src);
+        if (level + 1 == kd.levels) break; /* the last level holds leaves and NULL nodes only */
+        hipLaunchKernelGGL(k_kd_side, dim3(nb256), dim3(256), 0, st, kd, src);
+        hipLaunchKernelGGL(k_kd_pcount, dim3(nblk), dim3(256), 0, st, kd, src, nblk);
+        kd_scan(st, kd.ppart, 6 * nblk, kd.tpart, nullptr);
+        hipLaunchKernelGGL(k_kd_pprefix, dim3(nblk), dim3(256), 0, st, kd, src, nblk);
+        hipLaunchKernelGGL(k_kd_pmove, dim3(nb256), dim3(256), 0, st, kd, src);
+        src ^= 1;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* gather (IndirectRadianceEstimation.cu:164-209 + :211-221)           */
+/* ------------------------------------------------------------------ */
+__global__ __launch_bounds__(64) void k_ppm_gather_kd(GatherIn gi, PhotonBufs pb, KdBufs kd, Consts c) {
+    extern __shared__ uint32_t kd_stack[]; /* [entries][64] */
+    const uint32_t lane = threadIdx.x;
+    const uint32_t x = blockIdx.x * 8 + (lane & 7);
+    const uint32_t j = blockIdx.y * 8 + (lane >> 3);
+    const bool inimg = x < gi.W && j < gi.segments * gi.seg_rows;
+    const size_t i = (size_t)j * gi.W + x;
+    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+    float2 Cc = make_float2(0.f, 0.f);
+    if (inimg) {
+        const uint32_t seg = j / gi.seg_rows, lj = j - seg * gi.seg_rows;
+        const size_t plane = (size_t)gi.seg_rows * gi.W;
+        const uint8_t* b = gi.base + seg * gi.seg_bytes;
+        const size_t li = (size_t)lj * gi.W + x;
+        A = ((const float4*)b)[li];
+        B = ((const float4*)(b + plane * 16))[li];
+        Cc = ((const float2*)(b + plane * 32))[li];
+    }
+    const uint32_t flags = __float_as_uint(A.w);
+    f3 acc = mk1(0.0f);
+    uint32_t dP = 0;
+    if (inimg && (flags & PRD_HIT_NON_SPECULAR)) {
+        const f3 pos = mk(A.x, A.y, A.z), nrm = mk(B.x, B.y, B.z);
+        const float radius2 = c.ppm_radius2;
+        const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
+        const float inv2r2 = 1.0f / (2 * radius2);
+        const float invDen = 1.0f / (1 - expNegativeBeta);
+        const float4* tree = kd.tree;
+        uint32_t sc = 0, node = 0;
+        kd_stack[lane] = 0;
+        sc = 1;
+        const uint32_t max_sc = kd.levels + 2;
+        do {
+            if (node >= kd.tree_size || sc >= max_sc) break; /* unreachable on a well-formed tree */
+            const float4 a = tree[3 * (size_t)node];
+            dP++;
+            const uint32_t axis = __float_as_uint(a.w);
+            if (!(axis & KD_PPM_NULL)) {
+                const f3 diff = pos - mk(a.x, a.y, a.z);
+                const float distance2 = dot(diff, diff);
+                if (distance2 <= radius2) {
+                    const float4 b = tree[3 * (size_t)node + 1];
+                    const float4 cc = tree[3 * (size_t)node + 2];
+                    if (dot(-mk(b.w, cc.x, cc.y), nrm) >= 0) {
+                        const float e = orx_expf_unit((-beta * distance2) * inv2r2);
+                        const float wgt = alpha * (1 - (1 - e) * invDen);
+                        acc = acc + mk(b.x, b.y, b.z) * wgt;
+                    }
+                }
+                if (!(axis & KD_PPM_LEAF)) {
+                    const float d = (axis & KD_PPM_X) ? diff.x : (axis & KD_PPM_Y) ? diff.y : diff.z;
+                    const uint32_t selector = d < 0.0f ? 0u : 1u;
+                    if (d * d < radius2) kd_stack[(sc++) * 64 + lane] = (node << 1) + 2 - selector;
+                    node = (node << 1) + 1 + selector;
+                } else {
+                    node = kd_stack[(--sc) * 64 + lane];
+                }
+            } else {
+                node = kd_stack[(--sc) * 64 + lane];
+            }
+        } while (node);
+    }
+    if (inimg) {
+        const f3 att = mk(B.w, Cc.x, Cc.y);
+        const float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
+        const float s2 = 1.0f / c.emitted_f;
+        const f3 ind = ((acc * att) * s1) * s2;
+        gi.indirect[3 * i + 0] = ind.x;
+        gi.indirect[3 * i + 1] = ind.y;
+        gi.indirect[3 * i + 2] = ind.z;
+        if (gi.dbg) {
+            gi.dbg[2 * i] = 0;
+            gi.dbg[2 * i + 1] = dP;
+        }
+    }
+    uint64_t sp = dP;
+    for (int o = 32; o > 0; o >>= 1) sp += __shfl_xor(sp, o, 64);
+    if (lane == 0 && sp) {
+        atomicAdd((unsigned long long*)&pb.grid->photons_visited, (unsigned long long)sp);
+        atomicAdd((unsigned long long*)&pb.grid->photons_visited_total, (unsigned long long)sp);
+    }
+}
+void launch_ppm_gather_kd(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const KdBufs& kd, const Consts& c) {
+    const uint32_t rows = gi.segments * gi.seg_rows;
+    dim3 grid((gi.W + 7) / 8, (rows + 7) / 8);
+    hipLaunchKernelGGL(k_ppm_gather_kd, grid, dim3(64), (size_t)(kd.levels + 2) * 64 * 4, s, gi, pb, kd, c);
+}
+
+} // namespace orx

@@ -99,6 +99,30 @@ struct PhotonBufs {
     uint32_t* hwin;     /* [hnum] slot + 1 of the photon the cell keeps (0: empty) */
 };
 
+/* kd-tree photon map (orx_config.photon_map = 2, orx_kdtree.hip): the implicit
+ * balanced tree of OptixRenderer_CPUKdTree.cpp built on the device */
+struct KdBufs {
+    uint32_t S;          /* photon slots (bound on the valid photons) */
+    uint32_t tree_size;  /* m_photonKdTreeSize = pow2roundup(S + 1) - 1 (OptixRenderer.cpp:207) */
+    uint32_t levels;     /* log2(tree_size + 1): depth bound of any tree of <= S photons */
+    uint32_t ntiles;     /* radix-sort tiles of RS_TILE elements */
+    float4* tree;        /* [tree_size][3]: pos.xyz|axis bits, power.xyz|dir.x, dir.y dir.z */
+    uint32_t* ids[2][3]; /* [S] photon slots in position order, one list per axis, ping-pong */
+    uint32_t* keys[2];   /* [S] radix-sort keys */
+    uint32_t* nodepos;   /* [S] tree node of each position at the current level (0xffffffff: placed) */
+    uint8_t* side;       /* [S] by slot: 0 left, 1 right, 2 median of its segment at the current level */
+    uint2* seg;          /* [tree_size] segment [start, end) of each node (0xffffffff: not in the tree) */
+    float* box;          /* [tree_size][6] bbmin, bbmax handed down by buildKDTree */
+    uint32_t* ninfo;     /* [tree_size] split nodes: median << 2 | axis; else 0xffffffff */
+    uint32_t* P;         /* [6][S] exclusive (left, median) prefix per list */
+    uint32_t* ppart;     /* [6][S/1024] block counts, then their scan */
+    uint32_t* table;     /* [256][ntiles] radix digit counts, then their scan */
+    uint32_t* tpart;     /* scan partials */
+    uint32_t* vpart;     /* [S/1024] valid-slot block counts */
+    uint32_t* count;     /* [4]: [0] valid photons n */
+};
+void launch_kd_build(hipStream_t s, const PhotonBufs& pb, const KdBufs& kd);
+
 /* Stochastic-hash grid of one iteration: initializeStochasticHashPhotonMap
  * (OptixRenderer_SpatialHash.cu:286-302), computed on the host */
 struct HashParams {
@@ -155,6 +179,7 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
 void launch_hash_build(hipStream_t s, const PhotonBufs& pb, const HashParams& hp);
 void launch_ppm_gather_hash(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const HashParams& hp,
                             const Consts& c);
+void launch_ppm_gather_kd(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const KdBufs& kd, const Consts& c);
 /* mode 0: direct + output; 1: direct only; 2: output only */
 void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c, int mode = 0);
 void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c);

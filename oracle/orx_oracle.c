@@ -15,6 +15,7 @@
 #include "orx_oracle.h"
 #include "orx_detmath.h"
 
+#include <float.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -210,6 +211,7 @@ typedef struct { v3 c; float r; } sphere_t;
 
 typedef struct { v3 position, normal, attenuation, radiance; uint32_t flags; } hitpoint_t;
 typedef struct { v3 power, position, direction; } photon_t; /* Photon.h:10-33 */
+typedef struct kdphoton { photon_t p; uint32_t axis; } kdphoton_t; /* KD_TREE_CPU adds `axis` (Photon.h:27-29) */
 
 struct orc_renderer {
     orx_config cfg;
@@ -246,6 +248,9 @@ struct orc_renderer {
     /* stochastic hash (cfg.photon_map == 1): dslot slots per emitted photon, deposits per photon,
      * photonsHashTableCount and the slot + 1 each entry keeps */
     uint32_t dslot; uint8_t* ndep; uint32_t* hcount; uint32_t* hwin; size_t hnum;
+    /* kd-tree photon map (cfg.photon_map == 2): Photon records with their `axis` (Photon.h:27-29),
+     * the working copy of the slots and the implicit tree of kdsize nodes */
+    struct kdphoton* kdwork; struct kdphoton* kdtree; size_t kdsize; uint32_t kddepth;
     uint64_t sum_photons_visited, sum_cells_visited;
     /* VCM: pixelSizeFactor (OptixRenderer.cpp:306, :846), LVC-estimated flag (:83, :461, :847) */
     float psf_x, psf_y;
@@ -306,6 +311,8 @@ static void free_frame(orc_renderer* r) {
     r->vcount = NULL; r->vverts = NULL; r->vsplat = NULL; r->vcam = NULL; r->vcm_npx = 0; r->vcm_spx = 0;
     free(r->ndep); free(r->hcount); free(r->hwin);
     r->ndep = NULL; r->hcount = NULL; r->hwin = NULL;
+    free(r->kdwork); free(r->kdtree);
+    r->kdwork = NULL; r->kdtree = NULL; r->kdsize = 0;
 }
 void orc_destroy(orc_renderer* r) {
     if (!r) return;
@@ -947,6 +954,7 @@ static void trace_radiance(const orc_renderer* r, v3 o, v3 d, float tmin, rprd_t
 /* ------------------------------------------------------------------ */
 /* frame buffers                                                       */
 /* ------------------------------------------------------------------ */
+static uint32_t orc_pow2roundup(uint32_t x);
 static orx_status resize(orc_renderer* r, uint32_t W, uint32_t H) {
     free_frame(r);
     const uint32_t PW = r->cfg.photon_launch_width, PH = r->cfg.photon_launch_height;
@@ -968,6 +976,13 @@ static orx_status resize(orc_renderer* r, uint32_t W, uint32_t H) {
         r->hcount = (uint32_t*)calloc(r->hnum, 4);
         r->hwin = (uint32_t*)calloc(r->hnum, 4);
         if (!r->ndep || !r->hcount || !r->hwin) return fail(r, ORX_ERR_OUT_OF_MEMORY, "oracle: out of memory");
+    }
+    if (r->cfg.photon_map == 2) {
+        /* m_photonKdTreeSize = pow2roundup(NUM_PHOTONS + 1) - 1 (OptixRenderer.cpp:65-74, :207) */
+        r->kdsize = (size_t)orc_pow2roundup((uint32_t)S + 1u) - 1u;
+        r->kdwork = (kdphoton_t*)calloc(S + 1, sizeof(kdphoton_t));
+        r->kdtree = (kdphoton_t*)calloc(r->kdsize + 1, sizeof(kdphoton_t));
+        if (!r->kdwork || !r->kdtree) return fail(r, ORX_ERR_OUT_OF_MEMORY, "oracle: out of memory");
     }
     size_t G = r->cfg.photon_grid_max_size;
     r->rng = (uint32_t*)malloc((size_t)r->RW * r->RH * 6 * 4);
@@ -1477,6 +1492,192 @@ static void ppm_gather(orc_renderer* r, float ppmRadius, float ppmRadiusSquared,
     ppm_gather_src(r, &src, r->rows, r->indirect, r->dbg, ppmRadius, ppmRadiusSquared, emittedF);
 }
 
+/* ------------------------------------------------------------------ */
+/* kd-tree photon map (ACCELERATION_STRUCTURE_KD_TREE_CPU)             */
+/* ------------------------------------------------------------------ */
+/* pow2roundup (OptixRenderer.cpp:65-74) */
+static uint32_t orc_pow2roundup(uint32_t x) {
+    --x;
+    x |= x >> 1;
+    x |= x >> 2;
+    x |= x >> 4;
+    x |= x >> 8;
+    x |= x >> 16;
+    return x + 1;
+}
+#define PPM_X (1u << 0) /* config.h:12-16 */
+#define PPM_Y (1u << 1)
+#define PPM_Z (1u << 2)
+#define PPM_LEAF (1u << 3)
+#define PPM_NULL (1u << 4)
+
+static inline float kd_coord(const kdphoton_t* e, int axis) {
+    return axis == 0 ? e->p.position.x : axis == 1 ? e->p.position.y : e->p.position.z;
+}
+static inline void kd_swap(kdphoton_t* list, int a, int b) {
+    kdphoton_t t = list[a];
+    list[a] = list[b];
+    list[b] = t;
+}
+/* select.h `partition` (the variant that puts the pivot at its sorted position) */
+static int kd_partition(kdphoton_t* list, int left, int right, int pivotIndex, int axis) {
+    const kdphoton_t pivotValue = list[pivotIndex];
+    const float pv = kd_coord(&pivotValue, axis);
+    kd_swap(list, right, pivotIndex);
+    pivotIndex = right;
+    left--;
+    for (;;) {
+        do {
+            left++;
+        } while (left < right && kd_coord(&list[left], axis) < pv);
+        do {
+            right--;
+        } while (left < right && kd_coord(&list[right], axis) > pv);
+        if (left < right) {
+            kd_swap(list, left, right);
+        } else {
+            kd_swap(list, left, pivotIndex);
+            return left;
+        }
+    }
+}
+/* select.h `select`: pivot at the middle, loop until the k-th lands */
+static void kd_select(kdphoton_t* list, int left, int right, int k, int axis) {
+    for (;;) {
+        const int pivotIndex = (left + right) / 2;
+        const int pivotNewIndex = kd_partition(list, left, right, pivotIndex, axis);
+        if (k == pivotNewIndex) return;
+        if (k < pivotNewIndex) right = pivotNewIndex - 1;
+        else left = pivotNewIndex + 1;
+    }
+}
+/* max_component (OptixRenderer_CPUKdTree.cpp:14-25) */
+static int kd_max_component(v3 a) {
+    if (a.x > a.y && a.x > a.z) return 0;
+    if (a.y > a.z) return 1;
+    return 2;
+}
+/* buildKDTree (OptixRenderer_CPUKdTree.cpp:27-88) */
+static void kd_build(kdphoton_t* photons, int start, int end, uint32_t depth, kdphoton_t* kd_tree, size_t current_root,
+                     v3 bbmin, v3 bbmax, uint32_t* maxdepth) {
+    if (depth > *maxdepth) *maxdepth = depth;
+    if (end - start == 0) { /* NULL node: only axis and power are written */
+        kd_tree[current_root].axis = PPM_NULL;
+        kd_tree[current_root].p.power = mk1(0.0f);
+        return;
+    }
+    if (end - start == 1) {
+        photons[start].axis = PPM_LEAF;
+        kd_tree[current_root] = photons[start];
+        return;
+    }
+    const int axis = kd_max_component(sub(bbmax, bbmin));
+    const int median = (start + end) / 2;
+    kd_select(photons + start, 0, end - start - 1, median - start, axis);
+    photons[median].axis = axis == 0 ? PPM_X : axis == 1 ? PPM_Y : PPM_Z;
+    v3 rightMin = bbmin, leftMax = bbmax;
+    const v3 midPoint = photons[median].p.position;
+    if (axis == 0) { rightMin.x = midPoint.x; leftMax.x = midPoint.x; }
+    else if (axis == 1) { rightMin.y = midPoint.y; leftMax.y = midPoint.y; }
+    else { rightMin.z = midPoint.z; leftMax.z = midPoint.z; }
+    kd_tree[current_root] = photons[median];
+    kd_build(photons, start, median, depth + 1, kd_tree, 2 * current_root + 1, bbmin, leftMax, maxdepth);
+    kd_build(photons, median + 1, end, depth + 1, kd_tree, 2 * current_root + 2, rightMin, bbmax, maxdepth);
+}
+/* createPhotonKdTreeOnCPU (OptixRenderer_CPUKdTree.cpp:90-127): drop invalid photons by moving
+ * the last one into their place, bound the rest, build.  Nodes the build does not reach keep
+ * what earlier iterations left there (the reference never clears m_photonKdTree). */
+static void ppm_build_kdtree(orc_renderer* r) {
+    const size_t S = (size_t)r->cfg.photon_launch_width * r->prows * r->cfg.max_photon_deposits;
+    kdphoton_t* ph = r->kdwork;
+    for (size_t i = 0; i < S; i++) {
+        ph[i].p = r->photons[i];
+        ph[i].axis = 0;
+    }
+    uint32_t numValidPhotons = (uint32_t)(S >= r->kdsize ? r->kdsize : S);
+    for (uint32_t i = 0; i < numValidPhotons; ++i) {
+        if (!(fmax3(ph[i].p.power) > 0.0f)) {
+            ph[i] = ph[numValidPhotons - 1];
+            numValidPhotons--;
+            i--;
+        }
+    }
+    v3 bbmin = mk1(FLT_MAX), bbmax = mk1(-FLT_MAX);
+    for (uint32_t i = 0; i < numValidPhotons; ++i) {
+        bbmin = vmin(bbmin, ph[i].p.position);
+        bbmax = vmax(bbmax, ph[i].p.position);
+    }
+    uint32_t maxdepth = 0;
+    kd_build(ph, 0, (int)numValidPhotons, 0, r->kdtree, 0, bbmin, bbmax, &maxdepth);
+    r->kddepth = maxdepth;
+    r->valid = numValidPhotons;
+    r->ncells = (uint32_t)r->kdsize;
+}
+/* IndirectRadianceEstimation.cu:164-209 (the OptiX SDK PPM sample's traversal): visit a node,
+ * add its photon if valid, push the far child when the split plane is within the radius, go
+ * near.  The reference's stack of MAX_DEPTH = 21 entries overflows on trees deeper than 20
+ * levels (undefined behaviour there); the stack here holds a full 32-bit tree. */
+#define KD_STACK 40
+static void ppm_gather_kd_src(orc_renderer* r, const hp_src* src, uint32_t rows_total, v3* out, uint32_t* dbg,
+                              float ppmRadiusSquared, float emittedF) {
+    const uint32_t W = r->W, H = rows_total;
+    const kdphoton_t* tree = r->kdtree;
+    uint64_t sumP = 0;
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : sumP)
+    for (long long y = 0; y < (long long)H; y++) {
+        for (uint32_t x = 0; x < W; x++) {
+            const size_t px = (size_t)y * W + x;
+            const hitpoint_t rec = hp_fetch(r, src, px);
+            v3 acc = mk1(0.0f);
+            uint32_t dP = 0;
+            if (rec.flags & PRD_HIT_NON_SPECULAR) {
+                const float radius2 = ppmRadiusSquared;
+                const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
+                const float inv2r2 = 1.0f / (2 * radius2);
+                const float invDen = 1.0f / (1 - expNegativeBeta);
+                size_t stack[KD_STACK];
+                uint32_t sc = 0;
+                size_t node = 0;
+                stack[sc++] = 0;
+                do {
+                    const kdphoton_t* photon = &tree[node];
+                    dP++;
+                    const uint32_t axis = photon->axis;
+                    if (!(axis & PPM_NULL)) {
+                        const v3 diff = sub(rec.position, photon->p.position);
+                        const float distance2 = dot(diff, diff);
+                        if (distance2 <= radius2 && dot(neg(photon->p.direction), rec.normal) >= 0) {
+                            const float e = orx_expf_unit((-beta * distance2) * inv2r2);
+                            const float wgt = alpha * (1 - (1 - e) * invDen);
+                            acc = add(acc, scl(photon->p.power, wgt));
+                        }
+                        if (!(axis & PPM_LEAF)) {
+                            const float d = (axis & PPM_X) ? diff.x : (axis & PPM_Y) ? diff.y : diff.z;
+                            const size_t selector = d < 0.0f ? 0 : 1;
+                            if (d * d < radius2) stack[sc++] = (node << 1) + 2 - selector;
+                            node = (node << 1) + 1 + selector;
+                        } else {
+                            node = stack[--sc];
+                        }
+                    } else {
+                        node = stack[--sc];
+                    }
+                } while (node);
+            }
+            const float s1 = 1.0f / (ORX_PI_F * ppmRadiusSquared);
+            const float s2 = 1.0f / emittedF;
+            out[px] = scl(scl(mul(acc, rec.attenuation), s1), s2);
+            if (dbg) {
+                dbg[2 * px] = 0;
+                dbg[2 * px + 1] = dP;
+            }
+            sumP += dP;
+        }
+    }
+    r->sum_photons_visited = sumP;
+    r->sum_cells_visited = 0;
+}
+
 /* helpers/light.h:29-87 */
 static v3 light_contribution(const orc_renderer* r, const light_t* light, v3 pos, v3 normal, uint32_t* rs) {
     float lightFactor = 1;
@@ -1646,6 +1847,10 @@ orx_status orc_render_next_iteration(orc_renderer* r, uint64_t iter, uint64_t lo
         if (r->cfg.photon_map == 1) {
             ppm_build_hash(r, ppmRadius);
             ppm_gather_hash(r, ppmRadiusSquared, emittedF);
+        } else if (r->cfg.photon_map == 2) {
+            ppm_build_kdtree(r);
+            hp_src src = {r->hp, NULL, 0};
+            ppm_gather_kd_src(r, &src, r->rows, r->indirect, r->dbg, ppmRadiusSquared, emittedF);
         } else {
             orx_status s = ppm_build_grid(r);
             if (s != ORX_OK) return s;
@@ -1679,8 +1884,12 @@ orx_status orc_ppm_local_passes(orc_renderer* r, uint64_t iter, uint64_t local, 
     cam_t cam = camera_setup(&det->camera);
     ppm_eye_pass(r, &cam);
     ppm_photon_pass(r);
-    orx_status s = ppm_build_grid(r);
-    if (s != ORX_OK) return s;
+    if (r->cfg.photon_map == 2) {
+        ppm_build_kdtree(r);
+    } else {
+        orx_status s = ppm_build_grid(r);
+        if (s != ORX_OK) return s;
+    }
     r->last_radius = ppmRadius;
     r->last_radius2 = ppmRadius * ppmRadius;
     r->last_local = local;
@@ -1708,7 +1917,10 @@ orx_status orc_ppm_gather_external(orc_renderer* r, const void* hp, uint32_t seg
     if (!hp || !indirect || bytes < (size_t)segments * r->max_rows * r->W * 12) return ORX_ERR_INVALID_ARGUMENT;
     hp_src src = {NULL, (const float*)hp, r->max_rows};
     float emittedF = (float)(r->cfg.photon_launch_width * r->cfg.photon_launch_height);
-    ppm_gather_src(r, &src, segments * r->max_rows, (v3*)indirect, NULL, r->last_radius, r->last_radius2, emittedF);
+    if (r->cfg.photon_map == 2)
+        ppm_gather_kd_src(r, &src, segments * r->max_rows, (v3*)indirect, NULL, r->last_radius2, emittedF);
+    else
+        ppm_gather_src(r, &src, segments * r->max_rows, (v3*)indirect, NULL, r->last_radius, r->last_radius2, emittedF);
     return ORX_OK;
 }
 orx_status orc_ppm_finish(orc_renderer* r, const void* indirect, size_t bytes) {
@@ -1739,6 +1951,8 @@ orx_status orc_read_buffer(orc_renderer* r, int32_t id, void* dst, size_t bytes,
     case ORX_BUF_VCM_VERTEX_COUNT: need = r->vcm_npx * 4; break;
     case ORX_BUF_VCM_VERTICES: need = r->vcm_npx * VCM_MAX_VERTS * 64; break;
     case ORX_BUF_VCM_SPLAT: case ORX_BUF_VCM_CAMERA: need = r->vcm_npx * 12; break; /* own rows */
+    case ORX_BUF_KD_TREE: need = r->kdsize * 40; break;
+    case ORX_BUF_PHOTON_SLOTS: need = (size_t)r->cfg.photon_launch_width * r->prows * r->dslot * 36; break;
     default: return fail(r, ORX_ERR_INVALID_ARGUMENT, "unknown buffer id");
     }
     if (out_bytes) *out_bytes = need;
@@ -1778,6 +1992,17 @@ orx_status orc_read_buffer(orc_renderer* r, int32_t id, void* dst, size_t bytes,
     case ORX_BUF_VCM_VERTICES: memcpy(dst, r->vverts, need); break;
     case ORX_BUF_VCM_SPLAT: memcpy(dst, r->vsplat + (size_t)r->rank * r->max_rows * r->W, need); break;
     case ORX_BUF_VCM_CAMERA: memcpy(dst, r->vcam, need); break;
+    case ORX_BUF_PHOTON_SLOTS: /* slot order: the grid build swapped the unsorted slots into sort_tmp */
+        memcpy(dst, (r->cfg.photon_map == 0 && r->ncells) ? r->sort_tmp : r->photons, need);
+        break;
+    case ORX_BUF_KD_TREE: {
+        float* f = (float*)dst;
+        for (size_t i = 0; i < r->kdsize; i++) {
+            memcpy(f + 10 * i, &r->kdtree[i].p, 36);
+            memcpy(f + 10 * i + 9, &r->kdtree[i].axis, 4);
+        }
+        break;
+    }
     }
     return ORX_OK;
 }

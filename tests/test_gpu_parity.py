@@ -388,3 +388,45 @@ def test_stochastic_hash_parity(scene_name, W, H, P):
     assert g.mean() > 0
     gpu.destroy()
     ora.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene_name,W,H,P", [("Cornell", 64, 48, 64), ("CornellSmall", 48, 48, 32),
+                                              ("Cornell", 32, 32, 256)])
+def test_kdtree_parity(scene_name, W, H, P):
+    """photon_map = 2 (ACCELERATION_STRUCTURE_KD_TREE_CPU, built on the device): RNG, hit points,
+    photons and direct light are bit-exact; the device tree is a valid balanced kd-tree of the
+    reference's shape (median = (start+end)/2 at every node) over exactly the valid photons; the
+    indirect estimate matches within fp32 summation order.  Where several photons share a split
+    coordinate, select.h's sequential partition decides which go left on the CPU and the slot
+    order does here, so the subtrees below such a split hold different photons and the visit
+    counters differ slightly; the search is exact in both, so every pixel accepts the same photons."""
+    from test_kdtree import check_tree, read_tree
+
+    scene = scenes.scene_by_name(scene_name)
+    gpu, ora, det = make_pair(scene, W, H, P, _abi.PROGRESSIVE_PHOTON_MAPPING, photon_map=_abi.PHOTON_MAP_KD_TREE)
+    radius = scene.initial_ppm_radius()
+    for it in range(3):
+        gpu.renderNextIteration(it, it, radius, True, det)
+        ora.render_next_iteration(it, it, radius, det.to_abi())
+        for buf in (_abi.BUF_RNG, _abi.BUF_HITPOINTS, _abi.BUF_DIRECT):
+            g, o = gpu.read_buffer(buf, np.uint32), ora.read_buffer(buf, np.uint32)
+            assert g.shape == o.shape and np.count_nonzero(g != o) == 0, f"buffer {buf} differs (iteration {it})"
+        gs_, os_ = gpu.read_buffer(_abi.BUF_PHOTON_SLOTS).reshape(-1, 9), ora.read_buffer(_abi.BUF_PHOTON_SLOTS).reshape(-1, 9)
+        valid = os_[:, 0:3].max(1) > 0
+        assert np.array_equal(gs_[valid].view(np.uint32), os_[valid].view(np.uint32))
+        gph, gax = read_tree(gpu)
+        oph, oax = read_tree(ora)
+        assert gph.shape == oph.shape
+        idx = check_tree(gph, gax, os_[valid])
+        assert np.array_equal(idx, check_tree(oph, oax, os_[valid]))
+        gst, ost = gpu.stats(), ora.stats()
+        assert gst.valid_photons == ost.valid_photons == int(valid.sum())
+        assert gst.num_cells == ost.num_cells == gph.shape[0]
+        assert abs(int(gst.photons_visited) - int(ost.photons_visited)) <= 0.05 * ost.photons_visited
+        assert rel_l2(gpu.read_buffer(_abi.BUF_INDIRECT), ora.read_buffer(_abi.BUF_INDIRECT)) < 1e-5
+        radius = next_ppm_radius(radius, it)
+    g, o = gpu.getOutputBuffer(), ora.output()
+    assert rel_l2(g, o) < 1e-5 and g.mean() > 0
+    gpu.destroy()
+    ora.close()
