@@ -375,7 +375,7 @@ struct orx_renderer {
     DevBuf d_pos4, d_bstable, d_bspartials, d_bspairs, d_subofs;  /* bucket-sort grid build */
     DevBuf d_hcount, d_hwin;  /* stochastic hash table */
     /* kd-tree photon map (photon_map = 2, orx_kdtree.hip) */
-    DevBuf d_kdtree, d_kdids, d_kdkeys, d_kdnodepos, d_kdside, d_kdseg, d_kdbox, d_kdninfo, d_kdP, d_kdppart,
+    DevBuf d_kdtree, d_kdids, d_kdlst, d_kdnkey, d_kdkeys, d_kdnodepos, d_kdseg, d_kdbox, d_kdninfo, d_kdP, d_kdppart,
         d_kdtable, d_kdtpart, d_kdvpart, d_kdcount;
     KdBufs kd{};
     f3 aabb_lo{}, aabb_hi{};  /* IScene::getSceneAABB (the stochastic hash grid's bounds) */
@@ -913,7 +913,8 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
         HIPCHK(r, r->d_kdids.ensure(6 * S * 4 + 64));
         HIPCHK(r, r->d_kdkeys.ensure(2 * S * 4 + 64));
         HIPCHK(r, r->d_kdnodepos.ensure(S * 4 + 16));
-        HIPCHK(r, r->d_kdside.ensure(S + 16));
+        HIPCHK(r, r->d_kdlst.ensure(6 * S * 16 + 64));
+        HIPCHK(r, r->d_kdnkey.ensure(tree * 8 + 16));
         HIPCHK(r, r->d_kdseg.ensure(tree * 8 + 16));
         HIPCHK(r, r->d_kdbox.ensure(tree * 24 + 24));
         HIPCHK(r, r->d_kdninfo.ensure(tree * 4 + 16));
@@ -931,11 +932,14 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
         kd.ntiles = (uint32_t)ntiles;
         kd.tree = r->d_kdtree.as<float4>();
         for (int q = 0; q < 2; q++)
-            for (int a = 0; a < 3; a++) kd.ids[q][a] = r->d_kdids.as<uint32_t>() + (size_t)(3 * q + a) * S;
+            for (int a = 0; a < 3; a++) {
+                kd.ids[q][a] = r->d_kdids.as<uint32_t>() + (size_t)(3 * q + a) * S;
+                kd.lst[q][a] = r->d_kdlst.as<float4>() + (size_t)(3 * q + a) * S;
+            }
         kd.keys[0] = r->d_kdkeys.as<uint32_t>();
         kd.keys[1] = kd.keys[0] + S;
         kd.nodepos = r->d_kdnodepos.as<uint32_t>();
-        kd.side = r->d_kdside.as<uint8_t>();
+        kd.nkey = r->d_kdnkey.as<uint2>();
         kd.seg = r->d_kdseg.as<uint2>();
         kd.box = r->d_kdbox.as<float>();
         kd.ninfo = r->d_kdninfo.as<uint32_t>();

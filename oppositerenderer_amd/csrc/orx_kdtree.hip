@@ -17,14 +17,14 @@
  *     k_kd_nodes                node = its segment's median along the
  *                               box's longest axis (max_component), children
  *                               segments and boxes; NULL / LEAF nodes
- *     k_kd_side                 every element of a split segment: left,
- *                               median or right, from its rank in the
- *                               split axis' list
  *     k_kd_pcount, scan, k_kd_pprefix, k_kd_pmove   stable partition of all
  *                               three lists into [left | median | right]
  *
- * Each segment of every list stays sorted by its axis (ties by slot order), so
- * the median of a segment is read directly at (start+end)/2.  The tree's shape,
+ * Each segment of every list stays sorted by its axis' (ordered key, slot), so
+ * the median of a segment is read directly at (start+end)/2, and an element's
+ * side follows from comparing its own (key, slot) on the split axis with the
+ * median's: list entries carry the photon position and slot (16 B), so the
+ * partition passes stream the lists with no random reads.  The tree's shape,
  * axes and split coordinates depend only on the photon multiset, so they equal
  * the reference's; which of several photons with the same split coordinate
  * becomes the node is the one freedom (select.h breaks such ties by its
@@ -182,6 +182,14 @@ __global__ __launch_bounds__(256) void k_kd_keys(PhotonBufs pb, KdBufs kd, uint3
     kd.keys[0][i] = kd_f2ord(kd_comp(pb.pos4[s], axis));
     kd.ids[0][axis][i] = s;
 }
+/* sorted slots -> list records (position, slot) */
+__global__ __launch_bounds__(256) void k_kd_lists(PhotonBufs pb, KdBufs kd, uint32_t axis) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= kd.count[0]) return;
+    const uint32_t s = kd.ids[0][axis][i];
+    const float4 a = pb.pos4[s];
+    kd.lst[0][axis][i] = make_float4(a.x, a.y, a.z, __uint_as_float(s));
+}
 /* histogram of one digit per tile -> table[digit][tile] */
 __global__ __launch_bounds__(256) void k_rs_count(const uint32_t* keys, const uint32_t* count, uint32_t shift,
                                                   uint32_t* table, uint32_t ntiles) {
@@ -307,7 +315,8 @@ __global__ __launch_bounds__(256) void k_kd_nodes(PhotonBufs pb, KdBufs kd, uint
                 axis = (dx > dy && dx > dz) ? 0u : (dy > dz ? 1u : 2u); /* max_component :14-25 */
                 med = (se.x + se.y) / 2;
             }
-            const uint32_t s = kd.ids[src][axis][med];
+            const float4 e = kd.lst[src][axis][med];
+            const uint32_t s = __float_as_uint(e.w);
             const float4* sl = pb.slots + 4 * (size_t)s;
             const float4 a = sl[0], b = sl[1], c = sl[2];
             const uint32_t flag = size == 1 ? KD_PPM_LEAF : (KD_PPM_X << axis);
@@ -316,6 +325,7 @@ __global__ __launch_bounds__(256) void k_kd_nodes(PhotonBufs pb, KdBufs kd, uint
             rec[2] = make_float4(b.y, b.z, 0.f, 0.f);
             if (size > 1) {
                 info = (med << 2) | axis;
+                kd.nkey[node] = make_uint2(kd_f2ord(kd_comp(e, axis)), s);
                 if (has_children) {
                     const float* bx = kd.box + 6 * (size_t)node;
                     const float split = kd_comp(make_float4(a.x, a.y, a.z, 0.f), axis);
@@ -340,26 +350,24 @@ __global__ __launch_bounds__(256) void k_kd_nodes(PhotonBufs pb, KdBufs kd, uint
     }
 }
 
-/* every element of a split segment learns its side from its rank in the split axis' list */
-__global__ __launch_bounds__(256) void k_kd_side(KdBufs kd, uint32_t src) {
-    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
-    if (p >= kd.count[0]) return;
-    const uint32_t node = kd.nodepos[p];
-    if (node == KD_NONE) return;
-    const uint32_t info = kd.ninfo[node];
-    if (info == KD_NONE) return;
-    const uint32_t m = info >> 2, axis = info & 3u;
-    kd.side[kd.ids[src][axis][p]] = p < m ? 0 : (p == m ? 2 : 1);
+/* side of a list element in its split segment: (key, slot) on the split axis against the median's */
+__device__ __forceinline__ uint32_t kd_side(const float4& e, uint32_t axis, uint2 mk) {
+    const uint32_t k = kd_f2ord(kd_comp(e, axis)), sl = __float_as_uint(e.w);
+    if (k != mk.x) return k < mk.x ? 0u : 1u;
+    if (sl != mk.y) return sl < mk.y ? 0u : 1u;
+    return 2u;
 }
-
 /* per position: (left, median) indicators of the three lists, packed left | median << 16 */
 __device__ __forceinline__ void kd_pos_bits(const KdBufs& kd, uint32_t src, uint32_t p, uint32_t n, uint32_t v[3]) {
     v[0] = v[1] = v[2] = 0;
     if (p >= n) return;
     const uint32_t node = kd.nodepos[p];
-    if (node == KD_NONE || kd.ninfo[node] == KD_NONE) return;
+    if (node == KD_NONE) return;
+    const uint32_t info = kd.ninfo[node];
+    if (info == KD_NONE) return;
+    const uint2 mk = kd.nkey[node];
     for (int b = 0; b < 3; b++) {
-        const uint32_t sd = kd.side[kd.ids[src][b][p]];
+        const uint32_t sd = kd_side(kd.lst[src][b][p], info & 3u, mk);
         v[b] = sd == 0 ? 1u : (sd == 2 ? 0x10000u : 0u);
     }
 }
@@ -423,15 +431,16 @@ __global__ __launch_bounds__(256) void k_kd_pmove(KdBufs kd, uint32_t src) {
     }
     const uint32_t m = info >> 2;
     const uint32_t s = kd.seg[node].x;
+    const uint2 mk = kd.nkey[node];
     const size_t S = kd.S;
     for (int b = 0; b < 3; b++) {
-        const uint32_t id = kd.ids[src][b][p];
-        const uint32_t sd = kd.side[id];
+        const float4 e = kd.lst[src][b][p];
+        const uint32_t sd = kd_side(e, info & 3u, mk);
         if (sd == 2) continue;
         const uint32_t L = kd.P[(2 * b) * S + p] - kd.P[(2 * b) * S + s];
         const uint32_t M = kd.P[(2 * b + 1) * S + p] - kd.P[(2 * b + 1) * S + s];
         const uint32_t dst = sd == 0 ? s + L : m + 1 + (p - s) - L - M;
-        kd.ids[src ^ 1][b][dst] = id;
+        kd.lst[src ^ 1][b][dst] = e;
     }
     kd.nodepos[p] = p < m ? 2 * node + 1 : (p > m ? 2 * node + 2 : KD_NONE);
 }
@@ -465,6 +474,7 @@ void launch_kd_build(hipStream_t st, const PhotonBufs& pb, const KdBufs& kd) {
             std::swap(v0, v1);
         }
         /* four passes: the result is back in (keys[0], ids[0][axis]) */
+        hipLaunchKernelGGL(k_kd_lists, dim3(nb256), dim3(256), 0, st, pb, kd, axis);
     }
     hipLaunchKernelGGL(k_kd_root, dim3(1), dim3(64), 0, st, pb, kd);
     hipLaunchKernelGGL(k_kd_pos_init, dim3(nb256), dim3(256), 0, st, kd);
@@ -474,7 +484,6 @@ void launch_kd_build(hipStream_t st, const PhotonBufs& pb, const KdBufs& kd) {
         const uint32_t nodes = 1u << level;
         hipLaunchKernelGGL(k_kd_nodes, dim3((nodes + 255) / 256), dim3(256), 0, st, pb, kd, level, src);
         if (level + 1 == kd.levels) break; /* the last level holds leaves and NULL nodes only */
-        hipLaunchKernelGGL(k_kd_side, dim3(nb256), dim3(256), 0, st, kd, src);
         hipLaunchKernelGGL(k_kd_pcount, dim3(nblk), dim3(256), 0, st, kd, src, nblk);
         kd_scan(st, kd.ppart, 6 * nblk, kd.tpart, nullptr);
         hipLaunchKernelGGL(k_kd_pprefix, dim3(nblk), dim3(256), 0, st, kd, src, nblk);

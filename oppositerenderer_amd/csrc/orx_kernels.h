@@ -107,10 +107,11 @@ struct KdBufs {
     uint32_t levels;     /* log2(tree_size + 1): depth bound of any tree of <= S photons */
     uint32_t ntiles;     /* radix-sort tiles of RS_TILE elements */
     float4* tree;        /* [tree_size][3]: pos.xyz|axis bits, power.xyz|dir.x, dir.y dir.z */
-    uint32_t* ids[2][3]; /* [S] photon slots in position order, one list per axis, ping-pong */
+    uint32_t* ids[2][3]; /* [S] radix-sort slot lists (ids[1][0]: valid slots in slot order) */
+    float4* lst[2][3];   /* [S] per axis, position order: photon position | slot bits; ping-pong per level */
+    uint2* nkey;         /* [tree_size] split nodes: the median's (ordered key on the split axis, slot) */
     uint32_t* keys[2];   /* [S] radix-sort keys */
     uint32_t* nodepos;   /* [S] tree node of each position at the current level (0xffffffff: placed) */
-    uint8_t* side;       /* [S] by slot: 0 left, 1 right, 2 median of its segment at the current level */
     uint2* seg;          /* [tree_size] segment [start, end) of each node (0xffffffff: not in the tree) */
     float* box;          /* [tree_size][6] bbmin, bbmax handed down by buildKDTree */
     uint32_t* ninfo;     /* [tree_size] split nodes: median << 2 | axis; else 0xffffffff */
