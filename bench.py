@@ -167,10 +167,12 @@ def main():
     light_vertices = 0
     if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING:
         light_vertices = int(np.minimum(r.read_buffer(_abi.BUF_VCM_VERTEX_COUNT, np.uint32), 9).sum())
-    pbytes = roofline.pass_bytes(method, W, H, P * P, valid_avg, st.num_cells, light_vertices)
-    key = f"{scene.name}:{W}x{H}:{args.method}" + (f":P{P}" if method == 2 else "")
-    traffic = traffic_lookup(key, roofline.KERNELS_OF_PASS[dominant])
-    roof = roofline.roofline(dominant, pbytes[dominant], per_pass[dominant], traffic)
+    pmap = PHOTON_MAPS[args.photon_map]
+    pbytes = roofline.pass_bytes(method, W, H, P * P, valid_avg, st.num_cells, light_vertices, photon_map=pmap)
+    key = (f"{scene.name}:{W}x{H}:{args.method}" + (f":P{P}" if method == 2 else "")
+           + (f":{args.photon_map}" if pmap else ""))
+    traffic = traffic_lookup(key, roofline.kernels_of(dominant, pmap))
+    roof = roofline.roofline(dominant, pbytes[dominant], per_pass[dominant], traffic, photon_map=pmap)
     passes = {k: {"ms": round(v, 4), "algorithmic_GBps": round(pbytes.get(k, 0) / (v * 1e-3) / 1e9, 1)}
               for k, v in per_pass.items()}
     if method == _abi.PROGRESSIVE_PHOTON_MAPPING:

@@ -33,6 +33,17 @@ KERNELS_OF_PASS = {
 }
 
 
+# the other photon maps (orx_config.photon_map): the grid passes' event slots time their build and gather
+KERNELS_OF_PASS_MAP = {
+    1: {"grid_hash": ["k_hash_build"], "ppm_gather": ["k_ppm_gather_hash"]},
+    2: {"grid_hash": ["k_kd_*", "k_rs_*"], "ppm_gather": ["k_ppm_gather_kd"]},
+}
+
+
+def kernels_of(pass_name: str, photon_map: int = 0) -> list:
+    return KERNELS_OF_PASS_MAP.get(photon_map, {}).get(pass_name, KERNELS_OF_PASS.get(pass_name, [pass_name]))
+
+
 def paths_per_iteration(method: int, W: int, H: int, photons: int) -> int:
     """PT W*H; PPM W*H eye + emitted photon paths; VCM 2*W*H."""
     if method == _abi.PROGRESSIVE_PHOTON_MAPPING:
@@ -43,7 +54,8 @@ def paths_per_iteration(method: int, W: int, H: int, photons: int) -> int:
 
 
 def pass_bytes(method: int, W: int, H: int, photons: int, valid: float = 0.0, cells: int = 0,
-               light_vertices: float = 0.0, deposits_max: int = 4, grid_max: int = 1000000) -> dict:
+               light_vertices: float = 0.0, deposits_max: int = 4, grid_max: int = 1000000,
+               photon_map: int = 0) -> dict:
     """Bytes per launch of each pass.
 
     valid: grid-resident photons (deposits with power > 0); cells: grid cells G;
@@ -53,6 +65,16 @@ def pass_bytes(method: int, W: int, H: int, photons: int, valid: float = 0.0, ce
     slots = photons * deposits_max
     table = ((cells + 1023) // 1024) * ((slots + 16383) // 16384)
     R2 = 2 * R_RNG
+    if method == _abi.PROGRESSIVE_PHOTON_MAPPING and photon_map == 2:
+        # kd-tree: the build reads each valid photon's position once and writes its 48 B node;
+        # the gather reads every hitpoint and writes the indirect (node reads are visit-dependent)
+        return {
+            "ppm_eye": N * (R2 + 40),
+            "ppm_photon": photons * (R2 + 1) + valid * (36 + 12),
+            "grid_hash": photons * 1 + valid * (12 + 48),
+            "ppm_gather": N * (40 + 12) + valid * 48,
+            "ppm_direct_output": N * (40 + R2 + 12 + 12 + 24),
+        }
     if method == _abi.PROGRESSIVE_PHOTON_MAPPING:
         return {
             # RNG RMW + one 40 B hitpoint (pos|flags 16, normal-or-radiance|atten.x 16, atten.yz 8)
@@ -82,9 +104,9 @@ def pass_bytes(method: int, W: int, H: int, photons: int, valid: float = 0.0, ce
     return {"pt": N * (R2 + 24)}
 
 
-def roofline(pass_name: str, bytes_per_launch: float, ms_per_launch: float, traffic=None) -> dict:
+def roofline(pass_name: str, bytes_per_launch: float, ms_per_launch: float, traffic=None, photon_map: int = 0) -> dict:
     achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9 if ms_per_launch > 0 else 0.0
-    return {"kernel": "+".join(KERNELS_OF_PASS.get(pass_name, [pass_name])), "pass": pass_name, "bound": "hbm",
+    return {"kernel": "+".join(kernels_of(pass_name, photon_map)), "pass": pass_name, "bound": "hbm",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(ms_per_launch, 4)}
