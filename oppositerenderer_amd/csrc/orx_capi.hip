@@ -354,6 +354,14 @@ struct orx_renderer {
     hipStream_t aux = nullptr;   /* PPM direct pass, overlapped with the grid build and gather */
     hipEvent_t ev_photon_done = nullptr, ev_direct_done = nullptr;
     bool overlap_direct = false;
+    /* PPM iteration pipelining (world 1, uniform grid, own stream): the gather and output of
+     * iteration i run on gstream beside the eye/photon/grid passes of iteration i+1, each
+     * iteration on one of two buffer sets (hitpoints, direct, grid-ordered photons, offsets,
+     * grid parameters); ev_gdone[k] marks the end of the last gather+output on set k */
+    hipStream_t gstream = nullptr;
+    hipEvent_t ev_grid_done = nullptr, ev_gdone[2] = {nullptr, nullptr};
+    bool pipe_bufs = false, pend = false;
+    uint32_t pp = 0;
     std::string err;
     bool scene_ready = false;
     /* scene */
@@ -374,6 +382,7 @@ struct orx_renderer {
     DevBuf d_wray0, d_wray1, d_whit, d_wpath, d_wseg; /* wavefront photon pass queues */
     DevBuf d_pos4, d_bstable, d_bspartials, d_bspairs, d_subofs;  /* bucket-sort grid build */
     DevBuf d_hcount, d_hwin;  /* stochastic hash table */
+    DevBuf d_hp2, d_dir2, d_sorted2, d_subofs2, d_offsets2, d_grid2; /* second buffer set (pipelining) */
     /* kd-tree photon map (photon_map = 2, orx_kdtree.hip) */
     DevBuf d_kdtree, d_kdids, d_kdlst, d_kdnkey, d_kdkeys, d_kdnodepos, d_kdseg, d_kdbox, d_kdninfo, d_kdP, d_kdppart,
         d_kdtable, d_kdtpart, d_kdvpart, d_kdcount;
@@ -412,6 +421,8 @@ static orx_status set_err(orx_renderer* r, orx_status s, const std::string& m) {
             return set_err(r, e_ == hipErrorOutOfMemory ? ORX_ERR_OUT_OF_MEMORY : ORX_ERR_DEVICE,          \
                            std::string("HIP error in ") + #x + ": " + hipGetErrorString(e_));           \
     } while (0)
+
+static orx_status sync_all(orx_renderer* r);
 
 extern "C" {
 
@@ -455,6 +466,16 @@ static bool hash_config_ok(const orx_config& c) {
     return n && n <= (1ull << 31) && (n & (n - 1)) == 0 && c.max_photon_trace_depth <= 9;
 }
 
+/* the deferred gather yields to the next iteration's passes (ORX_GATHER_PRIORITY: 0 normal,
+ * 1 lowest, the default; measured equal on the hall) */
+static int gather_stream_priority() {
+    const char* e = getenv("ORX_GATHER_PRIORITY");
+    if (e && atoi(e) == 0) return 0;
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
+    return least;
+}
+
 orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out) {
     if (!out) return ORX_ERR_INVALID_ARGUMENT;
     *out = nullptr;
@@ -474,8 +495,13 @@ orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out)
     if (!r) return ORX_ERR_OUT_OF_MEMORY;
     r->device = hip_device;
     r->cfg = c;
-    if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
+    if (hipSetDevice(hip_device) != hipSuccess ||
+        hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&r->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithPriority(&r->gstream, hipStreamNonBlocking, gather_stream_priority()) != hipSuccess ||
+        hipEventCreateWithFlags(&r->ev_grid_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&r->ev_gdone[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&r->ev_gdone[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_photon_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_direct_done, hipEventDisableTiming) != hipSuccess) {
         delete r;
@@ -492,6 +518,10 @@ void orx_destroy(orx_renderer* r) {
     for (int p = 0; p < P_COUNT; p++)
         for (hipEvent_t e : r->ev[p]) hipEventDestroy(e);
     if (r->aux) hipStreamSynchronize(r->aux);
+    if (r->gstream) hipStreamSynchronize(r->gstream);
+    for (hipEvent_t e : {r->ev_grid_done, r->ev_gdone[0], r->ev_gdone[1]})
+        if (e) hipEventDestroy(e);
+    if (r->gstream) hipStreamDestroy(r->gstream);
     if (r->ev_photon_done) hipEventDestroy(r->ev_photon_done);
     if (r->ev_direct_done) hipEventDestroy(r->ev_direct_done);
     if (r->aux) hipStreamDestroy(r->aux);
@@ -517,6 +547,10 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     if (s->n_lights == 0 || !s->lights) return set_err(r, ORX_ERR_NO_LIGHTS, "No lights exists in this scene.");
     if (s->n_materials == 0 || !s->materials) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "scene has no materials");
     HIPCHK(r, hipSetDevice(r->device));
+    {
+        orx_status s0 = sync_all(r); /* in-flight passes read the scene being replaced */
+        if (s0 != ORX_OK) return s0;
+    }
     const uint32_t nq = s->n_quads, ns = s->n_spheres, nt = s->n_triangles, nm = s->n_materials;
     /* validate material indices and triangle vertex indices */
     for (uint32_t i = 0; i < nq; i++)
@@ -849,6 +883,22 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_bspartials.ensure((bs_nscan + 2) * 4));
     HIPCHK(r, r->d_bspairs.ensure(S * 8 + 16));
     HIPCHK(r, r->d_subofs.ensure(G2 * 4 * SUBX * nsub + 16));
+    /* second buffer set for PPM pipelining (single device, uniform grid) */
+    r->pipe_bufs = false;
+    r->pend = false;
+    if (r->world == 1 && r->cfg.photon_map == 0) {
+        HIPCHK(r, r->d_hp2.ensure(nhp * 40));
+        HIPCHK(r, r->d_dir2.ensure(nhp * 12));
+        HIPCHK(r, r->d_sorted2.ensure(9 * splane * 4));
+        HIPCHK(r, hipMemsetAsync(r->d_sorted2.p, 0, 9 * splane * 4, r->stream));
+        HIPCHK(r, r->d_subofs2.ensure(G2 * 4 * SUBX * nsub + 16));
+        HIPCHK(r, r->d_offsets2.ensure(G2 * 4));
+        HIPCHK(r, hipMemsetAsync(r->d_offsets2.p, 0, G2 * 4, r->stream));
+        HIPCHK(r, r->d_grid2.ensure(sizeof(GridParams)));
+        HIPCHK(r, hipMemsetAsync(r->d_grid2.p, 0, sizeof(GridParams), r->stream));
+        HIPCHK(r, hipMemsetAsync(r->d_hp2.p, 0, nhp * 40, r->stream));
+        r->pipe_bufs = true;
+    }
     const size_t wnseg = (nphot + 511) / 512 + 1;
     HIPCHK(r, r->d_wseg.ensure(2 * wnseg * 4));
     HIPCHK(r, hipMemsetAsync(r->d_wseg.p, 0, 2 * wnseg * 4, r->stream));
@@ -1029,13 +1079,46 @@ static inline void ev_end_on(orx_renderer* r, int p, hipStream_t st) {
     r->ev_n[p]++;
 }
 
+static inline hipStream_t cur_stream(orx_renderer* r) { return r->use_ext ? r->ext_stream : r->stream; }
+
+/* order everything later on the renderer's stream after a deferred gather + output */
+static void flush_pipeline(orx_renderer* r) {
+    if (!r->pend) return;
+    hipStreamWaitEvent(cur_stream(r), r->ev_gdone[r->pp], 0);
+    r->pend = false;
+}
+
 static orx_status sync_all(orx_renderer* r) {
+    flush_pipeline(r);
     HIPCHK(r, hipStreamSynchronize(r->stream));
     if (r->use_ext) HIPCHK(r, hipStreamSynchronize(r->ext_stream));
+    if (r->gstream) HIPCHK(r, hipStreamSynchronize(r->gstream));
     return ORX_OK;
 }
 
-static inline hipStream_t cur_stream(orx_renderer* r) { return r->use_ext ? r->ext_stream : r->stream; }
+static inline void swap_buf(DevBuf& a, DevBuf& b) {
+    std::swap(a.p, b.p);
+    std::swap(a.bytes, b.bytes);
+}
+/* switch to the other buffer set and point the kernels' views at it */
+static void swap_sets(orx_renderer* r) {
+    swap_buf(r->d_hp, r->d_hp2);
+    swap_buf(r->d_dir, r->d_dir2);
+    swap_buf(r->d_sorted, r->d_sorted2);
+    swap_buf(r->d_subofs, r->d_subofs2);
+    swap_buf(r->d_offsets, r->d_offsets2);
+    swap_buf(r->d_grid, r->d_grid2);
+    const size_t nhp = (size_t)r->max_rows * r->W;
+    r->px.hpA = r->d_hp.as<float4>();
+    r->px.hpB = r->d_hp.as<float4>() + nhp;
+    r->px.hpC = (float2*)(r->d_hp.as<float4>() + 2 * nhp);
+    r->px.direct = r->d_dir.as<float>();
+    r->pb.sorted = r->d_sorted.as<float>();
+    if (r->pb.subofs) r->pb.subofs = r->d_subofs.as<uint32_t>();
+    r->pb.offsets = r->d_offsets.as<uint32_t>();
+    r->pb.grid = r->d_grid.as<GridParams>();
+    r->pp ^= 1u;
+}
 
 static Consts make_consts(orx_renderer* r, float ppm_radius, uint64_t local_iteration_number) {
     Consts c;
@@ -1050,7 +1133,8 @@ static Consts make_consts(orx_renderer* r, float ppm_radius, uint64_t local_iter
 }
 
 /* resize / RNG init / output clear common to every method (OptixRenderer.cpp:531-557) */
-static orx_status begin_iteration(orx_renderer* r, uint64_t local_iteration_number, const orx_request* det) {
+static orx_status begin_iteration(orx_renderer* r, uint64_t local_iteration_number, const orx_request* det,
+                                  bool pipelined = false) {
     if (!r->scene_ready) return set_err(r, ORX_ERR_STATE, "Traced before OptixRenderer was initialized.");
     if (det->width == 0 || det->height == 0) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "zero-sized request");
     HIPCHK(r, hipSetDevice(r->device));
@@ -1060,13 +1144,17 @@ static orx_status begin_iteration(orx_renderer* r, uint64_t local_iteration_numb
         r->vcm_estimated = false;
     }
     if (det->width != r->W || det->height != r->H || !r->rng_ready) {
+        orx_status s0 = sync_all(r); /* nothing in flight may touch the buffers being replaced */
+        if (s0 != ORX_OK) return s0;
         orx_status st = resize(r, det->width, det->height);
         if (st != ORX_OK) return st;
         if (r->use_ext) HIPCHK(r, hipStreamSynchronize(r->stream)); /* resize work ran on the own stream */
     }
+    if (!pipelined) flush_pipeline(r);
     r->timed_iterations++;
+    /* the output accumulates on the gather stream when pipelined (after the previous output) */
     if (local_iteration_number == 0)
-        HIPCHK(r, hipMemsetAsync(r->d_out.p, 0, (size_t)r->max_rows * r->W * 12, cur_stream(r)));
+        HIPCHK(r, hipMemsetAsync(r->d_out.p, 0, (size_t)r->max_rows * r->W * 12, pipelined ? r->gstream : cur_stream(r)));
     return ORX_OK;
 }
 
@@ -1274,6 +1362,42 @@ static orx_status vcm_iteration(orx_renderer* r, const orx_request* det, float p
     return vcm_camera(r);
 }
 
+/* One PPM iteration whose gather and output are left running on gstream, overlapping the next
+ * iteration's eye, photon and grid passes (orx_render_next_iteration, single device).  Every
+ * kernel and its inputs are those of the serial schedule; only the buffer set alternates. */
+static orx_status ppm_pipelined_iteration(orx_renderer* r, const orx_request* det, float ppm_radius,
+                                          uint64_t local_iteration_number) {
+    const DevCamera cam = camera_setup(det->camera);
+    const Consts c = make_consts(r, ppm_radius, local_iteration_number);
+    hipStream_t st = r->stream;
+    swap_sets(r);
+    const uint32_t k = r->pp;
+    /* the set's previous gather + output (two iterations back) and, through the RNG chain
+     * (slot (x,y) is advanced by eye, photon and direct in turn), the last direct pass */
+    HIPCHK(r, hipStreamWaitEvent(st, r->ev_gdone[k], 0));
+    HIPCHK(r, hipStreamWaitEvent(st, r->ev_direct_done, 0));
+    HIPCHK(r, hipStreamWaitEvent(r->aux, r->ev_gdone[k], 0)); /* direct writes this set's direct buffer */
+    r->overlap_direct = true;
+    ppm_local_passes(r, cam, c); /* eye, photon, direct (aux), grid */
+    r->overlap_direct = false;
+    HIPCHK(r, hipEventRecord(r->ev_grid_done, st));
+    hipStream_t g = r->gstream;
+    HIPCHK(r, hipStreamWaitEvent(g, r->ev_grid_done, 0));
+    ev_begin_on(r, P_GATHER, g);
+    launch_ppm_gather(g, local_gather_in(r), r->pb, c);
+    ev_end_on(r, P_GATHER, g);
+    HIPCHK(r, hipStreamWaitEvent(g, r->ev_direct_done, 0));
+    ev_begin_on(r, P_DIRECT, g);
+    launch_ppm_direct_output(g, r->scene, r->px, c, 2);
+    ev_end_on(r, P_DIRECT, g);
+    HIPCHK(r, hipEventRecord(r->ev_gdone[k], g));
+    r->pend = true;
+    HIPCHK(r, hipGetLastError());
+    r->last_method = (uint64_t)det->method;
+    r->last_consts = c;
+    return ORX_OK;
+}
+
 orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
                                      float ppm_radius, int create_output, const orx_request* det) {
     (void)create_output; /* ignored by the reference engine too */
@@ -1288,8 +1412,18 @@ orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
         return ORX_ERR_UNSUPPORTED;
     if (det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world > 1)
         return set_err(r, ORX_ERR_STATE, "sharded PPM runs through orx_ppm_local_passes/_gather_external/_finish");
-    orx_status s0 = begin_iteration(r, local_iteration_number, det);
+    static const int pipeline_env = [] {
+        const char* e = getenv("ORX_PIPELINE");
+        return e ? atoi(e) : 1;
+    }();
+    const bool same_size = det->width == r->W && det->height == r->H && r->rng_ready;
+    const bool pipelined = pipeline_env && det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world == 1 &&
+                           r->cfg.photon_map == 0 && !r->use_ext && (r->pipe_bufs || !same_size);
+    orx_status s0 = begin_iteration(r, local_iteration_number, det, pipelined);
     if (s0 != ORX_OK) return s0;
+    if (pipelined && r->pipe_bufs)
+        return ppm_pipelined_iteration(r, det, ppm_radius, local_iteration_number);
+    if (pipelined) flush_pipeline(r);
     DevCamera cam = camera_setup(det->camera);
     Consts c = make_consts(r, ppm_radius, local_iteration_number);
     hipStream_t st = cur_stream(r);
@@ -1508,6 +1642,7 @@ orx_status orx_get_output_device(orx_renderer* r, void* dst, size_t bytes) {
     if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "destination too small");
     if (!r->d_out.p) return set_err(r, ORX_ERR_STATE, "no frame rendered yet");
     HIPCHK(r, hipSetDevice(r->device));
+    flush_pipeline(r);
     HIPCHK(r, hipMemcpyAsync(dst, r->d_out.p, need, hipMemcpyDeviceToDevice, cur_stream(r)));
     return ORX_OK;
 }
@@ -1706,6 +1841,14 @@ orx_status orx_get_stats(orx_renderer* r, orx_stats* out) {
         out->cells_visited_total = g.cells_visited_total;
         out->valid_photons_total = g.valid_total;
         out->gather_staged_total = g.union_photons_total;
+        if (r->pipe_bufs && r->d_grid2.p) { /* the other buffer set's share of the totals */
+            GridParams g2;
+            HIPCHK(r, hipMemcpy(&g2, r->d_grid2.p, sizeof g2, hipMemcpyDeviceToHost));
+            out->photons_visited_total += g2.photons_visited_total;
+            out->cells_visited_total += g2.cells_visited_total;
+            out->valid_photons_total += g2.valid_total;
+            out->gather_staged_total += g2.union_photons_total;
+        }
     }
     for (int p = 0; p < P_COUNT; p++) {
         double tot = 0.0;
@@ -1729,14 +1872,15 @@ orx_status orx_reset_timing(orx_renderer* r) {
     }
     for (int p = 0; p < P_COUNT; p++) r->ev_n[p] = 0;
     r->timed_iterations = 0;
-    if (r->d_grid.p) {
+    for (DevBuf* b : {&r->d_grid, &r->d_grid2}) {
+        if (!b->p || (b == &r->d_grid2 && !r->pipe_bufs)) continue;
         GridParams g;
-        HIPCHK(r, hipMemcpy(&g, r->d_grid.p, sizeof g, hipMemcpyDeviceToHost));
+        HIPCHK(r, hipMemcpy(&g, b->p, sizeof g, hipMemcpyDeviceToHost));
         g.photons_visited_total = 0;
         g.cells_visited_total = 0;
         g.valid_total = 0;
         g.union_photons_total = 0;
-        HIPCHK(r, hipMemcpy(r->d_grid.p, &g, sizeof g, hipMemcpyHostToDevice));
+        HIPCHK(r, hipMemcpy(b->p, &g, sizeof g, hipMemcpyHostToDevice));
     }
     return ORX_OK;
 }

@@ -430,3 +430,43 @@ def test_kdtree_parity(scene_name, W, H, P):
     assert rel_l2(g, o) < 1e-5 and g.mean() > 0
     gpu.destroy()
     ora.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipeline", ["1", "0"])
+def test_ppm_back_to_back_iterations(pipeline, monkeypatch):
+    """Iterations issued back to back with no read in between: with pipelining on (default) the
+    gather + output of iteration i run beside the eye/photon/grid passes of i+1 on the other
+    buffer set; the running sum after five iterations (and a resolution change in between)
+    matches the oracle as the serial schedule does."""
+    import subprocess, sys, os, json
+    code = r'''
+import json, sys, numpy as np
+sys.path.insert(0, "tests")
+import oracle_lib
+from oppositerenderer_amd import _abi, scenes
+from oppositerenderer_amd.renderer import OptixRenderer, RenderRequestDetails, next_ppm_radius
+scene = scenes.cornell()
+cfg = _abi.default_config(seed=1645301512, photon_launch_width=96, photon_launch_height=96)
+gpu = OptixRenderer(cfg); gpu.initialize(0); gpu.initScene(scene)
+ora = oracle_lib.OracleRenderer(_abi.default_config(seed=1645301512, photon_launch_width=96, photon_launch_height=96))
+ora.init_scene(scene)
+errs = []
+for W, H, n in ((64, 48, 5), (40, 40, 3)):
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    det = RenderRequestDetails(cam, scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W, H)
+    r = scene.initial_ppm_radius()
+    for it in range(n):
+        gpu.renderNextIteration(it, it, r, True, det)
+        ora.render_next_iteration(it, it, r, det.to_abi())
+        r = next_ppm_radius(r, it)
+    g, o = gpu.getOutputBuffer().astype(np.float64), ora.output().astype(np.float64)
+    errs.append(float(np.sqrt(((g - o) ** 2).sum() / (o ** 2).sum())))
+print(json.dumps(errs))
+'''
+    env = dict(os.environ, ORX_PIPELINE=pipeline)
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr[-2000:]
+    errs = json.loads(out.stdout.strip().splitlines()[-1])
+    assert all(e < 1e-5 for e in errs), errs
