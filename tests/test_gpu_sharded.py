@@ -13,8 +13,8 @@ pytestmark = pytest.mark.gpu
 SEED = 1645301512
 
 
-@pytest.mark.parametrize("world,W,H,P", [(2, 64, 48, 64), (3, 50, 41, 48)])
-def test_sharded_device_path_matches_single(world, W, H, P):
+@pytest.mark.parametrize("world,W,H,P,photon_map", [(2, 64, 48, 64, 0), (3, 50, 41, 48, 0), (2, 64, 48, 64, 2)])
+def test_sharded_device_path_matches_single(world, W, H, P, photon_map):
     dev = torch.device("cuda", 0)
     scene = scenes.cornell()
     cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
@@ -22,7 +22,8 @@ def test_sharded_device_path_matches_single(world, W, H, P):
     req = det.to_abi()
     shards = []
     for rank in range(world):
-        r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P * world))
+        r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P * world,
+                                              photon_map=photon_map))
         r.initialize(0)
         r.set_shard(rank, world)
         r.initScene(scene)
@@ -50,7 +51,8 @@ def test_sharded_device_path_matches_single(world, W, H, P):
     torch.cuda.synchronize()
     blocks = [b.output_local_tensor(mr).cpu().numpy().reshape(mr, W, 3) for b in shards]
     got = multigpu.assemble_rows(blocks, W, H, world)
-    single = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P * world))
+    single = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P * world,
+                                               photon_map=photon_map))
     single.initialize(0)
     single.initScene(scene)
     radius = scene.initial_ppm_radius()

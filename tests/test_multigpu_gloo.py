@@ -38,12 +38,12 @@ def request(scene, W, H, method=_abi.PROGRESSIVE_PHOTON_MAPPING):
     return req
 
 
-def worker(rank, world, port, out_path, W, H, P, iters, method=_abi.PROGRESSIVE_PHOTON_MAPPING):
+def worker(rank, world, port, out_path, W, H, P, iters, method=_abi.PROGRESSIVE_PHOTON_MAPPING, photon_map=0):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     scene = scenes.cornell()
-    cfg = _abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P * world)
+    cfg = _abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P * world, photon_map=photon_map)
     r = oracle_lib.OracleRenderer(cfg)
     oracle_lib.load().orc_set_threads(2)
     r.init_scene(scene)
@@ -64,14 +64,17 @@ def worker(rank, world, port, out_path, W, H, P, iters, method=_abi.PROGRESSIVE_
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,W,H", [(2, 48, 40), (3, 40, 37)])
-def test_sharded_ppm_matches_single(world, W, H):
+@pytest.mark.parametrize("world,W,H,photon_map", [(2, 48, 40, 0), (3, 40, 37, 0), (2, 48, 40, 2)])
+def test_sharded_ppm_matches_single(world, W, H, photon_map):
+    """photon_map 2: each rank builds a kd-tree over its own photons and gathers every rank's
+    hit points against it (the gather is linear in the photon set, like the grid's)."""
     P, iters = 32, 2
     out = os.path.join(tempfile.mkdtemp(), "img.npy")
-    mp.spawn(worker, args=(world, free_port(), out, W, H, P, iters), nprocs=world, join=True)
+    mp.spawn(worker, args=(world, free_port(), out, W, H, P, iters, _abi.PROGRESSIVE_PHOTON_MAPPING, photon_map),
+             nprocs=world, join=True)
     got = np.load(out)
     scene = scenes.cornell()
-    cfg = _abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P * world)
+    cfg = _abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P * world, photon_map=photon_map)
     r = oracle_lib.OracleRenderer(cfg)
     r.init_scene(scene)
     req = request(scene, W, H)
