@@ -253,6 +253,10 @@ typedef struct {
 orx_status orx_get_stats(orx_renderer* r, orx_stats* out);
 /* starts a new timed region for orx_get_stats' *_total and pass_ms fields */
 orx_status orx_reset_timing(orx_renderer* r);
+/* 1 if the last PPM iteration ran pipelined: its gather and output pass (ORX_PASS_PPM_GATHER and the
+ * output half of ORX_PASS_PPM_DIRECT) on a second stream beside the next iteration's eye, photon and
+ * grid passes, so their pass_ms are overlapped wall time; 0 otherwise */
+int orx_ppm_pipelined(const orx_renderer* r);
 
 /* ---- Multi-GPU sharding ----
  * Rank `rank` of `world` owns every RNG-slot row y with y % world == rank:

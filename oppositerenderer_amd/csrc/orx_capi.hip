@@ -360,7 +360,7 @@ struct orx_renderer {
      * grid parameters); ev_gdone[k] marks the end of the last gather+output on set k */
     hipStream_t gstream = nullptr;
     hipEvent_t ev_grid_done = nullptr, ev_gdone[2] = {nullptr, nullptr};
-    bool pipe_bufs = false, pend = false;
+    bool pipe_bufs = false, pend = false, last_pipelined = false;
     uint32_t pp = 0;
     std::string err;
     bool scene_ready = false;
@@ -1421,8 +1421,8 @@ orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
                            r->cfg.photon_map == 0 && !r->use_ext && (r->pipe_bufs || !same_size);
     orx_status s0 = begin_iteration(r, local_iteration_number, det, pipelined);
     if (s0 != ORX_OK) return s0;
-    if (pipelined && r->pipe_bufs)
-        return ppm_pipelined_iteration(r, det, ppm_radius, local_iteration_number);
+    r->last_pipelined = pipelined && r->pipe_bufs;
+    if (r->last_pipelined) return ppm_pipelined_iteration(r, det, ppm_radius, local_iteration_number);
     if (pipelined) flush_pipeline(r);
     DevCamera cam = camera_setup(det->camera);
     Consts c = make_consts(r, ppm_radius, local_iteration_number);
@@ -1862,6 +1862,8 @@ orx_status orx_get_stats(orx_renderer* r, orx_stats* out) {
     out->bvh_stack_entries = r->scene.stack_entries;
     return check_grid_error(r);
 }
+
+int orx_ppm_pipelined(const orx_renderer* r) { return r && r->last_pipelined ? 1 : 0; }
 
 orx_status orx_reset_timing(orx_renderer* r) {
     if (!r) return ORX_ERR_INVALID_ARGUMENT;
