@@ -968,7 +968,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
         HIPCHK(r, r->d_kdseg.ensure(tree * 8 + 16));
         HIPCHK(r, r->d_kdbox.ensure(tree * 24 + 24));
         HIPCHK(r, r->d_kdninfo.ensure(tree * 4 + 16));
-        HIPCHK(r, r->d_kdP.ensure(6 * S * 4 + 64));
+        HIPCHK(r, r->d_kdP.ensure(tree * 12 + 64));
         HIPCHK(r, r->d_kdppart.ensure(6 * nblk * 4 + 64));
         HIPCHK(r, r->d_kdtable.ensure(256 * ntiles * 4 + 64));
         HIPCHK(r, r->d_kdtpart.ensure(tp * 4));
@@ -993,7 +993,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
         kd.seg = r->d_kdseg.as<uint2>();
         kd.box = r->d_kdbox.as<float>();
         kd.ninfo = r->d_kdninfo.as<uint32_t>();
-        kd.P = r->d_kdP.as<uint32_t>();
+        kd.nodeP = r->d_kdP.as<uint32_t>();
         kd.ppart = r->d_kdppart.as<uint32_t>();
         kd.table = r->d_kdtable.as<uint32_t>();
         kd.tpart = r->d_kdtpart.as<uint32_t>();

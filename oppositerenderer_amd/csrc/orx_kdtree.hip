@@ -17,8 +17,10 @@
  *     k_kd_nodes                node = its segment's median along the
  *                               box's longest axis (max_component), children
  *                               segments and boxes; NULL / LEAF nodes
- *     k_kd_pcount, scan, k_kd_pprefix, k_kd_pmove   stable partition of all
- *                               three lists into [left | median | right]
+ *     k_kd_pcount, scan, k_kd_pmove   stable partition of all three lists
+ *                               into [left | median | right]
+ *   k_kd_subtree                once segments hold <= KD_CAP photons: one
+ *                               block per subtree, the same levels in LDS
  *
  * Each segment of every list stays sorted by its axis' (ordered key, slot), so
  * the median of a segment is read directly at (start+end)/2, and an element's
@@ -371,82 +373,249 @@ __device__ __forceinline__ void kd_pos_bits(const KdBufs& kd, uint32_t src, uint
         v[b] = sd == 0 ? 1u : (sd == 2 ? 0x10000u : 0u);
     }
 }
+/* Positions go 1024 per block in four coalesced rounds of 256 (position = block*1024 +
+ * round*256 + thread).  Pass 1 (k_kd_pcount): per block and list the left and median counts ->
+ * ppart, and for every segment that starts in the block the in-block exclusive prefix at its
+ * start -> nodeP.  After the scan of ppart, pass 2 (k_kd_pmove) recomputes the in-block prefix of
+ * each position, so the count of left (median) elements before position p within its segment
+ * [s, e) is  ppart[blk(p)] + inblock(p) - ppart[blk(s)] - nodeP. */
 __global__ __launch_bounds__(256) void k_kd_pcount(KdBufs kd, uint32_t src, uint32_t nblk) {
     __shared__ uint32_t l4[4];
     const uint32_t n = kd.count[0];
-    const uint32_t base = blockIdx.x * 1024 + threadIdx.x * 4;
-    uint32_t s[3] = {0, 0, 0};
+    uint32_t carry[3] = {0, 0, 0};
     for (int k = 0; k < 4; k++) {
+        const uint32_t p = blockIdx.x * 1024 + k * 256 + threadIdx.x;
         uint32_t v[3];
-        kd_pos_bits(kd, src, base + k, n, v);
-        for (int b = 0; b < 3; b++) s[b] += v[b];
-    }
-    for (int b = 0; b < 3; b++) {
-        uint32_t tot;
-        block_excl_scan256(s[b], l4, &tot);
-        if (threadIdx.x == 0) {
-            kd.ppart[(2 * b) * nblk + blockIdx.x] = tot & 0xffffu;
-            kd.ppart[(2 * b + 1) * nblk + blockIdx.x] = tot >> 16;
+        kd_pos_bits(kd, src, p, n, v);
+        uint32_t ex[3];
+        for (int b = 0; b < 3; b++) {
+            uint32_t tot;
+            ex[b] = carry[b] + block_excl_scan256(v[b], l4, &tot);
+            carry[b] += tot;
+        }
+        if (p < n) {
+            const uint32_t node = kd.nodepos[p];
+            if (node != KD_NONE && kd.ninfo[node] != KD_NONE && kd.seg[node].x == p)
+                for (int b = 0; b < 3; b++) kd.nodeP[3 * (size_t)node + b] = ex[b];
         }
     }
-}
-/* global exclusive (left, median) prefix of every position, per list, into P planes */
-__global__ __launch_bounds__(256) void k_kd_pprefix(KdBufs kd, uint32_t src, uint32_t nblk) {
-    __shared__ uint32_t l4[4];
-    const uint32_t n = kd.count[0];
-    const uint32_t base = blockIdx.x * 1024 + threadIdx.x * 4;
-    uint32_t v[4][3];
-    uint32_t s[3] = {0, 0, 0};
-    for (int k = 0; k < 4; k++) {
-        kd_pos_bits(kd, src, base + k, n, v[k]);
-        for (int b = 0; b < 3; b++) s[b] += v[k][b];
-    }
-    const size_t S = kd.S;
-    for (int b = 0; b < 3; b++) {
-        const uint32_t ex = block_excl_scan256(s[b], l4, nullptr);
-        uint32_t rl = kd.ppart[(2 * b) * nblk + blockIdx.x] + (ex & 0xffffu);
-        uint32_t rm = kd.ppart[(2 * b + 1) * nblk + blockIdx.x] + (ex >> 16);
-        for (int k = 0; k < 4; k++) {
-            const uint32_t p = base + k;
-            if (p < n) {
-                kd.P[(2 * b) * S + p] = rl;
-                kd.P[(2 * b + 1) * S + p] = rm;
-            }
-            rl += v[k][b] & 0xffffu;
-            rm += v[k][b] >> 16;
+    if (threadIdx.x == 0)
+        for (int b = 0; b < 3; b++) {
+            kd.ppart[(2 * b) * nblk + blockIdx.x] = carry[b] & 0xffffu;
+            kd.ppart[(2 * b + 1) * nblk + blockIdx.x] = carry[b] >> 16;
         }
-    }
 }
 /* stable partition of the three lists of every split segment into [left | median | right]
  * (the median leaves the lists: it is the node), and the positions' next-level nodes */
-__global__ __launch_bounds__(256) void k_kd_pmove(KdBufs kd, uint32_t src) {
-    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
-    if (p >= kd.count[0]) return;
-    const uint32_t node = kd.nodepos[p];
-    if (node == KD_NONE) return;
-    const uint32_t info = kd.ninfo[node];
-    if (info == KD_NONE) { /* a leaf: its element is the node */
-        kd.nodepos[p] = KD_NONE;
-        return;
+__global__ __launch_bounds__(256) void k_kd_pmove(KdBufs kd, uint32_t src, uint32_t nblk) {
+    __shared__ uint32_t l4[4];
+    const uint32_t n = kd.count[0];
+    uint32_t carry[3] = {0, 0, 0};
+    for (int k = 0; k < 4; k++) {
+        const uint32_t p = blockIdx.x * 1024 + k * 256 + threadIdx.x;
+        uint32_t v[3];
+        kd_pos_bits(kd, src, p, n, v);
+        uint32_t ex[3];
+        for (int b = 0; b < 3; b++) {
+            uint32_t tot;
+            ex[b] = carry[b] + block_excl_scan256(v[b], l4, &tot);
+            carry[b] += tot;
+        }
+        if (p >= n) continue;
+        const uint32_t node = kd.nodepos[p];
+        if (node == KD_NONE) continue;
+        const uint32_t info = kd.ninfo[node];
+        if (info == KD_NONE) { /* a leaf: its element is the node */
+            kd.nodepos[p] = KD_NONE;
+            continue;
+        }
+        const uint32_t m = info >> 2;
+        const uint32_t s = kd.seg[node].x;
+        const uint32_t sblk = s / 1024;
+        for (int b = 0; b < 3; b++) {
+            if (v[b] & 0x10000u) continue; /* the median */
+            const uint32_t np = kd.nodeP[3 * (size_t)node + b];
+            const uint32_t L = kd.ppart[(2 * b) * nblk + blockIdx.x] + (ex[b] & 0xffffu) -
+                               kd.ppart[(2 * b) * nblk + sblk] - (np & 0xffffu);
+            const uint32_t M = kd.ppart[(2 * b + 1) * nblk + blockIdx.x] + (ex[b] >> 16) -
+                               kd.ppart[(2 * b + 1) * nblk + sblk] - (np >> 16);
+            const uint32_t dst = (v[b] & 1u) ? s + L : m + 1 + (p - s) - L - M;
+            kd.lst[src ^ 1][b][dst] = kd.lst[src][b][p];
+        }
+        kd.nodepos[p] = p < m ? 2 * node + 1 : (p > m ? 2 * node + 2 : KD_NONE);
     }
-    const uint32_t m = info >> 2;
-    const uint32_t s = kd.seg[node].x;
-    const uint2 mk = kd.nkey[node];
-    const size_t S = kd.S;
-    for (int b = 0; b < 3; b++) {
-        const float4 e = kd.lst[src][b][p];
-        const uint32_t sd = kd_side(e, info & 3u, mk);
-        if (sd == 2) continue;
-        const uint32_t L = kd.P[(2 * b) * S + p] - kd.P[(2 * b) * S + s];
-        const uint32_t M = kd.P[(2 * b + 1) * S + p] - kd.P[(2 * b + 1) * S + s];
-        const uint32_t dst = sd == 0 ? s + L : m + 1 + (p - s) - L - M;
-        kd.lst[src ^ 1][b][dst] = e;
-    }
-    kd.nodepos[p] = p < m ? 2 * node + 1 : (p > m ? 2 * node + 2 : KD_NONE);
 }
 __global__ __launch_bounds__(256) void k_kd_pos_init(KdBufs kd) {
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
     if (p < kd.S) kd.nodepos[p] = p < kd.count[0] ? 0u : KD_NONE;
+}
+
+/* ------------------------------------------------------------------ */
+/* subtrees of at most KD_CAP photons, one block each, entirely in LDS  */
+/* ------------------------------------------------------------------ */
+/* Once every segment of a level holds at most KD_CAP photons, one 256-thread block takes a
+ * segment and builds its whole subtree: the same per-level median / stable three-list partition
+ * as the global levels, on 16-bit indices into an LDS copy of the segment's list records. */
+constexpr uint32_t KD_CAP = 512;
+constexpr uint32_t KD_HASH = 1024;
+constexpr uint16_t KD_NONE16 = 0xffffu;
+
+__device__ __forceinline__ void kd_put_node(const PhotonBufs& pb, const KdBufs& kd, size_t node, uint32_t flag,
+                                            uint32_t slot) {
+    const float4* sl = pb.slots + 4 * (size_t)slot;
+    const float4 a = sl[0], b = sl[1], c = sl[2];
+    float4* rec = kd.tree + 3 * node;
+    rec[0] = make_float4(a.x, a.y, a.z, __uint_as_float(flag));
+    rec[1] = make_float4(a.w, b.w, c.x, b.x);
+    rec[2] = make_float4(b.y, b.z, 0.f, 0.f);
+}
+
+__global__ __launch_bounds__(256) void k_kd_subtree(PhotonBufs pb, KdBufs kd, uint32_t level0, uint32_t src) {
+    __shared__ float4 E[KD_CAP];
+    __shared__ uint16_t L[2][3][KD_CAP];
+    __shared__ uint32_t Pp[3][KD_CAP];          /* exclusive (left | median << 16) prefix per list */
+    __shared__ uint16_t pnode[KD_CAP];          /* node (offset within its level) of each position */
+    __shared__ uint32_t hkey[KD_HASH];
+    __shared__ uint16_t hval[KD_HASH];
+    __shared__ uint16_t cs[2][KD_CAP], ce[2][KD_CAP]; /* segments of the current / next level */
+    __shared__ float cb[2][KD_CAP / 2][6];            /* boxes of split candidates (size >= 2) */
+    __shared__ uint32_t sinfo[KD_CAP / 2][3];         /* split nodes: m | axis << 16, median key, median slot */
+    __shared__ uint32_t l4[4];
+    __shared__ uint32_t any_split;
+    const uint32_t tid = threadIdx.x;
+    const size_t root = ((size_t)1 << level0) - 1 + blockIdx.x;
+    const uint2 se = kd.seg[root];
+    if (se.x == KD_NONE) return; /* uniform */
+    const uint32_t n0 = se.y - se.x;
+    for (uint32_t h = tid; h < KD_HASH; h += 256) hkey[h] = KD_NONE;
+    __syncthreads();
+    for (uint32_t i = tid; i < n0; i += 256) {
+        const float4 e = kd.lst[src][0][se.x + i];
+        E[i] = e;
+        L[0][0][i] = (uint16_t)i;
+        uint32_t h = (__float_as_uint(e.w) * 2654435761u) >> 22;
+        while (atomicCAS(&hkey[h], KD_NONE, __float_as_uint(e.w)) != KD_NONE) h = (h + 1) & (KD_HASH - 1);
+        hval[h] = (uint16_t)i;
+        pnode[i] = 0;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n0; i += 256)
+        for (int b = 1; b < 3; b++) {
+            const uint32_t sl = __float_as_uint(kd.lst[src][b][se.x + i].w);
+            uint32_t h = (sl * 2654435761u) >> 22;
+            while (hkey[h] != sl) h = (h + 1) & (KD_HASH - 1);
+            L[0][b][i] = hval[h];
+        }
+    if (tid == 0) {
+        cs[0][0] = 0;
+        ce[0][0] = (uint16_t)n0;
+        for (int q = 0; q < 6; q++) cb[0][0][q] = kd.box[6 * root + q];
+    }
+    __syncthreads();
+    uint32_t cur = 0, lv = 0;
+    for (uint32_t d = 0;; d++) {
+        /* nodes of depth d below the subtree root: buildKDTree's body */
+        const uint32_t count = 1u << d;
+        const size_t first = (root + 1) * ((size_t)1 << d) - 1;
+        if (tid == 0) any_split = 0;
+        __syncthreads();
+        for (uint32_t k = tid; k < count && k < KD_CAP; k += 256) {
+            const uint32_t s = cs[lv][k], e = ce[lv][k];
+            const size_t node = first + k;
+            const size_t c0 = 2 * node + 1;
+            const bool has_children = c0 + 1 < kd.tree_size && 2 * k + 1 < KD_CAP;
+            bool split = false;
+            if (s != KD_NONE16) {
+                const uint32_t size = e - s;
+                if (size == 0) {
+                    float4* rec = kd.tree + 3 * node;
+                    const float4 b = rec[1];
+                    rec[0].w = __uint_as_float(KD_PPM_NULL);
+                    rec[1] = make_float4(0.f, 0.f, 0.f, b.w);
+                } else if (size == 1) {
+                    kd_put_node(pb, kd, node, KD_PPM_LEAF, __float_as_uint(E[L[cur][0][s]].w));
+                } else {
+                    split = true; /* only depths <= 8 hold such nodes: k < KD_CAP / 2 */
+                }
+            }
+            if (split) {
+                const float* bx = cb[lv][k];
+                const float dx = bx[3] - bx[0], dy = bx[4] - bx[1], dz = bx[5] - bx[2];
+                const uint32_t axis = (dx > dy && dx > dz) ? 0u : (dy > dz ? 1u : 2u); /* max_component */
+                const uint32_t m = (s + e) / 2;
+                const float4 med = E[L[cur][axis][m]];
+                const uint32_t slot = __float_as_uint(med.w);
+                kd_put_node(pb, kd, node, KD_PPM_X << axis, slot);
+                sinfo[k][0] = m | (axis << 16);
+                sinfo[k][1] = kd_f2ord(kd_comp(med, axis));
+                sinfo[k][2] = slot;
+                any_split = 1;
+                if (has_children) {
+                    const float split_v = kd_comp(med, axis);
+                    const uint32_t nl = lv ^ 1u;
+                    cs[nl][2 * k] = (uint16_t)s;
+                    ce[nl][2 * k] = (uint16_t)m;
+                    cs[nl][2 * k + 1] = (uint16_t)(m + 1);
+                    ce[nl][2 * k + 1] = (uint16_t)e;
+                    /* children with >= 2 photons split again: hand down the cut boxes */
+                    if (m - s >= 2 && 2 * k < KD_CAP / 2)
+                        for (int q = 0; q < 6; q++) cb[nl][2 * k][q] = q == 3 + (int)axis ? split_v : bx[q];
+                    if (e - m - 1 >= 2 && 2 * k + 1 < KD_CAP / 2)
+                        for (int q = 0; q < 6; q++) cb[nl][2 * k + 1][q] = q == (int)axis ? split_v : bx[q];
+                }
+            } else if (2 * k + 1 < KD_CAP) {
+                cs[lv ^ 1u][2 * k] = KD_NONE16;
+                cs[lv ^ 1u][2 * k + 1] = KD_NONE16;
+            }
+        }
+        __syncthreads();
+        if (!any_split) break; /* uniform */
+        /* stable partition of the three lists around each split node's median */
+        const uint32_t p0 = 2 * tid, p1 = 2 * tid + 1;
+        uint32_t v[2][3];
+        for (int q = 0; q < 2; q++) {
+            const uint32_t p = q ? p1 : p0;
+            v[q][0] = v[q][1] = v[q][2] = 0;
+            if (p < n0 && pnode[p] != KD_NONE16 && cs[lv][pnode[p]] != KD_NONE16 &&
+                ce[lv][pnode[p]] - cs[lv][pnode[p]] >= 2) {
+                const uint32_t k = pnode[p];
+                const uint32_t axis = sinfo[k][0] >> 16;
+                const uint2 mk = make_uint2(sinfo[k][1], sinfo[k][2]);
+                for (int b = 0; b < 3; b++) {
+                    const uint32_t sd = kd_side(E[L[cur][b][p]], axis, mk);
+                    v[q][b] = sd == 0 ? 1u : (sd == 2 ? 0x10000u : 0u);
+                }
+            }
+        }
+        for (int b = 0; b < 3; b++) {
+            const uint32_t ex = block_excl_scan256(v[0][b] + v[1][b], l4, nullptr);
+            if (p0 < n0) Pp[b][p0] = ex;
+            if (p1 < n0) Pp[b][p1] = ex + v[0][b];
+        }
+        __syncthreads();
+        for (int q = 0; q < 2; q++) {
+            const uint32_t p = q ? p1 : p0;
+            if (p >= n0 || pnode[p] == KD_NONE16) continue;
+            const uint32_t k = pnode[p];
+            const uint32_t s = cs[lv][k], e = ce[lv][k];
+            if (s == KD_NONE16 || e - s < 2) { /* a leaf: its element is the node */
+                pnode[p] = KD_NONE16;
+                continue;
+            }
+            const uint32_t m = sinfo[k][0] & 0xffffu;
+            for (int b = 0; b < 3; b++) {
+                if (v[q][b] & 0x10000u) continue; /* the median */
+                const uint32_t Lc = (Pp[b][p] & 0xffffu) - (Pp[b][s] & 0xffffu);
+                const uint32_t Mc = (Pp[b][p] >> 16) - (Pp[b][s] >> 16);
+                const uint32_t dst = (v[q][b] & 1u) ? s + Lc : m + 1 + (p - s) - Lc - Mc;
+                L[cur ^ 1u][b][dst] = L[cur][b][p];
+            }
+            pnode[p] = p < m ? (uint16_t)(2 * k) : (p > m ? (uint16_t)(2 * k + 1) : KD_NONE16);
+        }
+        __syncthreads();
+        cur ^= 1u;
+        lv ^= 1u;
+    }
 }
 
 void launch_kd_build(hipStream_t st, const PhotonBufs& pb, const KdBufs& kd) {
@@ -479,15 +648,22 @@ void launch_kd_build(hipStream_t st, const PhotonBufs& pb, const KdBufs& kd) {
     hipLaunchKernelGGL(k_kd_root, dim3(1), dim3(64), 0, st, pb, kd);
     hipLaunchKernelGGL(k_kd_pos_init, dim3(nb256), dim3(256), 0, st, kd);
     const uint32_t nblk = nb1024;
+    /* global levels until every segment holds at most KD_CAP photons (a level-l segment holds at
+     * most floor(n / 2^l) <= S >> l), then one LDS block per subtree */
+    uint32_t lg = 0;
+    while ((S >> lg) > KD_CAP) lg++;
     uint32_t src = 0;
     for (uint32_t level = 0; level < kd.levels; level++) {
         const uint32_t nodes = 1u << level;
+        if (level == lg) {
+            hipLaunchKernelGGL(k_kd_subtree, dim3(nodes), dim3(256), 0, st, pb, kd, level, src);
+            break;
+        }
         hipLaunchKernelGGL(k_kd_nodes, dim3((nodes + 255) / 256), dim3(256), 0, st, pb, kd, level, src);
         if (level + 1 == kd.levels) break; /* the last level holds leaves and NULL nodes only */
         hipLaunchKernelGGL(k_kd_pcount, dim3(nblk), dim3(256), 0, st, kd, src, nblk);
         kd_scan(st, kd.ppart, 6 * nblk, kd.tpart, nullptr);
-        hipLaunchKernelGGL(k_kd_pprefix, dim3(nblk), dim3(256), 0, st, kd, src, nblk);
-        hipLaunchKernelGGL(k_kd_pmove, dim3(nb256), dim3(256), 0, st, kd, src);
+        hipLaunchKernelGGL(k_kd_pmove, dim3(nblk), dim3(256), 0, st, kd, src, nblk);
         src ^= 1;
     }
 }

@@ -115,7 +115,7 @@ struct KdBufs {
     uint2* seg;          /* [tree_size] segment [start, end) of each node (0xffffffff: not in the tree) */
     float* box;          /* [tree_size][6] bbmin, bbmax handed down by buildKDTree */
     uint32_t* ninfo;     /* [tree_size] split nodes: median << 2 | axis; else 0xffffffff */
-    uint32_t* P;         /* [6][S] exclusive (left, median) prefix per list */
+    uint32_t* nodeP;     /* [tree_size][3] per list: in-block exclusive (left | median << 16) prefix at the segment start */
     uint32_t* ppart;     /* [6][S/1024] block counts, then their scan */
     uint32_t* table;     /* [256][ntiles] radix digit counts, then their scan */
     uint32_t* tpart;     /* scan partials */
