@@ -981,6 +981,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
         kd.levels = levels;
         kd.ntiles = (uint32_t)ntiles;
         kd.tree = r->d_kdtree.as<float4>();
+        kd.tree_bc = kd.tree + tree + 1;
         for (int q = 0; q < 2; q++)
             for (int a = 0; a < 3; a++) {
                 kd.ids[q][a] = r->d_kdids.as<uint32_t>() + (size_t)(3 * q + a) * S;
@@ -1783,10 +1784,11 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
     case ORX_BUF_KD_TREE: { /* [tree_size][power3 position3 direction3 axis] */
         const size_t n = r->kd.tree_size;
         std::vector<float4> T(3 * n);
-        if (n) HIPCHK(r, d2h(T.data(), r->kd.tree, n * 48));
+        if (n) HIPCHK(r, d2h(T.data(), r->kd.tree, n * 16));
+        if (n) HIPCHK(r, d2h(T.data() + n, r->kd.tree_bc, n * 32));
         float* o = (float*)dst;
         for (size_t i = 0; i < n; i++) {
-            const float4 a = T[3 * i], b = T[3 * i + 1], c = T[3 * i + 2];
+            const float4 a = T[i], b = T[n + 2 * i], c = T[n + 2 * i + 1];
             const float v[10] = {b.x, b.y, b.z, a.x, a.y, a.z, b.w, c.x, c.y, a.w};
             std::memcpy(o + 10 * i, v, sizeof v);
         }

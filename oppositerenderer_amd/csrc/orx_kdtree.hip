@@ -55,6 +55,23 @@ __device__ __forceinline__ float kd_ord2f(uint32_t u) {
 }
 __device__ __forceinline__ float kd_comp(const float4& p, uint32_t a) { return a == 0 ? p.x : a == 1 ? p.y : p.z; }
 
+/* node record: A plane pos.xyz | axis bits (all the traversal reads), BC plane power.xyz | dir.x,
+ * dir.yz (read for photons within the radius) */
+__device__ __forceinline__ void kd_put_node(const PhotonBufs& pb, const KdBufs& kd, size_t node, uint32_t flag,
+                                            uint32_t slot) {
+    const float4* sl = pb.slots + 4 * (size_t)slot;
+    const float4 a = sl[0], b = sl[1], c = sl[2];
+    kd.tree[node] = make_float4(a.x, a.y, a.z, __uint_as_float(flag));
+    kd.tree_bc[2 * node] = make_float4(a.w, b.w, c.x, b.x);
+    kd.tree_bc[2 * node + 1] = make_float4(b.y, b.z, 0.f, 0.f);
+}
+/* NULL node: buildKDTree writes axis and power only (OptixRenderer_CPUKdTree.cpp:31-34) */
+__device__ __forceinline__ void kd_put_null(const KdBufs& kd, size_t node) {
+    kd.tree[node].w = __uint_as_float(KD_PPM_NULL);
+    const float4 b = kd.tree_bc[2 * node];
+    kd.tree_bc[2 * node] = make_float4(0.f, 0.f, 0.f, b.w);
+}
+
 /* exclusive scan of one uint32 per thread over a 256-thread block (4 waves) */
 __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* lds4, uint32_t* total) {
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -303,12 +320,9 @@ __global__ __launch_bounds__(256) void k_kd_nodes(PhotonBufs pb, KdBufs kd, uint
     const bool has_children = c0 + 1 < kd.tree_size;
     uint32_t info = KD_NONE;
     if (se.x != KD_NONE) {
-        float4* rec = kd.tree + 3 * (size_t)node;
         const uint32_t size = se.y - se.x;
         if (size == 0) { /* NULL node: axis and power */
-            const float4 b = rec[1];
-            rec[0].w = __uint_as_float(KD_PPM_NULL);
-            rec[1] = make_float4(0.f, 0.f, 0.f, b.w);
+            kd_put_null(kd, node);
         } else {
             uint32_t axis = 0, med = se.x;
             if (size > 1) {
@@ -319,12 +333,8 @@ __global__ __launch_bounds__(256) void k_kd_nodes(PhotonBufs pb, KdBufs kd, uint
             }
             const float4 e = kd.lst[src][axis][med];
             const uint32_t s = __float_as_uint(e.w);
-            const float4* sl = pb.slots + 4 * (size_t)s;
-            const float4 a = sl[0], b = sl[1], c = sl[2];
-            const uint32_t flag = size == 1 ? KD_PPM_LEAF : (KD_PPM_X << axis);
-            rec[0] = make_float4(a.x, a.y, a.z, __uint_as_float(flag));
-            rec[1] = make_float4(a.w, b.w, c.x, b.x);
-            rec[2] = make_float4(b.y, b.z, 0.f, 0.f);
+            kd_put_node(pb, kd, node, size == 1 ? KD_PPM_LEAF : (KD_PPM_X << axis), s);
+            const float4 a = pb.pos4[s];
             if (size > 1) {
                 info = (med << 2) | axis;
                 kd.nkey[node] = make_uint2(kd_f2ord(kd_comp(e, axis)), s);
@@ -460,15 +470,6 @@ constexpr uint32_t KD_CAP = 512;
 constexpr uint32_t KD_HASH = 1024;
 constexpr uint16_t KD_NONE16 = 0xffffu;
 
-__device__ __forceinline__ void kd_put_node(const PhotonBufs& pb, const KdBufs& kd, size_t node, uint32_t flag,
-                                            uint32_t slot) {
-    const float4* sl = pb.slots + 4 * (size_t)slot;
-    const float4 a = sl[0], b = sl[1], c = sl[2];
-    float4* rec = kd.tree + 3 * node;
-    rec[0] = make_float4(a.x, a.y, a.z, __uint_as_float(flag));
-    rec[1] = make_float4(a.w, b.w, c.x, b.x);
-    rec[2] = make_float4(b.y, b.z, 0.f, 0.f);
-}
 
 __global__ __launch_bounds__(256) void k_kd_subtree(PhotonBufs pb, KdBufs kd, uint32_t level0, uint32_t src) {
     __shared__ float4 E[KD_CAP];
@@ -528,10 +529,7 @@ __global__ __launch_bounds__(256) void k_kd_subtree(PhotonBufs pb, KdBufs kd, ui
             if (s != KD_NONE16) {
                 const uint32_t size = e - s;
                 if (size == 0) {
-                    float4* rec = kd.tree + 3 * node;
-                    const float4 b = rec[1];
-                    rec[0].w = __uint_as_float(KD_PPM_NULL);
-                    rec[1] = make_float4(0.f, 0.f, 0.f, b.w);
+                    kd_put_null(kd, node);
                 } else if (size == 1) {
                     kd_put_node(pb, kd, node, KD_PPM_LEAF, __float_as_uint(E[L[cur][0][s]].w));
                 } else {
@@ -699,21 +697,22 @@ __global__ __launch_bounds__(64) void k_ppm_gather_kd(GatherIn gi, PhotonBufs pb
         const float inv2r2 = 1.0f / (2 * radius2);
         const float invDen = 1.0f / (1 - expNegativeBeta);
         const float4* tree = kd.tree;
+        const float4* tree_bc = kd.tree_bc;
         uint32_t sc = 0, node = 0;
         kd_stack[lane] = 0;
         sc = 1;
         const uint32_t max_sc = kd.levels + 2;
         do {
             if (node >= kd.tree_size || sc >= max_sc) break; /* unreachable on a well-formed tree */
-            const float4 a = tree[3 * (size_t)node];
+            const float4 a = tree[node];
             dP++;
             const uint32_t axis = __float_as_uint(a.w);
             if (!(axis & KD_PPM_NULL)) {
                 const f3 diff = pos - mk(a.x, a.y, a.z);
                 const float distance2 = dot(diff, diff);
                 if (distance2 <= radius2) {
-                    const float4 b = tree[3 * (size_t)node + 1];
-                    const float4 cc = tree[3 * (size_t)node + 2];
+                    const float4 b = tree_bc[2 * (size_t)node];
+                    const float4 cc = tree_bc[2 * (size_t)node + 1];
                     if (dot(-mk(b.w, cc.x, cc.y), nrm) >= 0) {
                         const float e = orx_expf_unit((-beta * distance2) * inv2r2);
                         const float wgt = alpha * (1 - (1 - e) * invDen);

@@ -106,7 +106,8 @@ struct KdBufs {
     uint32_t tree_size;  /* m_photonKdTreeSize = pow2roundup(S + 1) - 1 (OptixRenderer.cpp:207) */
     uint32_t levels;     /* log2(tree_size + 1): depth bound of any tree of <= S photons */
     uint32_t ntiles;     /* radix-sort tiles of RS_TILE elements */
-    float4* tree;        /* [tree_size][3]: pos.xyz|axis bits, power.xyz|dir.x, dir.y dir.z */
+    float4* tree;        /* [tree_size]: pos.xyz | axis bits */
+    float4* tree_bc;     /* [tree_size][2]: power.xyz | dir.x, dir.y dir.z */
     uint32_t* ids[2][3]; /* [S] radix-sort slot lists (ids[1][0]: valid slots in slot order) */
     float4* lst[2][3];   /* [S] per axis, position order: photon position | slot bits; ping-pong per level */
     uint2* nkey;         /* [tree_size] split nodes: the median's (ordered key on the split axis, slot) */
