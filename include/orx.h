@@ -301,6 +301,14 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hitpoints_device
                                    void* indirect_device, size_t indirect_bytes);
 /* indirect_device: max_local_rows * W * 3 floats for the own rows */
 orx_status orx_ppm_finish(orx_renderer* r, const void* indirect_device, size_t indirect_bytes);
+/* Pipelined sharded PPM (uniform grid; call before the first iteration, like orx_set_shard):
+ * orx_ppm_gather_external and orx_ppm_finish of iteration i run on `side_stream` (a hipStream_t
+ * of the caller's, who also issues the indirect reduce-scatter there), overlapping iteration
+ * i+1's eye, photon and grid passes on the renderer's stream; the direct pass runs on an internal
+ * stream right after the photon pass.  Two buffer sets alternate, events order the RNG chain and
+ * buffer reuse; the caller makes `side_stream` wait for the hitpoint all-gather before the
+ * gather.  enable = 0 restores the serial phases. */
+orx_status orx_set_ppm_pipeline(orx_renderer* r, void* side_stream, int enable);
 
 /* One VCM iteration of a sharded renderer (OptixRenderer.cpp:675-795 split at
  * the light-tracing splats).  Light subpath i pairs with camera pixel i

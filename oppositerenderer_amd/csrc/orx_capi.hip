@@ -361,6 +361,9 @@ struct orx_renderer {
     hipStream_t gstream = nullptr;
     hipEvent_t ev_grid_done = nullptr, ev_gdone[2] = {nullptr, nullptr};
     bool pipe_bufs = false, pend = false, last_pipelined = false;
+    /* sharded PPM pipelining (orx_set_ppm_pipeline): gather + finish on the caller's side stream */
+    bool shard_pipe = false;
+    hipStream_t side = nullptr;
     uint32_t pp = 0;
     std::string err;
     bool scene_ready = false;
@@ -883,10 +886,10 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_bspartials.ensure((bs_nscan + 2) * 4));
     HIPCHK(r, r->d_bspairs.ensure(S * 8 + 16));
     HIPCHK(r, r->d_subofs.ensure(G2 * 4 * SUBX * nsub + 16));
-    /* second buffer set for PPM pipelining (single device, uniform grid) */
+    /* second buffer set for PPM pipelining (single device or orx_set_ppm_pipeline, uniform grid) */
     r->pipe_bufs = false;
     r->pend = false;
-    if (r->world == 1 && r->cfg.photon_map == 0) {
+    if ((r->world == 1 || r->shard_pipe) && r->cfg.photon_map == 0) {
         HIPCHK(r, r->d_hp2.ensure(nhp * 40));
         HIPCHK(r, r->d_dir2.ensure(nhp * 12));
         HIPCHK(r, r->d_sorted2.ensure(9 * splane * 4));
@@ -1081,6 +1084,8 @@ static inline void ev_end_on(orx_renderer* r, int p, hipStream_t st) {
 }
 
 static inline hipStream_t cur_stream(orx_renderer* r) { return r->use_ext ? r->ext_stream : r->stream; }
+/* the stream the deferred gather + output run on */
+static inline hipStream_t gather_stream(orx_renderer* r) { return r->shard_pipe ? r->side : r->gstream; }
 
 /* order everything later on the renderer's stream after a deferred gather + output */
 static void flush_pipeline(orx_renderer* r) {
@@ -1094,6 +1099,7 @@ static orx_status sync_all(orx_renderer* r) {
     HIPCHK(r, hipStreamSynchronize(r->stream));
     if (r->use_ext) HIPCHK(r, hipStreamSynchronize(r->ext_stream));
     if (r->gstream) HIPCHK(r, hipStreamSynchronize(r->gstream));
+    if (r->shard_pipe) HIPCHK(r, hipStreamSynchronize(r->side));
     return ORX_OK;
 }
 
@@ -1155,7 +1161,7 @@ static orx_status begin_iteration(orx_renderer* r, uint64_t local_iteration_numb
     r->timed_iterations++;
     /* the output accumulates on the gather stream when pipelined (after the previous output) */
     if (local_iteration_number == 0)
-        HIPCHK(r, hipMemsetAsync(r->d_out.p, 0, (size_t)r->max_rows * r->W * 12, pipelined ? r->gstream : cur_stream(r)));
+        HIPCHK(r, hipMemsetAsync(r->d_out.p, 0, (size_t)r->max_rows * r->W * 12, pipelined ? gather_stream(r) : cur_stream(r)));
     return ORX_OK;
 }
 
@@ -1469,6 +1475,7 @@ orx_status orx_ppm_local_passes(orx_renderer* r, uint64_t iteration_number, uint
     if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
     if (det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
         return set_err(r, ORX_ERR_INVALID_ARGUMENT, "orx_ppm_local_passes needs a PPM request");
+    r->last_pipelined = false;
     orx_status s0 = begin_iteration(r, local_iteration_number, det);
     if (s0 != ORX_OK) return s0;
     DevCamera cam = camera_setup(det->camera);
@@ -1486,10 +1493,21 @@ orx_status orx_ppm_local_eye(orx_renderer* r, uint64_t iteration_number, uint64_
     if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
     if (det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
         return set_err(r, ORX_ERR_INVALID_ARGUMENT, "orx_ppm_local_eye needs a PPM request");
-    orx_status s0 = begin_iteration(r, local_iteration_number, det);
+    orx_status s0 = begin_iteration(r, local_iteration_number, det, r->shard_pipe);
     if (s0 != ORX_OK) return s0;
     DevCamera cam = camera_setup(det->camera);
     Consts c = make_consts(r, ppm_radius, local_iteration_number);
+    r->last_pipelined = r->shard_pipe && r->pipe_bufs;
+    if (r->last_pipelined) {
+        /* the other buffer set; its last gather + finish (two iterations back) and, through the
+         * RNG chain, the last direct pass precede this eye pass */
+        swap_sets(r);
+        HIPCHK(r, hipStreamWaitEvent(cur_stream(r), r->ev_gdone[r->pp], 0));
+        HIPCHK(r, hipStreamWaitEvent(cur_stream(r), r->ev_direct_done, 0));
+        HIPCHK(r, hipStreamWaitEvent(r->aux, r->ev_gdone[r->pp], 0));
+    } else if (r->shard_pipe) {
+        flush_pipeline(r);
+    }
     ppm_eye(r, cam, c);
     HIPCHK(r, hipGetLastError());
     r->last_method = (uint64_t)det->method;
@@ -1501,7 +1519,10 @@ orx_status orx_ppm_local_photons(orx_renderer* r) {
     if (!r) return ORX_ERR_INVALID_ARGUMENT;
     if (!r->rng_ready) return set_err(r, ORX_ERR_STATE, "orx_ppm_local_eye first");
     HIPCHK(r, hipSetDevice(r->device));
+    r->overlap_direct = r->last_pipelined; /* direct pass on the aux stream right after the photons */
     ppm_photons_grid(r, r->last_consts);
+    r->overlap_direct = false;
+    if (r->last_pipelined) HIPCHK(r, hipEventRecord(r->ev_grid_done, cur_stream(r)));
     HIPCHK(r, hipGetLastError());
     return ORX_OK;
 }
@@ -1530,10 +1551,15 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hp, uint32_t seg
     gi.W = r->W;
     gi.indirect = (float*)indirect;
     gi.dbg = nullptr;
-    ev_begin(r, P_GATHER);
-    if (r->cfg.photon_map == 2) launch_ppm_gather_kd(cur_stream(r), gi, r->pb, r->kd, r->last_consts);
-    else launch_ppm_gather(cur_stream(r), gi, r->pb, r->last_consts);
-    ev_end(r, P_GATHER);
+    hipStream_t st = cur_stream(r);
+    if (r->last_pipelined) { /* on the side stream, after the grid build */
+        st = gather_stream(r);
+        HIPCHK(r, hipStreamWaitEvent(st, r->ev_grid_done, 0));
+    }
+    ev_begin_on(r, P_GATHER, st);
+    if (r->cfg.photon_map == 2) launch_ppm_gather_kd(st, gi, r->pb, r->kd, r->last_consts);
+    else launch_ppm_gather(st, gi, r->pb, r->last_consts);
+    ev_end_on(r, P_GATHER, st);
     HIPCHK(r, hipGetLastError());
     return ORX_OK;
 }
@@ -1543,12 +1569,37 @@ orx_status orx_ppm_finish(orx_renderer* r, const void* indirect, size_t bytes) {
     size_t need = (size_t)r->max_rows * r->W * 12;
     if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "indirect buffer too small");
     HIPCHK(r, hipSetDevice(r->device));
+    if (r->last_pipelined) { /* output only (direct ran beside the grid build), on the side stream */
+        hipStream_t g = gather_stream(r);
+        HIPCHK(r, hipMemcpyAsync(r->d_ind.p, indirect, need, hipMemcpyDeviceToDevice, g));
+        HIPCHK(r, hipStreamWaitEvent(g, r->ev_direct_done, 0));
+        ev_begin_on(r, P_DIRECT, g);
+        launch_ppm_direct_output(g, r->scene, r->px, r->last_consts, 2);
+        ev_end_on(r, P_DIRECT, g);
+        HIPCHK(r, hipEventRecord(r->ev_gdone[r->pp], g));
+        r->pend = true;
+        HIPCHK(r, hipGetLastError());
+        return ORX_OK;
+    }
     hipStream_t st = cur_stream(r);
     HIPCHK(r, hipMemcpyAsync(r->d_ind.p, indirect, need, hipMemcpyDeviceToDevice, st));
     ev_begin(r, P_DIRECT);
     launch_ppm_direct_output(st, r->scene, r->px, r->last_consts);
     ev_end(r, P_DIRECT);
     HIPCHK(r, hipGetLastError());
+    return ORX_OK;
+}
+
+orx_status orx_set_ppm_pipeline(orx_renderer* r, void* side_stream, int enable) {
+    if (!r) return ORX_ERR_INVALID_ARGUMENT;
+    if (enable && r->cfg.photon_map != 0)
+        return set_err(r, ORX_ERR_UNSUPPORTED, "PPM pipelining needs the uniform grid photon map");
+    HIPCHK(r, hipSetDevice(r->device));
+    orx_status s0 = sync_all(r);
+    if (s0 != ORX_OK) return s0;
+    r->shard_pipe = enable != 0;
+    r->side = enable ? (hipStream_t)side_stream : nullptr;
+    r->rng_ready = false; /* re-allocate the frame with the second buffer set (as orx_set_shard) */
     return ORX_OK;
 }
 

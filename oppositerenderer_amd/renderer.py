@@ -68,7 +68,7 @@ EXPORTED_SYMBOLS = (
     "orx_default_config", "orx_create", "orx_init_scene", "orx_render_next_iteration", "orx_get_output",
     "orx_get_output_device", "orx_width", "orx_height", "orx_output_bytes", "orx_emitted_photons_per_iteration",
     "orx_last_error", "orx_destroy", "orx_read_buffer", "orx_get_stats", "orx_reset_timing", "orx_ppm_pipelined",
-    "orx_set_shard",
+    "orx_set_shard", "orx_set_ppm_pipeline",
     "orx_stream",
 )
 

@@ -149,3 +149,65 @@ def test_sharded_device_pt_matches_single(world, W, H):
     for b in shards:
         b.r.destroy()
     single.destroy()
+
+
+@pytest.mark.parametrize("world,W,H,P", [(2, 64, 48, 64), (3, 50, 41, 48)])
+def test_sharded_device_pipelined_matches_single(world, W, H, P):
+    """orx_set_ppm_pipeline: gather + finish of iteration i on a side stream while iteration i+1's
+    eye/photon/grid passes run, issued back to back with no host synchronisation; the image equals
+    the single-GPU one (fp32 summation order)."""
+    dev = torch.device("cuda", 0)
+    scene = scenes.cornell()
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    det = RenderRequestDetails(cam, scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W, H)
+    req = det.to_abi()
+    side = torch.cuda.Stream(dev)
+    shards = []
+    for rank in range(world):
+        r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P * world))
+        r.initialize(0)
+        r.set_shard(rank, world)
+        r.initScene(scene)
+        b = multigpu.DeviceShard(r, torch, dev)
+        b.enable_pipeline(side)
+        shards.append(b)
+    main = torch.cuda.current_stream(dev)
+    mr = (H + world - 1) // world
+    sets = [([b.alloc(mr * W * 10) for b in shards], shards[0].alloc(world * mr * W * 10),
+             [b.alloc(world * mr * W * 3) for b in shards], shards[0].alloc(world * mr * W * 3)) for _ in range(2)]
+    radius = scene.initial_ppm_radius()
+    iters = 5
+    for it in range(iters):
+        hp_loc, hp_all, parts, total = sets[it % 2]
+        for b, t in zip(shards, hp_loc):
+            b.local_eye(it, it, radius, req)
+            b.export_hitpoints(t)
+        hp_all.copy_(torch.cat(hp_loc))  # the all-gather, on the compute stream
+        for b in shards:
+            b.local_photons()
+        with torch.cuda.stream(side):
+            side.wait_stream(main)
+            for b, part in zip(shards, parts):
+                b.gather_external(hp_all, world, part)
+            total.copy_(torch.stack(parts).sum(0))  # the reduce-scatter, on the side stream
+            blk = mr * W * 3
+            for k, b in enumerate(shards):
+                b.finish(total[k * blk:(k + 1) * blk].contiguous())
+        radius = next_ppm_radius(radius, it)
+    torch.cuda.synchronize()
+    blocks = [b.output_local_tensor(mr).cpu().numpy().reshape(mr, W, 3) for b in shards]
+    got = multigpu.assemble_rows(blocks, W, H, world)
+    single = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P * world))
+    single.initialize(0)
+    single.initScene(scene)
+    radius = scene.initial_ppm_radius()
+    for it in range(iters):
+        single.renderNextIteration(it, it, radius, True, det)
+        radius = next_ppm_radius(radius, it)
+    ref = single.getOutputBuffer()
+    err = np.sqrt(((got.astype(np.float64) - ref) ** 2).sum() / (ref.astype(np.float64) ** 2).sum())
+    assert err < 1e-5, err
+    assert all(b.r.pipelined() for b in shards)
+    for b in shards:
+        b.r.destroy()
+    single.destroy()
