@@ -1390,8 +1390,12 @@ static orx_status ppm_pipelined_iteration(orx_renderer* r, const orx_request* de
     HIPCHK(r, hipEventRecord(r->ev_grid_done, st));
     hipStream_t g = r->gstream;
     HIPCHK(r, hipStreamWaitEvent(g, r->ev_grid_done, 0));
+    static const size_t lds_pad = [] {
+        const char* e = getenv("ORX_GATHER_LDS_PAD_KB");
+        return e ? (size_t)atoi(e) * 1024 : (size_t)0;
+    }();
     ev_begin_on(r, P_GATHER, g);
-    launch_ppm_gather(g, local_gather_in(r), r->pb, c);
+    launch_ppm_gather(g, local_gather_in(r), r->pb, c, lds_pad);
     ev_end_on(r, P_GATHER, g);
     HIPCHK(r, hipStreamWaitEvent(g, r->ev_direct_done, 0));
     ev_begin_on(r, P_DIRECT, g);

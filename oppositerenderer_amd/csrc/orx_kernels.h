@@ -177,7 +177,8 @@ struct GatherIn {
     uint32_t* dbg;      /* [segments*seg_rows*W*2] or NULL */
 };
 /* variant 0: one thread per pixel, 8x8 wave tiles (default); 1: wave-cooperative LDS staging */
-void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c);
+/* lds_pad: unused dynamic LDS per block, to cap the gather's blocks per CU when it overlaps other passes */
+void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, size_t lds_pad = 0);
 void launch_hash_build(hipStream_t s, const PhotonBufs& pb, const HashParams& hp);
 void launch_ppm_gather_hash(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const HashParams& hp,
                             const Consts& c);

@@ -1378,10 +1378,10 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
     }
 }
 
-void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c) {
+void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, size_t lds_pad) {
     const uint32_t rows = gi.segments * gi.seg_rows;
     dim3 grid((gi.W + 15) / 16, (rows + 15) / 16);
-    hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), 0, s, gi, pb, c);
+    hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), lds_pad, s, gi, pb, c);
 }
 
 /* ------------------------------------------------------------------ */

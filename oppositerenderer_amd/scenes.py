@@ -442,4 +442,7 @@ def scene_by_name(name: str) -> Scene:
     if name.startswith("SyntheticHall"):
         from .synthetic import synthetic_hall
         return synthetic_hall()
+    if name.startswith("SyntheticConference"):
+        from .synthetic import synthetic_conference
+        return synthetic_conference()
     raise KeyError(f"unknown scene {name!r}")

@@ -144,6 +144,90 @@ def synthetic_hall(grid_n=64, column_seg=64, column_stack=56, box_n=8, seed=42, 
     return sc
 
 
+def synthetic_conference(grid_n=80, box_n=4, seed=43, scale=1.0 / 3.0) -> scenes.Scene:
+    """Seeded "Conference-class" room (BASELINE configs[4] stand-in, SURVEY 8(d) C5: ~331k
+    triangles): tessellated floor, ceiling and walls, rows of tables with chairs, a podium and a
+    projection wall, ceiling light fixtures; Lambert materials; two quad area lights, each
+    registered once."""
+    rng = np.random.default_rng(seed)
+    S = scale
+    L, Wd, Hh = 3200.0 * S, 2000.0 * S, 900.0 * S
+    sc = scenes.Scene("SyntheticConference")
+    mats = {
+        "floor": sc.add_material(scenes.Diffuse((0.35, 0.30, 0.28))),
+        "wall": sc.add_material(scenes.Diffuse((0.80, 0.78, 0.72))),
+        "ceiling": sc.add_material(scenes.Diffuse((0.85, 0.85, 0.85))),
+        "table": sc.add_material(scenes.Diffuse((0.55, 0.38, 0.22))),
+        "chair": sc.add_material(scenes.Diffuse((0.15, 0.18, 0.45))),
+        "metal": sc.add_material(scenes.Diffuse((0.6, 0.6, 0.62))),
+        "screen": sc.add_material(scenes.Diffuse((0.9, 0.9, 0.9))),
+    }
+    parts = []
+
+    def add(vnt, m):
+        parts.append((*vnt, m))
+
+    def box(lo, hi, m, n=box_n):
+        for p in _box(lo, hi, n):
+            add(p, m)
+
+    add(_grid((0, 0, 0), (0, 0, Wd), (L, 0, 0), grid_n, grid_n), mats["floor"])
+    add(_grid((0, Hh, 0), (L, 0, 0), (0, 0, Wd), grid_n, grid_n), mats["ceiling"])
+    add(_grid((0, 0, Wd), (0, Hh, 0), (L, 0, 0), grid_n, grid_n), mats["wall"])
+    add(_grid((0, 0, 0), (L, 0, 0), (0, Hh, 0), grid_n, grid_n), mats["wall"])
+    add(_grid((0, 0, 0), (0, Hh, 0), (0, 0, Wd), grid_n, grid_n), mats["screen"])  # projection wall, x=0
+    add(_grid((L, 0, 0), (0, 0, Wd), (0, Hh, 0), grid_n, grid_n), mats["wall"])
+    # podium in front of the projection wall
+    box((150 * S, 0, Wd * 0.5 - 150 * S), (300 * S, 110 * S, Wd * 0.5 + 150 * S), mats["table"], 8)
+    # rows of tables, each with chairs on the far side
+    nrow, ntab = 7, 3
+    for i in range(nrow):
+        x0 = 700 * S + i * 330 * S
+        for j in range(ntab):
+            z0 = 200 * S + j * 560 * S
+            tl, tw, th = 120 * S, 480 * S, 75 * S
+            box((x0, th - 5 * S, z0), (x0 + tl, th, z0 + tw), mats["table"], 8)
+            for lx, lz in ((x0 + 5 * S, z0 + 5 * S), (x0 + tl - 10 * S, z0 + 5 * S),
+                           (x0 + 5 * S, z0 + tw - 10 * S), (x0 + tl - 10 * S, z0 + tw - 10 * S)):
+                box((lx, 0, lz), (lx + 5 * S, th - 5 * S, lz + 5 * S), mats["metal"])
+            for c in range(8):
+                cz = z0 + (c + 0.5) * tw / 8 + rng.uniform(-4, 4) * S
+                cx = x0 + tl + 50 * S + rng.uniform(-8, 8) * S
+                sw = 45 * S
+                box((cx - sw / 2, 45 * S, cz - sw / 2), (cx + sw / 2, 50 * S, cz + sw / 2), mats["chair"])   # seat
+                box((cx + sw / 2, 50 * S, cz - sw / 2), (cx + sw / 2 + 5 * S, 95 * S, cz + sw / 2), mats["chair"])  # back
+                for dx, dz in ((-1, -1), (1, -1), (-1, 1), (1, 1)):
+                    lx, lz = cx + dx * (sw / 2 - 3 * S), cz + dz * (sw / 2 - 3 * S)
+                    box((lx - 2 * S, 0, lz - 2 * S), (lx + 2 * S, 45 * S, lz + 2 * S), mats["metal"])
+    # ceiling light fixtures
+    for i in range(6):
+        for j in range(4):
+            x, z = (500 + i * 450) * S, (300 + j * 470) * S
+            box((x - 60 * S, Hh - 25 * S, z - 20 * S), (x + 60 * S, Hh, z + 20 * S), mats["metal"], 10)
+    verts, norms, tris, tmat = [], [], [], []
+    base = 0
+    for v, n, t, m in parts:
+        verts.append(v)
+        norms.append(n)
+        tris.append(t + base)
+        tmat.append(np.full(len(t), m, np.uint32))
+        base += len(v)
+    sc.set_mesh(np.concatenate(verts).astype(np.float32), np.concatenate(tris).astype(np.uint32),
+                np.concatenate(tmat), np.concatenate(norms).astype(np.float32))
+    for ax in (L * 0.35, L * 0.7):  # two quad area lights under the ceiling, facing down
+        anchor = (ax - 200.0 * S, Hh - 30.0 * S, Wd * 0.5 - 150.0 * S)
+        light = scenes.AreaLight((2.0e5, 1.9e5, 1.7e5), anchor, (400.0 * S, 0.0, 0.0), (0.0, 0.0, 300.0 * S))
+        sc.lights.append(light)
+        em = sc.add_material(scenes.DiffuseEmitter(light.power, 1.0, light.inverse_area))
+        sc.add_parallelogram(light.position, light.v1, light.v2, em)
+    sc.aabb_min = np.array([-5, -5, -5], np.float32)
+    sc.aabb_max = np.array([L + 5, Hh + 5, Wd + 5], np.float32)
+    sc.default_camera = scenes.Camera(np.array([L - 100.0 * S, 300.0 * S, Wd * 0.5], np.float32),
+                                      np.array([0.0, 250.0 * S, Wd * 0.5], np.float32),
+                                      np.array([0.0, 1.0, 0.0], np.float32), 70.0, 45.0, 0.0)
+    return sc
+
+
 def _checker(n, cells, c0, c1, seed):
     """RGBA8 checkerboard with per-texel noise (uint8 [n, n, 4])."""
     rng = np.random.default_rng(seed)
