@@ -1124,7 +1124,12 @@ void launch_grid_bucket_place(hipStream_t s, const PhotonBufs& pb) {
     hipLaunchKernelGGL(k_bs_place, dim3(pb.bs_nchunk), dim3(BS_THREADS), 0, s, pb);
     const uint32_t cb = 1u << pb.bshift;
     const uint32_t nbmax = (pb.gmax * pb.nsub + cb - 1) / cb;
-    hipLaunchKernelGGL(k_bs_cells, dim3(nbmax + 1), dim3(1024), SUBX * cb * 4, s, pb, cb, bs_nscan(pb));
+    static const uint32_t cells_threads = [] {
+        const char* e = getenv("ORX_BS_CELLS_THREADS");
+        const int v = e ? atoi(e) : 512; /* 512: co-schedules better beside the pipelined gather */
+        return (uint32_t)(v == 256 || v == 1024 ? v : 512);
+    }();
+    hipLaunchKernelGGL(k_bs_cells, dim3(nbmax + 1), dim3(cells_threads), SUBX * cb * 4, s, pb, cb, bs_nscan(pb));
     if (pb.nsub > 1) {
         unsigned cblocks = (pb.gmax + 1 + 255) / 256;
         if (cblocks > 4096) cblocks = 4096;
