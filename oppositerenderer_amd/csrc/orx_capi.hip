@@ -386,6 +386,7 @@ struct orx_renderer {
     DevBuf d_pos4, d_bstable, d_bspartials, d_bspairs, d_subofs;  /* bucket-sort grid build */
     DevBuf d_hcount, d_hwin;  /* stochastic hash table */
     DevBuf d_hp2, d_dir2, d_sorted2, d_subofs2, d_offsets2, d_grid2; /* second buffer set (pipelining) */
+    DevBuf d_kdtree2; /* kd-tree photon map: the second tree */
     /* kd-tree photon map (photon_map = 2, orx_kdtree.hip) */
     DevBuf d_kdtree, d_kdids, d_kdlst, d_kdnkey, d_kdkeys, d_kdnodepos, d_kdseg, d_kdbox, d_kdninfo, d_kdP, d_kdppart,
         d_kdtable, d_kdtpart, d_kdvpart, d_kdcount;
@@ -889,7 +890,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     /* second buffer set for PPM pipelining (single device or orx_set_ppm_pipeline, uniform grid) */
     r->pipe_bufs = false;
     r->pend = false;
-    if ((r->world == 1 || r->shard_pipe) && r->cfg.photon_map == 0) {
+    if ((r->world == 1 || r->shard_pipe) && r->cfg.photon_map != 1) {
         HIPCHK(r, r->d_hp2.ensure(nhp * 40));
         HIPCHK(r, r->d_dir2.ensure(nhp * 12));
         HIPCHK(r, r->d_sorted2.ensure(9 * splane * 4));
@@ -963,6 +964,10 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
         const size_t ntiles = (S + 4095) / 4096;
         const size_t tp = std::max((256 * ntiles + 1023) / 1024, (6 * nblk + 1023) / 1024) + 16;
         HIPCHK(r, r->d_kdtree.ensure(tree * 48 + 48));
+        if (r->pipe_bufs) { /* pipelining: the next iteration builds into the other tree */
+            HIPCHK(r, r->d_kdtree2.ensure(tree * 48 + 48));
+            HIPCHK(r, hipMemsetAsync(r->d_kdtree2.p, 0, tree * 48 + 48, r->stream));
+        }
         HIPCHK(r, r->d_kdids.ensure(6 * S * 4 + 64));
         HIPCHK(r, r->d_kdkeys.ensure(2 * S * 4 + 64));
         HIPCHK(r, r->d_kdnodepos.ensure(S * 4 + 16));
@@ -1115,6 +1120,11 @@ static void swap_sets(orx_renderer* r) {
     swap_buf(r->d_subofs, r->d_subofs2);
     swap_buf(r->d_offsets, r->d_offsets2);
     swap_buf(r->d_grid, r->d_grid2);
+    if (r->cfg.photon_map == 2) {
+        swap_buf(r->d_kdtree, r->d_kdtree2);
+        r->kd.tree = r->d_kdtree.as<float4>();
+        r->kd.tree_bc = r->kd.tree + r->kd.tree_size + 1;
+    }
     const size_t nhp = (size_t)r->max_rows * r->W;
     r->px.hpA = r->d_hp.as<float4>();
     r->px.hpB = r->d_hp.as<float4>() + nhp;
@@ -1395,7 +1405,8 @@ static orx_status ppm_pipelined_iteration(orx_renderer* r, const orx_request* de
         return e ? (size_t)atoi(e) * 1024 : (size_t)0;
     }();
     ev_begin_on(r, P_GATHER, g);
-    launch_ppm_gather(g, local_gather_in(r), r->pb, c, lds_pad);
+    if (r->cfg.photon_map == 2) launch_ppm_gather_kd(g, local_gather_in(r), r->pb, r->kd, c);
+    else launch_ppm_gather(g, local_gather_in(r), r->pb, c, lds_pad);
     ev_end_on(r, P_GATHER, g);
     HIPCHK(r, hipStreamWaitEvent(g, r->ev_direct_done, 0));
     ev_begin_on(r, P_DIRECT, g);
@@ -1429,7 +1440,7 @@ orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
     }();
     const bool same_size = det->width == r->W && det->height == r->H && r->rng_ready;
     const bool pipelined = pipeline_env && det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world == 1 &&
-                           r->cfg.photon_map == 0 && !r->use_ext && (r->pipe_bufs || !same_size);
+                           r->cfg.photon_map != 1 && !r->use_ext && (r->pipe_bufs || !same_size);
     orx_status s0 = begin_iteration(r, local_iteration_number, det, pipelined);
     if (s0 != ORX_OK) return s0;
     r->last_pipelined = pipelined && r->pipe_bufs;
@@ -1596,8 +1607,8 @@ orx_status orx_ppm_finish(orx_renderer* r, const void* indirect, size_t bytes) {
 
 orx_status orx_set_ppm_pipeline(orx_renderer* r, void* side_stream, int enable) {
     if (!r) return ORX_ERR_INVALID_ARGUMENT;
-    if (enable && r->cfg.photon_map != 0)
-        return set_err(r, ORX_ERR_UNSUPPORTED, "PPM pipelining needs the uniform grid photon map");
+    if (enable && r->cfg.photon_map == 1)
+        return set_err(r, ORX_ERR_UNSUPPORTED, "PPM pipelining needs the uniform grid or kd-tree photon map");
     HIPCHK(r, hipSetDevice(r->device));
     orx_status s0 = sync_all(r);
     if (s0 != ORX_OK) return s0;

@@ -433,8 +433,8 @@ def test_kdtree_parity(scene_name, W, H, P):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pipeline", ["1", "0"])
-def test_ppm_back_to_back_iterations(pipeline, monkeypatch):
+@pytest.mark.parametrize("pipeline,photon_map", [("1", 0), ("0", 0), ("1", 2)])
+def test_ppm_back_to_back_iterations(pipeline, photon_map, monkeypatch):
     """Iterations issued back to back with no read in between: with pipelining on (default) the
     gather + output of iteration i run beside the eye/photon/grid passes of i+1 on the other
     buffer set; the running sum after five iterations (and a resolution change in between)
@@ -447,9 +447,11 @@ import oracle_lib
 from oppositerenderer_amd import _abi, scenes
 from oppositerenderer_amd.renderer import OptixRenderer, RenderRequestDetails, next_ppm_radius
 scene = scenes.cornell()
-cfg = _abi.default_config(seed=1645301512, photon_launch_width=96, photon_launch_height=96)
+pm = int(sys.argv[1])
+cfg = _abi.default_config(seed=1645301512, photon_launch_width=96, photon_launch_height=96, photon_map=pm)
 gpu = OptixRenderer(cfg); gpu.initialize(0); gpu.initScene(scene)
-ora = oracle_lib.OracleRenderer(_abi.default_config(seed=1645301512, photon_launch_width=96, photon_launch_height=96))
+ora = oracle_lib.OracleRenderer(_abi.default_config(seed=1645301512, photon_launch_width=96, photon_launch_height=96,
+                                                    photon_map=pm))
 ora.init_scene(scene)
 errs = []
 for W, H, n in ((64, 48, 5), (40, 40, 3)):
@@ -465,7 +467,8 @@ for W, H, n in ((64, 48, 5), (40, 40, 3)):
 print(json.dumps(errs))
 '''
     env = dict(os.environ, ORX_PIPELINE=pipeline)
-    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110,
+    out = subprocess.run([sys.executable, "-c", code, str(photon_map)], env=env, capture_output=True, text=True,
+                         timeout=110,
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert out.returncode == 0, out.stderr[-2000:]
     errs = json.loads(out.stdout.strip().splitlines()[-1])
