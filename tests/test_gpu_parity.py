@@ -473,3 +473,28 @@ print(json.dumps(errs))
     assert out.returncode == 0, out.stderr[-2000:]
     errs = json.loads(out.stdout.strip().splitlines()[-1])
     assert all(e < 1e-5 for e in errs), errs
+
+
+@pytest.mark.gpu
+def test_method_switches_without_reads():
+    """PPM (pipelined), PT and VCM iterations issued back to back with no read in between: the
+    deferred PPM gather/output is ordered before the next method's passes, the RNG chain runs
+    through all of them, and the final image matches the oracle running the same sequence."""
+    scene = scenes.cornell()
+    W, H, P = 48, 40, 64
+    gpu, ora, _ = make_pair(scene, W, H, P, _abi.PROGRESSIVE_PHOTON_MAPPING)
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    seq = [(_abi.PROGRESSIVE_PHOTON_MAPPING, 0), (_abi.PROGRESSIVE_PHOTON_MAPPING, 1), (_abi.PATH_TRACING, 0),
+           (_abi.PATH_TRACING, 1), (_abi.VCM_BIDIRECTIONAL_PATH_TRACING, 0), (_abi.PROGRESSIVE_PHOTON_MAPPING, 0),
+           (_abi.PROGRESSIVE_PHOTON_MAPPING, 1), (_abi.PROGRESSIVE_PHOTON_MAPPING, 2)]
+    radius = scene.initial_ppm_radius()
+    for it, (method, local) in enumerate(seq):
+        det = RenderRequestDetails(cam, scene.name, method, W, H)
+        gpu.renderNextIteration(it, local, radius, True, det)
+        ora.render_next_iteration(it, local, radius, det.to_abi())
+        radius = next_ppm_radius(radius, it)
+    g, o = gpu.getOutputBuffer(), ora.output()
+    assert rel_l2(g, o) < 1e-5 and g.mean() > 0
+    assert gpu.pipelined()
+    gpu.destroy()
+    ora.close()
