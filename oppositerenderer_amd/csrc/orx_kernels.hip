@@ -1020,13 +1020,20 @@ __global__ __launch_bounds__(BS_THREADS) void k_bs_place(PhotonBufs pb) {
     for (uint32_t b = threadIdx.x; b < nb; b += BS_THREADS) cur[b] = pb.bs_table[(size_t)b * pb.bs_nchunk + blockIdx.x];
     __syncthreads();
     const uint32_t c0 = blockIdx.x * BS_CHUNK;
-    for (uint32_t k = threadIdx.x; k < BS_CHUNK; k += BS_THREADS) {
-        const uint32_t s = c0 + k;
-        if (s >= pb.S) break;
-        const uint32_t key = pb.keys[s];
-        if (key != 0xffffffffu) {
-            const uint32_t pos = atomicAdd(&cur[(key / SUBX) >> pb.bshift], 1u);
-            pb.bs_pairs[pos] = make_uint2(key, s);
+    constexpr uint32_t U = 4;
+    for (uint32_t k0 = threadIdx.x; k0 < BS_CHUNK; k0 += U * BS_THREADS) {
+        uint32_t kv[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t s = c0 + k0 + u * BS_THREADS;
+            kv[u] = s < pb.S ? pb.keys[s] : 0xffffffffu;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            if (kv[u] != 0xffffffffu) {
+                const uint32_t pos = atomicAdd(&cur[(kv[u] / SUBX) >> pb.bshift], 1u);
+                pb.bs_pairs[pos] = make_uint2(kv[u], c0 + k0 + u * BS_THREADS);
+            }
         }
     }
 }
@@ -1047,7 +1054,17 @@ __global__ __launch_bounds__(1024) void k_bs_cells(PhotonBufs pb, uint32_t cb, u
     const uint32_t nf = SUBX * cb, f0 = b * nf;
     for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) lds[i] = 0;
     __syncthreads();
-    for (uint32_t i = start + threadIdx.x; i < end; i += blockDim.x) atomicAdd(&lds[pb.bs_pairs[i].x - f0], 1u);
+    for (uint32_t i0 = start + threadIdx.x; i0 < end; i0 += 4 * blockDim.x) {
+        uint32_t kv[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+            const uint32_t i = i0 + u * blockDim.x;
+            kv[u] = i < end ? pb.bs_pairs[i].x : 0xffffffffu;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++)
+            if (kv[u] != 0xffffffffu) atomicAdd(&lds[kv[u] - f0], 1u);
+    }
     __syncthreads();
     /* exclusive scan of lds[0..nf) by 1024 threads, nf/1024 entries each */
     __shared__ uint32_t wsum[16];
@@ -1081,10 +1098,19 @@ __global__ __launch_bounds__(1024) void k_bs_cells(PhotonBufs pb, uint32_t cb, u
         pb.grid->valid_total += total;
     }
     __syncthreads();
-    for (uint32_t i = start + threadIdx.x; i < end; i += blockDim.x) {
-        const uint2 kp = pb.bs_pairs[i];
-        const uint32_t pos = atomicAdd(&lds[kp.x - f0], 1u);
-        pb.perm[pos] = kp.y;
+    for (uint32_t i0 = start + threadIdx.x; i0 < end; i0 += 4 * blockDim.x) {
+        uint2 kv[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+            const uint32_t i = i0 + u * blockDim.x;
+            kv[u] = i < end ? pb.bs_pairs[i] : make_uint2(0xffffffffu, 0u);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++)
+            if (kv[u].x != 0xffffffffu) {
+                const uint32_t pos = atomicAdd(&lds[kv[u].x - f0], 1u);
+                pb.perm[pos] = kv[u].y;
+            }
     }
 }
 
