@@ -4,7 +4,7 @@
 The reference ships no fixtures and cannot run here, so these pin
 the oracle against drift: any change to the restatement that alters a result
 shows up as a fixture mismatch.  Each case: seed 1645301512 (config.h:50),
-small image, two iterations.  Usage: python tests/golden/make_golden.py
+small image, two iterations.  Usage: python tests/golden/make_golden.py [case ...]
 """
 import os
 import sys
@@ -31,14 +31,24 @@ CASES = {
                                  ["RNG", "VCM_VERTEX_COUNT", "VCM_CAMERA", "VCM_SPLAT", "OUTPUT"]),
     "cornellsmall_glossy_vcm": ("CornellSmallLargeSphere", _abi.VCM_BIDIRECTIONAL_PATH_TRACING, 24, 24, 32, 2,
                                 ["RNG", "VCM_VERTEX_COUNT", "VCM_CAMERA", "VCM_SPLAT", "OUTPUT"]),
+    # the other photon maps (config overrides as an eighth element) and the Texture material
+    "cornell_hash_ppm": ("Cornell", _abi.PROGRESSIVE_PHOTON_MAPPING, 32, 32, 64, 2,
+                         ["RNG", "HITPOINTS", "GRID_OFFSETS", "DIRECT", "INDIRECT", "OUTPUT"],
+                         {"photon_map": _abi.PHOTON_MAP_STOCHASTIC_HASH}),
+    "cornell_kd_ppm": ("Cornell", _abi.PROGRESSIVE_PHOTON_MAPPING, 32, 32, 64, 2,
+                       ["RNG", "HITPOINTS", "DIRECT", "INDIRECT", "OUTPUT"], {"photon_map": _abi.PHOTON_MAP_KD_TREE}),
+    "texturedroom_ppm": ("TexturedRoom", _abi.PROGRESSIVE_PHOTON_MAPPING, 24, 24, 48, 2,
+                         ["RNG", "HITPOINTS", "DIRECT", "INDIRECT", "OUTPUT"]),
 }
 INT_BUFFERS = {"RNG", "GRID_OFFSETS", "VCM_VERTEX_COUNT"}
 
 
 def render(case, renderer_factory):
-    scene_name, method, W, H, P, iters, bufs = CASES[case]
+    scene_name, method, W, H, P, iters, bufs = CASES[case][:7]
+    overrides = CASES[case][7] if len(CASES[case]) > 7 else {}
     scene = scenes.scene_by_name(scene_name)
-    r = renderer_factory(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P), scene)
+    r = renderer_factory(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P, **overrides),
+                         scene)
     cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
     req = _abi.OrxRequest()
     req.camera = cam.to_abi()
@@ -61,7 +71,7 @@ def oracle_factory(cfg, scene):
 
 def main():
     oracle_lib.load().orc_set_threads(1)
-    for case in CASES:
+    for case in (sys.argv[1:] or CASES):
         r, out = render(case, oracle_factory)
         r.close()
         np.savez_compressed(os.path.join(HERE, case + ".npz"), **out)
