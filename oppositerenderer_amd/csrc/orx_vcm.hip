@@ -721,7 +721,10 @@ __device__ inline bool connect_light(const DevScene& S, const Subpath& C, const 
 
 /* cameraPass (VCMCameraPass.cu:48-80), initCameraPayload (:100-135), cameraHit (vcm.h:527-628) */
 template <bool TEX>
-__global__ __launch_bounds__(64, 4) void k_vcm_camera(DevScene S, VcmBufs vb, VcmConsts c) {
+#ifndef ORX_VCM_CAMERA_WAVES
+#define ORX_VCM_CAMERA_WAVES 4 /* waves per SIMD the camera kernel is register-capped for (A/B: make vcm3) */
+#endif
+__global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScene S, VcmBufs vb, VcmConsts c) {
     ORX_STACK_DECL;
     uint32_t* stk = ORX_STACK_PTR;
     const uint32_t tilesX = (c.W + 7) / 8;
