@@ -387,6 +387,7 @@ struct orx_renderer {
     DevBuf d_hcount, d_hwin;  /* stochastic hash table */
     DevBuf d_hp2, d_dir2, d_sorted2, d_subofs2, d_offsets2, d_grid2; /* second buffer set (pipelining) */
     DevBuf d_kdtree2; /* kd-tree photon map: the second tree */
+    DevBuf d_slots2, d_hcount2, d_hwin2; /* stochastic hash: second deposit records and table */
     /* kd-tree photon map (photon_map = 2, orx_kdtree.hip) */
     DevBuf d_kdtree, d_kdids, d_kdlst, d_kdnkey, d_kdkeys, d_kdnodepos, d_kdseg, d_kdbox, d_kdninfo, d_kdP, d_kdppart,
         d_kdtable, d_kdtpart, d_kdvpart, d_kdcount;
@@ -890,7 +891,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     /* second buffer set for PPM pipelining (single device or orx_set_ppm_pipeline, uniform grid) */
     r->pipe_bufs = false;
     r->pend = false;
-    if ((r->world == 1 || r->shard_pipe) && r->cfg.photon_map != 1) {
+    if (r->world == 1 || r->shard_pipe) {
         HIPCHK(r, r->d_hp2.ensure(nhp * 40));
         HIPCHK(r, r->d_dir2.ensure(nhp * 12));
         HIPCHK(r, r->d_sorted2.ensure(9 * splane * 4));
@@ -945,6 +946,11 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
         const size_t hnum = (size_t)PW * PH * r->cfg.max_photon_deposits; /* NUM_PHOTONS */
         HIPCHK(r, r->d_hcount.ensure(hnum * 4));
         HIPCHK(r, r->d_hwin.ensure(hnum * 4));
+        if (r->pipe_bufs) {
+            HIPCHK(r, r->d_hcount2.ensure(hnum * 4));
+            HIPCHK(r, r->d_hwin2.ensure(hnum * 4));
+            HIPCHK(r, r->d_slots2.ensure(S * 64));
+        }
         pb.hnum = (uint32_t)hnum;
         pb.hcount = r->d_hcount.as<uint32_t>();
         pb.hwin = r->d_hwin.as<uint32_t>();
@@ -1120,6 +1126,14 @@ static void swap_sets(orx_renderer* r) {
     swap_buf(r->d_subofs, r->d_subofs2);
     swap_buf(r->d_offsets, r->d_offsets2);
     swap_buf(r->d_grid, r->d_grid2);
+    if (r->cfg.photon_map == 1) { /* the hash gather reads the deposit records and the table */
+        swap_buf(r->d_slots, r->d_slots2);
+        swap_buf(r->d_hcount, r->d_hcount2);
+        swap_buf(r->d_hwin, r->d_hwin2);
+        r->pb.slots = r->d_slots.as<float4>();
+        r->pb.hcount = r->d_hcount.as<uint32_t>();
+        r->pb.hwin = r->d_hwin.as<uint32_t>();
+    }
     if (r->cfg.photon_map == 2) {
         swap_buf(r->d_kdtree, r->d_kdtree2);
         r->kd.tree = r->d_kdtree.as<float4>();
@@ -1406,6 +1420,7 @@ static orx_status ppm_pipelined_iteration(orx_renderer* r, const orx_request* de
     }();
     ev_begin_on(r, P_GATHER, g);
     if (r->cfg.photon_map == 2) launch_ppm_gather_kd(g, local_gather_in(r), r->pb, r->kd, c);
+    else if (r->pb.hash) launch_ppm_gather_hash(g, local_gather_in(r), r->pb, hash_params(r, c.ppm_radius), c);
     else launch_ppm_gather(g, local_gather_in(r), r->pb, c, lds_pad);
     ev_end_on(r, P_GATHER, g);
     HIPCHK(r, hipStreamWaitEvent(g, r->ev_direct_done, 0));
@@ -1440,7 +1455,7 @@ orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
     }();
     const bool same_size = det->width == r->W && det->height == r->H && r->rng_ready;
     const bool pipelined = pipeline_env && det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world == 1 &&
-                           r->cfg.photon_map != 1 && !r->use_ext && (r->pipe_bufs || !same_size);
+                           !r->use_ext && (r->pipe_bufs || !same_size);
     orx_status s0 = begin_iteration(r, local_iteration_number, det, pipelined);
     if (s0 != ORX_OK) return s0;
     r->last_pipelined = pipelined && r->pipe_bufs;
