@@ -301,7 +301,8 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hitpoints_device
                                    void* indirect_device, size_t indirect_bytes);
 /* indirect_device: max_local_rows * W * 3 floats for the own rows */
 orx_status orx_ppm_finish(orx_renderer* r, const void* indirect_device, size_t indirect_bytes);
-/* Pipelined sharded PPM (uniform grid; call before the first iteration, like orx_set_shard):
+/* Pipelined sharded PPM (uniform grid or kd-tree: the hash is single-device, and pipelines on
+ * its own without this call; call before the first iteration, like orx_set_shard):
  * orx_ppm_gather_external and orx_ppm_finish of iteration i run on `side_stream` (a hipStream_t
  * of the caller's, who also issues the indirect reduce-scatter there), overlapping iteration
  * i+1's eye, photon and grid passes on the renderer's stream; the direct pass runs on an internal

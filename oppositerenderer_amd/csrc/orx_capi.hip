@@ -1623,7 +1623,7 @@ orx_status orx_ppm_finish(orx_renderer* r, const void* indirect, size_t bytes) {
 orx_status orx_set_ppm_pipeline(orx_renderer* r, void* side_stream, int enable) {
     if (!r) return ORX_ERR_INVALID_ARGUMENT;
     if (enable && r->cfg.photon_map == 1)
-        return set_err(r, ORX_ERR_UNSUPPORTED, "PPM pipelining needs the uniform grid or kd-tree photon map");
+        return set_err(r, ORX_ERR_UNSUPPORTED, "sharded PPM pipelining needs the uniform grid or kd-tree photon map");
     HIPCHK(r, hipSetDevice(r->device));
     orx_status s0 = sync_all(r);
     if (s0 != ORX_OK) return s0;
