@@ -857,11 +857,11 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_slots.ensure(S * 64));
     HIPCHK(r, r->d_vmask.ensure(nphot));
     const size_t splane = ((S + 4) + 3) & ~(size_t)3;
-    if (9 * splane * 4 > 0xffffff00ull) /* the gather addresses the nine planes with 32-bit buffer offsets */
+    if ((size_t)SP_PLANES * splane * 4 > 0xffffff00ull) /* the gather addresses the planes with 32-bit buffer offsets */
         return set_err(r, ORX_ERR_UNSUPPORTED, "photon slots per device exceed the 4 GiB sorted-photon window");
-    HIPCHK(r, r->d_sorted.ensure(9 * splane * 4));
+    HIPCHK(r, r->d_sorted.ensure(SP_PLANES * splane * 4));
     HIPCHK(r, r->d_perm.ensure(S * 4 + 16));
-    HIPCHK(r, hipMemsetAsync(r->d_sorted.p, 0, 9 * splane * 4, r->stream)); /* tail reads stay finite */
+    HIPCHK(r, hipMemsetAsync(r->d_sorted.p, 0, SP_PLANES * splane * 4, r->stream)); /* tail reads stay finite */
     HIPCHK(r, r->d_keys.ensure(S * 4));
     HIPCHK(r, r->d_ranks.ensure(S * 4));
     HIPCHK(r, r->d_hist.ensure(G2 * 4));
@@ -894,8 +894,8 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     if (r->world == 1 || r->shard_pipe) {
         HIPCHK(r, r->d_hp2.ensure(nhp * 40));
         HIPCHK(r, r->d_dir2.ensure(nhp * 12));
-        HIPCHK(r, r->d_sorted2.ensure(9 * splane * 4));
-        HIPCHK(r, hipMemsetAsync(r->d_sorted2.p, 0, 9 * splane * 4, r->stream));
+        HIPCHK(r, r->d_sorted2.ensure(SP_PLANES * splane * 4));
+        HIPCHK(r, hipMemsetAsync(r->d_sorted2.p, 0, SP_PLANES * splane * 4, r->stream));
         HIPCHK(r, r->d_subofs2.ensure(G2 * 4 * SUBX * nsub + 16));
         HIPCHK(r, r->d_offsets2.ensure(G2 * 4));
         HIPCHK(r, hipMemsetAsync(r->d_offsets2.p, 0, G2 * 4, r->stream));
@@ -1819,8 +1819,9 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
         /* nine SoA planes -> [n][power3 position3 direction3] (Photon.h:10-33 order) */
         const size_t n = g.valid, P = r->pb.splane;
         std::vector<float> pl(9 * n);
-        for (int q = 0; q < 9 && n; q++) HIPCHK(r, d2h(pl.data() + q * n, r->d_sorted.as<float>() + q * P, n * 4));
-        static const int order[9] = {6, 7, 8, 0, 1, 2, 3, 4, 5};
+        static const uint32_t order[9] = {SP_PX, SP_PY, SP_PZ, SP_X, SP_Y, SP_Z, SP_DX, SP_DY, SP_DZ};
+        for (int q = 0; q < 9 && n; q++)
+            HIPCHK(r, d2h(pl.data() + q * n, r->d_sorted.as<float>() + order[q] * P, n * 4));
         /* sub-row layout: present the reference's cell order (each cell = its
          * nsub sub-row pieces, k_bs_count); within a cell the order is free */
         std::vector<uint32_t> idx;
@@ -1841,7 +1842,7 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
         float* o = (float*)dst;
         for (size_t i = 0; i < n; i++) {
             const size_t src = idx.empty() ? i : idx[i];
-            for (int k = 0; k < 9; k++) o[9 * i + k] = pl[order[k] * n + src];
+            for (int k = 0; k < 9; k++) o[9 * i + k] = pl[k * n + src];
         }
         break;
     }

@@ -54,6 +54,9 @@ struct PixelBufs {
 };
 
 constexpr uint32_t BBOX_REPLICAS = 64;
+/* grid-ordered photon planes (PhotonBufs::sorted): position, the int8 direction
+ * prefilter word of the gather's facing test, exact direction, power */
+enum : uint32_t { SP_X = 0, SP_Y, SP_Z, SP_DIRQ, SP_DX, SP_DY, SP_DZ, SP_PX, SP_PY, SP_PZ, SP_PLANES };
 constexpr uint32_t SUBX = 4; /* sub-cells per grid cell along x (bucket-sort grid, gather chord trimming) */
 constexpr uint32_t SUBR = 2; /* sub-rows per grid cell along y and along z (bucket-sort grid, nsub = SUBR^2) */
 
@@ -66,7 +69,7 @@ struct PhotonBufs {
     float4* slots;      /* [S][4] 64-B deposit records: pos.xyz|power.x, dir.xyz|power.y, power.z, unused
                          * (one record per cache-line half: the grid permute reads it in one go) */
     uint8_t* vmask;     /* [S/D] bit k: deposit k stored with fmaxf(power) > 0 */
-    float* sorted;      /* grid-ordered photons, nine float planes (SoA): x y z | dir x y z | power x y z */
+    float* sorted;      /* grid-ordered photons, SP_PLANES float planes (SoA): x y z | dirq | dir x y z | power x y z */
     uint32_t splane;    /* plane stride in floats (multiple of 4, >= S + 4) */
     uint32_t* perm;     /* [S] grid position -> photon slot (counting-sort scatter target) */
     uint32_t* keys;     /* [S] */

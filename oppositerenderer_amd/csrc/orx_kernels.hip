@@ -857,7 +857,24 @@ __global__ __launch_bounds__(256) void k_grid_scatter(PhotonBufs pb) {
             if (key[q] <= G) pb.perm[off[q] + rank[q]] = s0 + q * T;
     }
 }
-/* grid order -> SoA planes: destination-major, so the nine plane writes are
+/* Direction prefilter word of a grid photon (sorted plane SP_DIRQ): the
+ * direction as three int8 snorm bytes q = rint(127 d).  The gather's facing
+ * test dot(d, n) <= 0 is decided from v_dot4_i32_i8(q, qn) (qn the same
+ * quantisation of the hit point's normal) whenever that integer dot lies
+ * outside +-DIRQ_BAND; inside the band the exact fp32 direction planes decide.
+ * Bound: |q/127 - d|_inf <= 0.5/127 + eps, so for |d|_1, |n|_1 <= 1.7325
+ *   |qd.qn - 127^2 d.n| <= 127^2 (0.5/127 (|d|_1 + |n|_1) + 3 (0.5/127)^2) <= 221
+ * and every decision taken from the integer dot equals the exact one.  A
+ * direction (or normal) outside that 1-norm bound (or NaN) quantises to 0,
+ * which always lands in the band. */
+constexpr int32_t DIRQ_BAND = 232;
+__device__ __forceinline__ uint32_t dir_q8(float x, float y, float z) {
+    if (!(fabsf(x) + fabsf(y) + fabsf(z) <= 1.7325f)) return 0u;
+    const int32_t qx = (int32_t)rintf(x * 127.f), qy = (int32_t)rintf(y * 127.f), qz = (int32_t)rintf(z * 127.f);
+    return ((uint32_t)qx & 0xffu) | (((uint32_t)qy & 0xffu) << 8) | (((uint32_t)qz & 0xffu) << 16);
+}
+
+/* grid order -> SoA planes: destination-major, so the ten plane writes are
  * coalesced and the source reads are whole float4s */
 __global__ __launch_bounds__(256) void k_grid_permute(PhotonBufs pb) {
     const uint32_t valid = pb.grid->valid;
@@ -882,15 +899,16 @@ __global__ __launch_bounds__(256) void k_grid_permute(PhotonBufs pb) {
         for (int q = 0; q < 4; q++) {
             if (src[q] == 0xffffffffu) continue;
             float* o = pb.sorted + d0 + q * T;
-            o[0] = a[q].x;
-            o[P] = a[q].y;
-            o[2 * P] = a[q].z;
-            o[3 * P] = b[q].x;
-            o[4 * P] = b[q].y;
-            o[5 * P] = b[q].z;
-            o[6 * P] = a[q].w;
-            o[7 * P] = b[q].w;
-            o[8 * P] = cz[q];
+            o[SP_X * P] = a[q].x;
+            o[SP_Y * P] = a[q].y;
+            o[SP_Z * P] = a[q].z;
+            o[SP_DIRQ * P] = __uint_as_float(dir_q8(b[q].x, b[q].y, b[q].z));
+            o[SP_DX * P] = b[q].x;
+            o[SP_DY * P] = b[q].y;
+            o[SP_DZ * P] = b[q].z;
+            o[SP_PX * P] = a[q].w;
+            o[SP_PY * P] = b[q].w;
+            o[SP_PZ * P] = cz[q];
         }
     }
 }
@@ -1194,193 +1212,251 @@ __device__ __forceinline__ HpRef hp_ref(const GatherIn& gi, uint32_t j, uint32_t
     return r;
 }
 
-/* Per-pixel gather, packed fp32: one lane per pixel (four 8x8 wave tiles per
- * 256-thread block, so neighbouring lanes share photons in L1).  The (z,y)
- * cell rows of the window are walked in the reference order
- * (IndirectRadianceEstimation.cu:95-129); within a row the photons go in
- * aligned groups of four: one dwordx4 load per SoA plane, two photons per
- * packed instruction.  The acceptance tests (d^2 <= r^2, dot(-w, n) >= 0) use
- * exactly the oracle's unfused operations, so the accepted photon set is
- * bit-identical; the kernel weight (photonPower, :59-67) and the sums, which
- * the device accumulates in a different order anyway, use fused
- * multiply-adds (v_pk_fma_f32): within ~1e-7 of the oracle per term. */
+/* Per-pixel gather, packed fp32: one lane per pixel, four 8x8 wave tiles per
+ * 256-thread block (neighbouring lanes share photons in L1), tiles dealt to
+ * the eight XCDs in contiguous bands (neighbouring tiles share one L2).
+ *
+ * The work of a lane is the list of sub-row chords of its window (see the
+ * photon-grid layout above); the reference walks the (z,y) cell rows of the
+ * window (IndirectRadianceEstimation.cu:95-129) and so would a nested loop
+ * here, but then a wave runs, per row and sub-row, as long as its longest
+ * lane: the sum of maxima.  Instead the chords are collected first (phase A:
+ * up to GQ non-empty [first, end) photon ranges per lane, in LDS) and then
+ * walked as one flat stream of batches (phase B), so the wave runs for the
+ * maximum of the lanes' sums.  A batch is four consecutive photons, one
+ * dwordx4 buffer load per SoA plane (one VGPR offset, plane offsets in
+ * SGPRs), two photons per packed instruction:
+ *   1. positions -> d^2 <= r^2 (the oracle's unfused operations);
+ *   2. if any lane photon is within r: the int8 direction word -> facing
+ *      test by v_dot4_i32_i8, exact fp32 directions only inside the band
+ *      (DIRQ_BAND; same decisions as the exact test, by the bound at dir_q8);
+ *   3. if any photon is accepted: powers, kernel weight, accumulation.
+ * So the accepted photon set is bit-identical to the reference's; the kernel
+ * weight (photonPower, :59-67) and the sums, which the device accumulates in
+ * a different order anyway, use fused multiply-adds (within ~1e-7 per term).
+ * The visit counters are the reference's whole-window counts (:113/:124). */
 typedef float v2f __attribute__((ext_vector_type(2)));
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4))); /* dword-aligned float4 */
 __device__ __forceinline__ v2f lo2(float4 v) { return v2f{v.x, v.y}; }
 __device__ __forceinline__ v2f hi2(float4 v) { return v2f{v.z, v.w}; }
 __device__ __forceinline__ v2f lo2(f4u v) { return v2f{v.x, v.y}; }
 __device__ __forceinline__ v2f hi2(f4u v) { return v2f{v.z, v.w}; }
-/* sorted-photon plane load: one buffer resource over the nine planes, the
- * plane's byte offset in an SGPR (soffset) and the photon's byte offset in a
- * VGPR, so the nine loads of a batch share one address register */
+/* sorted-photon plane load: one buffer resource over the planes, the plane's
+ * byte offset in an SGPR (soffset) and the photon's byte offset in a VGPR, so
+ * the loads of a batch share one address register */
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f4u ldp(__amdgpu_buffer_rsrc_t rs, uint32_t so, uint32_t bo) {
     const u4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)bo, (int)so, 0);
     return f4u{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
 }
+__device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
 
-__global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, Consts c) {
-    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (l & 7);
-    const uint32_t j = blockIdx.y * 16 + (w >> 1) * 8 + (l >> 3);
+constexpr uint32_t GQ = 8; /* chord ranges per lane per phase A (LDS: GQ * 8 B per lane) */
+
+/* NSUB: sub-rows per cell row (SUBR^2, or 1 for the cell-order layout);
+ * SUBOFS: sub-cell offsets present (bucket-sort grid) or cell offsets only
+ * (atomic-rank grid, ORX_GRID_ATOMIC=1) */
+template <uint32_t NSUB, bool SUBOFS>
+__global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
+                                                    uint32_t ntiles) {
+    __shared__ uint2 rq[GQ][256];
+    const uint32_t tid = threadIdx.x;
+    /* XCD-aware tile order: block b runs on XCD b % 8; XCD k takes tiles [k per, (k+1) per) */
+    const uint32_t per = (ntiles + 7) / 8;
+    const uint32_t tile = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    const uint32_t w = tid >> 6, l = tid & 63;
+    const uint32_t x = (tile % ntx) * 16 + (w & 1) * 8 + (l & 7);
+    const uint32_t j = (tile / ntx) * 16 + (w >> 1) * 8 + (l >> 3);
     const GridParams g = *pb.grid;
     uint32_t dC = 0, dP = 0;
     ORX_TS_DECL;
-    if (x < gi.W && j < gi.segments * gi.seg_rows) {
-        const size_t i = (size_t)j * gi.W + x;
+    const bool live = tile < ntiles && x < gi.W && j < gi.segments * gi.seg_rows;
+    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+    float2 Cc = make_float2(0.f, 0.f);
+    size_t i = 0;
+    if (live) {
+        i = (size_t)j * gi.W + x;
         const HpRef hr = hp_ref(gi, j, x);
-        const float4 A = hr.A[hr.li];
-        const float4 B = hr.B[hr.li];
-        const float2 Cc = hr.C[hr.li];
-        const uint32_t flags = __float_as_uint(A.w);
-        float ax = 0.f, ay = 0.f, az = 0.f;
-        if ((flags & PRD_HIT_NON_SPECULAR) && g.G) {
-            const f3 pos = mk(A.x, A.y, A.z);
-            const float radius2 = c.ppm_radius2;
-            const float radius = c.ppm_radius;
-            const float invCellSize = 1.f / g.cell;
-            const f3 np = pos - mk(g.ox, g.oy, g.oz);
-            const int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
-            const int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
-            const int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
-            const uint32_t x_lo = (uint32_t)(ixl > 0 ? ixl : 0);
-            const uint32_t y_lo = (uint32_t)(iyl > 0 ? iyl : 0);
-            const uint32_t z_lo = (uint32_t)(izl > 0 ? izl : 0);
-            const uint32_t ux = orx_f2u_sat((np.x + radius) * invCellSize);
-            const uint32_t uy = orx_f2u_sat((np.y + radius) * invCellSize);
-            const uint32_t uz = orx_f2u_sat((np.z + radius) * invCellSize);
-            const uint32_t x_hi = (g.gx - 1) < ux ? (g.gx - 1) : ux;
-            const uint32_t y_hi = (g.gy - 1) < uy ? (g.gy - 1) : uy;
-            const uint32_t z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
-            if (x_lo <= x_hi) {
-                const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
-                const float inv2r2 = 1.0f / (2 * radius2);
-                const float invDen = 1.0f / (1 - expNegativeBeta);
-                const float kx = -beta * inv2r2;
-                const float wB = alpha * invDen, wA = alpha - wB; /* w = A + B*exp(x) */
-                const v2f kx2 = v2f{kx, kx};
-                const v2f wc6 = wB * ORX_EXPU_C6, wc5 = wB * ORX_EXPU_C5, wc4 = wB * ORX_EXPU_C4;
-                const v2f wc3 = wB * ORX_EXPU_C3, wc2 = wB * ORX_EXPU_C2, wc1 = wB * ORX_EXPU_C1;
-                const v2f wc0 = v2f{wA + wB, wA + wB};
-                v2f accx = v2f{0.f, 0.f}, accy = accx, accz = accx;
-                const v2f px2 = v2f{pos.x, pos.x}, py2 = v2f{pos.y, pos.y}, pz2 = v2f{pos.z, pos.z};
-                const v2f nx2 = v2f{B.x, B.x}, ny2 = v2f{B.y, B.y}, nz2 = v2f{B.z, B.z};
-                const size_t P = pb.splane;
-                /* 9 * P * 4 < 4 GiB: checked on the host (resize) */
-                const __amdgpu_buffer_rsrc_t SR =
-                    __builtin_amdgcn_make_buffer_rsrc((void*)pb.sorted, 0, 0xffffffff, 0x00020000);
-                const uint32_t PB = (uint32_t)P * 4u;
-                /* Row culling: a (z,y) sub-row whose box (grown by a margin m
-                 * that covers the rounding of the cell / half-cell assignment)
-                 * lies outside the sphere holds no photon within r; otherwise
-                 * only the x quarters the chord [p.x - rx, p.x + rx] (+m)
-                 * touches are walked.  The visit counters stay the reference's
-                 * (whole window, IndirectRadianceEstimation.cu:113/:124). */
-                const float m = g.cell * 1e-3f;
-                const uint32_t nsub = pb.subofs ? pb.nsub : 1u;
-                const uint32_t hs = nsub > 1 ? SUBR : 1u;
-                const float hc = g.cell / (float)hs; /* exact: hs is 1 or 2 */
-                for (uint32_t z = z_lo; z <= z_hi; z++) {
-                    for (uint32_t yy = y_lo; yy <= y_hi; yy++) {
-                        const uint32_t row = yy * g.gx + z * g.gx * g.gy;
-                        const uint32_t from = x_lo + row;
-                        const uint32_t to = from + (x_hi - x_lo);
-                        dC++;
-                        dP += pb.offsets[to + 1] - pb.offsets[from];
-                      for (uint32_t sr = 0; sr < nsub; sr++) {
-                        const uint32_t hz = z * hs + sr / hs, hy = yy * hs + sr % hs;
-                        const float zc0 = g.oz + (float)hz * hc - m, zc1 = g.oz + (float)(hz + 1) * hc + m;
-                        const float dz = fmaxf(0.f, fmaxf(zc0 - pos.z, pos.z - zc1));
-                        const float yc0 = g.oy + (float)hy * hc - m, yc1 = g.oy + (float)(hy + 1) * hc + m;
-                        const float dy = fmaxf(0.f, fmaxf(yc0 - pos.y, pos.y - yc1));
-                        const float rem = radius2 - dy * dy - dz * dz;
-                        if (rem < 0.f) continue;
-                        const float rx = sqrtf(rem) + m;
-                        const int32_t cxl = orx_f2i_sat(orx_floorf((np.x - rx) * invCellSize));
-                        const int32_t cxh = orx_f2i_sat(orx_floorf((np.x + rx) * invCellSize));
-                        const uint32_t xl = cxl > (int32_t)x_lo ? (uint32_t)cxl : x_lo;
-                        const uint32_t xh = cxh < (int32_t)x_hi ? (uint32_t)cxh : x_hi;
-                        if (cxh < 0 || xl > xh) continue;
-                        uint32_t off, offTo;
-                        if (pb.subofs) { /* x-quarter trimming of the chord's end cells */
-                            const float sx = invCellSize * (float)SUBX;
-                            const int32_t q0 = orx_f2i_sat(orx_floorf((np.x - rx) * sx));
-                            const int32_t q1 = orx_f2i_sat(orx_floorf((np.x + rx) * sx));
-                            const uint32_t a0 = q0 > (int32_t)(SUBX * xl) ? (uint32_t)q0 : SUBX * xl;
-                            const uint32_t a1 = q1 < (int32_t)(SUBX * xh + SUBX - 1) ? (uint32_t)q1 : SUBX * xh + SUBX - 1;
-                            if (q1 < 0 || a0 > a1) continue;
-                            const uint32_t* so = pb.subofs + ((size_t)(yy + z * g.gy) * nsub + sr) * g.gx * SUBX;
-                            off = so[a0];
-                            offTo = so[a1 + 1];
-                        } else {
-                            off = pb.offsets[xl + row];
-                            offTo = pb.offsets[xh + row + 1];
-                        }
-                        ORX_TS_INC(ts_leaves, 1);
-                        ORX_TS_WAVE(ts_wl);
-                        /* batches start at `off` itself (dword-aligned dwordx4 loads), so only
-                         * the last batch of a range can hold photons past its end; the loads
-                         * address nine uniform plane bases with one 32-bit byte offset */
-                        const uint32_t e1 = offTo - 1, e2 = offTo - 2, e3 = offTo - 3;
-                        for (uint32_t kb = off; kb < offTo; kb += 4) {
-                            ORX_TS_INC(ts_nodes, 1);
-                            ORX_TS_WAVE(ts_wn);
-                            const uint32_t bo = kb << 2;
-                            const f4u X = ldp(SR, 0u, bo), Y = ldp(SR, PB, bo), Z = ldp(SR, 2u * PB, bo);
-                            const v2f dx0 = px2 - lo2(X), dx1 = px2 - hi2(X);
-                            const v2f dy0 = py2 - lo2(Y), dy1 = py2 - hi2(Y);
-                            const v2f dz0 = pz2 - lo2(Z), dz1 = pz2 - hi2(Z);
-                            const v2f d20 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
-                            const v2f d21 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
-                            bool in0 = d20.x <= radius2;
-                            bool in1 = kb < e1 && d20.y <= radius2;
-                            bool in2 = kb < e2 && d21.x <= radius2;
-                            bool in3 = kb < e3 && d21.y <= radius2;
-                            if (!(in0 | in1 | in2 | in3)) continue;
-                            const f4u DX = ldp(SR, 3u * PB, bo), DY = ldp(SR, 4u * PB, bo), DZ = ldp(SR, 5u * PB, bo);
-                            const f4u WX = ldp(SR, 6u * PB, bo), WY = ldp(SR, 7u * PB, bo), WZ = ldp(SR, 8u * PB, bo);
-                            /* dot(-dir, n) >= 0  <=>  dot(dir, n) <= 0 (negation is exact) */
-                            const v2f nd0 = (lo2(DX) * nx2 + lo2(DY) * ny2) + lo2(DZ) * nz2;
-                            const v2f nd1 = (hi2(DX) * nx2 + hi2(DY) * ny2) + hi2(DZ) * nz2;
-                            in0 = in0 && nd0.x <= 0.f;
-                            in1 = in1 && nd0.y <= 0.f;
-                            in2 = in2 && nd1.x <= 0.f;
-                            in3 = in3 && nd1.y <= 0.f;
-                            /* photonPower: alpha*(1 - (1 - exp(x)) / (1 - e^-beta)), x = -beta d^2 / 2r^2,
-                             * folded into one Horner chain w = (A + B) + x*B*p(x) with A = alpha*(1 - 1/den),
-                             * B = alpha/den, evaluated with fused multiply-adds, two photons per v_pk_fma_f32.
-                             * Rejected photons (whose x may lie outside [-beta/2, 0]) get weight 0 by
-                             * select, so their polynomial value is never used; everything accumulates
-                             * by pk_fma */
-                            const v2f x0 = d20 * kx2;
-                            const v2f x1 = d21 * kx2;
-                            v2f q0 = wc6, q1 = wc6;
-                            q0 = __builtin_elementwise_fma(q0, x0, wc5); q1 = __builtin_elementwise_fma(q1, x1, wc5);
-                            q0 = __builtin_elementwise_fma(q0, x0, wc4); q1 = __builtin_elementwise_fma(q1, x1, wc4);
-                            q0 = __builtin_elementwise_fma(q0, x0, wc3); q1 = __builtin_elementwise_fma(q1, x1, wc3);
-                            q0 = __builtin_elementwise_fma(q0, x0, wc2); q1 = __builtin_elementwise_fma(q1, x1, wc2);
-                            q0 = __builtin_elementwise_fma(q0, x0, wc1); q1 = __builtin_elementwise_fma(q1, x1, wc1);
-                            v2f w0 = __builtin_elementwise_fma(q0, x0, wc0), w1 = __builtin_elementwise_fma(q1, x1, wc0);
-                            ORX_TS_INC(ts_tris, (uint32_t)in0 + (uint32_t)in1 + (uint32_t)in2 + (uint32_t)in3);
-                            w0.x = in0 ? w0.x : 0.f;
-                            w0.y = in1 ? w0.y : 0.f;
-                            w1.x = in2 ? w1.x : 0.f;
-                            w1.y = in3 ? w1.y : 0.f;
-                            accx = __builtin_elementwise_fma(lo2(WX), w0, accx);
-                            accy = __builtin_elementwise_fma(lo2(WY), w0, accy);
-                            accz = __builtin_elementwise_fma(lo2(WZ), w0, accz);
-                            accx = __builtin_elementwise_fma(hi2(WX), w1, accx);
-                            accy = __builtin_elementwise_fma(hi2(WY), w1, accy);
-                            accz = __builtin_elementwise_fma(hi2(WZ), w1, accz);
-                        }
-                      }
-                    }
-                }
-                ax = accx.x + accx.y;
-                ay = accy.x + accy.y;
-                az = accz.x + accz.y;
-            }
+        A = hr.A[hr.li];
+        B = hr.B[hr.li];
+        Cc = hr.C[hr.li];
+    }
+    const uint32_t flags = __float_as_uint(A.w);
+    const f3 pos = mk(A.x, A.y, A.z);
+    const float radius2 = c.ppm_radius2;
+    const float radius = c.ppm_radius;
+    const float invCellSize = 1.f / g.cell;
+    const f3 np = pos - mk(g.ox, g.oy, g.oz);
+    uint32_t x_lo = 0, x_hi = 0, y_lo = 0, z_lo = 0, ny = 0, nrows = 0;
+    if (live && (flags & PRD_HIT_NON_SPECULAR) && g.G) {
+        const int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
+        const int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
+        const int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
+        x_lo = (uint32_t)(ixl > 0 ? ixl : 0);
+        y_lo = (uint32_t)(iyl > 0 ? iyl : 0);
+        z_lo = (uint32_t)(izl > 0 ? izl : 0);
+        const uint32_t ux = orx_f2u_sat((np.x + radius) * invCellSize);
+        const uint32_t uy = orx_f2u_sat((np.y + radius) * invCellSize);
+        const uint32_t uz = orx_f2u_sat((np.z + radius) * invCellSize);
+        x_hi = (g.gx - 1) < ux ? (g.gx - 1) : ux;
+        const uint32_t y_hi = (g.gy - 1) < uy ? (g.gy - 1) : uy;
+        const uint32_t z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
+        if (x_lo <= x_hi && y_lo <= y_hi && z_lo <= z_hi) {
+            ny = y_hi - y_lo + 1;
+            nrows = (z_hi - z_lo + 1) * ny;
         }
+    }
+    const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
+    const float inv2r2 = 1.0f / (2 * radius2);
+    const float invDen = 1.0f / (1 - expNegativeBeta);
+    const float kx = -beta * inv2r2;
+    const float wB = alpha * invDen, wA = alpha - wB; /* w = A + B*exp(x) */
+    const v2f kx2 = v2f{kx, kx};
+    const v2f wc6 = wB * ORX_EXPU_C6, wc5 = wB * ORX_EXPU_C5, wc4 = wB * ORX_EXPU_C4;
+    const v2f wc3 = wB * ORX_EXPU_C3, wc2 = wB * ORX_EXPU_C2, wc1 = wB * ORX_EXPU_C1;
+    const v2f wc0 = v2f{wA + wB, wA + wB};
+    v2f accx = v2f{0.f, 0.f}, accy = accx, accz = accx;
+    const v2f px2 = v2f{pos.x, pos.x}, py2 = v2f{pos.y, pos.y}, pz2 = v2f{pos.z, pos.z};
+    const v2f nx2 = v2f{B.x, B.x}, ny2 = v2f{B.y, B.y}, nz2 = v2f{B.z, B.z};
+    const int32_t nq = (int32_t)dir_q8(B.x, B.y, B.z);
+    /* SP_PLANES * splane * 4 < 4 GiB: checked on the host (resize) */
+    const __amdgpu_buffer_rsrc_t SR = __builtin_amdgcn_make_buffer_rsrc((void*)pb.sorted, 0, 0xffffffff, 0x00020000);
+    const uint32_t PB = pb.splane * 4u;
+    /* a sub-row's box grown by m (covers the rounding of the cell / half-cell
+     * assignment) that misses the sphere holds no photon within r; otherwise
+     * only the x quarters the chord [p.x - rx, p.x + rx] (+m) touches are walked */
+    const float m = g.cell * 1e-3f;
+    constexpr uint32_t HS = NSUB > 1 ? SUBR : 1u;
+    const float hc = g.cell / (float)HS; /* exact: HS is 1 or 2 */
+    uint32_t t = 0;
+    while (wave_any(t < nrows)) {
+        /* phase A: the next up to GQ non-empty chords of this lane's window, in LDS */
+        ORX_TS_WAVE(ts_wl); /* trav stats: wave-level phase-A rounds */
+        uint32_t n = 0;
+        while (t < nrows && n + NSUB <= GQ) {
+            const uint32_t zq = t / ny;
+            const uint32_t z = z_lo + zq, yy = y_lo + (t - zq * ny);
+            t++;
+            const uint32_t row = yy * g.gx + z * g.gx * g.gy;
+            const uint32_t from = x_lo + row;
+            const uint32_t to = from + (x_hi - x_lo);
+            dC++;
+            dP += pb.offsets[to + 1] - pb.offsets[from];
+            uint32_t offs[NSUB], ends[NSUB];
+#pragma unroll
+            for (uint32_t sr = 0; sr < NSUB; sr++) {
+                offs[sr] = ends[sr] = 0;
+                const uint32_t hz = z * HS + sr / HS, hy = yy * HS + sr % HS;
+                const float zc0 = g.oz + (float)hz * hc - m, zc1 = g.oz + (float)(hz + 1) * hc + m;
+                const float dz = fmaxf(0.f, fmaxf(zc0 - pos.z, pos.z - zc1));
+                const float yc0 = g.oy + (float)hy * hc - m, yc1 = g.oy + (float)(hy + 1) * hc + m;
+                const float dy = fmaxf(0.f, fmaxf(yc0 - pos.y, pos.y - yc1));
+                const float rem = radius2 - dy * dy - dz * dz;
+                if (rem < 0.f) continue;
+                const float rx = sqrtf(rem) + m;
+                const int32_t cxl = orx_f2i_sat(orx_floorf((np.x - rx) * invCellSize));
+                const int32_t cxh = orx_f2i_sat(orx_floorf((np.x + rx) * invCellSize));
+                const uint32_t xl = cxl > (int32_t)x_lo ? (uint32_t)cxl : x_lo;
+                const uint32_t xh = cxh < (int32_t)x_hi ? (uint32_t)cxh : x_hi;
+                if (cxh < 0 || xl > xh) continue;
+                if (SUBOFS) { /* x-quarter trimming of the chord's end cells */
+                    const float sx = invCellSize * (float)SUBX;
+                    const int32_t q0 = orx_f2i_sat(orx_floorf((np.x - rx) * sx));
+                    const int32_t q1 = orx_f2i_sat(orx_floorf((np.x + rx) * sx));
+                    const uint32_t a0 = q0 > (int32_t)(SUBX * xl) ? (uint32_t)q0 : SUBX * xl;
+                    const uint32_t a1 = q1 < (int32_t)(SUBX * xh + SUBX - 1) ? (uint32_t)q1 : SUBX * xh + SUBX - 1;
+                    if (q1 < 0 || a0 > a1) continue;
+                    const uint32_t* so = pb.subofs + ((size_t)(yy + z * g.gy) * NSUB + sr) * g.gx * SUBX;
+                    offs[sr] = so[a0];
+                    ends[sr] = so[a1 + 1];
+                } else {
+                    offs[sr] = pb.offsets[xl + row];
+                    ends[sr] = pb.offsets[xh + row + 1];
+                }
+            }
+#pragma unroll
+            for (uint32_t sr = 0; sr < NSUB; sr++)
+                if (ends[sr] > offs[sr]) rq[n++][tid] = make_uint2(offs[sr], ends[sr]);
+        }
+        /* phase B: one flat stream of batches over the collected chords */
+        uint32_t k = 0, kb = 0, kend = 0;
+        for (;;) {
+            while (kb >= kend && k < n) {
+                const uint2 r = rq[k++][tid];
+                kb = r.x;
+                kend = r.y;
+                ORX_TS_INC(ts_leaves, 1);
+            }
+            const bool has = kb < kend;
+            if (!wave_any(has)) break;
+            if (!has) continue;
+            ORX_TS_INC(ts_nodes, 1);
+            ORX_TS_WAVE(ts_wn);
+            const uint32_t bo = kb << 2;
+            const f4u X = ldp(SR, SP_X * PB, bo), Y = ldp(SR, SP_Y * PB, bo), Z = ldp(SR, SP_Z * PB, bo);
+            const v2f dx0 = px2 - lo2(X), dx1 = px2 - hi2(X);
+            const v2f dy0 = py2 - lo2(Y), dy1 = py2 - hi2(Y);
+            const v2f dz0 = pz2 - lo2(Z), dz1 = pz2 - hi2(Z);
+            const v2f d20 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
+            const v2f d21 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
+            bool in0 = d20.x <= radius2;
+            bool in1 = kb + 1 < kend && d20.y <= radius2;
+            bool in2 = kb + 2 < kend && d21.x <= radius2;
+            bool in3 = kb + 3 < kend && d21.y <= radius2;
+            kb += 4;
+            if (!(in0 | in1 | in2 | in3)) continue;
+            /* facing: dot(-dir, n) >= 0  <=>  dot(dir, n) <= 0 (negation is exact) */
+            const u4v Q = __builtin_amdgcn_raw_buffer_load_b128(SR, (int)bo, (int)(SP_DIRQ * PB), 0);
+            const int32_t q0 = __builtin_amdgcn_sdot4((int32_t)Q.x, nq, 0, false);
+            const int32_t q1 = __builtin_amdgcn_sdot4((int32_t)Q.y, nq, 0, false);
+            const int32_t q2 = __builtin_amdgcn_sdot4((int32_t)Q.z, nq, 0, false);
+            const int32_t q3 = __builtin_amdgcn_sdot4((int32_t)Q.w, nq, 0, false);
+            in0 = in0 && q0 <= DIRQ_BAND;
+            in1 = in1 && q1 <= DIRQ_BAND;
+            in2 = in2 && q2 <= DIRQ_BAND;
+            in3 = in3 && q3 <= DIRQ_BAND;
+            const bool u0 = in0 && q0 >= -DIRQ_BAND, u1 = in1 && q1 >= -DIRQ_BAND;
+            const bool u2 = in2 && q2 >= -DIRQ_BAND, u3 = in3 && q3 >= -DIRQ_BAND;
+            if (u0 | u1 | u2 | u3) { /* inside the band: the exact test */
+                const f4u DX = ldp(SR, SP_DX * PB, bo), DY = ldp(SR, SP_DY * PB, bo), DZ = ldp(SR, SP_DZ * PB, bo);
+                const v2f nd0 = (lo2(DX) * nx2 + lo2(DY) * ny2) + lo2(DZ) * nz2;
+                const v2f nd1 = (hi2(DX) * nx2 + hi2(DY) * ny2) + hi2(DZ) * nz2;
+                in0 = in0 && (!u0 || nd0.x <= 0.f);
+                in1 = in1 && (!u1 || nd0.y <= 0.f);
+                in2 = in2 && (!u2 || nd1.x <= 0.f);
+                in3 = in3 && (!u3 || nd1.y <= 0.f);
+            }
+            if (!(in0 | in1 | in2 | in3)) continue;
+            const f4u WX = ldp(SR, SP_PX * PB, bo), WY = ldp(SR, SP_PY * PB, bo), WZ = ldp(SR, SP_PZ * PB, bo);
+            /* photonPower: alpha*(1 - (1 - exp(x)) / (1 - e^-beta)), x = -beta d^2 / 2r^2,
+             * folded into one Horner chain w = (A + B) + x*B*p(x) with A = alpha*(1 - 1/den),
+             * B = alpha/den, evaluated with fused multiply-adds, two photons per v_pk_fma_f32.
+             * Rejected photons (whose x may lie outside [-beta/2, 0]) get weight 0 by
+             * select, so their polynomial value is never used */
+            const v2f x0 = d20 * kx2;
+            const v2f x1 = d21 * kx2;
+            v2f p0 = wc6, p1 = wc6;
+            p0 = __builtin_elementwise_fma(p0, x0, wc5); p1 = __builtin_elementwise_fma(p1, x1, wc5);
+            p0 = __builtin_elementwise_fma(p0, x0, wc4); p1 = __builtin_elementwise_fma(p1, x1, wc4);
+            p0 = __builtin_elementwise_fma(p0, x0, wc3); p1 = __builtin_elementwise_fma(p1, x1, wc3);
+            p0 = __builtin_elementwise_fma(p0, x0, wc2); p1 = __builtin_elementwise_fma(p1, x1, wc2);
+            p0 = __builtin_elementwise_fma(p0, x0, wc1); p1 = __builtin_elementwise_fma(p1, x1, wc1);
+            v2f w0 = __builtin_elementwise_fma(p0, x0, wc0), w1 = __builtin_elementwise_fma(p1, x1, wc0);
+            ORX_TS_INC(ts_tris, (uint32_t)in0 + (uint32_t)in1 + (uint32_t)in2 + (uint32_t)in3);
+            w0.x = in0 ? w0.x : 0.f;
+            w0.y = in1 ? w0.y : 0.f;
+            w1.x = in2 ? w1.x : 0.f;
+            w1.y = in3 ? w1.y : 0.f;
+            accx = __builtin_elementwise_fma(lo2(WX), w0, accx);
+            accy = __builtin_elementwise_fma(lo2(WY), w0, accy);
+            accz = __builtin_elementwise_fma(lo2(WZ), w0, accz);
+            accx = __builtin_elementwise_fma(hi2(WX), w1, accx);
+            accy = __builtin_elementwise_fma(hi2(WY), w1, accy);
+            accz = __builtin_elementwise_fma(hi2(WZ), w1, accz);
+        }
+    }
+    if (live) {
+        const float ax = accx.x + accx.y, ay = accy.x + accy.y, az = accz.x + accz.y;
         const f3 att = mk(B.w, Cc.x, Cc.y);
         const float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
         const float s2 = 1.0f / c.emitted_f;
@@ -1411,8 +1487,14 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
 
 void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, size_t lds_pad) {
     const uint32_t rows = gi.segments * gi.seg_rows;
-    dim3 grid((gi.W + 15) / 16, (rows + 15) / 16);
-    hipLaunchKernelGGL(k_ppm_gather, grid, dim3(256), lds_pad, s, gi, pb, c);
+    const uint32_t ntx = (gi.W + 15) / 16, nty = (rows + 15) / 16, ntiles = ntx * nty;
+    const dim3 grid(8 * ((ntiles + 7) / 8));
+    if (!pb.subofs)
+        hipLaunchKernelGGL((k_ppm_gather<1, false>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx, ntiles);
+    else if (pb.nsub == 1)
+        hipLaunchKernelGGL((k_ppm_gather<1, true>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx, ntiles);
+    else
+        hipLaunchKernelGGL((k_ppm_gather<SUBR * SUBR, true>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx, ntiles);
 }
 
 /* ------------------------------------------------------------------ */

@@ -1,0 +1,148 @@
+"""GPU parity at the BASELINE workloads' full sizes (BASELINE.json configs[0]-[3]).
+
+The parity tests in test_gpu_parity.py run toy sizes (<= 96x80 pixels, <= 128^2
+photons).  These run the bench's own workloads through liborx.so and the CPU
+oracle on the same seeds, so the multi-chunk bucket sort, the full 1e6-cell
+grid, the 2M-pixel gather and the full light-vertex cache are compared at the
+sizes bench.py times:
+
+  configs[0]  Cornell 256x256 PT, 1 spp                 output + RNG bit-exact
+  configs[1]  Cornell 1024x1024 PPM, 1024^2 photons      two iterations (radius update)
+  configs[2]  hall 1920x1080 PPM, 2048^2 photons         two iterations
+  configs[3]  hall 1920x1080 VCM                         first iteration (incl. the LVC estimate launch)
+
+Bars (north_star; same as check_ppm_iteration / check_vcm_iteration): RNG,
+hit points, grid offsets, per-cell photon multisets, direct light, visit
+counters, VCM vertex counts / light vertices / camera colours bit-exact;
+indirect and splats rel-L2 <= 1e-5 (summation order); output rel-L2 <= 1e-4.
+The oracle runs on the box's host cores (OMP_NUM_THREADS).
+"""
+import numpy as np
+import pytest
+
+import oracle_lib
+from oppositerenderer_amd import _abi, scenes, synthetic
+from oppositerenderer_amd.renderer import OptixRenderer, RenderRequestDetails, next_ppm_radius
+
+pytestmark = pytest.mark.gpu
+SEED = 1645301512
+
+
+def rel_l2(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.sqrt(((a - b) ** 2).sum()) / max(np.sqrt((b * b).sum()), 1e-30))
+
+
+def cell_sorted_photons(photons, offsets):
+    """Grid-ordered photons [n, 9] with each cell's rows put in a canonical
+    order (by a 64-bit hash of the row, then the row words): equal arrays
+    <=> every cell holds the same multiset of photons."""
+    rows = np.ascontiguousarray(photons.view(np.uint32).reshape(-1, 9))
+    off = offsets.astype(np.int64)
+    n = int(off[-1] - off[0])
+    assert rows.shape[0] == n, (rows.shape, n)
+    cell = np.repeat(np.arange(len(off) - 1, dtype=np.int64), np.diff(off))
+    h = np.zeros(n, np.uint64)
+    with np.errstate(over="ignore"):
+        for k in range(9):
+            h = (h * np.uint64(0x100000001B3)) ^ rows[:, k].astype(np.uint64)
+    order = np.lexsort(tuple(rows[:, k] for k in range(8, -1, -1)) + (h, cell))
+    return rows[order]
+
+
+def assert_same(gpu, ora, buf, what=None):
+    g, o = gpu.read_buffer(buf, np.uint32), ora.read_buffer(buf, np.uint32)
+    assert g.shape == o.shape, (what or buf, g.shape, o.shape)
+    mism = np.count_nonzero(g != o)
+    assert mism == 0, f"{what or buf}: {mism} of {g.size} words differ"
+
+
+def check_ppm_full(gpu, ora):
+    for buf, name in ((_abi.BUF_RNG, "rng"), (_abi.BUF_HITPOINTS, "hitpoints"), (_abi.BUF_GRID_OFFSETS, "offsets"),
+                      (_abi.BUF_DIRECT, "direct"), (_abi.BUF_DEBUG_VISITED, "visit counters")):
+        assert_same(gpu, ora, buf, name)
+    gs, os_ = gpu.stats(), ora.stats()
+    assert list(gs.grid_size) == list(os_.grid_size)
+    assert np.float32(gs.cell_size) == np.float32(os_.cell_size)
+    assert gs.valid_photons == os_.valid_photons
+    assert gs.photons_visited == os_.photons_visited
+    off = gpu.read_buffer(_abi.BUF_GRID_OFFSETS, np.uint32)
+    gp = cell_sorted_photons(gpu.read_buffer(_abi.BUF_PHOTONS), off)
+    op = cell_sorted_photons(ora.read_buffer(_abi.BUF_PHOTONS), off)
+    assert np.array_equal(gp, op), "per-cell photon multisets differ"
+    gi, oi = gpu.read_buffer(_abi.BUF_INDIRECT), ora.read_buffer(_abi.BUF_INDIRECT)
+    assert rel_l2(gi, oi) < 1e-5, rel_l2(gi, oi)
+    np.testing.assert_allclose(gi, oi, rtol=1e-4, atol=1e-6)
+
+
+def pair(scene, W, H, P, method):
+    cfg = _abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P)
+    gpu = OptixRenderer(cfg)
+    gpu.initialize(0)
+    gpu.initScene(scene)
+    ora = oracle_lib.OracleRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P))
+    ora.init_scene(scene)
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    return gpu, ora, RenderRequestDetails(cam, scene.name, method, W, H)
+
+
+def test_configs0_cornell256_pt():
+    scene = scenes.cornell()
+    gpu, ora, det = pair(scene, 256, 256, 1024, _abi.PATH_TRACING)
+    for it in range(2):
+        gpu.renderNextIteration(it, it, 1.0, True, det)
+        ora.render_next_iteration(it, it, 1.0, det.to_abi())
+        assert_same(gpu, ora, _abi.BUF_RNG, "rng")
+    g, o = gpu.getOutputBuffer(), ora.output()
+    assert g.mean() > 0
+    assert np.array_equal(g.view(np.uint32), o.view(np.uint32)), rel_l2(g, o)
+    gpu.destroy()
+    ora.close()
+
+
+@pytest.mark.parametrize("which", ["configs1_cornell1024_ppm", "configs2_hall1080p_ppm"])
+def test_full_size_ppm(which):
+    if which.startswith("configs1"):
+        scene, W, H, P = scenes.cornell(), 1024, 1024, 1024
+    else:
+        scene, W, H, P = synthetic.synthetic_hall(), 1920, 1080, 2048
+    gpu, ora, det = pair(scene, W, H, P, _abi.PROGRESSIVE_PHOTON_MAPPING)
+    radius = scene.initial_ppm_radius()
+    for it in range(2):
+        gpu.renderNextIteration(it, it, radius, True, det)
+        ora.render_next_iteration(it, it, radius, det.to_abi())
+        check_ppm_full(gpu, ora)
+        radius = next_ppm_radius(radius, it)
+    g, o = gpu.getOutputBuffer(), ora.output()
+    assert g.mean() > 0
+    assert rel_l2(g, o) < 1e-4, rel_l2(g, o)
+    gpu.destroy()
+    ora.close()
+
+
+def test_configs3_hall1080p_vcm():
+    scene = synthetic.synthetic_hall()
+    W, H = 1920, 1080
+    gpu, ora, det = pair(scene, W, H, 64, _abi.VCM_BIDIRECTIONAL_PATH_TRACING)
+    radius = scene.initial_ppm_radius()
+    gpu.renderNextIteration(0, 0, radius, True, det)
+    ora.render_next_iteration(0, 0, radius, det.to_abi())
+    for buf, name in ((_abi.BUF_RNG, "rng"), (_abi.BUF_VCM_VERTEX_COUNT, "vertex counts"),
+                      (_abi.BUF_VCM_CAMERA, "camera colours")):
+        assert_same(gpu, ora, buf, name)
+    cnt = np.minimum(gpu.read_buffer(_abi.BUF_VCM_VERTEX_COUNT, np.uint32), 9)
+    assert cnt.sum() > W * H // 2
+    gv = gpu.read_buffer(_abi.BUF_VCM_VERTICES, np.uint32).reshape(9, -1, 16)  # 9 x W*H x 64 B
+    ov = ora.read_buffer(_abi.BUF_VCM_VERTICES, np.uint32).reshape(9, -1, 16)
+    for k in range(9):  # one vertex level at a time: only stored vertices are defined
+        sel = cnt > k
+        assert np.array_equal(gv[k][sel], ov[k][sel]), f"light vertices of level {k} differ"
+    del gv, ov
+    gs, os_ = gpu.read_buffer(_abi.BUF_VCM_SPLAT), ora.read_buffer(_abi.BUF_VCM_SPLAT)
+    assert rel_l2(gs, os_) < 1e-5, rel_l2(gs, os_)
+    g, o = gpu.getOutputBuffer(), ora.output()
+    assert np.isfinite(g).all() and g.mean() > 0
+    assert rel_l2(g, o) < 1e-4, rel_l2(g, o)
+    gpu.destroy()
+    ora.close()
