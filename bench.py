@@ -3,21 +3,27 @@
 ms/frame on MI355X, with a live HBM-roofline figure for the dominant kernel and
 the CPU oracle timed on the host cores beside it.
 
-Workload: the metric's own configuration, "1080p Sponza PPM" (BASELINE.json
-configs[2]): the seeded synthetic Sponza-class hall
-(oppositerenderer_amd/synthetic.py, 261,120 triangles, one quad area light),
-1920x1080, PPM with a 2048x2048 photon launch (4,194,304 emitted photons,
-<= 4 deposits each), r0 = IScene::getSceneInitialPPMRadiusEstimate,
-alpha = 2/3, seed 1645301512.  paths/iteration = W*H eye paths + emitted
-photon paths.  --scene Cornell --width 1024 --height 1024
---photon-launch 1024 gives configs[1]; --method vcm gives configs[3].
+Workloads (--config, BASELINE.json "configs"; SURVEY 8(d) C1-C5, synthetic
+stand-ins for the absent Sponza/Conference assets):
+  0  Cornell 256x256, PT, 1 spp
+  1  Cornell 1024x1024, PPM, 1024^2 = 1,048,576 photons/iter
+  2  SyntheticHall 1920x1080, PPM, 2048^2 = 4,194,304 photons/iter   <- default: the metric's
+     "1080p Sponza PPM" (261,120 triangles, one quad area light)
+  3  SyntheticHall 1920x1080, VCM
+  4  SyntheticConference 3840x2160, PPM, 4096^2 = 16,777,216 photons/iter
+PPM: r0 = IScene::getSceneInitialPPMRadiusEstimate, alpha = 2/3, seed
+1645301512; paths/iteration = W*H eye paths + emitted photon paths.
+--scene/--width/--height/--photon-launch/--method override the config's values.
 
-Single GPU:  python bench.py [--steps K --warmup W]
-Multi GPU:   torchrun --nproc-per-node N bench.py --gpus N   (one rank per GPU;
-             see DESIGN.md "Multi-GPU" for the sharding and the RCCL exchange)
+Single GPU:  python bench.py [--config C] [--steps K --warmup W]
+Multi GPU:   torchrun --nproc-per-node N bench.py --gpus N   (one rank per GPU, RCCL).
+             Default --scaling strong: the workload is fixed (its photon launch rows and
+             pixel rows are dealt round-robin to the ranks); --scaling weak gives every
+             rank a full photon launch.  See DESIGN.md "Multi-GPU".
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -29,60 +35,126 @@ import numpy as np  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 
+CONFIGS = {
+    0: dict(scene="Cornell", width=256, height=256, method="pt", photon_launch=1024),
+    1: dict(scene="Cornell", width=1024, height=1024, method="ppm", photon_launch=1024),
+    2: dict(scene="SyntheticHall", width=1920, height=1080, method="ppm", photon_launch=2048),
+    3: dict(scene="SyntheticHall", width=1920, height=1080, method="vcm", photon_launch=2048),
+    4: dict(scene="SyntheticConference", width=3840, height=2160, method="ppm", photon_launch=4096),
+}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=32)
     p.add_argument("--warmup", type=int, default=4)
-    p.add_argument("--width", type=int, default=1920)
-    p.add_argument("--height", type=int, default=1080)
-    p.add_argument("--photon-launch", type=int, default=2048)
-    p.add_argument("--scene", default="SyntheticHall")
-    p.add_argument("--method", choices=["ppm", "vcm", "pt"], default="ppm")
+    p.add_argument("--config", type=int, choices=sorted(CONFIGS), default=2,
+                   help="BASELINE.json configs[i] (2 = the metric's 1080p Sponza-class PPM)")
+    p.add_argument("--width", type=int)
+    p.add_argument("--height", type=int)
+    p.add_argument("--photon-launch", type=int)
+    p.add_argument("--scene")
+    p.add_argument("--method", choices=["ppm", "vcm", "pt"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=20.0)
     p.add_argument("--gather-variant", type=int, default=0)
     p.add_argument("--photon-map", choices=["grid", "hash", "kd"], default="grid",
                    help="uniform grid (the reference's shipped configuration), stochastic hash (single GPU) "
                         "or kd-tree (ACCELERATION_STRUCTURE_KD_TREE_CPU, built on the device)")
+    p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                   help="multi-GPU PPM: strong = fixed global photon launch split by rows over the ranks "
+                        "(the default); weak = a full photon launch per rank")
     p.add_argument("--force-sharded", action="store_true",
                    help="run the torch.distributed/RCCL sharded path even with one rank (tests the N>1 code)")
-    return p.parse_args()
+    p.add_argument("--no-serial-pass-times", action="store_true",
+                   help="skip the few serial (unpipelined) iterations after the timed region that give each "
+                        "pass's stand-alone time")
+    a = p.parse_args(argv)
+    for k, v in CONFIGS[a.config].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    return a
 
 
 METHODS = {"ppm": 2, "vcm": 1, "pt": 0}  # orx_method (include/orx.h)
+PHOTON_MAPS = {"grid": 0, "hash": 1, "kd": 2}  # orx_config.photon_map
+_METHOD_NAME = {0: "PT", 1: "VCM", 2: "PPM"}
 
 
 def traffic_lookup(key, kernels):
     """PMC-measured HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, the gfx950
     correction of MI355X_MICROARCH.md) recorded by tools/profile_traffic.py for
     this exact workload, or None."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
-        table = json.load(open(path)).get(key, {})
+        table = json.load(open(os.path.join(ROOT, "profiles", "traffic.json"))).get(key, {})
     except (OSError, ValueError):
         return None
     vals = [table[k]["bytes_per_launch"] for k in kernels if k in table]
     return int(sum(vals)) if vals else None
 
 
-PHOTON_MAPS = {"grid": 0, "hash": 1, "kd": 2}  # orx_config.photon_map
+def bound_lookup(key, kernels):
+    """What bounds the kernel, from the committed PMC passes (profiles/bound.json, written by
+    tools/pmc_bound.py): VALU issue, the vector-memory address path (TA) or HBM."""
+    try:
+        table = json.load(open(os.path.join(ROOT, "profiles", "bound.json"))).get(key, {})
+    except (OSError, ValueError):
+        return None
+    for k in kernels:
+        if k in table:
+            return table[k]
+    return None
+
+
+def host_cpu():
+    """Threads the CPU baseline may use on this host and what they are: the process's CPU
+    affinity, capped by a cgroup CPU quota and by OMP_NUM_THREADS when either is set (on the
+    GPU box the harness grants one GPU's share of the node's cores and says so through
+    OMP_NUM_THREADS)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            quota = q / per if q > 0 else None
+        except (OSError, ValueError):
+            pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    threads = aff
+    if quota:
+        threads = min(threads, max(1, int(math.floor(quota))))
+    if omp:
+        threads = min(threads, omp)
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return threads, {"affinity_cpus": aff, "cgroup_cpu_quota": quota, "omp_num_threads": omp,
+                     "node_cpus": os.cpu_count(), "model": model}
 
 
 def cpu_baseline(scene, method, W, H, P, seconds, photon_map=0):
-    """Oracle (oracle/liborx_oracle.so: the C/OpenMP restatement of the
-    reference passes) on the host cores, same scene, resolution, photon count
-    and seed as the GPU line: one untimed warm-up iteration (allocation, RNG
-    init, VCM estimate launch), then timed iterations until `seconds` of CPU
-    wall time are spent (at least one, at most 8); median."""
+    """Oracle (oracle/liborx_oracle.so: the C/OpenMP restatement of the reference
+    passes) on the host cores, same scene, resolution, photon count and seed as
+    the GPU line.  Iterations 0, 1, ... are timed (iteration 0 includes the RNG
+    initialisation and, for VCM, the light-subpath estimate launch) until
+    `seconds` of CPU wall time are spent (at least one, at most 8); median."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     from oppositerenderer_amd import _abi, roofline
     from oppositerenderer_amd.renderer import next_ppm_radius
 
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    cores, info = host_cpu()
     lib = oracle_lib.load()
     lib.orc_set_threads(cores)
     cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
@@ -94,12 +166,10 @@ def cpu_baseline(scene, method, W, H, P, seconds, photon_map=0):
     r = oracle_lib.OracleRenderer(cfg)
     r.init_scene(scene)
     radius = scene.initial_ppm_radius()
-    r.render_next_iteration(0, 0, radius, req)
-    radius = next_ppm_radius(radius, 0)
     times = []
     t_start = time.perf_counter()
-    it = 1
-    while it <= 8 and (it == 1 or (time.perf_counter() - t_start) < seconds):
+    it = 0
+    while it < 8 and (it == 0 or (time.perf_counter() - t_start) < seconds):
         t0 = time.perf_counter()
         r.render_next_iteration(it, it, radius, req)
         times.append(time.perf_counter() - t0)
@@ -109,13 +179,34 @@ def cpu_baseline(scene, method, W, H, P, seconds, photon_map=0):
     t = float(np.median(times))
     paths = roofline.paths_per_iteration(method, W, H, P * P)
     return {"value": round(paths / t / 1e6, 3), "unit": "Mpaths/s", "cores": cores, "kind": "port",
-            "ms_per_step": round(t * 1e3, 2),
-            "sample": f"oracle (C/OpenMP restatement, {cores} threads) on the full workload: {scene.name} {W}x{H} "
-                      f"{_METHOD_NAME[method]}" + (f", {P * P} photons/iter" if method == 2 else "") +
-                      f"; median of {len(times)} iteration(s) after 1 warm-up"}
+            "ms_per_step": round(t * 1e3, 2), "value_per_core": round(paths / t / 1e6 / cores, 4),
+            "host": info,
+            "sample": f"oracle (C/OpenMP restatement of the reference passes, {cores} threads) on the full "
+                      f"workload: {scene.name} {W}x{H} {_METHOD_NAME[method]}"
+                      + (f", {P * P} photons/iter" if method == 2 else "") +
+                      f"; median of {len(times)} iteration(s) from iteration 0"}
 
 
-_METHOD_NAME = {0: "PT", 1: "VCM", 2: "PPM"}
+def roofline_block(pass_ms, pbytes, key, photon_map, serial_ms=None, overlapped=()):
+    """The roofline entry for the kernel with the largest measured time per launch in the timed
+    schedule (what rocprofv3 --stats shows dominant), with its stand-alone (serial) time when the
+    schedule overlaps it with other passes."""
+    from oppositerenderer_amd import roofline
+    dominant = max(pass_ms, key=pass_ms.get)
+    kernels = roofline.kernels_of(dominant, photon_map)
+    roof = roofline.roofline(dominant, pbytes[dominant], pass_ms[dominant], traffic_lookup(key, kernels),
+                             photon_map=photon_map)
+    b = bound_lookup(key, kernels)
+    if b:
+        roof.update(b)
+    else:
+        roof["bound"] = "unmeasured"
+    roof["overlapped"] = dominant in overlapped
+    if serial_ms and dominant in serial_ms:
+        roof["serial_ms"] = round(serial_ms[dominant], 4)
+        roof["serial_achieved"] = round(pbytes[dominant] / (serial_ms[dominant] * 1e-3) / 1e9, 1)
+        roof["serial_frac"] = round(roof["serial_achieved"] / roofline.HBM_PEAK_GBS, 5)
+    return dominant, roof
 
 
 def main():
@@ -124,7 +215,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus > 1 or world > 1 or args.force_sharded:
         from oppositerenderer_amd import multigpu
-        return multigpu.bench_main(args, METRIC)
+        return multigpu.bench_main(args, METRIC, cpu_baseline=None if args.no_cpu_baseline else cpu_baseline)
 
     from oppositerenderer_amd import _abi, roofline, scenes
     from oppositerenderer_amd.renderer import OptixRenderer, RenderRequestDetails, next_ppm_radius
@@ -132,9 +223,9 @@ def main():
     method = METHODS[args.method]
     W, H, P = args.width, args.height, args.photon_launch
     scene = scenes.scene_by_name(args.scene)
+    pmap = PHOTON_MAPS[args.photon_map]
     cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P,
-                              gather_variant=args.gather_variant,
-                              photon_map=PHOTON_MAPS[args.photon_map])
+                              gather_variant=args.gather_variant, photon_map=pmap)
     r = OptixRenderer(cfg)
     r.initialize(local_rank)
     r.initScene(scene)
@@ -153,7 +244,7 @@ def main():
         r.renderNextIteration(it, it, radius, False, det)
         radius = next_ppm_radius(radius, it)
         it += 1
-    st = r.stats()  # synchronises
+    st = r.stats()  # synchronises (the last iteration's deferred gather included)
     wall = time.perf_counter() - t0
     ms_per_step = wall * 1e3 / args.steps
     paths = roofline.paths_per_iteration(method, W, H, P * P)
@@ -163,41 +254,59 @@ def main():
     per_pass = {name: st.pass_ms[i] / n_it for i, name in enumerate(_abi.PASS_NAMES)}
     per_pass = {k: v for k, v in per_pass.items() if v > 0}
     # pipelined PPM: the gather and output run on a side stream beside the next iteration's
-    # passes, so their times are overlapped wall time; the roofline names the longest pass on
-    # the critical chain (eye -> photon -> grid)
+    # passes, so every pass time is wall time under interference; a few serial iterations after
+    # the timed region give each pass's stand-alone time
     pipelined = method == _abi.PROGRESSIVE_PHOTON_MAPPING and r.pipelined()
     overlapped = ["ppm_gather", "ppm_direct_output"] if pipelined else []
-    critical = {k: v for k, v in per_pass.items() if k not in overlapped} or per_pass
-    dominant = max(critical, key=critical.get)
+    serial = None
+    if pipelined and not args.no_serial_pass_times:
+        r.set_iteration_pipelining(0)
+        for k in range(4):
+            if k == 1:
+                r.stats()
+                r.reset_timing()
+            r.renderNextIteration(it, it, radius, False, det)
+            radius = next_ppm_radius(radius, it)
+            it += 1
+        ss = r.stats()
+        sn = max(1, ss.timed_iterations)
+        serial = {name: ss.pass_ms[i] / sn for i, name in enumerate(_abi.PASS_NAMES) if ss.pass_ms[i] > 0}
+        r.set_iteration_pipelining(-1)
     valid_avg = st.valid_photons_total / n_it
     light_vertices = 0
     if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING:
         light_vertices = int(np.minimum(r.read_buffer(_abi.BUF_VCM_VERTEX_COUNT, np.uint32), 9).sum())
-    pmap = PHOTON_MAPS[args.photon_map]
     pbytes = roofline.pass_bytes(method, W, H, P * P, valid_avg, st.num_cells, light_vertices, photon_map=pmap)
     key = (f"{scene.name}:{W}x{H}:{args.method}" + (f":P{P}" if method == 2 else "")
            + (f":{args.photon_map}" if pmap else ""))
-    traffic = traffic_lookup(key, roofline.kernels_of(dominant, pmap))
-    roof = roofline.roofline(dominant, pbytes[dominant], per_pass[dominant], traffic, photon_map=pmap)
+    dominant, roof = roofline_block(per_pass, pbytes, key, pmap, serial, overlapped)
+    if pipelined:
+        chain = {k: round(v, 4) for k, v in per_pass.items() if k not in overlapped}
+        roof["critical_chain_ms"] = chain
     passes = {k: {"ms": round(v, 4), "algorithmic_GBps": round(pbytes.get(k, 0) / (v * 1e-3) / 1e9, 1)}
               for k, v in per_pass.items()}
+    if serial:
+        for k, v in serial.items():
+            if k in passes:
+                passes[k]["serial_ms"] = round(v, 4)
     if method == _abi.PROGRESSIVE_PHOTON_MAPPING:
-        gms = per_pass.get("ppm_gather", 0.0)
         visited = st.photons_visited_total / n_it
+        gms = (serial or per_pass).get("ppm_gather", 0.0)
         roof["gather_visited_photons_per_launch"] = int(visited)
         roof["gather_visited_photon_GBps"] = round(visited * 36 / (gms * 1e-3) / 1e9, 1) if gms > 0 else None
     data = ("synthetic: seeded procedural scene (" + scene.name + "), XORWOW streams seeded 1645301512; "
             "no assets or checkpoints")
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mpaths/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f32", "data": data,
         "config": {"workload": f"{scene.name} {W}x{H} {_METHOD_NAME[method]}"
                                + (f", {P * P} photons/iter" if method == 2 else ""),
+                   "baseline_config": args.config,
                    "scene": scene.name, "width": W, "height": H, "method": _METHOD_NAME[method],
                    "photons_per_iteration": P * P if method == 2 else 0, "paths_per_iteration": paths,
                    "photon_map": {"grid": "uniform grid", "hash": "stochastic hash", "kd": "kd-tree"}[args.photon_map],
-                   "parallelism": "single GPU"},
+                   "pipelined": bool(pipelined), "parallelism": "single GPU"},
         "roofline": roof,
         "passes": passes,
         "dominant_pass": dominant,
@@ -205,8 +314,7 @@ def main():
     }
     if not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(scene, method, W, H, P, args.cpu_seconds,
-                                               photon_map=PHOTON_MAPS[args.photon_map])
+            out["cpu_baseline"] = cpu_baseline(scene, method, W, H, P, args.cpu_seconds, photon_map=pmap)
         except Exception as e:  # the baseline must never hide the GPU line
             out["cpu_baseline"] = {"error": repr(e)}
     r.destroy()

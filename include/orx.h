@@ -257,6 +257,10 @@ orx_status orx_reset_timing(orx_renderer* r);
  * output half of ORX_PASS_PPM_DIRECT) on a second stream beside the next iteration's eye, photon and
  * grid passes, so their pass_ms are overlapped wall time; 0 otherwise */
 int orx_ppm_pipelined(const orx_renderer* r);
+/* Single-device PPM iteration pipelining: 1 on, 0 off (serial passes), -1 the ORX_PIPELINE
+ * environment default (on).  Takes effect at the next iteration (an outstanding pipelined
+ * iteration is finished first); images are identical either way. */
+orx_status orx_set_iteration_pipelining(orx_renderer* r, int mode);
 
 /* ---- Multi-GPU sharding ----
  * Rank `rank` of `world` owns every RNG-slot row y with y % world == rank:

@@ -363,6 +363,7 @@ struct orx_renderer {
     bool pipe_bufs = false, pend = false, last_pipelined = false;
     /* sharded PPM pipelining (orx_set_ppm_pipeline): gather + finish on the caller's side stream */
     bool shard_pipe = false;
+    int pipe_mode = -1; /* orx_set_iteration_pipelining: -1 = ORX_PIPELINE env */
     hipStream_t side = nullptr;
     uint32_t pp = 0;
     std::string err;
@@ -1454,7 +1455,8 @@ orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
         return e ? atoi(e) : 1;
     }();
     const bool same_size = det->width == r->W && det->height == r->H && r->rng_ready;
-    const bool pipelined = pipeline_env && det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world == 1 &&
+    const int pipe_on = r->pipe_mode >= 0 ? r->pipe_mode : pipeline_env;
+    const bool pipelined = pipe_on && det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world == 1 &&
                            !r->use_ext && (r->pipe_bufs || !same_size);
     orx_status s0 = begin_iteration(r, local_iteration_number, det, pipelined);
     if (s0 != ORX_OK) return s0;
@@ -1948,6 +1950,11 @@ orx_status orx_get_stats(orx_renderer* r, orx_stats* out) {
 }
 
 int orx_ppm_pipelined(const orx_renderer* r) { return r && r->last_pipelined ? 1 : 0; }
+orx_status orx_set_iteration_pipelining(orx_renderer* r, int mode) {
+    if (!r || mode < -1 || mode > 1) return ORX_ERR_INVALID_ARGUMENT;
+    r->pipe_mode = mode;
+    return ORX_OK;
+}
 
 orx_status orx_reset_timing(orx_renderer* r) {
     if (!r) return ORX_ERR_INVALID_ARGUMENT;

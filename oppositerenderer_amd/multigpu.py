@@ -14,9 +14,11 @@ so RNG state never crosses GPUs.  Per PPM iteration:
 
 The gather is linear in the photon set and normalises by the global emitted
 count, so the result equals one GPU running the union photon launch, up to
-fp32 summation order.  Scaling is WEAK: each rank traces a full
-photon_launch_width x photon_launch_height batch (global launch height =
-N x per-rank height) and 1/N of the eye/direct pixels.
+fp32 summation order.  The photon launch is global: rank g traces the launch
+rows y % N == g, so a fixed photon_launch_width x photon_launch_height
+workload is split over the ranks (strong scaling, the bench default);
+bench_main's weak mode instead sets the global launch height to N x the
+per-rank height.
 
 Backends: `DeviceShard` drives liborx.so with torch device tensors on the
 renderer's (= torch's current) stream; tests drive the CPU oracle through
@@ -241,8 +243,11 @@ class DeviceShard:
         return t
 
 
-def bench_main(args, metric):
-    """bench.py --gpus N under torchrun: weak scaling, one rank per GPU."""
+def bench_main(args, metric, cpu_baseline=None):
+    """bench.py --gpus N under torchrun, one rank per GPU.  PPM: strong scaling by default (the
+    global photon launch P x P and the W x H pixels are fixed and dealt to the ranks by rows);
+    args.scaling == "weak" gives every rank a full P x P photon launch.  cpu_baseline: bench.py's
+    oracle timing, run on rank 0 when there is one rank."""
     import torch
     import torch.distributed as dist
 
@@ -264,7 +269,9 @@ def bench_main(args, metric):
     dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     W, H, P = args.width, args.height, args.photon_launch
     scene = scenes.scene_by_name(args.scene)
-    cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P * world,
+    weak = getattr(args, "scaling", "strong") == "weak"
+    PH = P * world if weak else P  # global photon launch height
+    cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=PH,
                               gather_variant=args.gather_variant)
     r = OptixRenderer(cfg)
     r.initialize(local_rank)
@@ -306,9 +313,9 @@ def bench_main(args, metric):
     st = r.stats()
     if rank == 0:
         from . import roofline
-        # PPM: weak scaling (each rank emits its own P*P photon batch); VCM: the
-        # W*H light + W*H camera subpaths are split over the ranks (strong scaling)
-        paths = 2 * W * H if vcm else W * H if pt else W * H + P * P * world
+        # PPM: the global launch P x PH (PH = P strong, P * world weak); VCM: the W*H light +
+        # W*H camera subpaths are split over the ranks (strong scaling)
+        paths = 2 * W * H if vcm else W * H if pt else W * H + P * PH
         n_it = max(1, st.timed_iterations)
         per_pass = {name: st.pass_ms[i] / n_it for i, name in enumerate(_abi.PASS_NAMES)}
         per_pass = {k: v for k, v in per_pass.items() if v > 0}
@@ -324,8 +331,8 @@ def bench_main(args, metric):
             lv = int(np.minimum(r.read_buffer(_abi.BUF_VCM_VERTEX_COUNT, np.uint32), 9).sum())
             pb = roofline.pass_bytes(mcode, W, rows0, 0, light_vertices=lv)
         else:
-            # rank 0's passes: its own photon batch, its pixel rows (eye/direct), all pixels (gather)
-            pb = roofline.pass_bytes(mcode, W, H, P * P, valid_avg, st.num_cells)
+            # rank 0's passes: its own photon rows, its pixel rows (eye/direct), all pixels (gather)
+            pb = roofline.pass_bytes(mcode, W, H, P * local_rows(PH, 0, world), valid_avg, st.num_cells)
             for k in ("ppm_eye", "ppm_direct_output"):
                 pb[k] = pb[k] * rows0 / H
         roof = roofline.roofline(dominant, pb[dominant], per_pass[dominant], None)
@@ -333,7 +340,7 @@ def bench_main(args, metric):
             "metric": metric, "value": round(paths * args.steps / t_max / 1e6, 3), "unit": "Mpaths/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t_max * 1e3 / args.steps, 4), "higher_is_better": True,
-            "scaling": "strong" if (vcm or pt) else "weak",
+            "scaling": "weak" if (weak and not (vcm or pt)) else "strong",
             "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic: seeded procedural scene ({scene.name}), XORWOW streams seeded 1645301512",
             "config": ({"workload": f"{scene.name} {W}x{H} PT, 1 spp/iter (strong scaling)",
@@ -346,8 +353,10 @@ def bench_main(args, metric):
                         "paths_per_iteration": paths,
                         "parallelism": f"row-interleaved RNG/pixel ownership x{world}, "
                                        "RCCL reduce_scatter(light-tracing splats)"} if vcm else
-                       {"workload": f"{scene.name} {W}x{H} PPM, {P * P} photons/iter per GPU (weak scaling)",
-                        "scene": scene.name, "width": W, "height": H, "photons_per_iteration": P * P * world,
+                       {"workload": (f"{scene.name} {W}x{H} PPM, {P * P:,} photons/iter per GPU (weak scaling)" if weak
+                                     else f"{scene.name} {W}x{H} PPM, {P * PH:,} photons/iter total (strong scaling)"),
+                        "baseline_config": getattr(args, "config", None),
+                        "scene": scene.name, "width": W, "height": H, "photons_per_iteration": P * PH,
                         "paths_per_iteration": paths,
                         "parallelism": f"row-interleaved RNG/pixel/photon ownership x{world}, "
                                        "RCCL all_gather(hitpoints) + reduce_scatter(indirect)"}),
@@ -356,6 +365,11 @@ def bench_main(args, metric):
             "dominant_pass": dominant,
             "overlapped_passes": overlapped,
         }
+        if cpu_baseline is not None and world == 1:  # the oracle on the host cores, N = 1 only
+            try:
+                out["cpu_baseline"] = cpu_baseline(scene, mcode, W, H, P, getattr(args, "cpu_seconds", 20.0))
+            except Exception as e:  # the baseline must never hide the GPU line
+                out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), file=json_out, flush=True)
     r.destroy()
     dist.barrier()

@@ -58,6 +58,8 @@ def load_library(path: str = LIB_PATH):
     lib.orx_reset_timing.restype = C.c_int
     lib.orx_ppm_pipelined.argtypes = [C.c_void_p]
     lib.orx_ppm_pipelined.restype = C.c_int
+    lib.orx_set_iteration_pipelining.argtypes = [C.c_void_p, C.c_int]
+    lib.orx_set_iteration_pipelining.restype = C.c_int
     lib.orx_stream.argtypes = [C.c_void_p]
     lib.orx_stream.restype = C.c_void_p
     _lib = lib
@@ -68,6 +70,7 @@ EXPORTED_SYMBOLS = (
     "orx_default_config", "orx_create", "orx_init_scene", "orx_render_next_iteration", "orx_get_output",
     "orx_get_output_device", "orx_width", "orx_height", "orx_output_bytes", "orx_emitted_photons_per_iteration",
     "orx_last_error", "orx_destroy", "orx_read_buffer", "orx_get_stats", "orx_reset_timing", "orx_ppm_pipelined",
+    "orx_set_iteration_pipelining",
     "orx_set_shard", "orx_set_ppm_pipeline",
     "orx_stream",
 )
@@ -196,6 +199,10 @@ class OptixRenderer:
     def pipelined(self) -> bool:
         """Whether the last PPM iteration overlapped its gather + output with the next passes."""
         return bool(self._lib.orx_ppm_pipelined(self._h))
+
+    def set_iteration_pipelining(self, mode: int):
+        """Single-device PPM pipelining: 1 on, 0 serial passes, -1 the ORX_PIPELINE default."""
+        self._check(self._lib.orx_set_iteration_pipelining(self._h, mode))
 
     def reset_timing(self):
         """Start a new timed region for stats().pass_ms / *_total (HIP events, no host timing)."""

@@ -106,7 +106,7 @@ def pass_bytes(method: int, W: int, H: int, photons: int, valid: float = 0.0, ce
 
 def roofline(pass_name: str, bytes_per_launch: float, ms_per_launch: float, traffic=None, photon_map: int = 0) -> dict:
     achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9 if ms_per_launch > 0 else 0.0
-    return {"kernel": "+".join(kernels_of(pass_name, photon_map)), "pass": pass_name, "bound": "hbm",
+    return {"kernel": "+".join(kernels_of(pass_name, photon_map)), "pass": pass_name,
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(ms_per_launch, 4)}

@@ -215,9 +215,10 @@ def test_sharded_device_pipelined_matches_single(world, W, H, P):
 
 @pytest.mark.slow
 def test_full_size_conference_sharded_equals_single():
-    """configs[4] at full size on one GPU: 3840x2160, 4096^2 photons per iteration, the
-    Conference-class scene; two row-interleaved shards (each half of the photon launch, RNG rows
-    and pixel rows, exchanging hit points and partial indirect through torch ops) reproduce the
+    """configs[4] at full size on one GPU, in the bench's default multi-GPU mode (strong scaling:
+    the 4096^2 = 16,777,216 photons/iter and 3840x2160 pixels are fixed and split over the
+    shards): two row-interleaved shards (each half of the photon launch rows, RNG rows and pixel
+    rows, exchanging hit points and partial indirect through torch ops) reproduce the
     single-renderer image — the size-independent property behind the 8-GPU pixel/photon
     sharding (the oracle would need minutes at this size)."""
     dev = torch.device("cuda", 0)

@@ -38,12 +38,15 @@ def request(scene, W, H, method=_abi.PROGRESSIVE_PHOTON_MAPPING):
     return req
 
 
-def worker(rank, world, port, out_path, W, H, P, iters, method=_abi.PROGRESSIVE_PHOTON_MAPPING, photon_map=0):
+def worker(rank, world, port, out_path, W, H, P, iters, method=_abi.PROGRESSIVE_PHOTON_MAPPING, photon_map=0,
+           PH=None):
+    """PH: global photon launch height (default P * world: every rank a full P x P batch)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     scene = scenes.cornell()
-    cfg = _abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P * world, photon_map=photon_map)
+    PH = P * world if PH is None else PH
+    cfg = _abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=PH, photon_map=photon_map)
     r = oracle_lib.OracleRenderer(cfg)
     oracle_lib.load().orc_set_threads(2)
     r.init_scene(scene)
@@ -64,17 +67,22 @@ def worker(rank, world, port, out_path, W, H, P, iters, method=_abi.PROGRESSIVE_
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,W,H,photon_map", [(2, 48, 40, 0), (3, 40, 37, 0), (2, 48, 40, 2)])
-def test_sharded_ppm_matches_single(world, W, H, photon_map):
+@pytest.mark.parametrize("world,W,H,photon_map,scaling", [(2, 48, 40, 0, "weak"), (3, 40, 37, 0, "weak"),
+                                                            (2, 48, 40, 2, "weak"), (2, 48, 40, 0, "strong"),
+                                                            (3, 40, 37, 0, "strong"), (2, 48, 40, 2, "strong")])
+def test_sharded_ppm_matches_single(world, W, H, photon_map, scaling):
     """photon_map 2: each rank builds a kd-tree over its own photons and gathers every rank's
-    hit points against it (the gather is linear in the photon set, like the grid's)."""
-    P, iters = 32, 2
+    hit points against it (the gather is linear in the photon set, like the grid's).
+    strong: a fixed 48 x 41 global photon launch (the bench's default multi-GPU mode) whose
+    rows are dealt to the ranks (41 rows: uneven shares); weak: a full 32 x 32 batch per rank."""
+    P, iters = (32, 2) if scaling == "weak" else (48, 2)
+    PH = P * world if scaling == "weak" else 41
     out = os.path.join(tempfile.mkdtemp(), "img.npy")
-    mp.spawn(worker, args=(world, free_port(), out, W, H, P, iters, _abi.PROGRESSIVE_PHOTON_MAPPING, photon_map),
+    mp.spawn(worker, args=(world, free_port(), out, W, H, P, iters, _abi.PROGRESSIVE_PHOTON_MAPPING, photon_map, PH),
              nprocs=world, join=True)
     got = np.load(out)
     scene = scenes.cornell()
-    cfg = _abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P * world, photon_map=photon_map)
+    cfg = _abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=PH, photon_map=photon_map)
     r = oracle_lib.OracleRenderer(cfg)
     r.init_scene(scene)
     req = request(scene, W, H)
