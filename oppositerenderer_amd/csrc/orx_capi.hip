@@ -889,22 +889,10 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_bspartials.ensure((bs_nscan + 2) * 4));
     HIPCHK(r, r->d_bspairs.ensure(S * 8 + 16));
     HIPCHK(r, r->d_subofs.ensure(G2 * 4 * SUBX * nsub + 16));
-    /* second buffer set for PPM pipelining (single device or orx_set_ppm_pipeline, uniform grid) */
+    /* the second buffer set of PPM pipelining is allocated on the first pipelined iteration
+     * (ensure_second_set); the sharded pipeline (orx_set_ppm_pipeline) wants it at once */
     r->pipe_bufs = false;
     r->pend = false;
-    if (r->world == 1 || r->shard_pipe) {
-        HIPCHK(r, r->d_hp2.ensure(nhp * 40));
-        HIPCHK(r, r->d_dir2.ensure(nhp * 12));
-        HIPCHK(r, r->d_sorted2.ensure(SP_PLANES * splane * 4));
-        HIPCHK(r, hipMemsetAsync(r->d_sorted2.p, 0, SP_PLANES * splane * 4, r->stream));
-        HIPCHK(r, r->d_subofs2.ensure(G2 * 4 * SUBX * nsub + 16));
-        HIPCHK(r, r->d_offsets2.ensure(G2 * 4));
-        HIPCHK(r, hipMemsetAsync(r->d_offsets2.p, 0, G2 * 4, r->stream));
-        HIPCHK(r, r->d_grid2.ensure(sizeof(GridParams)));
-        HIPCHK(r, hipMemsetAsync(r->d_grid2.p, 0, sizeof(GridParams), r->stream));
-        HIPCHK(r, hipMemsetAsync(r->d_hp2.p, 0, nhp * 40, r->stream));
-        r->pipe_bufs = true;
-    }
     const size_t wnseg = (nphot + 511) / 512 + 1;
     HIPCHK(r, r->d_wseg.ensure(2 * wnseg * 4));
     HIPCHK(r, hipMemsetAsync(r->d_wseg.p, 0, 2 * wnseg * 4, r->stream));
@@ -947,11 +935,6 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
         const size_t hnum = (size_t)PW * PH * r->cfg.max_photon_deposits; /* NUM_PHOTONS */
         HIPCHK(r, r->d_hcount.ensure(hnum * 4));
         HIPCHK(r, r->d_hwin.ensure(hnum * 4));
-        if (r->pipe_bufs) {
-            HIPCHK(r, r->d_hcount2.ensure(hnum * 4));
-            HIPCHK(r, r->d_hwin2.ensure(hnum * 4));
-            HIPCHK(r, r->d_slots2.ensure(S * 64));
-        }
         pb.hnum = (uint32_t)hnum;
         pb.hcount = r->d_hcount.as<uint32_t>();
         pb.hwin = r->d_hwin.as<uint32_t>();
@@ -971,10 +954,6 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
         const size_t ntiles = (S + 4095) / 4096;
         const size_t tp = std::max((256 * ntiles + 1023) / 1024, (6 * nblk + 1023) / 1024) + 16;
         HIPCHK(r, r->d_kdtree.ensure(tree * 48 + 48));
-        if (r->pipe_bufs) { /* pipelining: the next iteration builds into the other tree */
-            HIPCHK(r, r->d_kdtree2.ensure(tree * 48 + 48));
-            HIPCHK(r, hipMemsetAsync(r->d_kdtree2.p, 0, tree * 48 + 48, r->stream));
-        }
         HIPCHK(r, r->d_kdids.ensure(6 * S * 4 + 64));
         HIPCHK(r, r->d_kdkeys.ensure(2 * S * 4 + 64));
         HIPCHK(r, r->d_kdnodepos.ensure(S * 4 + 16));
@@ -1115,6 +1094,41 @@ static orx_status sync_all(orx_renderer* r) {
     return ORX_OK;
 }
 
+/* The second buffer set of PPM pipelining: only what the photon map of the renderer
+ * alternates between consecutive iterations (the buffers the deferred gather of iteration i
+ * reads while iteration i+1 writes its own): hit points, direct light, grid parameters, and
+ * the uniform grid's sorted photons and offsets, or the hash's deposit records and table, or
+ * the kd-tree.  Allocated on the first pipelined iteration after a resize, so PT/VCM-only
+ * renderers and the serial schedule never hold it. */
+static orx_status ensure_second_set(orx_renderer* r) {
+    if (r->pipe_bufs) return ORX_OK;
+    const size_t nhp = (size_t)r->max_rows * r->W;
+    HIPCHK(r, r->d_hp2.ensure(nhp * 40));
+    HIPCHK(r, hipMemsetAsync(r->d_hp2.p, 0, nhp * 40, r->stream));
+    HIPCHK(r, r->d_dir2.ensure(nhp * 12));
+    HIPCHK(r, r->d_grid2.ensure(sizeof(GridParams)));
+    HIPCHK(r, hipMemsetAsync(r->d_grid2.p, 0, sizeof(GridParams), r->stream));
+    const size_t G2 = (size_t)r->cfg.photon_grid_max_size + 2;
+    if (r->cfg.photon_map == 0) {
+        const size_t bytes = (size_t)SP_PLANES * r->pb.splane * 4;
+        HIPCHK(r, r->d_sorted2.ensure(bytes));
+        HIPCHK(r, hipMemsetAsync(r->d_sorted2.p, 0, bytes, r->stream)); /* tail reads stay finite */
+        HIPCHK(r, r->d_subofs2.ensure(r->d_subofs.bytes));
+        HIPCHK(r, r->d_offsets2.ensure(G2 * 4));
+        HIPCHK(r, hipMemsetAsync(r->d_offsets2.p, 0, G2 * 4, r->stream));
+    } else if (r->cfg.photon_map == 1) {
+        HIPCHK(r, r->d_hcount2.ensure((size_t)r->pb.hnum * 4));
+        HIPCHK(r, r->d_hwin2.ensure((size_t)r->pb.hnum * 4));
+        HIPCHK(r, r->d_slots2.ensure((size_t)r->pb.S * 64));
+    } else {
+        const size_t bytes = (size_t)r->kd.tree_size * 48 + 48;
+        HIPCHK(r, r->d_kdtree2.ensure(bytes));
+        HIPCHK(r, hipMemsetAsync(r->d_kdtree2.p, 0, bytes, r->stream));
+    }
+    r->pipe_bufs = true;
+    return ORX_OK;
+}
+
 static inline void swap_buf(DevBuf& a, DevBuf& b) {
     std::swap(a.p, b.p);
     std::swap(a.bytes, b.bytes);
@@ -1123,10 +1137,12 @@ static inline void swap_buf(DevBuf& a, DevBuf& b) {
 static void swap_sets(orx_renderer* r) {
     swap_buf(r->d_hp, r->d_hp2);
     swap_buf(r->d_dir, r->d_dir2);
-    swap_buf(r->d_sorted, r->d_sorted2);
-    swap_buf(r->d_subofs, r->d_subofs2);
-    swap_buf(r->d_offsets, r->d_offsets2);
     swap_buf(r->d_grid, r->d_grid2);
+    if (r->cfg.photon_map == 0) {
+        swap_buf(r->d_sorted, r->d_sorted2);
+        swap_buf(r->d_subofs, r->d_subofs2);
+        swap_buf(r->d_offsets, r->d_offsets2);
+    }
     if (r->cfg.photon_map == 1) { /* the hash gather reads the deposit records and the table */
         swap_buf(r->d_slots, r->d_slots2);
         swap_buf(r->d_hcount, r->d_hcount2);
@@ -1454,12 +1470,12 @@ orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number,
         const char* e = getenv("ORX_PIPELINE");
         return e ? atoi(e) : 1;
     }();
-    const bool same_size = det->width == r->W && det->height == r->H && r->rng_ready;
     const int pipe_on = r->pipe_mode >= 0 ? r->pipe_mode : pipeline_env;
     const bool pipelined = pipe_on && det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world == 1 &&
-                           !r->use_ext && (r->pipe_bufs || !same_size);
+                           !r->use_ext;
     orx_status s0 = begin_iteration(r, local_iteration_number, det, pipelined);
     if (s0 != ORX_OK) return s0;
+    if (pipelined && (s0 = ensure_second_set(r)) != ORX_OK) return s0;
     r->last_pipelined = pipelined && r->pipe_bufs;
     if (r->last_pipelined) return ppm_pipelined_iteration(r, det, ppm_radius, local_iteration_number);
     if (pipelined) flush_pipeline(r);
@@ -1527,6 +1543,7 @@ orx_status orx_ppm_local_eye(orx_renderer* r, uint64_t iteration_number, uint64_
         return set_err(r, ORX_ERR_INVALID_ARGUMENT, "orx_ppm_local_eye needs a PPM request");
     orx_status s0 = begin_iteration(r, local_iteration_number, det, r->shard_pipe);
     if (s0 != ORX_OK) return s0;
+    if (r->shard_pipe && (s0 = ensure_second_set(r)) != ORX_OK) return s0;
     DevCamera cam = camera_setup(det->camera);
     Consts c = make_consts(r, ppm_radius, local_iteration_number);
     r->last_pipelined = r->shard_pipe && r->pipe_bufs;

@@ -433,8 +433,9 @@ def test_kdtree_parity(scene_name, W, H, P):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pipeline,photon_map", [("1", 0), ("0", 0), ("1", 1), ("1", 2)])
-def test_ppm_back_to_back_iterations(pipeline, photon_map, monkeypatch):
+@pytest.mark.parametrize("pipeline,photon_map,large", [("1", 0, False), ("0", 0, False), ("1", 1, False),
+                                                       ("1", 2, False), ("1", 1, True), ("1", 0, True)])
+def test_ppm_back_to_back_iterations(pipeline, photon_map, large, monkeypatch):
     """Iterations issued back to back with no read in between: with pipelining on (default) the
     gather + output of iteration i run beside the eye/photon/grid passes of i+1 on the other
     buffer set; the running sum after five iterations (and a resolution change in between)
@@ -447,15 +448,16 @@ import oracle_lib
 from oppositerenderer_amd import _abi, scenes
 from oppositerenderer_amd.renderer import OptixRenderer, RenderRequestDetails, next_ppm_radius
 scene = scenes.cornell()
-pm = int(sys.argv[1])
-P = 64 if pm == 1 else 96  # the hash table needs a power-of-two deposit count
+pm, large = int(sys.argv[1]), sys.argv[2] == "1"
+P = 256 if large else (64 if pm == 1 else 96)  # the hash table needs a power-of-two deposit count
+sizes = ((1920, 24, 4), (1280, 16, 2)) if large else ((64, 48, 5), (40, 40, 3))  # 1080p-class rows
 cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P, photon_map=pm)
 gpu = OptixRenderer(cfg); gpu.initialize(0); gpu.initScene(scene)
 ora = oracle_lib.OracleRenderer(_abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P,
                                                     photon_map=pm))
 ora.init_scene(scene)
 errs = []
-for W, H, n in ((64, 48, 5), (40, 40, 3)):
+for W, H, n in sizes:
     cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
     det = RenderRequestDetails(cam, scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W, H)
     r = scene.initial_ppm_radius()
@@ -465,15 +467,16 @@ for W, H, n in ((64, 48, 5), (40, 40, 3)):
         r = next_ppm_radius(r, it)
     g, o = gpu.getOutputBuffer().astype(np.float64), ora.output().astype(np.float64)
     errs.append(float(np.sqrt(((g - o) ** 2).sum() / (o ** 2).sum())))
-print(json.dumps(errs))
+print(json.dumps({"errs": errs, "pipelined": gpu.pipelined()}))
 '''
     env = dict(os.environ, ORX_PIPELINE=pipeline)
-    out = subprocess.run([sys.executable, "-c", code, str(photon_map)], env=env, capture_output=True, text=True,
-                         timeout=110,
+    out = subprocess.run([sys.executable, "-c", code, str(photon_map), "1" if large else "0"], env=env,
+                         capture_output=True, text=True, timeout=110,
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert out.returncode == 0, out.stderr[-2000:]
-    errs = json.loads(out.stdout.strip().splitlines()[-1])
-    assert all(e < 1e-5 for e in errs), errs
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert all(e < 1e-5 for e in res["errs"]), res
+    assert res["pipelined"] == (pipeline == "1"), res  # no silent fallback to the serial schedule
 
 
 @pytest.mark.gpu
@@ -497,5 +500,34 @@ def test_method_switches_without_reads():
     g, o = gpu.getOutputBuffer(), ora.output()
     assert rel_l2(g, o) < 1e-5 and g.mean() > 0
     assert gpu.pipelined()
+    gpu.destroy()
+    ora.close()
+
+
+@pytest.mark.gpu
+def test_pipelining_starts_after_other_methods():
+    """The second buffer set of PPM pipelining is allocated on the first pipelined iteration, not
+    at the resize: PT first (no second set), then PPM at the same size pipelines, then a serial
+    stretch (orx_set_iteration_pipelining(0)) and pipelining again, all matching the oracle."""
+    scene = scenes.cornell()
+    W, H, P = 48, 40, 64
+    gpu, ora, _ = make_pair(scene, W, H, P, _abi.PATH_TRACING)
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    radius = scene.initial_ppm_radius()
+    seen = []
+    for it, (method, local, mode) in enumerate([(_abi.PATH_TRACING, 0, -1), (_abi.PROGRESSIVE_PHOTON_MAPPING, 0, -1),
+                                                (_abi.PROGRESSIVE_PHOTON_MAPPING, 1, -1),
+                                                (_abi.PROGRESSIVE_PHOTON_MAPPING, 2, 0),
+                                                (_abi.PROGRESSIVE_PHOTON_MAPPING, 3, 1),
+                                                (_abi.PROGRESSIVE_PHOTON_MAPPING, 4, 1)]):
+        gpu.set_iteration_pipelining(mode)
+        det = RenderRequestDetails(cam, scene.name, method, W, H)
+        gpu.renderNextIteration(it, local, radius, True, det)
+        ora.render_next_iteration(it, local, radius, det.to_abi())
+        seen.append(gpu.pipelined())
+        radius = next_ppm_radius(radius, it)
+    assert seen == [False, True, True, False, True, True], seen
+    g, o = gpu.getOutputBuffer(), ora.output()
+    assert rel_l2(g, o) < 1e-5 and g.mean() > 0
     gpu.destroy()
     ora.close()
