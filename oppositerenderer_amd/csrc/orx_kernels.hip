@@ -1485,10 +1485,332 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
     }
 }
 
+/* Wave-broadcast gather over the union of a wave's chords.
+ *
+ * The per-lane gather above is bound by the vector-memory address path: every
+ * dwordx4 photon load costs the TA ~16-20 cycles whatever the lanes share, for
+ * four photons of one lane.  Here a wave walks, sub-row by sub-row, the union
+ * of its 64 lanes' chords and reads each photon ONCE through the scalar unit
+ * (s_load into SGPRs, operands of every lane's VALU instructions): no per-lane
+ * photon traffic at all, and the cost per photon is the lanes' arithmetic.
+ * Each lane accepts exactly the photons of its own chord range (the per-lane
+ * kernel's candidate set, [subofs[a0], subofs[a1 + 1]) inside its reference
+ * window) that pass its distance and facing tests, so the accepted set per
+ * pixel is the per-lane kernel's (= the reference's); the union only adds
+ * photons a lane rejects.  Lanes are 8x8 pixel tiles (hitpoints of neighbouring
+ * pixels are near each other in the scene), or, with `order`, consecutive
+ * hitpoints of a list sorted by position (tighter unions).
+ * Per batch of four photons: positions -> d^2 test and the lane's range test;
+ * a batch no lane accepts ends there (one ballot); then the int8 direction
+ * words -> facing, exact directions only inside the band; then powers. */
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+/* uniform 16-B read of a photon plane through the scalar unit */
+__device__ __forceinline__ f4u sload4(const float* __restrict__ plane, uint32_t k) {
+    return *reinterpret_cast<const f4u*>(plane + k);
+}
+__device__ __forceinline__ u4v sload4u(const float* __restrict__ plane, uint32_t k) {
+    return *reinterpret_cast<const u4v*>(plane + k);
+}
+struct UChunk { /* lane k: photon c + k of the chunk */
+    float X, Y, Z, WX, WY, WZ;
+    uint32_t Q;
+};
+__device__ __forceinline__ UChunk uload_chunk(const float* __restrict__ SX, const float* __restrict__ SY,
+                                              const float* __restrict__ SZ, const float* __restrict__ SQ,
+                                              const float* __restrict__ SPX, const float* __restrict__ SPY,
+                                              const float* __restrict__ SPZ, uint32_t k) {
+    UChunk b;
+    b.X = SX[k];
+    b.Y = SY[k];
+    b.Z = SZ[k];
+    b.Q = __float_as_uint(SQ[k]);
+    b.WX = SPX[k];
+    b.WY = SPY[k];
+    b.WZ = SPZ[k];
+    return b;
+}
+/* photons e..e+3 of a chunk to every lane (uniform e): four v_readlane into SGPRs */
+__device__ __forceinline__ f4u bcast4(float v, uint32_t e) {
+    return f4u{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)e)),
+               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)e + 1)),
+               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)e + 2)),
+               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)e + 3))};
+}
+__device__ __forceinline__ u4v bcast4u(uint32_t v, uint32_t e) {
+    return u4v{(uint32_t)__builtin_amdgcn_readlane((int)v, (int)e), (uint32_t)__builtin_amdgcn_readlane((int)v, (int)e + 1),
+               (uint32_t)__builtin_amdgcn_readlane((int)v, (int)e + 2),
+               (uint32_t)__builtin_amdgcn_readlane((int)v, (int)e + 3)};
+}
+
+template <uint32_t NSUB, bool SORTED>
+__global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
+                                                          uint32_t ntiles, const uint32_t* __restrict__ order,
+                                                          uint32_t norder) {
+    const uint32_t tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    uint32_t x = 0, j = 0;
+    bool live;
+    if (SORTED) {
+        const uint32_t g = (blockIdx.x * 4 + w) * 64 + l;
+        live = g < norder;
+        const uint32_t pix = live ? order[g] : 0u;
+        j = pix / gi.W;
+        x = pix - j * gi.W;
+    } else {
+        const uint32_t per = (ntiles + 7) / 8;
+        const uint32_t tile = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+        x = (tile % ntx) * 16 + (w & 1) * 8 + (l & 7);
+        j = (tile / ntx) * 16 + (w >> 1) * 8 + (l >> 3);
+        live = tile < ntiles && x < gi.W && j < gi.segments * gi.seg_rows;
+    }
+    const GridParams g = *pb.grid;
+    uint32_t dC = 0, dP = 0;
+    ORX_TS_DECL;
+    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+    float2 Cc = make_float2(0.f, 0.f);
+    size_t i = 0;
+    if (live) {
+        i = (size_t)j * gi.W + x;
+        const HpRef hr = hp_ref(gi, j, x);
+        A = hr.A[hr.li];
+        B = hr.B[hr.li];
+        Cc = hr.C[hr.li];
+    }
+    const uint32_t flags = __float_as_uint(A.w);
+    const f3 pos = mk(A.x, A.y, A.z);
+    const float radius2 = c.ppm_radius2;
+    const float radius = c.ppm_radius;
+    const float invCellSize = 1.f / g.cell;
+    const f3 np = pos - mk(g.ox, g.oy, g.oz);
+    uint32_t x_lo = 1, x_hi = 0, y_lo = 1, y_hi = 0, z_lo = 1, z_hi = 0;
+    bool act = false;
+    if (live && (flags & PRD_HIT_NON_SPECULAR) && g.G) {
+        const int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
+        const int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
+        const int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
+        x_lo = (uint32_t)(ixl > 0 ? ixl : 0);
+        y_lo = (uint32_t)(iyl > 0 ? iyl : 0);
+        z_lo = (uint32_t)(izl > 0 ? izl : 0);
+        const uint32_t ux = orx_f2u_sat((np.x + radius) * invCellSize);
+        const uint32_t uy = orx_f2u_sat((np.y + radius) * invCellSize);
+        const uint32_t uz = orx_f2u_sat((np.z + radius) * invCellSize);
+        x_hi = (g.gx - 1) < ux ? (g.gx - 1) : ux;
+        y_hi = (g.gy - 1) < uy ? (g.gy - 1) : uy;
+        z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
+        act = x_lo <= x_hi && y_lo <= y_hi && z_lo <= z_hi;
+        /* the reference's visit counters: every (z,y) row of the window, whole rows (:113/:124) */
+        for (uint32_t z = z_lo; act && z <= z_hi; z++)
+            for (uint32_t yy = y_lo; yy <= y_hi; yy++) {
+                const uint32_t from = x_lo + yy * g.gx + z * g.gx * g.gy;
+                dC++;
+                dP += pb.offsets[from + (x_hi - x_lo) + 1] - pb.offsets[from];
+            }
+    }
+    const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
+    const float inv2r2 = 1.0f / (2 * radius2);
+    const float invDen = 1.0f / (1 - expNegativeBeta);
+    const float kx = -beta * inv2r2;
+    const float wB = alpha * invDen, wA = alpha - wB;
+    const v2f kx2 = v2f{kx, kx};
+    const v2f wc6 = wB * ORX_EXPU_C6, wc5 = wB * ORX_EXPU_C5, wc4 = wB * ORX_EXPU_C4;
+    const v2f wc3 = wB * ORX_EXPU_C3, wc2 = wB * ORX_EXPU_C2, wc1 = wB * ORX_EXPU_C1;
+    const v2f wc0 = v2f{wA + wB, wA + wB};
+    v2f accx = v2f{0.f, 0.f}, accy = accx, accz = accx;
+    const v2f px2 = v2f{pos.x, pos.x}, py2 = v2f{pos.y, pos.y}, pz2 = v2f{pos.z, pos.z};
+    const v2f nx2 = v2f{B.x, B.x}, ny2 = v2f{B.y, B.y}, nz2 = v2f{B.z, B.z};
+    const int32_t nq = (int32_t)dir_q8(B.x, B.y, B.z);
+    const float* __restrict__ SX = pb.sorted + (size_t)SP_X * pb.splane;
+    const float* __restrict__ SY = pb.sorted + (size_t)SP_Y * pb.splane;
+    const float* __restrict__ SZ = pb.sorted + (size_t)SP_Z * pb.splane;
+    const float* __restrict__ SQ = pb.sorted + (size_t)SP_DIRQ * pb.splane;
+    const float* __restrict__ SDX = pb.sorted + (size_t)SP_DX * pb.splane;
+    const float* __restrict__ SDY = pb.sorted + (size_t)SP_DY * pb.splane;
+    const float* __restrict__ SDZ = pb.sorted + (size_t)SP_DZ * pb.splane;
+    const float* __restrict__ SPX = pb.sorted + (size_t)SP_PX * pb.splane;
+    const float* __restrict__ SPY = pb.sorted + (size_t)SP_PY * pb.splane;
+    const float* __restrict__ SPZ = pb.sorted + (size_t)SP_PZ * pb.splane;
+    const float m = g.cell * 1e-3f;
+    constexpr uint32_t HS = NSUB > 1 ? SUBR : 1u;
+    const float hc = g.cell / (float)HS;
+    /* the union of the lanes' windows (rows) */
+    const uint32_t UZ0 = wave_min_u32(act ? z_lo : 0xffffffffu), UZ1 = wave_max_u32(act ? z_hi : 0u);
+    const uint32_t UY0 = wave_min_u32(act ? y_lo : 0xffffffffu), UY1 = wave_max_u32(act ? y_hi : 0u);
+    for (uint32_t z = UZ0; z <= UZ1 && UZ0 <= UZ1; z++) {
+        for (uint32_t yy = UY0; yy <= UY1; yy++) {
+            const bool inrow = act && z >= z_lo && z <= z_hi && yy >= y_lo && yy <= y_hi;
+            const uint32_t rowc = yy + z * g.gy;
+            for (uint32_t sr = 0; sr < NSUB; sr++) {
+                /* this lane's chord on the sub-row (the per-lane kernel's), as quarter indices */
+                uint32_t a0 = 0xffffffffu, a1 = 0u;
+                if (inrow) {
+                    const uint32_t hz = z * HS + sr / HS, hy = yy * HS + sr % HS;
+                    const float zc0 = g.oz + (float)hz * hc - m, zc1 = g.oz + (float)(hz + 1) * hc + m;
+                    const float dz = fmaxf(0.f, fmaxf(zc0 - pos.z, pos.z - zc1));
+                    const float yc0 = g.oy + (float)hy * hc - m, yc1 = g.oy + (float)(hy + 1) * hc + m;
+                    const float dy = fmaxf(0.f, fmaxf(yc0 - pos.y, pos.y - yc1));
+                    const float rem = radius2 - dy * dy - dz * dz;
+                    if (rem >= 0.f) {
+                        const float rx = sqrtf(rem) + m;
+                        const int32_t cxl = orx_f2i_sat(orx_floorf((np.x - rx) * invCellSize));
+                        const int32_t cxh = orx_f2i_sat(orx_floorf((np.x + rx) * invCellSize));
+                        const uint32_t xl = cxl > (int32_t)x_lo ? (uint32_t)cxl : x_lo;
+                        const uint32_t xh = cxh < (int32_t)x_hi ? (uint32_t)cxh : x_hi;
+                        if (cxh >= 0 && xl <= xh) {
+                            const float sx = invCellSize * (float)SUBX;
+                            const int32_t q0 = orx_f2i_sat(orx_floorf((np.x - rx) * sx));
+                            const int32_t q1 = orx_f2i_sat(orx_floorf((np.x + rx) * sx));
+                            const uint32_t b0 = q0 > (int32_t)(SUBX * xl) ? (uint32_t)q0 : SUBX * xl;
+                            const uint32_t b1 =
+                                q1 < (int32_t)(SUBX * xh + SUBX - 1) ? (uint32_t)q1 : SUBX * xh + SUBX - 1;
+                            if (q1 >= 0 && b0 <= b1) {
+                                a0 = b0;
+                                a1 = b1;
+                            }
+                        }
+                    }
+                }
+                const uint32_t A0 = wave_min_u32(a0), A1 = wave_max_u32(a1);
+                if (A0 > A1) continue;
+                const uint32_t* so = pb.subofs + ((size_t)rowc * NSUB + sr) * g.gx * SUBX;
+                const uint32_t U0 = so[A0], U1 = so[A1 + 1]; /* uniform: scalar loads */
+                if (U0 >= U1) continue;
+                /* this lane's candidates: [lo, lo + len) */
+                uint32_t lo = 0, len = 0;
+                if (a0 <= a1) {
+                    lo = so[a0];
+                    len = so[a1 + 1] - lo;
+                }
+                ORX_TS_INC(ts_nodes, len);              /* trav stats: lane candidate photons */
+                if (l == 0) ORX_TS_INC(ts_wn, U1 - U0); /* union photons of the wave */
+                ORX_TS_INC(ts_leaves, 1);
+                /* chunks of 64 photons: lane k loads photon c + k of every plane it needs (one
+                 * coalesced dwordx4 per plane and 16 lanes... per chunk, the next chunk's loads
+                 * in flight while this one is evaluated), then batches of four are broadcast to
+                 * all lanes with v_readlane into SGPR operands */
+                uint32_t c = U0;
+                UChunk cur = uload_chunk(SX, SY, SZ, SQ, SPX, SPY, SPZ, c + l);
+                while (c < U1) {
+                    const uint32_t cn = c + 64;
+                    const UChunk nxt = uload_chunk(SX, SY, SZ, SQ, SPX, SPY, SPZ, (cn < U1 ? cn : c) + l);
+                    const uint32_t ce = U1 - c < 64 ? U1 - c : 64;
+                    for (uint32_t e = 0; e < ce; e += 4) {
+                        const uint32_t kb = c + e;
+                        const f4u X = bcast4(cur.X, e), Y = bcast4(cur.Y, e), Z = bcast4(cur.Z, e);
+                        const uint32_t t = kb - lo;
+                        const v2f dx0 = px2 - lo2(X), dx1 = px2 - hi2(X);
+                        const v2f dy0 = py2 - lo2(Y), dy1 = py2 - hi2(Y);
+                        const v2f dz0 = pz2 - lo2(Z), dz1 = pz2 - hi2(Z);
+                        const v2f d20 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
+                        const v2f d21 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
+                        bool in0 = t < len && d20.x <= radius2;
+                        bool in1 = t + 1 < len && d20.y <= radius2;
+                        bool in2 = t + 2 < len && d21.x <= radius2;
+                        bool in3 = t + 3 < len && d21.y <= radius2;
+                        if (!wave_any(in0 | in1 | in2 | in3)) continue;
+                        const u4v Q = bcast4u(cur.Q, e);
+                        const int32_t q0 = __builtin_amdgcn_sdot4((int32_t)Q.x, nq, 0, false);
+                        const int32_t q1 = __builtin_amdgcn_sdot4((int32_t)Q.y, nq, 0, false);
+                        const int32_t q2 = __builtin_amdgcn_sdot4((int32_t)Q.z, nq, 0, false);
+                        const int32_t q3 = __builtin_amdgcn_sdot4((int32_t)Q.w, nq, 0, false);
+                        in0 = in0 && q0 <= DIRQ_BAND;
+                        in1 = in1 && q1 <= DIRQ_BAND;
+                        in2 = in2 && q2 <= DIRQ_BAND;
+                        in3 = in3 && q3 <= DIRQ_BAND;
+                        const bool u0 = in0 && q0 >= -DIRQ_BAND, u1 = in1 && q1 >= -DIRQ_BAND;
+                        const bool u2 = in2 && q2 >= -DIRQ_BAND, u3 = in3 && q3 >= -DIRQ_BAND;
+                        if (wave_any(u0 | u1 | u2 | u3)) { /* inside the band: the exact test (rare) */
+                            const uint32_t ku = (uint32_t)__builtin_amdgcn_readfirstlane((int)kb);
+                            const f4u DX = sload4(SDX, ku), DY = sload4(SDY, ku), DZ = sload4(SDZ, ku);
+                            const v2f nd0 = (lo2(DX) * nx2 + lo2(DY) * ny2) + lo2(DZ) * nz2;
+                            const v2f nd1 = (hi2(DX) * nx2 + hi2(DY) * ny2) + hi2(DZ) * nz2;
+                            in0 = in0 && (!u0 || nd0.x <= 0.f);
+                            in1 = in1 && (!u1 || nd0.y <= 0.f);
+                            in2 = in2 && (!u2 || nd1.x <= 0.f);
+                            in3 = in3 && (!u3 || nd1.y <= 0.f);
+                        }
+                        if (!wave_any(in0 | in1 | in2 | in3)) continue;
+                        const f4u WX = bcast4(cur.WX, e), WY = bcast4(cur.WY, e), WZ = bcast4(cur.WZ, e);
+                        const v2f x0 = d20 * kx2;
+                        const v2f x1 = d21 * kx2;
+                        v2f p0 = wc6, p1 = wc6;
+                        p0 = __builtin_elementwise_fma(p0, x0, wc5); p1 = __builtin_elementwise_fma(p1, x1, wc5);
+                        p0 = __builtin_elementwise_fma(p0, x0, wc4); p1 = __builtin_elementwise_fma(p1, x1, wc4);
+                        p0 = __builtin_elementwise_fma(p0, x0, wc3); p1 = __builtin_elementwise_fma(p1, x1, wc3);
+                        p0 = __builtin_elementwise_fma(p0, x0, wc2); p1 = __builtin_elementwise_fma(p1, x1, wc2);
+                        p0 = __builtin_elementwise_fma(p0, x0, wc1); p1 = __builtin_elementwise_fma(p1, x1, wc1);
+                        v2f w0 = __builtin_elementwise_fma(p0, x0, wc0), w1 = __builtin_elementwise_fma(p1, x1, wc0);
+                        w0.x = in0 ? w0.x : 0.f;
+                        w0.y = in1 ? w0.y : 0.f;
+                        w1.x = in2 ? w1.x : 0.f;
+                        w1.y = in3 ? w1.y : 0.f;
+                        ORX_TS_INC(ts_tris, (uint32_t)in0 + (uint32_t)in1 + (uint32_t)in2 + (uint32_t)in3);
+                        accx = __builtin_elementwise_fma(lo2(WX), w0, accx);
+                        accy = __builtin_elementwise_fma(lo2(WY), w0, accy);
+                        accz = __builtin_elementwise_fma(lo2(WZ), w0, accz);
+                        accx = __builtin_elementwise_fma(hi2(WX), w1, accx);
+                        accy = __builtin_elementwise_fma(hi2(WY), w1, accy);
+                        accz = __builtin_elementwise_fma(hi2(WZ), w1, accz);
+                    }
+                    cur = nxt;
+                    c = cn;
+                }
+            }
+        }
+    }
+#ifdef ORX_TRAV_STATS
+    atomicAdd((unsigned long long*)&pb.grid->st_lane_batches, (unsigned long long)ts_nodes);
+    atomicAdd((unsigned long long*)&pb.grid->st_wave_batches, (unsigned long long)ts_wn);
+    atomicAdd((unsigned long long*)&pb.grid->st_lane_rows, (unsigned long long)ts_leaves);
+    atomicAdd((unsigned long long*)&pb.grid->st_accepted, (unsigned long long)ts_tris);
+#endif
+    if (live) {
+        const float ax = accx.x + accx.y, ay = accy.x + accy.y, az = accz.x + accz.y;
+        const f3 att = mk(B.w, Cc.x, Cc.y);
+        const float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
+        const float s2 = 1.0f / c.emitted_f;
+        const f3 ind = ((mk(ax, ay, az) * att) * s1) * s2;
+        gi.indirect[3 * i + 0] = ind.x;
+        gi.indirect[3 * i + 1] = ind.y;
+        gi.indirect[3 * i + 2] = ind.z;
+        if (gi.dbg) {
+            gi.dbg[2 * i] = dC;
+            gi.dbg[2 * i + 1] = dP;
+        }
+    }
+    const uint64_t sp = wave_sum_u64(dP), sc = wave_sum_u64(dC);
+    if ((threadIdx.x & 63) == 0 && sp) {
+        atomicAdd((unsigned long long*)&pb.grid->photons_visited, (unsigned long long)sp);
+        atomicAdd((unsigned long long*)&pb.grid->cells_visited, (unsigned long long)sc);
+        atomicAdd((unsigned long long*)&pb.grid->photons_visited_total, (unsigned long long)sp);
+        atomicAdd((unsigned long long*)&pb.grid->cells_visited_total, (unsigned long long)sc);
+    }
+}
+
 void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, size_t lds_pad) {
     const uint32_t rows = gi.segments * gi.seg_rows;
     const uint32_t ntx = (gi.W + 15) / 16, nty = (rows + 15) / 16, ntiles = ntx * nty;
     const dim3 grid(8 * ((ntiles + 7) / 8));
+    /* ORX_GATHER_UNION=0: the per-lane kernel (A/B); measured: equal stand-alone on the hall,
+     * faster overlapped (no TA traffic beside the TA-bound photon pass), 1.7x on the 4K conference */
+    static const int union_gather = [] {
+        const char* e = getenv("ORX_GATHER_UNION");
+        return e ? atoi(e) : 1;
+    }();
+    if (union_gather && pb.subofs) {
+        if (pb.nsub == 1)
+            hipLaunchKernelGGL((k_ppm_gather_union<1, false>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx, ntiles,
+                               nullptr, 0u);
+        else
+            hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR, false>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx,
+                               ntiles, nullptr, 0u);
+        return;
+    }
     if (!pb.subofs)
         hipLaunchKernelGGL((k_ppm_gather<1, false>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx, ntiles);
     else if (pb.nsub == 1)

@@ -17,6 +17,8 @@ lib.orx_trav_stats_read.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_in
 scene_name = sys.argv[1] if len(sys.argv) > 1 else "SyntheticHall"
 method = {"ppm": 2, "vcm": 1, "pt": 0}[sys.argv[2] if len(sys.argv) > 2 else "ppm"]
 W, H, P = (1920, 1080, 2048) if scene_name.startswith("Synthetic") else (1024, 1024, 1024)
+if len(sys.argv) > 3:  # WxHxP
+    W, H, P = (int(v) for v in sys.argv[3].split("x"))
 sc = scenes.scene_by_name(scene_name)
 r = renderer.OptixRenderer(_abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P))
 r.initialize(0)
@@ -35,7 +37,12 @@ for it in range(3):
         print(f"it{it} {name:8s} rays {v[b]:12d}  nodes/ray {v[b + 1] / rays:6.2f}  leaves/ray {v[b + 2] / rays:6.2f}"
               f"  tris/ray {v[b + 3] / rays:6.2f}  SIMT node {v[b + 1] / max(1, 64 * wn):5.3f}"
               f"  leaf {v[b + 2] / max(1, 64 * wl):5.3f}")
-    if method == 2:
+    if method == 2 and os.environ.get("ORX_GATHER_UNION", "0") != "0":
+        lc, up, nr = v[12], v[13], v[14]
+        print(f"it{it} union    lane candidates/px {lc / (W * H):8.1f}  union photons/px {64 * up / (W * H):8.1f}"
+              f"  union factor {64 * up / max(1, lc):5.2f}  accepted/px {v[16] / (W * H):7.1f}"
+              f"  lane sub-rows/px {nr / (W * H):6.1f}")
+    elif method == 2:
         lb, wb, lr, wr = v[12:16]
         print(f"it{it} gather   batches/px {lb / (W * H):8.1f}  SIMT batch {lb / max(1, 64 * wb):5.3f}"
               f"  rows/px {lr / (W * H):6.1f}  SIMT row {lr / max(1, 64 * wr):5.3f}"
