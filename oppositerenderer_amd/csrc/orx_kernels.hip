@@ -1549,10 +1549,102 @@ __device__ __forceinline__ u4v bcast4u(uint32_t v, uint32_t e) {
                (uint32_t)__builtin_amdgcn_readlane((int)v, (int)e + 3)};
 }
 
-template <uint32_t NSUB, bool SORTED>
+/* The union kernel's per-batch constants and accumulators (LDS-broadcast form) */
+struct UAcc {
+    v2f accx, accy, accz;
+};
+struct UConst {
+    v2f px2, py2, pz2, nx2, ny2, nz2, kx2, wc6, wc5, wc4, wc3, wc2, wc1, wc0;
+    int32_t nq;
+    const float* SDX;
+    const float* SDY;
+    const float* SDZ;
+};
+/* One 64-photon chunk of a sub-row's union, staged in the wave's LDS image L[7][64]
+ * (x y z dirq px py pz; slots past the sub-row's end hold x = +inf, so no lane can
+ * accept them).  Batches of four photons are read by every lane from the same LDS
+ * address (ds_read_b128 broadcast: LDS-array cycles, no VALU), then:
+ *   d^2 <= r2 (r2 = -1 for a lane without a chord on this sub-row), and with RANGE the
+ *   lane's chord test [lo, lo + len); the facing prefilter; the weight and sums.
+ * RANGE = false when every lane's chord is its whole margin-grown extent on the
+ * sub-row (not cut by its reference window): then a union photon outside the chord
+ * is farther than r from the lane's hit point (the margin argument of the chord
+ * trimming), so the distance test alone decides, as the per-lane kernel's chord +
+ * distance tests do. */
+template <bool RANGE>
+__device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uint32_t c, uint32_t ce, uint32_t lo,
+                                                uint32_t len, float r2, const UConst& k, UAcc& a) {
+    const float4* L4 = reinterpret_cast<const float4*>(L);
+    for (uint32_t e = 0; e < ce; e += 4) {
+        const uint32_t kb = c + e;
+        const float4 X = L4[e >> 2], Y = L4[16 + (e >> 2)], Z = L4[32 + (e >> 2)];
+        const v2f dx0 = k.px2 - lo2(X), dx1 = k.px2 - hi2(X);
+        const v2f dy0 = k.py2 - lo2(Y), dy1 = k.py2 - hi2(Y);
+        const v2f dz0 = k.pz2 - lo2(Z), dz1 = k.pz2 - hi2(Z);
+        const v2f d20 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
+        const v2f d21 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
+        bool in0 = d20.x <= r2, in1 = d20.y <= r2, in2 = d21.x <= r2, in3 = d21.y <= r2;
+        if (RANGE) {
+            const uint32_t t = kb - lo;
+            in0 = in0 && t < len;
+            in1 = in1 && t + 1 < len;
+            in2 = in2 && t + 2 < len;
+            in3 = in3 && t + 3 < len;
+        }
+        if (!wave_any(in0 | in1 | in2 | in3)) continue;
+        const uint4 Q = reinterpret_cast<const uint4*>(L4)[48 + (e >> 2)];
+        const int32_t q0 = __builtin_amdgcn_sdot4((int32_t)Q.x, k.nq, 0, false);
+        const int32_t q1 = __builtin_amdgcn_sdot4((int32_t)Q.y, k.nq, 0, false);
+        const int32_t q2 = __builtin_amdgcn_sdot4((int32_t)Q.z, k.nq, 0, false);
+        const int32_t q3 = __builtin_amdgcn_sdot4((int32_t)Q.w, k.nq, 0, false);
+        in0 = in0 && q0 <= DIRQ_BAND;
+        in1 = in1 && q1 <= DIRQ_BAND;
+        in2 = in2 && q2 <= DIRQ_BAND;
+        in3 = in3 && q3 <= DIRQ_BAND;
+        const bool u0 = in0 && q0 >= -DIRQ_BAND, u1 = in1 && q1 >= -DIRQ_BAND;
+        const bool u2 = in2 && q2 >= -DIRQ_BAND, u3 = in3 && q3 >= -DIRQ_BAND;
+        if (wave_any(u0 | u1 | u2 | u3)) { /* inside the band: the exact test (rare) */
+            const uint32_t ku = (uint32_t)__builtin_amdgcn_readfirstlane((int)kb);
+            const f4u DX = sload4(k.SDX, ku), DY = sload4(k.SDY, ku), DZ = sload4(k.SDZ, ku);
+            const v2f nd0 = (lo2(DX) * k.nx2 + lo2(DY) * k.ny2) + lo2(DZ) * k.nz2;
+            const v2f nd1 = (hi2(DX) * k.nx2 + hi2(DY) * k.ny2) + hi2(DZ) * k.nz2;
+            in0 = in0 && (!u0 || nd0.x <= 0.f);
+            in1 = in1 && (!u1 || nd0.y <= 0.f);
+            in2 = in2 && (!u2 || nd1.x <= 0.f);
+            in3 = in3 && (!u3 || nd1.y <= 0.f);
+        }
+        if (!wave_any(in0 | in1 | in2 | in3)) continue;
+        const float4 WX = L4[64 + (e >> 2)], WY = L4[80 + (e >> 2)], WZ = L4[96 + (e >> 2)];
+        const v2f x0 = d20 * k.kx2;
+        const v2f x1 = d21 * k.kx2;
+        v2f p0 = k.wc6, p1 = k.wc6;
+        p0 = __builtin_elementwise_fma(p0, x0, k.wc5); p1 = __builtin_elementwise_fma(p1, x1, k.wc5);
+        p0 = __builtin_elementwise_fma(p0, x0, k.wc4); p1 = __builtin_elementwise_fma(p1, x1, k.wc4);
+        p0 = __builtin_elementwise_fma(p0, x0, k.wc3); p1 = __builtin_elementwise_fma(p1, x1, k.wc3);
+        p0 = __builtin_elementwise_fma(p0, x0, k.wc2); p1 = __builtin_elementwise_fma(p1, x1, k.wc2);
+        p0 = __builtin_elementwise_fma(p0, x0, k.wc1); p1 = __builtin_elementwise_fma(p1, x1, k.wc1);
+        v2f w0 = __builtin_elementwise_fma(p0, x0, k.wc0), w1 = __builtin_elementwise_fma(p1, x1, k.wc0);
+        w0.x = in0 ? w0.x : 0.f;
+        w0.y = in1 ? w0.y : 0.f;
+        w1.x = in2 ? w1.x : 0.f;
+        w1.y = in3 ? w1.y : 0.f;
+        a.accx = __builtin_elementwise_fma(lo2(WX), w0, a.accx);
+        a.accy = __builtin_elementwise_fma(lo2(WY), w0, a.accy);
+        a.accz = __builtin_elementwise_fma(lo2(WZ), w0, a.accz);
+        a.accx = __builtin_elementwise_fma(hi2(WX), w1, a.accx);
+        a.accy = __builtin_elementwise_fma(hi2(WY), w1, a.accy);
+        a.accz = __builtin_elementwise_fma(hi2(WZ), w1, a.accz);
+    }
+}
+
+/* BC: photon broadcast form — 0: v_readlane from the chunk registers; 1: the wave's LDS
+ * image (union_chunk_lds) with the chord test dropped on sub-rows where no lane's chord is
+ * cut by its window */
+template <uint32_t NSUB, bool SORTED, int BC>
 __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
                                                           uint32_t ntiles, const uint32_t* __restrict__ order,
                                                           uint32_t norder) {
+    __shared__ float ulds[BC == 1 ? 4 : 1][BC == 1 ? 7 * 64 : 1];
     const uint32_t tid = threadIdx.x, w = tid >> 6, l = tid & 63;
     uint32_t x = 0, j = 0;
     bool live;
@@ -1638,6 +1730,12 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
     const float m = g.cell * 1e-3f;
     constexpr uint32_t HS = NSUB > 1 ? SUBR : 1u;
     const float hc = g.cell / (float)HS;
+    UConst UK;
+    UAcc UA;
+    if (BC == 1) {
+        UK = UConst{px2, py2, pz2, nx2, ny2, nz2, kx2, wc6, wc5, wc4, wc3, wc2, wc1, wc0, nq, SDX, SDY, SDZ};
+        UA = UAcc{accx, accy, accz};
+    }
     /* the union of the lanes' windows (rows) */
     const uint32_t UZ0 = wave_min_u32(act ? z_lo : 0xffffffffu), UZ1 = wave_max_u32(act ? z_hi : 0u);
     const uint32_t UY0 = wave_min_u32(act ? y_lo : 0xffffffffu), UY1 = wave_max_u32(act ? y_hi : 0u);
@@ -1646,8 +1744,11 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
             const bool inrow = act && z >= z_lo && z <= z_hi && yy >= y_lo && yy <= y_hi;
             const uint32_t rowc = yy + z * g.gy;
             for (uint32_t sr = 0; sr < NSUB; sr++) {
-                /* this lane's chord on the sub-row (the per-lane kernel's), as quarter indices */
+                /* this lane's chord on the sub-row (the per-lane kernel's), as quarter indices;
+                 * cut: the chord is shorter than the margin-grown extent [q0, q1] inside the grid
+                 * (its reference window ends inside it) */
                 uint32_t a0 = 0xffffffffu, a1 = 0u;
+                bool cut = false;
                 if (inrow) {
                     const uint32_t hz = z * HS + sr / HS, hy = yy * HS + sr % HS;
                     const float zc0 = g.oz + (float)hz * hc - m, zc1 = g.oz + (float)(hz + 1) * hc + m;
@@ -1671,6 +1772,8 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
                             if (q1 >= 0 && b0 <= b1) {
                                 a0 = b0;
                                 a1 = b1;
+                                const int32_t qmax = (int32_t)(SUBX * g.gx) - 1;
+                                cut = (int32_t)b0 > (q0 > 0 ? q0 : 0) || (int32_t)b1 < (q1 < qmax ? q1 : qmax);
                             }
                         }
                     }
@@ -1689,6 +1792,34 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
                 ORX_TS_INC(ts_nodes, len);              /* trav stats: lane candidate photons */
                 if (l == 0) ORX_TS_INC(ts_wn, U1 - U0); /* union photons of the wave */
                 ORX_TS_INC(ts_leaves, 1);
+                if (BC == 1) {
+                    /* a lane without a chord here accepts nothing (its window excludes the
+                     * sub-row, or its sphere misses it) */
+                    const float r2 = a0 <= a1 ? radius2 : -1.f;
+                    const bool range = wave_any(cut);
+                    float* L = ulds[w];
+                    uint32_t cc = U0;
+                    UChunk cur = uload_chunk(SX, SY, SZ, SQ, SPX, SPY, SPZ, cc + l);
+                    while (cc < U1) {
+                        const uint32_t cn = cc + 64;
+                        const UChunk nxt = uload_chunk(SX, SY, SZ, SQ, SPX, SPY, SPZ, (cn < U1 ? cn : cc) + l);
+                        const uint32_t ce = U1 - cc < 64 ? U1 - cc : 64;
+                        L[l] = cc + l < U1 ? cur.X : INFINITY;
+                        L[64 + l] = cur.Y;
+                        L[128 + l] = cur.Z;
+                        L[192 + l] = __uint_as_float(cur.Q);
+                        L[256 + l] = cur.WX;
+                        L[320 + l] = cur.WY;
+                        L[384 + l] = cur.WZ;
+                        __builtin_amdgcn_wave_barrier();
+                        if (range) union_chunk_lds<true>(L, cc, ce, lo, len, r2, UK, UA);
+                        else union_chunk_lds<false>(L, cc, ce, lo, len, r2, UK, UA);
+                        __builtin_amdgcn_wave_barrier();
+                        cur = nxt;
+                        cc = cn;
+                    }
+                    continue;
+                }
                 /* chunks of 64 photons: lane k loads photon c + k of every plane it needs (one
                  * coalesced dwordx4 per plane and 16 lanes... per chunk, the next chunk's loads
                  * in flight while this one is evaluated), then batches of four are broadcast to
@@ -1763,6 +1894,11 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
             }
         }
     }
+    if (BC == 1) {
+        accx = UA.accx;
+        accy = UA.accy;
+        accz = UA.accz;
+    }
 #ifdef ORX_TRAV_STATS
     atomicAdd((unsigned long long*)&pb.grid->st_lane_batches, (unsigned long long)ts_nodes);
     atomicAdd((unsigned long long*)&pb.grid->st_wave_batches, (unsigned long long)ts_wn);
@@ -1796,19 +1932,30 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
     const uint32_t rows = gi.segments * gi.seg_rows;
     const uint32_t ntx = (gi.W + 15) / 16, nty = (rows + 15) / 16, ntiles = ntx * nty;
     const dim3 grid(8 * ((ntiles + 7) / 8));
-    /* ORX_GATHER_UNION=0: the per-lane kernel (A/B); measured: equal stand-alone on the hall,
-     * faster overlapped (no TA traffic beside the TA-bound photon pass), 1.7x on the 4K conference */
+    /* ORX_GATHER_UNION: 2 (default) the union kernel with LDS-broadcast batches; 1 the union
+     * kernel with v_readlane broadcasts; 0 the per-lane kernel.  Measured (serial hall gather /
+     * pipelined hall frame / 4K conference frame): 0: 2.5 ms / 7.9 ms / 120 ms;
+     * 1: 2.81 / 7.68 / 77.2; 2: 1.91 / 7.02 / 53.3 */
     static const int union_gather = [] {
         const char* e = getenv("ORX_GATHER_UNION");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 2;
     }();
-    if (union_gather && pb.subofs) {
+    if (union_gather == 2 && pb.subofs) {
         if (pb.nsub == 1)
-            hipLaunchKernelGGL((k_ppm_gather_union<1, false>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx, ntiles,
+            hipLaunchKernelGGL((k_ppm_gather_union<1, false, 1>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx, ntiles,
                                nullptr, 0u);
         else
-            hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR, false>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx,
-                               ntiles, nullptr, 0u);
+            hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR, false, 1>), grid, dim3(256), lds_pad, s, gi, pb, c,
+                               ntx, ntiles, nullptr, 0u);
+        return;
+    }
+    if (union_gather && pb.subofs) {
+        if (pb.nsub == 1)
+            hipLaunchKernelGGL((k_ppm_gather_union<1, false, 0>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx, ntiles,
+                               nullptr, 0u);
+        else
+            hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR, false, 0>), grid, dim3(256), lds_pad, s, gi, pb, c,
+                               ntx, ntiles, nullptr, 0u);
         return;
     }
     if (!pb.subofs)
