@@ -74,7 +74,17 @@ def parse(argv=None):
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
+    a.config = matching_config(a)
     return a
+
+
+def matching_config(a):
+    """The BASELINE configs[] entry the resolved workload is (e.g. --method vcm on the default
+    config is configs[3]); None for a workload that is none of them."""
+    for i, cfg in CONFIGS.items():
+        if all(getattr(a, k) == v for k, v in cfg.items() if not (k == "photon_launch" and cfg["method"] != "ppm")):
+            return i
+    return None
 
 
 METHODS = {"ppm": 2, "vcm": 1, "pt": 0}  # orx_method (include/orx.h)

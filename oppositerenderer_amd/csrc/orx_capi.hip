@@ -412,7 +412,7 @@ struct orx_renderer {
     bool vcm_kd = false;      /* d_vkd sized for the current vcm_npx */
     VcmBufs vcm_vb{};
     VcmConsts vcm_c{};
-    DevBuf d_vcount, d_vverts, d_vsplat, d_vcam, d_vkd, d_vshq, d_tstats;
+    DevBuf d_vcount, d_vverts, d_vsplat, d_vcam, d_vkd, d_vshq, d_vwork, d_tstats;
     std::vector<DevLight> host_lights;
 };
 
@@ -1338,9 +1338,11 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
     vb.splat = r->d_vsplat.as<float>();
     vb.splat_in = vb.splat + (size_t)r->rank * r->max_rows * r->W * 3;
     {
-        const size_t waves = (size_t)((r->W + 7) / 8) * ((r->rows + 7) / 8);
+        const size_t waves = vcm_camera_waves(((r->W + 7) / 8) * ((r->rows + 7) / 8));
         HIPCHK(r, r->d_vshq.ensure(waves * VCM_SHQ_PER_WAVE * 16 + 16));
         vb.shq = r->d_vshq.as<float4>();
+        HIPCHK(r, r->d_vwork.ensure(16));
+        vb.work = r->d_vwork.as<uint32_t>();
     }
     vb.cam = r->d_vcam.as<float>();
     vb.output = r->d_out.as<float>();

@@ -209,6 +209,7 @@ struct VcmBufs {
     const float* splat_in; /* [rows][W][3] summed splats of the own rows (camera pass) */
     float* cam;         /* [W*H*3] camera subpath colour of this iteration */
     float* output;      /* [W*H*3] running sum */
+    uint32_t* work;     /* [2] camera-pass, light-pass work-item counters (zeroed by the launches) */
 };
 struct VcmConsts {
     f3 eye, lookdir, u, v;          /* Camera (Camera.cpp:333-345) */
@@ -222,5 +223,6 @@ struct VcmConsts {
 };
 void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c, bool estimate);
 void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c);
+uint32_t vcm_camera_waves(uint32_t tiles); /* persistent camera-pass waves for `tiles` 8x8 tiles */
 
 }  // namespace orx

@@ -492,20 +492,25 @@ __device__ inline void connect_camera(const DevScene& S, const Subpath& L, const
     }
 }
 
-/* lightPass (VCMLightPass.cu:52-93), initLightPayload (:120-176), lightHit (vcm.h:210-309) */
+/* lightPass (VCMLightPass.cu:52-93), initLightPayload (:120-176), lightHit (vcm.h:210-309)
+ *
+ * Persistent waves with per-lane refill, as the camera pass below: a lane whose light
+ * subpath has ended starts the next subpath of its wave's 64-subpath work item, one
+ * bounce per round.  Each subpath's arithmetic and RNG stream are unchanged. */
 /* TEX: the scene has Texture materials (vb.vE != NULL); the texel fetch is
  * compiled out otherwise, it costs the camera kernel ~10% through spills */
-template <bool ESTIMATE, bool TEX>
-__global__ __launch_bounds__(64, 4) void k_vcm_light(DevScene S, VcmBufs vb, VcmConsts c) {
-    ORX_STACK_DECL;
-    uint32_t* stk = ORX_STACK_PTR;
-    const uint32_t p = blockIdx.x * 64u + threadIdx.x; /* own-row subpath: x + j*W */
-    if (p >= c.lcount) return;
+struct LightSub {
+    uint32_t p;
+    size_t slot;
+    uint32_t nverts;
+};
+__device__ __forceinline__ void light_start(const DevScene& S, const VcmBufs& vb, const VcmConsts& c, uint32_t p,
+                                            LightSub& ls, Rng& rs, Subpath& L) {
     const uint32_t x = p % c.W, j = p / c.W;
-    const size_t slot = (size_t)j * vb.RW + x; /* RNG planes hold the own rows */
-    Rng rs = rng_load(vb.rng, slot);
-    uint32_t nverts = 0;
-    Subpath L;
+    ls.p = p;
+    ls.slot = (size_t)j * vb.RW + x; /* RNG planes hold the own rows */
+    ls.nverts = 0;
+    rs = rng_load(vb.rng, ls.slot);
     L.throughput = mk1(1.f);
     L.color = mk1(0.f);
     L.depth = 0;
@@ -572,41 +577,98 @@ __global__ __launch_bounds__(64, 4) void k_vcm_light(DevScene S, VcmBufs vb, Vcm
     L.dVCM = directPdfW / emissionPdfW;
     L.dVC = light.type == LIGHT_AREA ? cosAtLight / emissionPdfW : 0.f;
     L.dVM = L.dVC * c.misVc;
+}
 
+template <bool ESTIMATE, bool TEX>
+__global__ __launch_bounds__(64, 4) void k_vcm_light(DevScene S, VcmBufs vb, VcmConsts c) {
+    ORX_STACK_DECL;
+    uint32_t* stk = ORX_STACK_PTR;
+    const uint32_t lane = threadIdx.x & 63;
+    LightSub ls;
+    ls.p = 0;
+    ls.slot = 0;
+    ls.nverts = 0;
+    Rng rs = {};
+    Subpath L = {};
+    bool alive = false;
+    uint32_t next = 0, end = 0; /* the wave's current work item range (uniform) */
+    bool exhausted = false;
     for (;;) {
-        Hit h;
-        if (!trace_closest(S, L.origin, L.direction, VCM_RAY_LEN_MIN, RT_DEFAULT_MAX, h, stk)) break;
-        const uint32_t mi = prim_material(S, h);
-        const DevMaterial& m = S.mats[mi];
-        const f3 hit = L.origin + L.direction * h.t;
-        if (m.type == MAT_EMITTER) break;
-        VBsdf bs;
-        f3 N;
-        const f3 kd = TEX && m.type == MAT_TEXTURE ? tex_color(S, m, h) : m.Kd;
-        if (!material_bsdf(m, kd, geometric_normal(S, h), L.direction, true, bs, N)) break;
-        L.depth++;
-        const float cosIn = dot(N, -L.direction);
-        if (cosIn < VCM_EPS_COSINE) break;
-        mis_on_hit(L, cosIn, h.t);
-        const bool spec = bs.is_specular();
-        if (!spec) {
-            const uint32_t k = nverts++;
-            if (!ESTIMATE && k < VCM_MAX_VERTS) {
-                const size_t o = (size_t)k * c.lcount + p;
-                vb.vA[o] = make_float4(hit.x, hit.y, hit.z, __uint_as_float(mi));
-                vb.vB[o] = make_float4(L.throughput.x, L.throughput.y, L.throughput.z, L.dVCM);
-                vb.vC[o] = make_float4(N.x, N.y, N.z, L.dVC);
-                vb.vD[o] = make_float4(bs.fix.x, bs.fix.y, bs.fix.z, L.dVM);
-                if (TEX && m.type == MAT_TEXTURE) vb.vE[o] = make_float4(kd.x, kd.y, kd.z, 0.f);
+        for (;;) { /* refill: lanes without a subpath start the next ones of the wave's item */
+            const uint64_t need = __ballot(!alive);
+            if (!need) break;
+            if (next >= end) {
+                if (exhausted) break;
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(vb.work + 1, 64u);
+                base = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)base, 0, 64));
+                if (base >= c.lcount) {
+                    exhausted = true;
+                    break;
+                }
+                next = base;
+                end = base + 64u < c.lcount ? base + 64u : c.lcount;
             }
-            if (!ESTIMATE) connect_camera(S, L, bs, hit, c, vb.splat, stk);
+            const uint32_t avail = end - next;
+            const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+            if (!alive && rank < avail) {
+                light_start(S, vb, c, next + rank, ls, rs, L);
+                alive = true;
+            }
+            const uint32_t n = (uint32_t)__popcll(need);
+            next += n < avail ? n : avail;
         }
-        if (c.maxPathLen < L.depth + 2) break;
-        sample_scattering(L, hit, bs, c, rs);
-        if (L.done) break;
+        if (!__ballot(alive)) break; /* only once the work is exhausted */
+        if (!alive) continue;
+        /* one bounce */
+        bool end_path = false;
+        Hit h;
+        if (!trace_closest(S, L.origin, L.direction, VCM_RAY_LEN_MIN, RT_DEFAULT_MAX, h, stk)) {
+            end_path = true;
+        } else {
+            const uint32_t mi = prim_material(S, h);
+            const DevMaterial& m = S.mats[mi];
+            const f3 hit = L.origin + L.direction * h.t;
+            VBsdf bs;
+            f3 N;
+            const f3 kd = TEX && m.type == MAT_TEXTURE ? tex_color(S, m, h) : m.Kd;
+            if (m.type == MAT_EMITTER || !material_bsdf(m, kd, geometric_normal(S, h), L.direction, true, bs, N)) {
+                end_path = true;
+            } else {
+                L.depth++;
+                const float cosIn = dot(N, -L.direction);
+                if (cosIn < VCM_EPS_COSINE) {
+                    end_path = true;
+                } else {
+                    mis_on_hit(L, cosIn, h.t);
+                    const bool spec = bs.is_specular();
+                    if (!spec) {
+                        const uint32_t k = ls.nverts++;
+                        if (!ESTIMATE && k < VCM_MAX_VERTS) {
+                            const size_t o = (size_t)k * c.lcount + ls.p;
+                            vb.vA[o] = make_float4(hit.x, hit.y, hit.z, __uint_as_float(mi));
+                            vb.vB[o] = make_float4(L.throughput.x, L.throughput.y, L.throughput.z, L.dVCM);
+                            vb.vC[o] = make_float4(N.x, N.y, N.z, L.dVC);
+                            vb.vD[o] = make_float4(bs.fix.x, bs.fix.y, bs.fix.z, L.dVM);
+                            if (TEX && m.type == MAT_TEXTURE) vb.vE[o] = make_float4(kd.x, kd.y, kd.z, 0.f);
+                        }
+                        if (!ESTIMATE) connect_camera(S, L, bs, hit, c, vb.splat, stk);
+                    }
+                    if (c.maxPathLen < L.depth + 2) {
+                        end_path = true;
+                    } else {
+                        sample_scattering(L, hit, bs, c, rs);
+                        if (L.done) end_path = true;
+                    }
+                }
+            }
+        }
+        if (end_path) {
+            vb.vcount[ls.p] = ls.nverts;
+            rng_store(vb.rng, ls.slot, rs);
+            alive = false;
+        }
     }
-    vb.vcount[p] = nverts;
-    rng_store(vb.rng, slot, rs);
 }
 
 /* connectVertices (vcm.h:315-400) against light vertex k of this subpath */
@@ -719,24 +781,28 @@ __device__ inline bool connect_light(const DevScene& S, const Subpath& C, const 
     return true;
 }
 
-/* cameraPass (VCMCameraPass.cu:48-80), initCameraPayload (:100-135), cameraHit (vcm.h:527-628) */
-template <bool TEX>
+/* cameraPass (VCMCameraPass.cu:48-80), initCameraPayload (:100-135), cameraHit (vcm.h:527-628)
+ *
+ * Persistent waves with per-lane refill: a wave takes 64-pixel work items (one 8x8 tile
+ * each) from a device counter and a lane whose camera subpath has ended starts the next
+ * pixel of the wave's item at the top of the following round, so the rounds stay full
+ * instead of running, per wave, as long as its longest subpath (the one-pixel-per-lane
+ * form measured a node-loop SIMT efficiency of 0.21).  Each subpath's arithmetic is
+ * unchanged; only which lane runs it, and when, differs. */
 #ifndef ORX_VCM_CAMERA_WAVES
 #define ORX_VCM_CAMERA_WAVES 4 /* waves per SIMD the camera kernel is register-capped for (A/B: make vcm3) */
 #endif
-__global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScene S, VcmBufs vb, VcmConsts c) {
-    ORX_STACK_DECL;
-    uint32_t* stk = ORX_STACK_PTR;
-    const uint32_t tilesX = (c.W + 7) / 8;
-    const uint32_t x = (blockIdx.x % tilesX) * 8 + (threadIdx.x & 7);
-    const uint32_t j = (blockIdx.x / tilesX) * 8 + (threadIdx.x >> 3); /* own row j = image row rank + j*world */
-    /* lanes outside the image stay in the wave (they take part in the shadow-ray flushes) */
-    const bool inimg = x < c.W && j < c.rows;
-    const uint32_t y = c.rank + j * c.world;
-    const uint32_t p = inimg ? x + j * c.W : 0u;
-    const size_t slot = inimg ? (size_t)j * vb.RW + x : 0;
-    Rng rs = rng_load(vb.rng, slot);
-    Subpath C;
+struct CamPixel {
+    uint32_t p;
+    size_t slot;
+    uint32_t nverts;
+};
+__device__ __forceinline__ void camera_start(const VcmBufs& vb, const VcmConsts& c, uint32_t x, uint32_t j,
+                                             CamPixel& px, Rng& rs, Subpath& C) {
+    const uint32_t y = c.rank + j * c.world; /* own row j = image row rank + j*world */
+    px.p = x + j * c.W;
+    px.slot = (size_t)j * vb.RW + x;
+    rs = rng_load(vb.rng, px.slot);
     C.throughput = mk1(1.0f);
     C.color = mk1(0.f);
     C.depth = 0;
@@ -755,19 +821,78 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
     const float areaSamplePdf = 1.f / pixelArea;
     const float cameraPdfW = areaSamplePdf * i2s;
     C.dVCM = (float)c.count / cameraPdfW;
-    const uint32_t nverts = inimg ? vb.vcount[p] : 0u;
+    px.nverts = vb.vcount[px.p];
+}
+__device__ __forceinline__ void camera_finish(const VcmBufs& vb, const CamPixel& px, const Rng& rs, const Subpath& C) {
+    const size_t o3 = 3 * (size_t)px.p;
+    vb.cam[o3 + 0] = C.color.x;
+    vb.cam[o3 + 1] = C.color.y;
+    vb.cam[o3 + 2] = C.color.z;
+    const float ox = vb.output[o3 + 0] + vb.splat_in[o3 + 0];
+    const float oy = vb.output[o3 + 1] + vb.splat_in[o3 + 1];
+    const float oz = vb.output[o3 + 2] + vb.splat_in[o3 + 2];
+    vb.output[o3 + 0] = ox + C.color.x;
+    vb.output[o3 + 1] = oy + C.color.y;
+    vb.output[o3 + 2] = oz + C.color.z;
+    rng_store(vb.rng, px.slot, rs);
+}
+
+template <bool TEX>
+__global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScene S, VcmBufs vb, VcmConsts c) {
+    ORX_STACK_DECL;
+    uint32_t* stk = ORX_STACK_PTR;
+    const uint32_t tilesX = (c.W + 7) / 8;
+    const uint32_t total = tilesX * ((c.rows + 7) / 8) * 64u; /* work item = tile * 64 + lane of the tile */
+    const uint32_t lane = threadIdx.x & 63;
     /* The connections' shadow rays are deferred to a per-wave queue and traced
      * by all 64 lanes together (lanes whose subpath has ended help too): traced
      * in place, inside the divergent per-vertex loop, they ran at ~8 % lane
      * utilisation.  Every subpath still adds its unoccluded contributions in
      * the reference order (light sample, then light vertices 0..n-1), so the
      * colour is unchanged bit for bit. */
-    const uint32_t lane = threadIdx.x & 63;
     float4* q = vb.shq + (size_t)blockIdx.x * VCM_SHQ_PER_WAVE;   /* [64 * 10][2] entries */
     float4* qhit = q + 2 * 64 * (VCM_MAX_VERTS + 1);              /* [64] connection points */
-    bool alive = inimg;
+    CamPixel px;
+    px.p = 0;
+    px.slot = 0;
+    px.nverts = 0;
+    Rng rs = {};
+    Subpath C = {};
+    bool alive = false;
+    uint32_t next = 0, end = 0; /* the wave's current work item range (uniform) */
+    bool exhausted = false;
     for (;;) {
-        if (!__ballot(alive)) break;
+        /* refill: lanes without a subpath start the next pixels of the wave's item */
+        for (;;) {
+            const uint64_t need = __ballot(!alive);
+            if (!need) break;
+            if (next >= end) {
+                if (exhausted) break;
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(vb.work, 64u);
+                base = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)base, 0, 64));
+                if (base >= total) {
+                    exhausted = true;
+                    break;
+                }
+                next = base;
+                end = base + 64u;
+            }
+            const uint32_t avail = end - next;
+            const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+            if (!alive && rank < avail) {
+                const uint32_t item = next + rank, tile = item >> 6;
+                const uint32_t x = (tile % tilesX) * 8 + (item & 7), j = (tile / tilesX) * 8 + ((item >> 3) & 7);
+                if (x < c.W && j < c.rows) {
+                    camera_start(vb, c, x, j, px, rs, C);
+                    alive = true;
+                }
+            }
+            const uint32_t n = (uint32_t)__popcll(need);
+            next += n < avail ? n : avail;
+        }
+        const bool was_alive = alive;
+        if (!__ballot(was_alive)) break; /* only once the work is exhausted */
         uint32_t npend = 0;
         bool spec = true, last = false;
         VBsdf bs;
@@ -821,7 +946,7 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
         uint32_t qbase = 0;
         {
             /* upper bound first (1 + n vertices), real count after building */
-            const uint32_t nv = nverts < VCM_MAX_VERTS ? nverts : VCM_MAX_VERTS;
+            const uint32_t nv = px.nverts < VCM_MAX_VERTS ? px.nverts : VCM_MAX_VERTS;
             const uint32_t want = conn ? 1u + nv : 0u;
             uint32_t incl = want;
             for (int o = 1; o < 64; o <<= 1) {
@@ -839,7 +964,7 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
                     npend++;
                 }
                 for (uint32_t k = 0; k < nv; ++k) {
-                    if (connect_vertex<TEX>(S, C, bs, hit, vb, (size_t)k * c.lcount + p, c, sd, sl, ad)) {
+                    if (connect_vertex<TEX>(S, C, bs, hit, vb, (size_t)k * c.lcount + px.p, c, sd, sl, ad)) {
                         q[2 * (qbase + npend)] = make_float4(sd.x, sd.y, sd.z, sl);
                         q[2 * (qbase + npend) + 1] = make_float4(ad.x, ad.y, ad.z, __uint_as_float(lane));
                         npend++;
@@ -848,10 +973,10 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
                 /* unused reserved rows: no test */
                 for (uint32_t k = npend; k < want; ++k) q[2 * (qbase + k)] = make_float4(0.f, 0.f, 0.f, -1.f);
             }
-            const uint32_t total = __shfl(incl, 63, 64);
+            const uint32_t total_q = __shfl(incl, 63, 64);
             __threadfence_block();
             /* all lanes trace the wave's shadow rays; the result goes into .w of the contribution row */
-            for (uint32_t e = lane; e < total; e += 64) {
+            for (uint32_t e = lane; e < total_q; e += 64) {
                 const float4 r0 = q[2 * e];
                 if (r0.w < 0.f) continue;
                 const float4 r1 = q[2 * e + 1];
@@ -874,24 +999,37 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
                 if (C.done) alive = false;
             }
         }
+        if (was_alive && !alive) camera_finish(vb, px, rs, C);
     }
-    if (!inimg) return;
-    const size_t o3 = 3 * (size_t)p;
-    vb.cam[o3 + 0] = C.color.x;
-    vb.cam[o3 + 1] = C.color.y;
-    vb.cam[o3 + 2] = C.color.z;
-    const float ox = vb.output[o3 + 0] + vb.splat_in[o3 + 0];
-    const float oy = vb.output[o3 + 1] + vb.splat_in[o3 + 1];
-    const float oz = vb.output[o3 + 2] + vb.splat_in[o3 + 2];
-    vb.output[o3 + 0] = ox + C.color.x;
-    vb.output[o3 + 1] = oy + C.color.y;
-    vb.output[o3 + 2] = oz + C.color.z;
-    rng_store(vb.rng, slot, rs);
+}
+
+/* persistent light-pass waves: as many as can be resident at once (4 per SIMD) */
+static uint32_t vcm_light_waves(uint32_t items) {
+    static uint32_t resident = 0;
+    if (!resident) {
+        int dev = 0, cus = 256;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        resident = (uint32_t)cus * 4u * 4u;
+    }
+    return items < resident ? items : resident;
+}
+/* persistent camera-pass waves: as many as can be resident at once */
+uint32_t vcm_camera_waves(uint32_t tiles) {
+    static uint32_t resident = 0;
+    if (!resident) {
+        int dev = 0, cus = 256;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        resident = (uint32_t)cus * 4u * ORX_VCM_CAMERA_WAVES;
+    }
+    return tiles < resident ? tiles : resident;
 }
 
 void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c, bool estimate) {
-    const uint32_t blocks = (c.lcount + 63) / 64;
+    const uint32_t blocks = vcm_light_waves((c.lcount + 63) / 64);
     if (blocks == 0) return;
+    hipMemsetAsync(vb.work + 1, 0, 4, s);
     const size_t lds = ORX_STACK_BYTES(S);
     if (vb.vE) {
         if (estimate) hipLaunchKernelGGL((k_vcm_light<true, true>), dim3(blocks), dim3(64), lds, s, S, vb, c);
@@ -902,8 +1040,9 @@ void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const
     }
 }
 void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
-    const uint32_t blocks = ((c.W + 7) / 8) * ((c.rows + 7) / 8);
+    const uint32_t blocks = vcm_camera_waves(((c.W + 7) / 8) * ((c.rows + 7) / 8));
     if (blocks == 0) return;
+    hipMemsetAsync(vb.work, 0, 4, s);
     if (vb.vE) hipLaunchKernelGGL(k_vcm_camera<true>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
     else hipLaunchKernelGGL(k_vcm_camera<false>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
 }
