@@ -437,9 +437,11 @@ extern "C" {
 int orx_trav_stats_read(orx_renderer* r, unsigned long long* out, int reset) {
     if (!r || !r->scene.trav_stats || hipDeviceSynchronize() != hipSuccess) return 1;
     if (hipMemcpy(out, r->scene.trav_stats, 96, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-    /* [16]: gather photons accepted (out must hold 17 values) */
+    /* [16]: gather photons accepted (out must hold 21 values) */
     if (r->pb.grid && hipMemcpy(out + 16, &r->pb.grid->st_accepted, 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-    if (reset && hipMemset(r->scene.trav_stats, 0, 128) != hipSuccess) return 1;
+    /* [17..20]: closest-hit node visits to BVH4 nodes with index < 21, 85, 341, 1365 (the top 2..5 levels) */
+    if (hipMemcpy(out + 17, r->scene.trav_stats + 16, 32, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+    if (reset && hipMemset(r->scene.trav_stats, 0, 256) != hipSuccess) return 1;
     /* [12..15]: gather lane batches, wave batches, lane rows, wave rows */
     if (r->pb.grid) {
         if (hipMemcpy(out + 12, &r->pb.grid->st_lane_batches, 32, hipMemcpyDeviceToHost) != hipSuccess) return 1;
@@ -806,8 +808,8 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     S.bvh_nodes = nodes4;
     S.stack_entries = nt ? stack_bound + 1 : 0;
 #ifdef ORX_TRAV_STATS
-    HIPCHK(r, r->d_tstats.ensure(128));
-    HIPCHK(r, hipMemset(r->d_tstats.p, 0, 128));
+    HIPCHK(r, r->d_tstats.ensure(256));
+    HIPCHK(r, hipMemset(r->d_tstats.p, 0, 256));
     S.trav_stats = r->d_tstats.as<unsigned long long>();
 #else
     S.trav_stats = nullptr;

@@ -402,10 +402,8 @@ __device__ __forceinline__ RayBox ray_box(f3 o, f3 d) {
  * axis is picked once per node from the ray's direction signs, so a child
  * costs 6 fma + 4 min/max (identical values to the min/max slab form).
  * Returns entry distances (+inf for misses) and child refs. */
-__device__ __forceinline__ void node_test(const DevBvh4* nodes, uint32_t idx, const RayBox& rb, float tmin, float tmax,
-                                          float t[4], uint32_t c[4]) {
-    const float4* p = reinterpret_cast<const float4*>(nodes + idx);
-    const float4 A = p[0], B = p[1], C = p[2], D = p[3];
+__device__ __forceinline__ void node_test_q(const float4 A, const float4 B, const float4 C, const float4 D,
+                                            const RayBox& rb, float tmin, float tmax, float t[4], uint32_t c[4]) {
     const uint32_t ex = __float_as_uint(A.w);
     const float sx = __uint_as_float((ex & 0xffu) << 23);
     const float sy = __uint_as_float(((ex >> 8) & 0xffu) << 23);
@@ -445,6 +443,11 @@ __device__ __forceinline__ void node_test(const DevBvh4* nodes, uint32_t idx, co
             t[i] = (t0 <= t1 && c[i] != ORX_EMPTY) ? t0 : INFINITY;
         }
     }
+}
+__device__ __forceinline__ void node_test(const DevBvh4* nodes, uint32_t idx, const RayBox& rb, float tmin, float tmax,
+                                          float t[4], uint32_t c[4]) {
+    const float4* p = reinterpret_cast<const float4*>(nodes + idx);
+    node_test_q(p[0], p[1], p[2], p[3], rb, tmin, tmax, t, c);
 }
 typedef float v2t __attribute__((ext_vector_type(2)));
 /* fp32-box node test: t = fma(bound, inv, -o*inv), two children per
@@ -487,6 +490,23 @@ __device__ __forceinline__ void cswap(float& ta, uint32_t& ca, float& tb, uint32
     ca = c;
 }
 
+/* Traversal policies (trace_closest_t / trace_any_t): the stack (StackL: the
+ * lane's column of the dynamic-LDS array [stack_entries][64]) and the node
+ * source (NodesG: S.bvh4).  Measured and dropped: a short LDS stack continued
+ * in global memory (5-8 waves per SIMD) and the top 85 / 341 nodes in LDS
+ * (DESIGN.md §4); neither made the photon pass faster. */
+struct StackL {
+    uint32_t* s;
+    __device__ __forceinline__ void push(int& sp, uint32_t v) const { s[(sp++) * 64] = v; }
+    __device__ __forceinline__ uint32_t pop(int& sp) const { return s[(--sp) * 64]; }
+};
+struct NodesG {
+    __device__ __forceinline__ void test(const DevScene& S, uint32_t idx, const RayBox& rb, float tmin, float tmax,
+                                         float t[4], uint32_t c[4]) const {
+        node_test(S.bvh4, idx, rb, tmin, tmax, t, c);
+    }
+};
+
 /* Optional traversal statistics (build with -DORX_TRAV_STATS): rays, inner
  * nodes visited, leaves visited, triangle tests — per ray type (closest/any). */
 #ifdef ORX_TRAV_STATS
@@ -494,6 +514,18 @@ __device__ __forceinline__ void cswap(float& ta, uint32_t& ca, float& tb, uint32
 #define ORX_TS_INC(v, n) (v) += (n)
 /* wave-level loop iterations: counted by the wave's first active lane */
 #define ORX_TS_WAVE(v) (v) += ((uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1) == (threadIdx.x & 63u))
+#define ORX_TS_DECL_TOP uint32_t ts_top[4] = {0, 0, 0, 0}
+#define ORX_TS_TOP(idx)                                                     \
+    do {                                                                    \
+        ts_top[0] += (idx) < 21u;                                           \
+        ts_top[1] += (idx) < 85u;                                           \
+        ts_top[2] += (idx) < 341u;                                          \
+        ts_top[3] += (idx) < 1365u;                                         \
+    } while (0)
+#define ORX_TS_FLUSH_TOP()                                                  \
+    do {                                                                    \
+        for (int q_ = 0; q_ < 4; q_++) atomicAdd(&S.trav_stats[16 + q_], (unsigned long long)ts_top[q_]); \
+    } while (0)
 #define ORX_TS_FLUSH(base)                                                  \
     do {                                                                    \
         atomicAdd(&S.trav_stats[(base) + 0], 1ull);                       \
@@ -505,6 +537,9 @@ __device__ __forceinline__ void cswap(float& ta, uint32_t& ca, float& tb, uint32
     } while (0)
 #else
 #define ORX_TS_DECL
+#define ORX_TS_DECL_TOP
+#define ORX_TS_TOP(idx)
+#define ORX_TS_FLUSH_TOP()
 #define ORX_TS_INC(v, n)
 #define ORX_TS_WAVE(v)
 #define ORX_TS_FLUSH(base)
@@ -516,7 +551,9 @@ __device__ __forceinline__ void cswap(float& ta, uint32_t& ca, float& tb, uint32
  * Triangles: near-first BVH4 traversal; the hit children of a node are
  * sorted by entry distance, the nearest is taken and the others are pushed
  * far-to-near on the lane's LDS stack. */
-__device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& h, uint32_t* stk) {
+template <class STK, class NODES>
+__device__ inline bool trace_closest_t(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& h, const STK& stk,
+                                       const NODES& nodes) {
     float best = tmax;
     int32_t bp = -1;
     uint32_t bslot = 0;
@@ -543,6 +580,7 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
         int sp = 0;
         uint32_t ref = 0; /* root */
         ORX_TS_DECL;
+        ORX_TS_DECL_TOP;
         /* speculative while-while (Aila & Laine 2009): a lane that reaches a
          * leaf postpones it and keeps descending until every lane of the wave
          * holds a leaf, then all process theirs together */
@@ -551,8 +589,9 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
             while (!(ref & ORX_LEAF) && ref != ORX_DONE) {
                 float ct[4];
                 uint32_t cc[4];
-                node_test(S.bvh4, ref, rb, tmin, best, ct, cc);
+                nodes.test(S, ref, rb, tmin, best, ct, cc);
                 ORX_TS_INC(ts_nodes, 1);
+                ORX_TS_TOP(ref);
                 ORX_TS_WAVE(ts_wn);
                 cswap(ct[0], cc[0], ct[1], cc[1]);
                 cswap(ct[2], cc[2], ct[3], cc[3]);
@@ -560,16 +599,16 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
                 cswap(ct[1], cc[1], ct[3], cc[3]);
                 cswap(ct[1], cc[1], ct[2], cc[2]);
                 if (ct[0] != INFINITY) {
-                    if (ct[3] != INFINITY) stk[(sp++) * 64] = cc[3];
-                    if (ct[2] != INFINITY) stk[(sp++) * 64] = cc[2];
-                    if (ct[1] != INFINITY) stk[(sp++) * 64] = cc[1];
+                    if (ct[3] != INFINITY) stk.push(sp, cc[3]);
+                    if (ct[2] != INFINITY) stk.push(sp, cc[2]);
+                    if (ct[1] != INFINITY) stk.push(sp, cc[1]);
                     ref = cc[0];
                 } else {
-                    ref = sp ? stk[(--sp) * 64] : ORX_DONE;
+                    ref = sp ? stk.pop(sp) : ORX_DONE;
                 }
                 if ((ref & ORX_LEAF) && !(lf & ORX_LEAF)) {
                     lf = ref;
-                    ref = sp ? stk[(--sp) * 64] : ORX_DONE;
+                    ref = sp ? stk.pop(sp) : ORX_DONE;
                 }
                 if (!__ballot(!(lf & ORX_LEAF))) break;
             }
@@ -594,10 +633,11 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
                     }
                 }
                 lf = ref; /* another leaf postponed behind it: process it too */
-                if (ref & ORX_LEAF) ref = sp ? stk[(--sp) * 64] : ORX_DONE;
+                if (ref & ORX_LEAF) ref = sp ? stk.pop(sp) : ORX_DONE;
             }
         }
         ORX_TS_FLUSH(0);
+        ORX_TS_FLUSH_TOP();
     }
     if (bp < 0) return false;
     h.t = best;
@@ -607,6 +647,10 @@ __device__ inline bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, 
     h.g = bg;
     h.sn = sn;
     return true;
+}
+__device__ __forceinline__ bool trace_closest(const DevScene& S, f3 o, f3 d, float tmin, float tmax, Hit& h,
+                                              uint32_t* stk) {
+    return trace_closest_t(S, o, d, tmin, tmax, h, StackL{stk}, NodesG{});
 }
 /* Resumable closest-hit traversal for the wavefront passes: the same
  * computation as trace_closest, split so that a persistent kernel can run one
@@ -709,7 +753,9 @@ __device__ __forceinline__ void trace_round(const DevScene& S, TraceState& T, ui
 
 /* any hit in (tmin,tmax): every material's RayType::SHADOW any-hit is
  * gatherAnyHitOnNonEmitter (Material.cpp:18-26, DirectRadianceEstimation.cu:79-83) */
-__device__ inline bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, float tmax, uint32_t* stk) {
+template <class STK, class NODES>
+__device__ inline bool trace_any_t(const DevScene& S, f3 o, f3 d, float tmin, float tmax, const STK& stk,
+                                   const NODES& nodes) {
     float t;
     for (uint32_t i = 0; i < S.nq; i++)
         if (isect_quad(S.quads[i], o, d, tmin, tmax, t)) return true;
@@ -727,21 +773,21 @@ __device__ inline bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, floa
             while (!(ref & ORX_LEAF) && ref != ORX_DONE) {
                 float ct[4];
                 uint32_t cc[4];
-                node_test(S.bvh4, ref, rb, tmin, tmax, ct, cc);
+                nodes.test(S, ref, rb, tmin, tmax, ct, cc);
                 ORX_TS_INC(ts_nodes, 1);
                 ORX_TS_WAVE(ts_wn);
                 uint32_t next = ORX_DONE;
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
                     if (ct[i] != INFINITY) {
-                        if (next != ORX_DONE) stk[(sp++) * 64] = next;
+                        if (next != ORX_DONE) stk.push(sp, next);
                         next = cc[i];
                     }
                 }
-                ref = next != ORX_DONE ? next : (sp ? stk[(--sp) * 64] : ORX_DONE);
+                ref = next != ORX_DONE ? next : (sp ? stk.pop(sp) : ORX_DONE);
                 if ((ref & ORX_LEAF) && !(lf & ORX_LEAF)) {
                     lf = ref;
-                    ref = sp ? stk[(--sp) * 64] : ORX_DONE;
+                    ref = sp ? stk.pop(sp) : ORX_DONE;
                 }
                 if (!__ballot(!(lf & ORX_LEAF))) break;
             }
@@ -759,12 +805,16 @@ __device__ inline bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, floa
                     }
                 }
                 lf = ref;
-                if (ref & ORX_LEAF) ref = sp ? stk[(--sp) * 64] : ORX_DONE;
+                if (ref & ORX_LEAF) ref = sp ? stk.pop(sp) : ORX_DONE;
             }
         }
         ORX_TS_FLUSH(4);
     }
     return false;
+}
+
+__device__ __forceinline__ bool trace_any(const DevScene& S, f3 o, f3 d, float tmin, float tmax, uint32_t* stk) {
+    return trace_any_t(S, o, d, tmin, tmax, StackL{stk}, NodesG{});
 }
 
 __device__ __forceinline__ uint32_t prim_material(const DevScene& S, const Hit& h) {

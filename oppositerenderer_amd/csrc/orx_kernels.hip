@@ -174,10 +174,123 @@ __device__ __forceinline__ void photon_emit(const DevScene& S, const PixelBufs& 
     P.mask = 0;
 }
 
+/* One bounce of a photon path (Diffuse.cu:92-135, Glossy.cu:94-137, Mirror.cu:65-77,
+ * Glass.cu:164-205, DiffuseEmitter.cu:56-59); false once the path has ended (its
+ * deposit mask and RNG state are then stored). */
+template <class STK, class NODES>
+__device__ __forceinline__ bool photon_bounce(const DevScene& S, const PixelBufs& px, const PhotonBufs& pb,
+                                              const Consts& c, PhotonPath& P, Rng& rs, const STK& stk,
+                                              const NODES& nodes, float& lo_x, float& lo_y, float& lo_z,
+                                              float& hi_x, float& hi_y, float& hi_z) {
+    bool done = false;
+    Hit h;
+    if (!trace_closest_t(S, P.o, P.d, P.tmin, RT_DEFAULT_MAX, h, stk, nodes)) {
+        done = true;
+    } else {
+        const DevMaterial& m = S.mats[prim_material(S, h)];
+        const f3 hitPoint = P.o + P.d * h.t;
+        if (m.type == MAT_DIFFUSE || m.type == MAT_GLOSSY || m.type == MAT_TEXTURE) {
+            /* Texture.cu:116-175 differs only in Kd = texel colour,
+             * the weight cutoff (0.01) and the new ray's tmin (0.01) */
+            const bool tex = m.type == MAT_TEXTURE;
+            const f3 N = shading_normal(S, h);
+            if (P.depth >= 1 && P.numStored < pb.D) {
+                const uint32_t si = P.p_local * pb.D + P.numStored;
+                float4* rec = pb.slots + 4 * (size_t)si;
+                rec[0] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, P.power.x);
+                pb.pos4[si] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, 0.f);
+                rec[1] = make_float4(P.d.x, P.d.y, P.d.z, P.power.y);
+                rec[2].x = P.power.z;
+                /* the hash's STORE_PHOTON (store_photon.h:19-25) counts every deposit */
+                if (fmax3(P.power) > 0 || pb.hash) {
+                    P.mask |= 1u << P.numStored;
+                    lo_x = fminf(lo_x, hitPoint.x); lo_y = fminf(lo_y, hitPoint.y); lo_z = fminf(lo_z, hitPoint.z);
+                    hi_x = fmaxf(hi_x, hitPoint.x); hi_y = fmaxf(hi_y, hitPoint.y); hi_z = fmaxf(hi_z, hitPoint.z);
+                }
+                P.numStored++;
+            }
+            const f3 Kd = tex ? tex_color(S, m, h) : m.Kd;
+            P.power = P.power * Kd;
+            P.weight *= fmax3(Kd);
+            if (P.depth >= 3) {
+                float probContinue = favgf(Kd);
+                float probSample = rnd(rs);
+                if (probSample >= probContinue) done = true;
+                else P.power = P.power / probContinue;
+            }
+            if (!done) {
+                P.depth++;
+                if (P.depth >= c.max_photon_depth || (double)P.weight < (tex ? 0.01 : 0.001) ||
+                    P.numStored >= pb.Dlim) {
+                    done = true;
+                } else {
+                    float s0 = rnd(rs);
+                    float s1 = rnd(rs);
+                    P.d = sample_hemisphere_cos(N, s0, s1);
+                    P.o = hitPoint;
+                    P.tmin = tex ? 0.01f : 0.0001f;
+                }
+            }
+        } else if (m.type == MAT_EMITTER) {
+            done = true;
+        } else if (m.type == MAT_MIRROR) {
+            const f3 N = shading_normal(S, h);
+            P.depth++;
+            if (P.depth <= c.max_photon_depth) {
+                P.power = P.power * m.Kr;
+                P.d = reflect(P.d, N);
+                P.o = hitPoint;
+                P.tmin = 0.0001f;
+            } else {
+                done = true;
+            }
+        } else {
+            const f3 wsn = shading_normal(S, h);
+            const bool outside = dot(wsn, P.d) < 0;
+            const f3 N = outside ? wsn : -wsn;
+            const float n1 = outside ? 1.0f : m.ior, n2 = outside ? m.ior : 1.0f;
+            f3 refr;
+            bool valid;
+            const float refl = glass_reflect_factor(P.d, N, n1, n2, refr, valid);
+            const float sample = rnd(rs);
+            const f3 nd = (sample <= refl) ? reflect(P.d, N) : refr;
+            P.depth++;
+            if (P.depth <= c.max_photon_depth) {
+                P.o = hitPoint;
+                P.d = nd;
+                P.tmin = 0.0001f;
+            } else {
+                done = true;
+            }
+        }
+    }
+    if (done) {
+        pb.vmask[P.p_local] = (uint8_t)P.mask;
+        rng_store(px.rng, P.slot, rs);
+        return false;
+    }
+    return true;
+}
+__device__ __forceinline__ void photon_bbox_flush(const PhotonBufs& pb, float lo_x, float lo_y, float lo_z, float hi_x,
+                                                  float hi_y, float hi_z, uint32_t rep, uint32_t lane) {
+    /* wave AABB -> device-wide ordered-int atomics (one lane per component) */
+    lo_x = wave_min(lo_x); lo_y = wave_min(lo_y); lo_z = wave_min(lo_z);
+    hi_x = wave_max(hi_x); hi_y = wave_max(hi_y); hi_z = wave_max(hi_z);
+    /* 64 replicas per component keep same-address atomic contention low */
+    if (lane < 6) {
+        float v = lane == 0 ? lo_x : lane == 1 ? lo_y : lane == 2 ? lo_z : lane == 3 ? hi_x : lane == 4 ? hi_y : hi_z;
+        if (lane < 3) {
+            if (v != INFINITY) atomicMin(&pb.bbox[lane * BBOX_REPLICAS + rep], f2ord(v));
+        } else {
+            if (v != -INFINITY) atomicMax(&pb.bbox[lane * BBOX_REPLICAS + rep], f2ord(v));
+        }
+    }
+}
+
 template <bool PERSISTENT>
 __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, PhotonBufs pb, Consts c) {
     ORX_STACK_DECL;
-    uint32_t* stk = ORX_STACK_PTR;
+    const StackL stk{ORX_STACK_PTR};
     const uint32_t lane = threadIdx.x;
     const uint32_t total = pb.prows * pb.PW;
     float lo_x = INFINITY, lo_y = INFINITY, lo_z = INFINITY;
@@ -220,121 +333,18 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
             next += n < avail ? n : avail;
         }
         if (!__ballot(alive)) break;
-        if (alive) {
-            /* one bounce: Diffuse.cu:92-135, Glossy.cu:94-137, Mirror.cu:65-77,
-             * Glass.cu:164-205, DiffuseEmitter.cu:56-59 */
-            bool done = false;
-            Hit h;
-            if (!trace_closest(S, P.o, P.d, P.tmin, RT_DEFAULT_MAX, h, stk)) {
-                done = true;
-            } else {
-                const DevMaterial& m = S.mats[prim_material(S, h)];
-                const f3 hitPoint = P.o + P.d * h.t;
-                if (m.type == MAT_DIFFUSE || m.type == MAT_GLOSSY || m.type == MAT_TEXTURE) {
-                    /* Texture.cu:116-175 differs only in Kd = texel colour,
-                     * the weight cutoff (0.01) and the new ray's tmin (0.01) */
-                    const bool tex = m.type == MAT_TEXTURE;
-                    const f3 N = shading_normal(S, h);
-                    if (P.depth >= 1 && P.numStored < pb.D) {
-                        const uint32_t si = P.p_local * pb.D + P.numStored;
-                        float4* rec = pb.slots + 4 * (size_t)si;
-                        rec[0] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, P.power.x);
-                        pb.pos4[si] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, 0.f);
-                        rec[1] = make_float4(P.d.x, P.d.y, P.d.z, P.power.y);
-                        rec[2].x = P.power.z;
-                        /* the hash's STORE_PHOTON (store_photon.h:19-25) counts every deposit */
-                        if (fmax3(P.power) > 0 || pb.hash) {
-                            P.mask |= 1u << P.numStored;
-                            lo_x = fminf(lo_x, hitPoint.x); lo_y = fminf(lo_y, hitPoint.y); lo_z = fminf(lo_z, hitPoint.z);
-                            hi_x = fmaxf(hi_x, hitPoint.x); hi_y = fmaxf(hi_y, hitPoint.y); hi_z = fmaxf(hi_z, hitPoint.z);
-                        }
-                        P.numStored++;
-                    }
-                    const f3 Kd = tex ? tex_color(S, m, h) : m.Kd;
-                    P.power = P.power * Kd;
-                    P.weight *= fmax3(Kd);
-                    if (P.depth >= 3) {
-                        float probContinue = favgf(Kd);
-                        float probSample = rnd(rs);
-                        if (probSample >= probContinue) done = true;
-                        else P.power = P.power / probContinue;
-                    }
-                    if (!done) {
-                        P.depth++;
-                        if (P.depth >= c.max_photon_depth || (double)P.weight < (tex ? 0.01 : 0.001) ||
-                            P.numStored >= pb.Dlim) {
-                            done = true;
-                        } else {
-                            float s0 = rnd(rs);
-                            float s1 = rnd(rs);
-                            P.d = sample_hemisphere_cos(N, s0, s1);
-                            P.o = hitPoint;
-                            P.tmin = tex ? 0.01f : 0.0001f;
-                        }
-                    }
-                } else if (m.type == MAT_EMITTER) {
-                    done = true;
-                } else if (m.type == MAT_MIRROR) {
-                    const f3 N = shading_normal(S, h);
-                    P.depth++;
-                    if (P.depth <= c.max_photon_depth) {
-                        P.power = P.power * m.Kr;
-                        P.d = reflect(P.d, N);
-                        P.o = hitPoint;
-                        P.tmin = 0.0001f;
-                    } else {
-                        done = true;
-                    }
-                } else {
-                    const f3 wsn = shading_normal(S, h);
-                    const bool outside = dot(wsn, P.d) < 0;
-                    const f3 N = outside ? wsn : -wsn;
-                    const float n1 = outside ? 1.0f : m.ior, n2 = outside ? m.ior : 1.0f;
-                    f3 refr;
-                    bool valid;
-                    const float refl = glass_reflect_factor(P.d, N, n1, n2, refr, valid);
-                    const float sample = rnd(rs);
-                    const f3 nd = (sample <= refl) ? reflect(P.d, N) : refr;
-                    P.depth++;
-                    if (P.depth <= c.max_photon_depth) {
-                        P.o = hitPoint;
-                        P.d = nd;
-                        P.tmin = 0.0001f;
-                    } else {
-                        done = true;
-                    }
-                }
-            }
-            if (done) {
-                pb.vmask[P.p_local] = (uint8_t)P.mask;
-                rng_store(px.rng, P.slot, rs);
-                alive = false;
-            }
-        }
+        if (alive) alive = photon_bounce(S, px, pb, c, P, rs, stk, NodesG{}, lo_x, lo_y, lo_z, hi_x, hi_y, hi_z);
     }
-    /* wave AABB -> device-wide ordered-int atomics (one lane per component) */
-    lo_x = wave_min(lo_x); lo_y = wave_min(lo_y); lo_z = wave_min(lo_z);
-    hi_x = wave_max(hi_x); hi_y = wave_max(hi_y); hi_z = wave_max(hi_z);
-    /* 64 replicas per component keep same-address atomic contention low */
-    const uint32_t rep = blockIdx.x & (BBOX_REPLICAS - 1);
-    if (lane < 6) {
-        float v = lane == 0 ? lo_x : lane == 1 ? lo_y : lane == 2 ? lo_z : lane == 3 ? hi_x : lane == 4 ? hi_y : hi_z;
-        if (lane < 3) {
-            if (v != INFINITY) atomicMin(&pb.bbox[lane * BBOX_REPLICAS + rep], f2ord(v));
-        } else {
-            if (v != -INFINITY) atomicMax(&pb.bbox[lane * BBOX_REPLICAS + rep], f2ord(v));
-        }
-    }
+    photon_bbox_flush(pb, lo_x, lo_y, lo_z, hi_x, hi_y, hi_z, blockIdx.x & (BBOX_REPLICAS - 1), lane);
 }
+
 void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c) {
-    /* persistent grid: enough one-wave blocks to fill every SIMD several
-     * times over; each block drains the shared photon counter */
     const uint32_t total = pb.prows * pb.PW;
     static const int persistent = [] {
         const char* e = getenv("ORX_PHOTON_PERSISTENT");
         return e ? atoi(e) : 0;
     }();
-    if (persistent) {
+    if (persistent) { /* per-lane refill (A/B): one-wave blocks drain the shared photon counter */
         const uint32_t blocks = std::min<uint32_t>((total + 63) / 64, 256u * 4u * 8u);
         hipMemsetAsync(pb.work, 0, 4, s);
         hipLaunchKernelGGL(k_ppm_photon<true>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, px, pb, c);

@@ -24,7 +24,7 @@ r = renderer.OptixRenderer(_abi.default_config(seed=1645301512, photon_launch_wi
 r.initialize(0)
 r.initScene(sc)
 det = renderer.RenderRequestDetails(sc.default_camera.set_aspect_ratio(W / H), sc.name, method, W, H)
-buf = (C.c_ulonglong * 17)()
+buf = (C.c_ulonglong * 21)()
 radius = sc.initial_ppm_radius()
 for it in range(3):
     r.renderNextIteration(it, it, radius, False, det)
@@ -37,6 +37,8 @@ for it in range(3):
         print(f"it{it} {name:8s} rays {v[b]:12d}  nodes/ray {v[b + 1] / rays:6.2f}  leaves/ray {v[b + 2] / rays:6.2f}"
               f"  tris/ray {v[b + 3] / rays:6.2f}  SIMT node {v[b + 1] / max(1, 64 * wn):5.3f}"
               f"  leaf {v[b + 2] / max(1, 64 * wl):5.3f}")
+    print(f"it{it} closest node visits in the top BVH4 levels (index < 21/85/341/1365): "
+          + " ".join(f"{v[17 + q] / max(1, v[1]):5.3f}" for q in range(4)))
     if method == 2 and os.environ.get("ORX_GATHER_UNION", "0") != "0":
         lc, up, nr = v[12], v[13], v[14]
         print(f"it{it} union    lane candidates/px {lc / (W * H):8.1f}  union photons/px {64 * up / (W * H):8.1f}"
