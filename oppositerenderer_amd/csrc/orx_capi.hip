@@ -10,6 +10,7 @@
  * on the device and are summed in-kernel).
  */
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <cmath>
@@ -1043,7 +1044,18 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     return ORX_OK;
 }
 
+/* roctx ranges around every pass (the role of the reference's NVTX ranges,
+ * renderer/helpers/nsight.h:17-199): visible in `rocprofv3 --marker-trace`;
+ * they span the host-side enqueue, the HIP events above time the device work */
+static const char* const PASS_NAME[P_COUNT] = {
+    "OptixEntryPoint::RAYTRACE_PASS (ppm_eye)",   "OptixEntryPoint::PHOTON_PASS (ppm_photon)",
+    "Creating photon map (grid_hash)",            "Creating photon map (grid_scan)",
+    "Creating photon map (grid_scatter)",         "OptixEntryPoint::INDIRECT_RADIANCE_ESTIMATION (ppm_gather)",
+    "OptixEntryPoint::PPM_DIRECT_RADIANCE_ESTIMATION_PASS (ppm_direct_output)",
+    "OptixEntryPoint::PT_RAYTRACE_PASS (pt)",     "OptixEntryPoint::VCM_LIGHT_PASS (vcm_light)",
+    "OptixEntryPoint::VCM_CAMERA_PASS (vcm_camera)"};
 static inline void ev_begin(orx_renderer* r, int p) {
+    roctxRangePushA(PASS_NAME[p]);
     if (!r->timing || r->ev_n[p] >= EV_POOL) return;
     auto& v = r->ev[p];
     size_t need = 2 * (size_t)r->ev_n[p] + 2;
@@ -1055,12 +1067,14 @@ static inline void ev_begin(orx_renderer* r, int p) {
     hipEventRecord(v[2 * r->ev_n[p]], r->use_ext ? r->ext_stream : r->stream);
 }
 static inline void ev_end(orx_renderer* r, int p) {
+    roctxRangePop();
     if (!r->timing || r->ev_n[p] >= EV_POOL || r->ev[p].size() < 2 * (size_t)r->ev_n[p] + 2) return;
     hipEventRecord(r->ev[p][2 * r->ev_n[p] + 1], r->use_ext ? r->ext_stream : r->stream);
     r->ev_n[p]++;
 }
 /* the same on an explicit stream (the overlapped direct pass) */
 static inline void ev_begin_on(orx_renderer* r, int p, hipStream_t st) {
+    roctxRangePushA(PASS_NAME[p]);
     if (!r->timing || r->ev_n[p] >= EV_POOL) return;
     auto& v = r->ev[p];
     while (v.size() < 2 * (size_t)r->ev_n[p] + 2) {
@@ -1071,6 +1085,7 @@ static inline void ev_begin_on(orx_renderer* r, int p, hipStream_t st) {
     hipEventRecord(v[2 * r->ev_n[p]], st);
 }
 static inline void ev_end_on(orx_renderer* r, int p, hipStream_t st) {
+    roctxRangePop();
     if (!r->timing || r->ev_n[p] >= EV_POOL || r->ev[p].size() < 2 * (size_t)r->ev_n[p] + 2) return;
     hipEventRecord(r->ev[p][2 * r->ev_n[p] + 1], st);
     r->ev_n[p]++;
@@ -1456,11 +1471,21 @@ static orx_status ppm_pipelined_iteration(orx_renderer* r, const orx_request* de
     return ORX_OK;
 }
 
+static orx_status render_next_iteration(orx_renderer* r, uint64_t local_iteration_number, float ppm_radius,
+                                        const orx_request* det);
 orx_status orx_render_next_iteration(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
                                      float ppm_radius, int create_output, const orx_request* det) {
     (void)create_output; /* ignored by the reference engine too */
-    (void)iteration_number;
     if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
+    char range[48]; /* OptixRenderer.cpp:518-520 */
+    snprintf(range, sizeof range, "OptixRenderer::Trace Iteration %llu", (unsigned long long)iteration_number);
+    roctxRangePushA(range);
+    const orx_status st = render_next_iteration(r, local_iteration_number, ppm_radius, det);
+    roctxRangePop();
+    return st;
+}
+static orx_status render_next_iteration(orx_renderer* r, uint64_t local_iteration_number, float ppm_radius,
+                                        const orx_request* det) {
     if (det->method != ORX_METHOD_PATH_TRACING && det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING &&
         det->method != ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING)
         return set_err(r, ORX_ERR_UNSUPPORTED, "render method not supported by this build");

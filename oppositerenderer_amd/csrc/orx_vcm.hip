@@ -579,8 +579,11 @@ __device__ __forceinline__ void light_start(const DevScene& S, const VcmBufs& vb
     L.dVM = L.dVC * c.misVc;
 }
 
+#ifndef ORX_VCM_LIGHT_WAVES
+#define ORX_VCM_LIGHT_WAVES 3 /* waves per SIMD the light kernel is register-capped for (4: 3.63 ms, 3: 3.33) */
+#endif
 template <bool ESTIMATE, bool TEX>
-__global__ __launch_bounds__(64, 4) void k_vcm_light(DevScene S, VcmBufs vb, VcmConsts c) {
+__global__ __launch_bounds__(64, ORX_VCM_LIGHT_WAVES) void k_vcm_light(DevScene S, VcmBufs vb, VcmConsts c) {
     ORX_STACK_DECL;
     uint32_t* stk = ORX_STACK_PTR;
     const uint32_t lane = threadIdx.x & 63;
@@ -973,6 +976,17 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
                 /* unused reserved rows: no test */
                 for (uint32_t k = npend; k < want; ++k) q[2 * (qbase + k)] = make_float4(0.f, 0.f, 0.f, -1.f);
             }
+            /* the next vertex's direction before the shadow tests: it consumes the RNG after
+             * the connections (the reference order) and needs neither their outcome nor the
+             * colour, and the BSDF is then dead during the traversals (fewer live registers) */
+            if (alive) {
+                if (last) {
+                    alive = false;
+                } else {
+                    sample_scattering(C, hit, bs, c, rs);
+                    if (C.done) alive = false;
+                }
+            }
             const uint32_t total_q = __shfl(incl, 63, 64);
             __threadfence_block();
             /* all lanes trace the wave's shadow rays; the result goes into .w of the contribution row */
@@ -991,14 +1005,6 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
                 if (r0.w == -3.f) C.color = C.color + mk(r1.x, r1.y, r1.z);
             }
         }
-        if (alive) {
-            if (last) {
-                alive = false;
-            } else {
-                sample_scattering(C, hit, bs, c, rs);
-                if (C.done) alive = false;
-            }
-        }
         if (was_alive && !alive) camera_finish(vb, px, rs, C);
     }
 }
@@ -1010,7 +1016,7 @@ static uint32_t vcm_light_waves(uint32_t items) {
         int dev = 0, cus = 256;
         hipGetDevice(&dev);
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        resident = (uint32_t)cus * 4u * 4u;
+        resident = (uint32_t)cus * 4u * ORX_VCM_LIGHT_WAVES;
     }
     return items < resident ? items : resident;
 }
