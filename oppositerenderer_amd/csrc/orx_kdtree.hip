@@ -673,8 +673,9 @@ __global__ __launch_bounds__(64) void k_ppm_gather_kd(GatherIn gi, PhotonBufs pb
     extern __shared__ uint32_t kd_stack[]; /* [entries][64] */
     const uint32_t lane = threadIdx.x;
     const uint32_t x = blockIdx.x * 8 + (lane & 7);
-    const uint32_t j = blockIdx.y * 8 + (lane >> 3);
-    const bool inimg = x < gi.W && j < gi.segments * gi.seg_rows;
+    const uint32_t y = blockIdx.y * 8 + (lane >> 3);
+    const uint32_t j = gather_row(gi, y);
+    const bool inimg = x < gi.W && y < gi.segments * gi.seg_rows;
     const size_t i = (size_t)j * gi.W + x;
     float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
     float2 Cc = make_float2(0.f, 0.f);
@@ -762,8 +763,9 @@ __global__ __launch_bounds__(64) void k_ppm_gather_kd_wave(GatherIn gi, PhotonBu
     extern __shared__ uint32_t kd_wstack[]; /* [entries][3]: node, mask lo, mask hi */
     const uint32_t lane = threadIdx.x;
     const uint32_t x = blockIdx.x * 8 + (lane & 7);
-    const uint32_t j = blockIdx.y * 8 + (lane >> 3);
-    const bool inimg = x < gi.W && j < gi.segments * gi.seg_rows;
+    const uint32_t y = blockIdx.y * 8 + (lane >> 3);
+    const uint32_t j = gather_row(gi, y);
+    const bool inimg = x < gi.W && y < gi.segments * gi.seg_rows;
     const size_t i = (size_t)j * gi.W + x;
     float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
     float2 Cc = make_float2(0.f, 0.f);

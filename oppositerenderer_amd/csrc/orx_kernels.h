@@ -179,6 +179,16 @@ struct GatherIn {
     float* indirect;    /* [segments*seg_rows*W*3] */
     uint32_t* dbg;      /* [segments*seg_rows*W*2] or NULL */
 };
+/* The gather kernels tile IMAGE rows y.  With several row-interleaved segments (the
+ * sharded gather: segment s = rank s holds image rows y = s + lj*segments) the hit points
+ * and the indirect output are segment-major, row j = s*seg_rows + lj: tiling j directly
+ * would give a wave 8 image rows that are `segments` apart (a union that grows with the
+ * rank count); tiling y keeps a wave's pixels neighbours in the image. */
+__device__ __forceinline__ uint32_t gather_row(const GatherIn& gi, uint32_t y) {
+    if (gi.segments <= 1) return y;
+    const uint32_t s = y % gi.segments, lj = y / gi.segments;
+    return s * gi.seg_rows + lj;
+}
 /* variant 0: one thread per pixel, 8x8 wave tiles (default); 1: wave-cooperative LDS staging */
 /* lds_pad: unused dynamic LDS per block, to cap the gather's blocks per CU when it overlaps other passes */
 void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, size_t lds_pad = 0);

@@ -1261,13 +1261,41 @@ __device__ __forceinline__ f4u ldp(__amdgpu_buffer_rsrc_t rs, uint32_t so, uint3
 }
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
 
+/* The reference's visit counters of a window (IndirectRadianceEstimation.cu:113/:124): every
+ * (z,y) row from x_lo to x_hi, whole rows, two offset reads per row.  Eight rows' reads are
+ * issued before any is used (one memory round trip per eight rows instead of per row). */
+__device__ __forceinline__ void window_visits(const uint32_t* __restrict__ offsets, uint32_t gx, uint32_t gy,
+                                              uint32_t x_lo, uint32_t x_hi, uint32_t y_lo, uint32_t ny,
+                                              uint32_t z_lo, uint32_t nrows, uint32_t& dC, uint32_t& dP) {
+    uint32_t z = z_lo, yy = y_lo;
+    for (uint32_t t0 = 0; t0 < nrows; t0 += 8) {
+        uint32_t a[8], b[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) {
+            a[k] = b[k] = 0;
+            if (t0 + k < nrows) {
+                const uint32_t from = x_lo + yy * gx + z * gx * gy;
+                a[k] = offsets[from];
+                b[k] = offsets[from + (x_hi - x_lo) + 1];
+                if (++yy == y_lo + ny) yy = y_lo, z++;
+            }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) dP += b[k] - a[k];
+    }
+    dC += nrows;
+}
+
 constexpr uint32_t GQ = 8; /* chord ranges per lane per phase A (LDS: GQ * 8 B per lane) */
 
 /* NSUB: sub-rows per cell row (SUBR^2, or 1 for the cell-order layout);
  * SUBOFS: sub-cell offsets present (bucket-sort grid) or cell offsets only
  * (atomic-rank grid, ORX_GRID_ATOMIC=1) */
 template <uint32_t NSUB, bool SUBOFS>
-__global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
+#ifndef ORX_GATHER_LANE_WAVES
+#define ORX_GATHER_LANE_WAVES 6 /* waves per SIMD the per-lane gather is register-capped for (no spills) */
+#endif
+__global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
                                                     uint32_t ntiles) {
     __shared__ uint2 rq[GQ][256];
     const uint32_t tid = threadIdx.x;
@@ -1276,11 +1304,12 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
     const uint32_t tile = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
     const uint32_t w = tid >> 6, l = tid & 63;
     const uint32_t x = (tile % ntx) * 16 + (w & 1) * 8 + (l & 7);
-    const uint32_t j = (tile / ntx) * 16 + (w >> 1) * 8 + (l >> 3);
+    const uint32_t y = (tile / ntx) * 16 + (w >> 1) * 8 + (l >> 3);
+    const uint32_t j = gather_row(gi, y);
     const GridParams g = *pb.grid;
     uint32_t dC = 0, dP = 0;
     ORX_TS_DECL;
-    const bool live = tile < ntiles && x < gi.W && j < gi.segments * gi.seg_rows;
+    const bool live = tile < ntiles && x < gi.W && y < gi.segments * gi.seg_rows;
     float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
     float2 Cc = make_float2(0.f, 0.f);
     size_t i = 0;
@@ -1314,6 +1343,7 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
         if (x_lo <= x_hi && y_lo <= y_hi && z_lo <= z_hi) {
             ny = y_hi - y_lo + 1;
             nrows = (z_hi - z_lo + 1) * ny;
+            window_visits(pb.offsets, g.gx, g.gy, x_lo, x_hi, y_lo, ny, z_lo, nrows, dC, dP);
         }
     }
     const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
@@ -1348,10 +1378,6 @@ __global__ __launch_bounds__(256) void k_ppm_gather(GatherIn gi, PhotonBufs pb, 
             const uint32_t z = z_lo + zq, yy = y_lo + (t - zq * ny);
             t++;
             const uint32_t row = yy * g.gx + z * g.gx * g.gy;
-            const uint32_t from = x_lo + row;
-            const uint32_t to = from + (x_hi - x_lo);
-            dC++;
-            dP += pb.offsets[to + 1] - pb.offsets[from];
             uint32_t offs[NSUB], ends[NSUB];
 #pragma unroll
             for (uint32_t sr = 0; sr < NSUB; sr++) {
@@ -1668,8 +1694,9 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
         const uint32_t per = (ntiles + 7) / 8;
         const uint32_t tile = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
         x = (tile % ntx) * 16 + (w & 1) * 8 + (l & 7);
-        j = (tile / ntx) * 16 + (w >> 1) * 8 + (l >> 3);
-        live = tile < ntiles && x < gi.W && j < gi.segments * gi.seg_rows;
+        const uint32_t y = (tile / ntx) * 16 + (w >> 1) * 8 + (l >> 3);
+        j = gather_row(gi, y);
+        live = tile < ntiles && x < gi.W && y < gi.segments * gi.seg_rows;
     }
     const GridParams g = *pb.grid;
     uint32_t dC = 0, dP = 0;
@@ -1706,13 +1733,9 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
         y_hi = (g.gy - 1) < uy ? (g.gy - 1) : uy;
         z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
         act = x_lo <= x_hi && y_lo <= y_hi && z_lo <= z_hi;
-        /* the reference's visit counters: every (z,y) row of the window, whole rows (:113/:124) */
-        for (uint32_t z = z_lo; act && z <= z_hi; z++)
-            for (uint32_t yy = y_lo; yy <= y_hi; yy++) {
-                const uint32_t from = x_lo + yy * g.gx + z * g.gx * g.gy;
-                dC++;
-                dP += pb.offsets[from + (x_hi - x_lo) + 1] - pb.offsets[from];
-            }
+        if (act) /* the reference's visit counters: every (z,y) row of the window, whole rows */
+            window_visits(pb.offsets, g.gx, g.gy, x_lo, x_hi, y_lo, y_hi - y_lo + 1, z_lo,
+                          (z_hi - z_lo + 1) * (y_hi - y_lo + 1), dC, dP);
     }
     const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
     const float inv2r2 = 1.0f / (2 * radius2);
@@ -1946,10 +1969,15 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
      * kernel with v_readlane broadcasts; 0 the per-lane kernel.  Measured (serial hall gather /
      * pipelined hall frame / 4K conference frame): 0: 2.5 ms / 7.9 ms / 120 ms;
      * 1: 2.81 / 7.68 / 77.2; 2: 1.91 / 7.02 / 53.3 */
-    static const int union_gather = [] {
+    static const int union_env = [] {
         const char* e = getenv("ORX_GATHER_UNION");
-        return e ? atoi(e) : 2;
+        return e ? atoi(e) : -1;
     }();
+    /* The sharded gather (segments = ranks) meets 1/N of the photons: at N >= 4 the wave union's
+     * per-sub-row work outweighs the photons it shares, and the per-lane kernel is faster
+     * (hall 1080p, tools/shard_model.py: N=8 0.93 ms per-lane against 1.20 union; N=2 1.65
+     * against 1.42) */
+    const int union_gather = union_env >= 0 ? union_env : (gi.segments >= 4 ? 0 : 2);
     if (union_gather == 2 && pb.subofs) {
         if (pb.nsub == 1)
             hipLaunchKernelGGL((k_ppm_gather_union<1, false, 1>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx, ntiles,
@@ -2046,8 +2074,9 @@ void launch_hash_build(hipStream_t s, const PhotonBufs& pb, const HashParams& hp
  * unfused arithmetic, so the sum is the oracle's bit for bit. */
 __global__ __launch_bounds__(64) void k_ppm_gather_hash(GatherIn gi, PhotonBufs pb, HashParams hp, Consts c) {
     const uint32_t x = blockIdx.x * 8 + (threadIdx.x & 7);
-    const uint32_t j = blockIdx.y * 8 + (threadIdx.x >> 3);
-    const bool inimg = x < gi.W && j < gi.segments * gi.seg_rows;
+    const uint32_t y = blockIdx.y * 8 + (threadIdx.x >> 3);
+    const uint32_t j = gather_row(gi, y);
+    const bool inimg = x < gi.W && y < gi.segments * gi.seg_rows;
     const size_t i = (size_t)j * gi.W + x;
     float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
     float2 Cc = make_float2(0.f, 0.f);

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out/t gpurun_out/sm
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t/gputest.log 2>&1 || { tail -30 gpurun_out/t/gputest.log; exit 1; }
+tail -2 gpurun_out/t/gputest.log
+timeout -k 10 400 python -u tools/shard_model.py 1 2 4 8 > gpurun_out/sm/model_default.txt 2>&1 && cut -c1-120 gpurun_out/sm/model_default.txt | grep N=
+timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/t/bench.log 2>&1 && tail -1 gpurun_out/t/bench.log | cut -c1-300

@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Per-rank cost of the strong-scaling sharded PPM at world size N, measured on one GPU.
+
+A renderer is set up as rank 0 of N (own pixel rows y = 0 mod N, own photon-launch rows
+of the fixed global launch), and its phases are run and timed one after the other with
+torch events: local passes (eye, photon, grid, direct), hit-point export, the gather of ALL
+W*H hit points against the local photons, and the finish (direct + output of the own rows).
+The full-image hit points come from a second, unsharded renderer's eye pass on the
+same camera and radius, rearranged into the ranks' row-interleaved segments (what the
+all-gather delivers).  The collectives are not run; their volumes are printed so the exchange
+over xGMI can be added by hand.  Usage: shard_model.py [N ...]  (default 1 2 4 8), hall 1080p, 2048^2."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from oppositerenderer_amd import _abi, multigpu, synthetic  # noqa: E402
+from oppositerenderer_amd.renderer import OptixRenderer, RenderRequestDetails, next_ppm_radius  # noqa: E402
+
+SEED = 1645301512
+
+
+def run(world, W=1920, H=1080, P=2048, iters=6, warm=2):
+    dev = torch.device("cuda", 0)
+    scene = synthetic.synthetic_hall()
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    det = RenderRequestDetails(cam, scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W, H)
+    req = det.to_abi()
+    gv = int(os.environ.get("MODEL_GATHER_VARIANT", "0"))  # 1: whole cell rows (no sub-rows)
+    r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P, gather_variant=gv))
+    r.initialize(0)
+    r.set_shard(0, world)
+    r.initScene(scene)
+    b = multigpu.DeviceShard(r, torch, dev)
+    full = OptixRenderer(_abi.default_config(seed=SEED + 1, photon_launch_width=16, photon_launch_height=16))
+    full.initialize(0)
+    full.initScene(scene)
+    fb = multigpu.DeviceShard(full, torch, dev)
+    fhp = fb.alloc(H * W * 10)
+    mr = (H + world - 1) // world
+    hp = b.alloc(mr * W * 10)
+
+    def segments(t):
+        """[H][W] planes A (4), B (4), C (2) -> N segments of mr rows, rows y = s + lj*N"""
+        A = t[:H * W * 4].view(H, W, 4)
+        B = t[H * W * 4:H * W * 8].view(H, W, 4)
+        Cc = t[H * W * 8:].view(H, W, 2)
+        out = []
+        for s_ in range(world):
+            for P_, k in ((A, 4), (B, 4), (Cc, 2)):
+                blk = torch.zeros(mr, W, k, device=dev)
+                rows = P_[s_::world]
+                blk[:rows.shape[0]] = rows
+                out.append(blk.reshape(-1))
+        return torch.cat(out)
+
+    part = b.alloc(world * mr * W * 3)
+    radius = scene.initial_ppm_radius()
+    names = ("local", "export", "gather", "finish")
+    tot = dict.fromkeys(names, 0.0)
+    for it in range(iters):
+        if it == warm:
+            r.reset_timing()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        ev[0].record()
+        b.local_passes(it, it, radius, req)
+        ev[1].record()
+        b.export_hitpoints(hp)
+        ev[2].record()
+        fb.local_passes(it, it, radius, req)
+        hp_all = segments(fhp) if fb.export_hitpoints(fhp) is None else None
+        ev[3].record()
+        b.gather_external(hp_all, world, part)
+        ev[4].record()
+        b.finish(part[:mr * W * 3].contiguous())
+        ev[5].record()
+        torch.cuda.synchronize()
+        if it >= warm:
+            tot["local"] += ev[0].elapsed_time(ev[1])
+            tot["export"] += ev[1].elapsed_time(ev[2])
+            tot["gather"] += ev[3].elapsed_time(ev[4])
+            tot["finish"] += ev[4].elapsed_time(ev[5])
+        radius = next_ppm_radius(radius, it)
+    n = iters - warm
+    ms = {k: round(v / n, 3) for k, v in tot.items()}
+    st = r.stats()
+    ni = max(1, st.timed_iterations)
+    passes = {name: round(st.pass_ms[i] / ni, 3) for i, name in enumerate(_abi.PASS_NAMES) if st.pass_ms[i] > 0}
+    allgather_mb = world * mr * W * 40 / 1e6
+    rs_mb = world * mr * W * 12 / 1e6
+    r.destroy()
+    full.destroy()
+    return ms, passes, allgather_mb, rs_mb
+
+
+if __name__ == "__main__":
+    worlds = [int(v) for v in sys.argv[1:]] or [1, 2, 4, 8]
+    for n in worlds:
+        ms, passes, ag, rs = run(n)
+        print(f"N={n}: per-rank serial {sum(ms.values()):.3f} ms {ms} | all-gather {ag:.0f} MB, "
+              f"reduce-scatter {rs:.0f} MB | passes {passes}", flush=True)
