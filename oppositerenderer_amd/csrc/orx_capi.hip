@@ -355,6 +355,12 @@ struct orx_renderer {
     hipStream_t aux = nullptr;   /* PPM direct pass, overlapped with the grid build and gather */
     hipEvent_t ev_photon_done = nullptr, ev_direct_done = nullptr;
     bool overlap_direct = false;
+    /* pipelined PPM: the eye pass of iteration i+1 runs on aux right behind the direct pass of i
+     * (the RNG chain), beside the grid build of i; ev_eye_done orders the photon pass after it.
+     * eye_chain: aux is already ordered after every earlier renderer-stream write the eye pass
+     * reads (the previous call was a pipelined iteration, nothing else enqueued since) */
+    hipEvent_t ev_eye_done = nullptr, ev_main = nullptr;
+    bool eye_chain = false;
     /* PPM iteration pipelining (world 1, uniform grid, own stream): the gather and output of
      * iteration i run on gstream beside the eye/photon/grid passes of iteration i+1, each
      * iteration on one of two buffer sets (hitpoints, direct, grid-ordered photons, offsets,
@@ -512,7 +518,9 @@ orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out)
         hipEventCreateWithFlags(&r->ev_gdone[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_gdone[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_photon_done, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&r->ev_direct_done, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&r->ev_direct_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&r->ev_eye_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&r->ev_main, hipEventDisableTiming) != hipSuccess) {
         delete r;
         return ORX_ERR_DEVICE;
     }
@@ -533,6 +541,8 @@ void orx_destroy(orx_renderer* r) {
     if (r->gstream) hipStreamDestroy(r->gstream);
     if (r->ev_photon_done) hipEventDestroy(r->ev_photon_done);
     if (r->ev_direct_done) hipEventDestroy(r->ev_direct_done);
+    if (r->ev_eye_done) hipEventDestroy(r->ev_eye_done);
+    if (r->ev_main) hipEventDestroy(r->ev_main);
     if (r->aux) hipStreamDestroy(r->aux);
     if (r->stream) hipStreamDestroy(r->stream);
     delete r;
@@ -1097,6 +1107,7 @@ static inline hipStream_t gather_stream(orx_renderer* r) { return r->shard_pipe 
 
 /* order everything later on the renderer's stream after a deferred gather + output */
 static void flush_pipeline(orx_renderer* r) {
+    r->eye_chain = false;
     if (!r->pend) return;
     hipStreamWaitEvent(cur_stream(r), r->ev_gdone[r->pp], 0);
     r->pend = false;
@@ -1105,6 +1116,7 @@ static void flush_pipeline(orx_renderer* r) {
 static orx_status sync_all(orx_renderer* r) {
     flush_pipeline(r);
     HIPCHK(r, hipStreamSynchronize(r->stream));
+    HIPCHK(r, hipStreamSynchronize(r->aux));
     if (r->use_ext) HIPCHK(r, hipStreamSynchronize(r->ext_stream));
     if (r->gstream) HIPCHK(r, hipStreamSynchronize(r->gstream));
     if (r->shard_pipe) HIPCHK(r, hipStreamSynchronize(r->side));
@@ -1261,6 +1273,7 @@ static HashParams hash_params(const orx_renderer* r, float ppm_radius) {
 static void ppm_photons_grid(orx_renderer* r, const Consts& c) {
     hipStream_t st = cur_stream(r);
     ev_begin(r, P_PHOTON);
+    r->eye_chain = false;
     static const int wavefront = [] {
         const char* e = getenv("ORX_PHOTON_WAVEFRONT");
         return e ? atoi(e) : 0;
@@ -1442,10 +1455,23 @@ static orx_status ppm_pipelined_iteration(orx_renderer* r, const orx_request* de
     /* the set's previous gather + output (two iterations back) and, through the RNG chain
      * (slot (x,y) is advanced by eye, photon and direct in turn), the last direct pass */
     HIPCHK(r, hipStreamWaitEvent(st, r->ev_gdone[k], 0));
-    HIPCHK(r, hipStreamWaitEvent(st, r->ev_direct_done, 0));
-    HIPCHK(r, hipStreamWaitEvent(r->aux, r->ev_gdone[k], 0)); /* direct writes this set's direct buffer */
+    HIPCHK(r, hipStreamWaitEvent(r->aux, r->ev_gdone[k], 0)); /* eye and direct write this set */
+    /* The eye pass needs the RNG slots after the direct pass of i (aux, stream order) and this
+     * set free (above); not the grid build of i, which is still running on st.  So it runs on
+     * aux beside that grid build, and the photon pass waits for it (RNG chain) and, in stream
+     * order, for the grid build (the deposit records it reads).  Without an unbroken chain of
+     * pipelined iterations aux first waits for everything enqueued on st. */
+    if (!r->eye_chain) {
+        HIPCHK(r, hipEventRecord(r->ev_main, st));
+        HIPCHK(r, hipStreamWaitEvent(r->aux, r->ev_main, 0));
+    }
+    ev_begin_on(r, P_EYE, r->aux);
+    launch_ppm_eye(r->aux, r->scene, cam, r->px, c);
+    ev_end_on(r, P_EYE, r->aux);
+    HIPCHK(r, hipEventRecord(r->ev_eye_done, r->aux));
+    HIPCHK(r, hipStreamWaitEvent(st, r->ev_eye_done, 0));
     r->overlap_direct = true;
-    ppm_local_passes(r, cam, c); /* eye, photon, direct (aux), grid */
+    ppm_photons_grid(r, c); /* photon, direct (aux), grid */
     r->overlap_direct = false;
     HIPCHK(r, hipEventRecord(r->ev_grid_done, st));
     hipStream_t g = r->gstream;
@@ -1465,6 +1491,7 @@ static orx_status ppm_pipelined_iteration(orx_renderer* r, const orx_request* de
     ev_end_on(r, P_DIRECT, g);
     HIPCHK(r, hipEventRecord(r->ev_gdone[k], g));
     r->pend = true;
+    r->eye_chain = true;
     HIPCHK(r, hipGetLastError());
     r->last_method = (uint64_t)det->method;
     r->last_consts = c;

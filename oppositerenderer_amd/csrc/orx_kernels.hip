@@ -884,11 +884,26 @@ __device__ __forceinline__ uint32_t dir_q8(float x, float y, float z) {
     return ((uint32_t)qx & 0xffu) | (((uint32_t)qy & 0xffu) << 8) | (((uint32_t)qz & 0xffu) << 16);
 }
 
+/* one grid photon: a deposit record -> the SoA planes at grid
+ * position dst (the reference's sorted photon array, SpatialHash.cu:193-196) */
+__device__ __forceinline__ void grid_put(const PhotonBufs& pb, uint32_t dst, const float4 a, const float4 b, float cz) {
+    const size_t P = pb.splane;
+    float* o = pb.sorted + dst;
+    o[SP_X * P] = a.x;
+    o[SP_Y * P] = a.y;
+    o[SP_Z * P] = a.z;
+    o[SP_DIRQ * P] = __uint_as_float(dir_q8(b.x, b.y, b.z));
+    o[SP_DX * P] = b.x;
+    o[SP_DY * P] = b.y;
+    o[SP_DZ * P] = b.z;
+    o[SP_PX * P] = a.w;
+    o[SP_PY * P] = b.w;
+    o[SP_PZ * P] = cz;
+}
 /* grid order -> SoA planes: destination-major, so the ten plane writes are
  * coalesced and the source reads are whole float4s */
 __global__ __launch_bounds__(256) void k_grid_permute(PhotonBufs pb) {
     const uint32_t valid = pb.grid->valid;
-    const size_t P = pb.splane;
     const uint32_t T = gridDim.x * blockDim.x;
     for (uint32_t d0 = blockIdx.x * blockDim.x + threadIdx.x; d0 < valid; d0 += 4 * T) {
         uint32_t src[4];
@@ -906,20 +921,8 @@ __global__ __launch_bounds__(256) void k_grid_permute(PhotonBufs pb) {
             }
         }
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            if (src[q] == 0xffffffffu) continue;
-            float* o = pb.sorted + d0 + q * T;
-            o[SP_X * P] = a[q].x;
-            o[SP_Y * P] = a[q].y;
-            o[SP_Z * P] = a[q].z;
-            o[SP_DIRQ * P] = __uint_as_float(dir_q8(b[q].x, b[q].y, b[q].z));
-            o[SP_DX * P] = b[q].x;
-            o[SP_DY * P] = b[q].y;
-            o[SP_DZ * P] = b[q].z;
-            o[SP_PX * P] = a[q].w;
-            o[SP_PY * P] = b[q].w;
-            o[SP_PZ * P] = cz[q];
-        }
+        for (int q = 0; q < 4; q++)
+            if (src[q] != 0xffffffffu) grid_put(pb, d0 + q * T, a[q], b[q], cz[q]);
     }
 }
 /* ------------------------------------------------------------------ */
@@ -1189,6 +1192,8 @@ void launch_grid_bucket_place(hipStream_t s, const PhotonBufs& pb) {
         if (cblocks > 4096) cblocks = 4096;
         hipLaunchKernelGGL(k_grid_coarse_offsets, dim3(cblocks), dim3(256), 0, s, pb);
     }
+    /* applying the permutation inside k_bs_cells (one block per bucket, scattered
+     * record reads at its occupancy) measured 3.5 ms against 0.5 ms for this pass */
     unsigned blocks = (pb.S + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(k_grid_permute, dim3(blocks), dim3(256), 0, s, pb);
@@ -1816,9 +1821,16 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
                 const uint32_t* so = pb.subofs + ((size_t)rowc * NSUB + sr) * g.gx * SUBX;
                 const uint32_t U0 = so[A0], U1 = so[A1 + 1]; /* uniform: scalar loads */
                 if (U0 >= U1) continue;
-                /* this lane's candidates: [lo, lo + len) */
+                /* this lane's candidates: [lo, lo + len); the LDS-broadcast form needs them
+                 * only on sub-rows where some lane's chord is cut (two scattered loads) */
+#ifdef ORX_TRAV_STATS
+                constexpr bool need_all = true;
+#else
+                constexpr bool need_all = BC != 1;
+#endif
+                const bool range = BC == 1 ? wave_any(cut) : true;
                 uint32_t lo = 0, len = 0;
-                if (a0 <= a1) {
+                if ((need_all || range) && a0 <= a1) {
                     lo = so[a0];
                     len = so[a1 + 1] - lo;
                 }
@@ -1829,7 +1841,6 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
                     /* a lane without a chord here accepts nothing (its window excludes the
                      * sub-row, or its sphere misses it) */
                     const float r2 = a0 <= a1 ? radius2 : -1.f;
-                    const bool range = wave_any(cut);
                     float* L = ulds[w];
                     uint32_t cc = U0;
                     UChunk cur = uload_chunk(SX, SY, SZ, SQ, SPX, SPY, SPZ, cc + l);
