@@ -104,6 +104,15 @@ def traffic_lookup(key, kernels):
     return int(sum(vals)) if vals else None
 
 
+def profiled_kernels(key, kernels):
+    """The pass's kernels the committed PMC profile of this workload saw dispatched (None: no profile)."""
+    try:
+        table = json.load(open(os.path.join(ROOT, "profiles", "traffic.json"))).get(key, {})
+    except (OSError, ValueError):
+        return None
+    return [k for k in kernels if k in table] or None
+
+
 def bound_lookup(key, kernels):
     """What bounds the kernel, from the committed PMC passes (profiles/bound.json, written by
     tools/pmc_bound.py): VALU issue, the vector-memory address path (TA) or HBM."""
@@ -204,8 +213,9 @@ def roofline_block(pass_ms, pbytes, key, photon_map, serial_ms=None, overlapped=
     from oppositerenderer_amd import roofline
     dominant = max(pass_ms, key=pass_ms.get)
     kernels = roofline.kernels_of(dominant, photon_map)
+    seen = profiled_kernels(key, kernels)
     roof = roofline.roofline(dominant, pbytes[dominant], pass_ms[dominant], traffic_lookup(key, kernels),
-                             photon_map=photon_map)
+                             photon_map=photon_map, kernels=seen)
     b = bound_lookup(key, kernels)
     if b:
         roof.update(b)

@@ -178,6 +178,7 @@ struct GatherIn {
     uint32_t segments, seg_rows, W;
     float* indirect;    /* [segments*seg_rows*W*3] */
     uint32_t* dbg;      /* [segments*seg_rows*W*2] or NULL */
+    uint32_t tshape;    /* wave pixel tile of the union gather: 0 = 8x8, 1 = 16x4, 2 = 4x16 */
 };
 /* The gather kernels tile IMAGE rows y.  With several row-interleaved segments (the
  * sharded gather: segment s = rank s holds image rows y = s + lj*segments) the hit points

@@ -1698,8 +1698,10 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
     } else {
         const uint32_t per = (ntiles + 7) / 8;
         const uint32_t tile = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
-        x = (tile % ntx) * 16 + (w & 1) * 8 + (l & 7);
-        const uint32_t y = (tile / ntx) * 16 + (w >> 1) * 8 + (l >> 3);
+        const uint32_t ox = gi.tshape == 0 ? (w & 1) * 8 + (l & 7) : gi.tshape == 1 ? (l & 15) : w * 4 + (l & 3);
+        const uint32_t oy = gi.tshape == 0 ? (w >> 1) * 8 + (l >> 3) : gi.tshape == 1 ? w * 4 + (l >> 4) : (l >> 2);
+        x = (tile % ntx) * 16 + ox;
+        const uint32_t y = (tile / ntx) * 16 + oy;
         j = gather_row(gi, y);
         live = tile < ntiles && x < gi.W && y < gi.segments * gi.seg_rows;
     }
@@ -1989,30 +1991,36 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
      * (hall 1080p, tools/shard_model.py: N=8 0.93 ms per-lane against 1.20 union; N=2 1.65
      * against 1.42) */
     const int union_gather = union_env >= 0 ? union_env : (gi.segments >= 4 ? 0 : 2);
+    static const uint32_t tshape = [] {
+        const char* e = getenv("ORX_GATHER_TILE");
+        return e ? (uint32_t)atoi(e) % 3u : 0u;
+    }();
+    GatherIn gt = gi;
+    gt.tshape = tshape;
     if (union_gather == 2 && pb.subofs) {
         if (pb.nsub == 1)
-            hipLaunchKernelGGL((k_ppm_gather_union<1, false, 1>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx, ntiles,
+            hipLaunchKernelGGL((k_ppm_gather_union<1, false, 1>), grid, dim3(256), lds_pad, s, gt, pb, c, ntx, ntiles,
                                nullptr, 0u);
         else
-            hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR, false, 1>), grid, dim3(256), lds_pad, s, gi, pb, c,
+            hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR, false, 1>), grid, dim3(256), lds_pad, s, gt, pb, c,
                                ntx, ntiles, nullptr, 0u);
         return;
     }
     if (union_gather && pb.subofs) {
         if (pb.nsub == 1)
-            hipLaunchKernelGGL((k_ppm_gather_union<1, false, 0>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx, ntiles,
+            hipLaunchKernelGGL((k_ppm_gather_union<1, false, 0>), grid, dim3(256), lds_pad, s, gt, pb, c, ntx, ntiles,
                                nullptr, 0u);
         else
-            hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR, false, 0>), grid, dim3(256), lds_pad, s, gi, pb, c,
+            hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR, false, 0>), grid, dim3(256), lds_pad, s, gt, pb, c,
                                ntx, ntiles, nullptr, 0u);
         return;
     }
     if (!pb.subofs)
-        hipLaunchKernelGGL((k_ppm_gather<1, false>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx, ntiles);
+        hipLaunchKernelGGL((k_ppm_gather<1, false>), grid, dim3(256), lds_pad, s, gt, pb, c, ntx, ntiles);
     else if (pb.nsub == 1)
-        hipLaunchKernelGGL((k_ppm_gather<1, true>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx, ntiles);
+        hipLaunchKernelGGL((k_ppm_gather<1, true>), grid, dim3(256), lds_pad, s, gt, pb, c, ntx, ntiles);
     else
-        hipLaunchKernelGGL((k_ppm_gather<SUBR * SUBR, true>), grid, dim3(256), lds_pad, s, gi, pb, c, ntx, ntiles);
+        hipLaunchKernelGGL((k_ppm_gather<SUBR * SUBR, true>), grid, dim3(256), lds_pad, s, gt, pb, c, ntx, ntiles);
 }
 
 /* ------------------------------------------------------------------ */

@@ -24,8 +24,9 @@ KERNELS_OF_PASS = {
     # k_grid_hash / k_scan_* / k_grid_scatter with the same pass split
     "grid_hash": ["k_grid_setup", "k_bs_count"],
     "grid_scan": ["k_bs_scan_reduce", "k_bs_scan_partials", "k_bs_scan_apply"],
-    "grid_scatter": ["k_bs_place", "k_bs_cells", "k_grid_permute"],
-    "ppm_gather": ["k_ppm_gather"],
+    "grid_scatter": ["k_bs_place", "k_bs_cells", "k_grid_coarse_offsets", "k_grid_permute"],
+    # the wave-union kernel (default below 4 segments) or the per-lane kernel; one of them per launch
+    "ppm_gather": ["k_ppm_gather_union", "k_ppm_gather"],
     "ppm_direct_output": ["k_ppm_direct_output"],
     "pt": ["k_pt"],
     "vcm_light": ["k_vcm_light"],
@@ -104,9 +105,11 @@ def pass_bytes(method: int, W: int, H: int, photons: int, valid: float = 0.0, ce
     return {"pt": N * (R2 + 24)}
 
 
-def roofline(pass_name: str, bytes_per_launch: float, ms_per_launch: float, traffic=None, photon_map: int = 0) -> dict:
+def roofline(pass_name: str, bytes_per_launch: float, ms_per_launch: float, traffic=None, photon_map: int = 0,
+             kernels=None) -> dict:
+    """kernels: the pass's kernels the profile of this workload saw dispatched (default: all of the pass)"""
     achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9 if ms_per_launch > 0 else 0.0
-    return {"kernel": "+".join(kernels_of(pass_name, photon_map)), "pass": pass_name,
+    return {"kernel": "+".join(kernels or kernels_of(pass_name, photon_map)), "pass": pass_name,
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(ms_per_launch, 4)}

@@ -1,5 +1,3 @@
 set -o pipefail
-mkdir -p gpurun_out/t
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t/gputest.log 2>&1 || { tail -30 gpurun_out/t/gputest.log; exit 1; }
-tail -2 gpurun_out/t/gputest.log
-bash tools/gpu_lib_ab.sh "base cur" --method vcm --steps 12 --warmup 3
+bash tools/gpu_ab.sh ORX_GATHER_TILE "0 1 2" --steps 16 --warmup 4 &&
+bash tools/gpu_ab.sh ORX_GATHER_TILE "0 1 2" --config 4 --steps 4 --warmup 2
