@@ -159,9 +159,13 @@ typedef struct {
     uint32_t vcm_max_path_length;     /* VCM_MAX_PATH_LENGTH = 10 */
     uint32_t seed;                    /* 0: 574133*clock()+47844152748*time() like SpatialHash.cu:322; else DEBUG_RANDOM_SEED */
     uint32_t debug_counters;          /* 1: keep per-pixel cells/photons visited (OptixRenderer.cpp:872-953) */
-    uint32_t gather_variant;          /* photon-grid layout for the gather: 0 (default) photons ordered by
-                                         cell-row quarter sub-rows (y and z halves) and x quarters; 1 photons in
-                                         cell order with x quarters only.  Any other value: ORX_ERR_INVALID_ARGUMENT */
+    uint32_t gather_variant;          /* photon-grid layout for the gather: 2 photons ordered by cell-row
+                                         quarter sub-rows (y and z halves) and x quarters; 1 photons in cell
+                                         order with x quarters only; 0 (default) the faster of the two for the
+                                         renderer: sub-rows on a single device, cell order for a shard of
+                                         world >= 2 (orx_set_shard: it holds 1/N of the photons, so the
+                                         per-sub-row work outweighs the photons it trims).  The image does not
+                                         depend on it.  Any other value: ORX_ERR_INVALID_ARGUMENT */
     uint32_t photon_map;              /* ACCELERATION_STRUCTURE (config.h): 0 uniform grid (the shipped
                                          configuration), 1 stochastic hash (OptixRenderer_SpatialHash.cu:286-302,
                                          store_photon.h, IndirectRadianceEstimation.cu:131-162; needs

@@ -499,7 +499,7 @@ orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out)
     else orx_default_config(&c);
     if (c.max_photon_deposits == 0 || c.max_photon_deposits > 8 || c.photon_launch_width == 0 ||
         c.photon_launch_height == 0 || c.photon_grid_max_size == 0 || c.photon_grid_max_size > (1u << 26) ||
-        c.gather_variant > 1 || c.photon_map > 2 || (c.photon_map == 1 && !hash_config_ok(c)) ||
+        c.gather_variant > 2 || c.photon_map > 2 || (c.photon_map == 1 && !hash_config_ok(c)) ||
         (c.photon_map == 2 && (uint64_t)c.photon_launch_width * c.photon_launch_height * c.max_photon_deposits >
                                   (1ull << 28)))
         return ORX_ERR_INVALID_ARGUMENT;
@@ -890,7 +890,11 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_wpath.ensure(nphot * 32 + 32));
     /* bucket-sort grid build: at most 2048 buckets of 2^bshift virtual cells
      * (nsub sub-rows per cell row, k_bs_count) */
-    const uint32_t nsub = r->cfg.gather_variant == 1 ? 1u : SUBR * SUBR;
+    /* sub-row layout on one device; a shard of world >= 2 gathers all W*H hit points against 1/N
+     * of the photons and runs faster on whole cell rows (tools/shard_model.py, hall 1080p:
+     * per-rank gather N=2 1.40 -> 1.32 ms, N=8 0.96 -> 0.90 ms, grid build shorter too) */
+    const bool cell_order = r->cfg.gather_variant == 1 || (r->cfg.gather_variant == 0 && r->world >= 2);
+    const uint32_t nsub = cell_order ? 1u : SUBR * SUBR;
     const size_t vmax = (size_t)r->cfg.photon_grid_max_size * nsub;
     uint32_t bshift = 10;
     while (((vmax + (1u << bshift) - 1) >> bshift) > 2048) bshift++;

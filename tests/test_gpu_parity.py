@@ -79,7 +79,7 @@ def check_ppm_iteration(gpu, ora):
     np.testing.assert_allclose(gi, oi, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("gather_variant", [0, 1])
+@pytest.mark.parametrize("gather_variant", [0, 1, 2])
 @pytest.mark.parametrize("scene_name,W,H,P", [("Cornell", 64, 64, 128), ("Cornell", 96, 80, 64),
                                               ("CornellSmall", 64, 64, 128)])
 def test_ppm_parity(scene_name, W, H, P, gather_variant):
