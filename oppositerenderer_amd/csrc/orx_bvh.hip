@@ -364,8 +364,7 @@ __global__ void k_bvh_collapse(CollapseBufs C, const CollapseItem* __restrict__ 
     nd.ox = lo[0];
     nd.oy = lo[1];
     nd.oz = lo[2];
-    nd.exps = 0;
-    nd.pad[0] = nd.pad[1] = 0;
+    nd.sx = nd.sy = nd.sz = 1.f;
     bool ok = true;
     for (int k = 0; k < 3; k++) {
         nd.qlo[k] = nd.qhi[k] = 0;
@@ -389,7 +388,7 @@ __global__ void k_bvh_collapse(CollapseBufs C, const CollapseItem* __restrict__ 
             for (int i = 0; i < 4; i++) wl |= ql[i] << (8 * i), wh |= qh[i] << (8 * i);
             nd.qlo[k] = wl;
             nd.qhi[k] = wh;
-            nd.exps |= (uint32_t)(e + 127) << (8 * k);
+            (k == 0 ? nd.sx : k == 1 ? nd.sy : nd.sz) = ldexpf(1.0f, e); /* 2^e, exact for e in [-126, 127] */
             break;
         }
     }

@@ -255,7 +255,7 @@ struct Bvh4Builder {
                 for (int i = 0; i < 4; i++) wl |= ql[i] << (8 * i), wh |= qh[i] << (8 * i);
                 nd.qlo[k] = wl;
                 nd.qhi[k] = wh;
-                nd.exps |= (uint32_t)(e + 127) << (8 * k);
+                (k == 0 ? nd.sx : k == 1 ? nd.sy : nd.sz) = ldexpf(1.0f, e); /* 2^e, exact for e in [-126, 127] */
                 break;
             }
         }

@@ -238,16 +238,18 @@ struct DevBvhNode {
  * from the binary SAH tree.  Child boxes are quantised to 8 bits per bound
  * against the node's origin with a power-of-two scale per axis, rounded
  * outward (so every decoded box contains the child's conservative box):
- *   lo_k(child i) = origin_k + qlo_k[i] * 2^(e_k - 127)
+ *   lo_k(child i) = origin_k + qlo_k[i] * s_k,   s_k = 2^e_k
+ * The scales are stored as floats (the x scale in the first 16 B, y and z in
+ * the last), so the node test reads them instead of decoding exponent bytes.
  * Child reference: inner node index, or ORX_LEAF | first << 3 | (count - 1)
  * for a triangle range in leaf order, or ORX_EMPTY. */
 struct DevBvh4 {
     float ox, oy, oz;
-    uint32_t exps;     /* e_x | e_y << 8 | e_z << 16 (biased float exponents of the scales) */
+    float sx;          /* 2^e_x */
     uint32_t qlo[3];   /* per axis: byte i = child i */
     uint32_t qhi[3];
     uint32_t child[4];
-    uint32_t pad[2];
+    float sy, sz;      /* 2^e_y, 2^e_z */
 };
 /* fp32 variant (ORX_BVH_FP32): 128 B, child bounds unquantised, SoA by
  * axis so the near/far bound quadruples are picked by address */
@@ -404,10 +406,7 @@ __device__ __forceinline__ RayBox ray_box(f3 o, f3 d) {
  * Returns entry distances (+inf for misses) and child refs. */
 __device__ __forceinline__ void node_test_q(const float4 A, const float4 B, const float4 C, const float4 D,
                                             const RayBox& rb, float tmin, float tmax, float t[4], uint32_t c[4]) {
-    const uint32_t ex = __float_as_uint(A.w);
-    const float sx = __uint_as_float((ex & 0xffu) << 23);
-    const float sy = __uint_as_float(((ex >> 8) & 0xffu) << 23);
-    const float sz = __uint_as_float(((ex >> 16) & 0xffu) << 23);
+    const float sx = A.w, sy = D.z, sz = D.w;
     const float ax = (A.x - rb.o.x) * rb.inv.x, bx = sx * rb.inv.x;
     const float ay = (A.y - rb.o.y) * rb.inv.y, by = sy * rb.inv.y;
     const float az = (A.z - rb.o.z) * rb.inv.z, bz = sz * rb.inv.z;
@@ -794,6 +793,22 @@ __device__ inline bool trace_any_t(const DevScene& S, f3 o, f3 d, float tmin, fl
                 nodes.test(S, ref, rb, tmin, tmax, ct, cc);
                 ORX_TS_INC(ts_nodes, 1);
                 ORX_TS_WAVE(ts_wn);
+#ifndef ORX_TRAV_BRANCHED_PUSH
+                /* branch-free: every hit child is written to the stack (the order does not
+                 * matter for any hit), the last one is taken back from registers */
+                const int h0 = ct[0] != INFINITY, h1 = ct[1] != INFINITY, h2 = ct[2] != INFINITY,
+                          h3 = ct[3] != INFINITY;
+                stk.put(sp, cc[0]);
+                sp += h0;
+                stk.put(sp, cc[1]);
+                sp += h1;
+                stk.put(sp, cc[2]);
+                sp += h2;
+                stk.put(sp, cc[3]);
+                sp += h3;
+                const uint32_t next = h3 ? cc[3] : h2 ? cc[2] : h1 ? cc[1] : h0 ? cc[0] : ORX_DONE;
+                sp -= next != ORX_DONE;
+#else
                 uint32_t next = ORX_DONE;
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
@@ -802,6 +817,7 @@ __device__ inline bool trace_any_t(const DevScene& S, f3 o, f3 d, float tmin, fl
                         next = cc[i];
                     }
                 }
+#endif
                 ref = next != ORX_DONE ? next : (sp ? stk.pop(sp) : ORX_DONE);
                 if ((ref & ORX_LEAF) && !(lf & ORX_LEAF)) {
                     lf = ref;

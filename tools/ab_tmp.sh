@@ -1,5 +1,6 @@
 set -o pipefail
-mkdir -p gpurun_out/t gpurun_out/sm
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "parity or shard" > gpurun_out/t/gputest.log 2>&1 || { tail -30 gpurun_out/t/gputest.log; exit 1; }
+mkdir -p gpurun_out/t
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t/gputest.log 2>&1 || { tail -30 gpurun_out/t/gputest.log; exit 1; }
 tail -2 gpurun_out/t/gputest.log
-timeout -k 10 300 python -u tools/shard_model.py 1 2 4 8 > gpurun_out/sm/auto.txt 2>&1 && cut -c1-160 gpurun_out/sm/auto.txt
+bash tools/gpu_lib_ab.sh "base cur" --steps 24 --warmup 4 &&
+bash tools/gpu_lib_ab.sh "base cur" --method vcm --steps 12 --warmup 3
