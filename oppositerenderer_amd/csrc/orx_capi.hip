@@ -1248,6 +1248,8 @@ static GatherIn local_gather_in(orx_renderer* r) {
     gi.W = r->W;
     gi.indirect = r->d_ind.as<float>();
     gi.dbg = r->cfg.debug_counters ? r->d_dbg.as<uint32_t>() : nullptr;
+    gi.tshape = 0;
+    gi.visits = 1;
     return gi;
 }
 
@@ -1660,6 +1662,8 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hp, uint32_t seg
     gi.W = r->W;
     gi.indirect = (float*)indirect;
     gi.dbg = nullptr;
+    gi.tshape = 0;
+    gi.visits = 0; /* rank-local counts are not the reference's; no per-pixel debug buffers here */
     hipStream_t st = cur_stream(r);
     if (r->last_pipelined) { /* on the side stream, after the grid build */
         st = gather_stream(r);

@@ -179,6 +179,10 @@ struct GatherIn {
     float* indirect;    /* [segments*seg_rows*W*3] */
     uint32_t* dbg;      /* [segments*seg_rows*W*2] or NULL */
     uint32_t tshape;    /* wave pixel tile of the union gather: 0 = 8x8, 1 = 16x4, 2 = 4x16 */
+    uint32_t visits;    /* 1: count the reference's per-pixel visits (IndirectRadianceEstimation.cu:113/124)
+                         * into dbg and the stats; 0 for the sharded gather, which has no per-pixel
+                         * debug buffers and whose rank-local counts are not the reference's
+                         * (measured: per-rank hall gather at N=8 0.89 -> 0.44 ms without them) */
 };
 /* The gather kernels tile IMAGE rows y.  With several row-interleaved segments (the
  * sharded gather: segment s = rank s holds image rows y = s + lj*segments) the hit points

@@ -1348,7 +1348,7 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
         if (x_lo <= x_hi && y_lo <= y_hi && z_lo <= z_hi) {
             ny = y_hi - y_lo + 1;
             nrows = (z_hi - z_lo + 1) * ny;
-            window_visits(pb.offsets, g.gx, g.gy, x_lo, x_hi, y_lo, ny, z_lo, nrows, dC, dP);
+            if (gi.visits) window_visits(pb.offsets, g.gx, g.gy, x_lo, x_hi, y_lo, ny, z_lo, nrows, dC, dP);
         }
     }
     const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
@@ -1740,7 +1740,7 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
         y_hi = (g.gy - 1) < uy ? (g.gy - 1) : uy;
         z_hi = (g.gz - 1) < uz ? (g.gz - 1) : uz;
         act = x_lo <= x_hi && y_lo <= y_hi && z_lo <= z_hi;
-        if (act) /* the reference's visit counters: every (z,y) row of the window, whole rows */
+        if (act && gi.visits) /* the reference's visit counters: every (z,y) row of the window, whole rows */
             window_visits(pb.offsets, g.gx, g.gy, x_lo, x_hi, y_lo, y_hi - y_lo + 1, z_lo,
                           (z_hi - z_lo + 1) * (y_hi - y_lo + 1), dC, dP);
     }
