@@ -1986,11 +1986,11 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
         const char* e = getenv("ORX_GATHER_UNION");
         return e ? atoi(e) : -1;
     }();
-    /* The sharded gather (segments = ranks) meets 1/N of the photons: at N >= 4 the wave union's
-     * per-sub-row work outweighs the photons it shares, and the per-lane kernel is faster
-     * (hall 1080p, tools/shard_model.py: N=8 0.93 ms per-lane against 1.20 union; N=2 1.65
-     * against 1.42) */
-    const int union_gather = union_env >= 0 ? union_env : (gi.segments >= 4 ? 0 : 2);
+    /* The sharded gather (segments = ranks, cell-order layout, no visit counters) meets 1/N of
+     * the photons: at N >= 8 the wave union's per-row work outweighs the photons it shares, and
+     * the per-lane kernel is faster (hall 1080p, tools/shard_model.py, per-rank gather union /
+     * per-lane: N=2 1.29 / 1.56 ms, N=4 0.73 / 0.80, N=8 0.47 / 0.43) */
+    const int union_gather = union_env >= 0 ? union_env : (gi.segments >= 8 ? 0 : 2);
     static const uint32_t tshape = [] {
         const char* e = getenv("ORX_GATHER_TILE");
         return e ? (uint32_t)atoi(e) % 3u : 0u;
