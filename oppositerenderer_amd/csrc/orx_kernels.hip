@@ -76,13 +76,27 @@ void launch_rng_init(hipStream_t s, RngPlanes rng, uint32_t RW, uint32_t rows, u
                        seed);
 }
 
+/* Pixel tile of a 64-lane wave for the per-pixel passes (eye, direct, PT): 8x8 local pixels
+ * on one device; a shard owns image rows rank + world*j, so 8 local rows would span 8*world
+ * image rows (incoherent primary and shadow rays): 16x4 local pixels for 2-4 ranks, 32x2 for 8+ */
+__host__ __device__ __forceinline__ uint32_t pix_tile_shift(uint32_t world) { return world >= 8 ? 2u : world >= 2 ? 1u : 0u; }
+__device__ __forceinline__ void pix_tile(const PixelBufs& px, uint32_t& x, uint32_t& j) {
+    const uint32_t sh = pix_tile_shift(px.world), tw = 8u << sh;
+    x = blockIdx.x * tw + (threadIdx.x & (tw - 1));
+    j = blockIdx.y * (8u >> sh) + (threadIdx.x >> (3 + sh));
+}
+static dim3 pix_grid(const PixelBufs& px) {
+    const uint32_t sh = pix_tile_shift(px.world), tw = 8u << sh, th = 8u >> sh;
+    return dim3((px.W + tw - 1) / tw, (px.rows + th - 1) / th);
+}
+
 /* ------------------------------------------------------------------ */
 /* PPM eye pass                                                        */
 /* ------------------------------------------------------------------ */
 __global__ __launch_bounds__(64) void k_ppm_eye(DevScene S, DevCamera cam, PixelBufs px, Consts c) {
     ORX_STACK_DECL;
-    uint32_t x = blockIdx.x * 8 + (threadIdx.x & 7);
-    uint32_t j = blockIdx.y * 8 + (threadIdx.x >> 3);
+    uint32_t x, j;
+    pix_tile(px, x, j);
     if (x >= px.W || j >= px.rows) return;
     uint32_t y = px.rank + px.world * j;
     size_t slot = (size_t)j * px.RW + x;
@@ -102,7 +116,7 @@ __global__ __launch_bounds__(64) void k_ppm_eye(DevScene S, DevCamera cam, Pixel
     rng_store(px.rng, slot, rs);
 }
 void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c) {
-    dim3 grid((px.W + 7) / 8, (px.rows + 7) / 8);
+    const dim3 grid = pix_grid(px);
     hipLaunchKernelGGL(k_ppm_eye, grid, dim3(64), ORX_STACK_BYTES(S), s, S, cam, px, c);
 }
 
@@ -2174,8 +2188,8 @@ void launch_ppm_gather_hash(hipStream_t s, const GatherIn& gi, const PhotonBufs&
 template <int MODE>
 __global__ __launch_bounds__(64) void k_ppm_direct_output(DevScene S, PixelBufs px, Consts c) {
     ORX_STACK_DECL;
-    const uint32_t x = blockIdx.x * 8 + (threadIdx.x & 7);
-    const uint32_t j = blockIdx.y * 8 + (threadIdx.x >> 3);
+    uint32_t x, j;
+    pix_tile(px, x, j);
     if (x >= px.W || j >= px.rows) return;
     const size_t i = (size_t)j * px.W + x;
     if (MODE == 2) {
@@ -2230,7 +2244,7 @@ __global__ __launch_bounds__(64) void k_ppm_direct_output(DevScene S, PixelBufs 
     px.output[3 * i + 2] = out.z;
 }
 void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs& px, const Consts& c, int mode) {
-    dim3 grid((px.W + 7) / 8, (px.rows + 7) / 8);
+    const dim3 grid = pix_grid(px);
     if (mode == 1) hipLaunchKernelGGL(k_ppm_direct_output<1>, grid, dim3(64), ORX_STACK_BYTES(S), s, S, px, c);
     else if (mode == 2) hipLaunchKernelGGL(k_ppm_direct_output<2>, grid, dim3(64), 0, s, S, px, c);
     else hipLaunchKernelGGL(k_ppm_direct_output<0>, grid, dim3(64), ORX_STACK_BYTES(S), s, S, px, c);
@@ -2241,8 +2255,8 @@ void launch_ppm_direct_output(hipStream_t s, const DevScene& S, const PixelBufs&
 /* ------------------------------------------------------------------ */
 __global__ __launch_bounds__(64) void k_pt(DevScene S, DevCamera cam, PixelBufs px, Consts c) {
     ORX_STACK_DECL;
-    const uint32_t x = blockIdx.x * 8 + (threadIdx.x & 7);
-    const uint32_t j = blockIdx.y * 8 + (threadIdx.x >> 3);
+    uint32_t x, j;
+    pix_tile(px, x, j);
     if (x >= px.W || j >= px.rows) return;
     const uint32_t y = px.rank + px.world * j;
     const size_t i = (size_t)j * px.W + x;
@@ -2299,7 +2313,7 @@ __global__ __launch_bounds__(64) void k_pt(DevScene S, DevCamera cam, PixelBufs 
     rng_store(px.rng, slot, rs);
 }
 void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c) {
-    dim3 grid((px.W + 7) / 8, (px.rows + 7) / 8);
+    const dim3 grid = pix_grid(px);
     hipLaunchKernelGGL(k_pt, grid, dim3(64), ORX_STACK_BYTES(S), s, S, cam, px, c);
 }
 
