@@ -277,7 +277,10 @@ def main():
     # passes, so every pass time is wall time under interference; a few serial iterations after
     # the timed region give each pass's stand-alone time
     pipelined = method == _abi.PROGRESSIVE_PHOTON_MAPPING and r.pipelined()
-    overlapped = ["ppm_gather", "ppm_direct_output"] if pipelined else []
+    # pipelined (single device): gather + output of iteration i beside iteration i+1's passes, the
+    # direct pass beside the grid build, and the eye pass of i+1 on the direct pass's stream beside
+    # the grid build of i, so the chain per frame is photon pass + grid build
+    overlapped = ["ppm_eye", "ppm_gather", "ppm_direct_output"] if pipelined else []
     serial = None
     if pipelined and not args.no_serial_pass_times:
         r.set_iteration_pipelining(0)
