@@ -301,6 +301,9 @@ __device__ __forceinline__ void photon_bbox_flush(const PhotonBufs& pb, float lo
     }
 }
 
+#ifndef ORX_PHOTON_CHUNK
+#define ORX_PHOTON_CHUNK 64 /* photons per counter fetch of a persistent wave */
+#endif
 template <bool PERSISTENT>
 __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, PhotonBufs pb, Consts c) {
     ORX_STACK_DECL;
@@ -314,7 +317,7 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
     bool alive = false;
     /* the wave's private range [next, end) of photon indices, refilled
      * CHUNK at a time from the device counter (one atomic per chunk) */
-    constexpr uint32_t CHUNK = 256;
+    constexpr uint32_t CHUNK = ORX_PHOTON_CHUNK;
     uint32_t next = 0, end = 0;
     for (;;) {
         /* refill: lanes without a path take consecutive photon indices */
@@ -359,7 +362,12 @@ void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, co
         return e ? atoi(e) : 0;
     }();
     if (persistent) { /* per-lane refill (A/B): one-wave blocks drain the shared photon counter */
-        const uint32_t blocks = std::min<uint32_t>((total + 63) / 64, 256u * 4u * 8u);
+        /* one wave per resident slot (4 per SIMD at this kernel's registers and LDS stack) */
+        static const uint32_t waves = [] {
+            const char* e = getenv("ORX_PHOTON_PERSISTENT_WAVES");
+            return e ? (uint32_t)atoi(e) : 256u * 4u * 4u;
+        }();
+        const uint32_t blocks = std::min<uint32_t>((total + 63) / 64, waves);
         hipMemsetAsync(pb.work, 0, 4, s);
         hipLaunchKernelGGL(k_ppm_photon<true>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, px, pb, c);
     } else {
