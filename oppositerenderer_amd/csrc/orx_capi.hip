@@ -870,7 +870,9 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_dbg.ensure(nhp * 8));
     HIPCHK(r, r->d_slots.ensure(S * 64));
     HIPCHK(r, r->d_vmask.ensure(nphot));
-    const size_t splane = ((S + 4) + 3) & ~(size_t)3;
+    /* 64 photons of tail padding per plane: the union gather loads whole 64-photon chunks (and
+     * prefetches the next one) up to index U1 + 63 of the last plane */
+    const size_t splane = ((S + 64) + 3) & ~(size_t)3;
     if ((size_t)SP_PLANES * splane * 4 > 0xffffff00ull) /* the gather addresses the planes with 32-bit buffer offsets */
         return set_err(r, ORX_ERR_UNSUPPORTED, "photon slots per device exceed the 4 GiB sorted-photon window");
     HIPCHK(r, r->d_sorted.ensure(SP_PLANES * splane * 4));
@@ -1158,6 +1160,9 @@ static orx_status ensure_second_set(orx_renderer* r) {
         HIPCHK(r, r->d_kdtree2.ensure(bytes));
         HIPCHK(r, hipMemsetAsync(r->d_kdtree2.p, 0, bytes, r->stream));
     }
+    /* the zero-fills above ran on the own stream; on a caller stream (the sharded pipeline) the
+     * eye pass and grid build of this iteration write these buffers right after swap_sets */
+    if (r->use_ext) HIPCHK(r, hipStreamSynchronize(r->stream));
     r->pipe_bufs = true;
     return ORX_OK;
 }

@@ -897,11 +897,14 @@ __global__ __launch_bounds__(256) void k_grid_scatter(PhotonBufs pb) {
  * Bound: |q/127 - d|_inf <= 0.5/127 + eps, so for |d|_1, |n|_1 <= 1.7325
  *   |qd.qn - 127^2 d.n| <= 127^2 (0.5/127 (|d|_1 + |n|_1) + 3 (0.5/127)^2) <= 221
  * and every decision taken from the integer dot equals the exact one.  A
- * direction (or normal) outside that 1-norm bound (or NaN) quantises to 0,
- * which always lands in the band. */
+ * direction (or normal) outside that 1-norm bound, with a component above 1 in
+ * magnitude (which would wrap in the byte) or NaN quantises to 0, which always
+ * lands in the band. */
 constexpr int32_t DIRQ_BAND = 232;
 __device__ __forceinline__ uint32_t dir_q8(float x, float y, float z) {
-    if (!(fabsf(x) + fabsf(y) + fabsf(z) <= 1.7325f)) return 0u;
+    /* the 1-norm bound of the error estimate, and |c| <= 1 so rint(127 c) fits an int8 */
+    if (!(fabsf(x) + fabsf(y) + fabsf(z) <= 1.7325f) || !(fmaxf(fabsf(x), fmaxf(fabsf(y), fabsf(z))) <= 1.0f))
+        return 0u;
     const int32_t qx = (int32_t)rintf(x * 127.f), qy = (int32_t)rintf(y * 127.f), qz = (int32_t)rintf(z * 127.f);
     return ((uint32_t)qx & 0xffu) | (((uint32_t)qy & 0xffu) << 8) | (((uint32_t)qz & 0xffu) << 16);
 }
