@@ -16,7 +16,9 @@ PPM: r0 = IScene::getSceneInitialPPMRadiusEstimate, alpha = 2/3, seed
 --scene/--width/--height/--photon-launch/--method override the config's values.
 
 Single GPU:  python bench.py [--config C] [--steps K --warmup W]
-Multi GPU:   torchrun --nproc-per-node N bench.py --gpus N   (one rank per GPU, RCCL).
+Multi GPU:   python bench.py --gpus N   (bench.py starts N rank processes itself, one per GPU,
+             RCCL over xGMI), or under a launcher that sets WORLD_SIZE/RANK/LOCAL_RANK
+             (torchrun --nproc-per-node N bench.py --gpus N).
              Default --scaling strong: the workload is fixed (its photon launch rows and
              pixel rows are dealt round-robin to the ranks); --scaling weak gives every
              rank a full photon launch.  See DESIGN.md "Multi-GPU".
@@ -229,8 +231,51 @@ def roofline_block(pass_ms, pbytes, key, photon_map, serial_ms=None, overlapped=
     return dominant, roof
 
 
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes (RANK = LOCAL_RANK =
+    0..N-1, rendezvous on 127.0.0.1) and wait for them.  This process never touches the GPU
+    (nothing here initialises HIP), so the ranks are children, never an exec of this process.
+    Rank 0 prints the JSON line on the inherited stdout.  If a rank fails, the others are
+    stopped (they would wait in a collective forever) and the exit code is the failure's."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for rank in range(n):
+        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:
+                    q.terminate()
+                for q in procs:
+                    try:
+                        q.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                procs = []
+                break
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus > 1 or world > 1 or args.force_sharded:

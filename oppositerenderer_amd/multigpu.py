@@ -243,16 +243,44 @@ class DeviceShard:
         return t
 
 
+def device_shard_factory(cfg, rank, world, local_rank, scene):
+    """The product backend of the multi-GPU bench: liborx.so on HIP device `local_rank`
+    (raises without a GPU or without liborx.so; there is no CPU fallback)."""
+    import torch
+
+    from .renderer import OptixRenderer
+
+    torch.cuda.set_device(local_rank)
+    r = OptixRenderer(cfg)
+    r.initialize(local_rank)
+    r.set_shard(rank, world)
+    r.initScene(scene)
+    return DeviceShard(r, torch, torch.device("cuda", local_rank))
+
+
+def _resolve_factory():
+    """ORX_SHARD_BACKEND=module:function swaps the shard backend; only the CPU launcher test
+    (tests/test_bench_launch.py) sets it, to run the orchestration under gloo on the oracle."""
+    spec = os.environ.get("ORX_SHARD_BACKEND")
+    if not spec:
+        return device_shard_factory, "hip"
+    import importlib
+
+    mod, fn = spec.split(":")
+    return getattr(importlib.import_module(mod), fn), spec
+
+
 def bench_main(args, metric, cpu_baseline=None):
-    """bench.py --gpus N under torchrun, one rank per GPU.  PPM: strong scaling by default (the
-    global photon launch P x P and the W x H pixels are fixed and dealt to the ranks by rows);
-    args.scaling == "weak" gives every rank a full P x P photon launch.  cpu_baseline: bench.py's
-    oracle timing, run on rank 0 when there is one rank."""
+    """bench.py --gpus N, one rank per GPU (bench.py starts the ranks itself when no launcher
+    set WORLD_SIZE).  PPM: strong scaling by default (the global photon launch P x P and the
+    W x H pixels are fixed and dealt to the ranks by rows); args.scaling == "weak" gives every
+    rank a full P x P photon launch.  cpu_baseline: bench.py's oracle timing, run on rank 0 when
+    there is one rank."""
     import torch
     import torch.distributed as dist
 
     from . import _abi, scenes
-    from .renderer import OptixRenderer, RenderRequestDetails, next_ppm_radius
+    from .renderer import RenderRequestDetails, next_ppm_radius
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -262,28 +290,34 @@ def bench_main(args, metric, cpu_baseline=None):
     vcm = method == "vcm"
     pt = method == "pt"
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    factory, backend_name = _resolve_factory()
+    on_gpu = backend_name == "hip"
     # RCCL prints its version banner on fd 1: keep stdout for the one JSON line
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
-    torch.cuda.set_device(local_rank)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    if on_gpu:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        dist.init_process_group("gloo")
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
     W, H, P = args.width, args.height, args.photon_launch
     scene = scenes.scene_by_name(args.scene)
     weak = getattr(args, "scaling", "strong") == "weak"
     PH = P * world if weak else P  # global photon launch height
     cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=PH,
                               gather_variant=args.gather_variant)
-    r = OptixRenderer(cfg)
-    r.initialize(local_rank)
-    r.set_shard(rank, world)
-    r.initScene(scene)
+    backend = factory(cfg, rank, world, local_rank, scene)
+    r = backend.r
     cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
     mcode = (_abi.VCM_BIDIRECTIONAL_PATH_TRACING if vcm else _abi.PATH_TRACING if pt
              else _abi.PROGRESSIVE_PHOTON_MAPPING)
     det = RenderRequestDetails(cam, scene.name, mcode, W, H)
     req = det.to_abi()
-    dev = torch.device("cuda", local_rank)
-    backend = DeviceShard(r, torch, dev)
     radius = scene.initial_ppm_radius()
     if vcm or pt:
         sharded = (ShardedVCM if vcm else ShardedPT)(backend, dist, world, rank, W, H)
@@ -294,22 +328,24 @@ def bench_main(args, metric, cpu_baseline=None):
         sharded.iteration(it, it, radius, req)
         radius = next_ppm_radius(radius, it)
         it += 1
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
-    r.reset_timing()
-    torch.cuda.synchronize()
+    if hasattr(r, "reset_timing"):
+        r.reset_timing()
+    sync()
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sharded.iteration(it, it, radius, req)
         radius = next_ppm_radius(radius, it)
         it += 1
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", local_rank) if on_gpu else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_max = float(t.item())
+    world_size = dist.get_world_size()
     st = r.stats()
     if rank == 0:
         from . import roofline
@@ -322,7 +358,7 @@ def bench_main(args, metric, cpu_baseline=None):
         # pipelined PPM: gather and output overlap the next iteration (side stream)
         overlapped = ["ppm_gather", "ppm_direct_output"] if getattr(sharded, "pipe", False) else []
         critical = {k: v for k, v in per_pass.items() if k not in overlapped} or per_pass
-        dominant = max(critical, key=critical.get)
+        dominant = max(critical, key=critical.get) if critical else None
         valid_avg = st.valid_photons_total / n_it
         rows0 = local_rows(H, 0, world)
         if pt:
@@ -335,10 +371,10 @@ def bench_main(args, metric, cpu_baseline=None):
             pb = roofline.pass_bytes(mcode, W, H, P * local_rows(PH, 0, world), valid_avg, st.num_cells)
             for k in ("ppm_eye", "ppm_direct_output"):
                 pb[k] = pb[k] * rows0 / H
-        roof = roofline.roofline(dominant, pb[dominant], per_pass[dominant], None)
+        roof = roofline.roofline(dominant, pb[dominant], per_pass[dominant], None) if dominant else None
         out = {
             "metric": metric, "value": round(paths * args.steps / t_max / 1e6, 3), "unit": "Mpaths/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "n_gpus": world_size, "world_size": world_size, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t_max * 1e3 / args.steps, 4), "higher_is_better": True,
             "scaling": "weak" if (weak and not (vcm or pt)) else "strong",
             "vs_baseline": None, "dtype": "f32",
@@ -365,12 +401,17 @@ def bench_main(args, metric, cpu_baseline=None):
             "dominant_pass": dominant,
             "overlapped_passes": overlapped,
         }
+        if not on_gpu:
+            out["backend"] = f"{backend_name} (launcher test, not a measurement)"
         if cpu_baseline is not None and world == 1:  # the oracle on the host cores, N = 1 only
             try:
                 out["cpu_baseline"] = cpu_baseline(scene, mcode, W, H, P, getattr(args, "cpu_seconds", 20.0))
             except Exception as e:  # the baseline must never hide the GPU line
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), file=json_out, flush=True)
-    r.destroy()
+    if hasattr(r, "destroy"):
+        r.destroy()
+    elif hasattr(r, "close"):
+        r.close()
     dist.barrier()
     dist.destroy_process_group()

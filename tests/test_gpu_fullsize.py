@@ -9,7 +9,11 @@ sizes bench.py times:
   configs[0]  Cornell 256x256 PT, 1 spp                 output + RNG bit-exact
   configs[1]  Cornell 1024x1024 PPM, 1024^2 photons      two iterations (radius update)
   configs[2]  hall 1920x1080 PPM, 2048^2 photons         two iterations
-  configs[3]  hall 1920x1080 VCM                         first iteration (incl. the LVC estimate launch)
+  configs[3]  hall 1920x1080 VCM                         two iterations (the first runs the LVC estimate
+                                                         launch; the second is the bench's steady state)
+  configs[4]  conference 3840x2160 PPM, 4096^2 photons   one iteration on one device, and the same frame
+                                                         through eight row-interleaved shards (strong
+                                                         scaling, the 8-GPU bench's partition)
 
 Bars (north_star; same as check_ppm_iteration / check_vcm_iteration): RNG,
 hit points, grid offsets, per-cell photon multisets, direct light, visit
@@ -36,18 +40,19 @@ def rel_l2(a, b):
 
 def cell_sorted_photons(photons, offsets):
     """Grid-ordered photons [n, 9] with each cell's rows put in a canonical
-    order (by a 64-bit hash of the row, then the row words): equal arrays
-    <=> every cell holds the same multiset of photons."""
+    order (by a 64-bit hash of the row): equal arrays <=> every cell holds the
+    same multiset of photons (two different rows of one cell with equal hashes
+    would only make equal multisets compare unequal, never the reverse)."""
     rows = np.ascontiguousarray(photons.view(np.uint32).reshape(-1, 9))
     off = offsets.astype(np.int64)
     n = int(off[-1] - off[0])
     assert rows.shape[0] == n, (rows.shape, n)
-    cell = np.repeat(np.arange(len(off) - 1, dtype=np.int64), np.diff(off))
+    cell = np.repeat(np.arange(len(off) - 1, dtype=np.int32), np.diff(off))
     h = np.zeros(n, np.uint64)
     with np.errstate(over="ignore"):
         for k in range(9):
             h = (h * np.uint64(0x100000001B3)) ^ rows[:, k].astype(np.uint64)
-    order = np.lexsort(tuple(rows[:, k] for k in range(8, -1, -1)) + (h, cell))
+    order = np.lexsort((h, cell))
     return rows[order]
 
 
@@ -121,13 +126,7 @@ def test_full_size_ppm(which):
     ora.close()
 
 
-def test_configs3_hall1080p_vcm():
-    scene = synthetic.synthetic_hall()
-    W, H = 1920, 1080
-    gpu, ora, det = pair(scene, W, H, 64, _abi.VCM_BIDIRECTIONAL_PATH_TRACING)
-    radius = scene.initial_ppm_radius()
-    gpu.renderNextIteration(0, 0, radius, True, det)
-    ora.render_next_iteration(0, 0, radius, det.to_abi())
+def check_vcm_full(gpu, ora, W, H):
     for buf, name in ((_abi.BUF_RNG, "rng"), (_abi.BUF_VCM_VERTEX_COUNT, "vertex counts"),
                       (_abi.BUF_VCM_CAMERA, "camera colours")):
         assert_same(gpu, ora, buf, name)
@@ -141,8 +140,91 @@ def test_configs3_hall1080p_vcm():
     del gv, ov
     gs, os_ = gpu.read_buffer(_abi.BUF_VCM_SPLAT), ora.read_buffer(_abi.BUF_VCM_SPLAT)
     assert rel_l2(gs, os_) < 1e-5, rel_l2(gs, os_)
+
+
+def test_configs3_hall1080p_vcm():
+    """Iteration 0 (with the light-vertex-count estimate launch, OptixRenderer.cpp:699-773) and
+    iteration 1, the steady state bench.py times: the camera pass continues each slot's RNG
+    stream from the light pass of the same iteration (VCMLightPass.cu:88, VCMCameraPass.cu:79,
+    112) and the vertex cache is rewritten."""
+    scene = synthetic.synthetic_hall()
+    W, H = 1920, 1080
+    gpu, ora, det = pair(scene, W, H, 64, _abi.VCM_BIDIRECTIONAL_PATH_TRACING)
+    radius = scene.initial_ppm_radius()
+    for it in range(2):
+        gpu.renderNextIteration(it, it, radius, True, det)
+        ora.render_next_iteration(it, it, radius, det.to_abi())
+        check_vcm_full(gpu, ora, W, H)
+        radius = next_ppm_radius(radius, it)
     g, o = gpu.getOutputBuffer(), ora.output()
     assert np.isfinite(g).all() and g.mean() > 0
     assert rel_l2(g, o) < 1e-4, rel_l2(g, o)
     gpu.destroy()
     ora.close()
+
+
+def test_configs4_conference4k_ppm_single_and_8_shards():
+    """configs[4] (IndirectRadianceEstimation.cu:69-227, OptixRenderer.cpp:569-673) at full size:
+    conference 3840x2160, 4096^2 = 16,777,216 emitted photons, one iteration.
+
+    1. One device against the oracle with check_ppm_full's bars (RNG, hit points, offsets,
+       per-cell photon multisets, direct, visit counters bit-exact; indirect rel-L2 <= 1e-5).
+    2. The same frame through eight row-interleaved shards in the 8-GPU bench's strong-scaling
+       partition (each shard: 1/8 of the pixel rows, photon launch rows and RNG rows; cell-order
+       photon layout and the per-lane gather that world >= 8 selects), exchanging hit points and
+       partial indirect through torch ops, against the oracle's output: rel-L2 <= 1e-5."""
+    import torch
+
+    from oppositerenderer_amd import multigpu
+
+    scene = synthetic.synthetic_conference()
+    W, H, P = 3840, 2160, 4096
+    gpu, ora, det = pair(scene, W, H, P, _abi.PROGRESSIVE_PHOTON_MAPPING)
+    radius = scene.initial_ppm_radius()
+    gpu.renderNextIteration(0, 0, radius, True, det)
+    ora.render_next_iteration(0, 0, radius, det.to_abi())
+    check_ppm_full(gpu, ora)
+    assert gpu.stats().valid_photons > P * P // 2
+    g, o = gpu.getOutputBuffer(), ora.output()
+    assert g.mean() > 0
+    assert rel_l2(g, o) < 1e-4, rel_l2(g, o)
+    gpu.destroy()
+    ora.close()
+    del g
+    torch.cuda.empty_cache()
+
+    world = 8
+    dev = torch.device("cuda", 0)
+    req = det.to_abi()
+    shards = []
+    for rank in range(world):
+        r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P))
+        r.initialize(0)
+        r.set_shard(rank, world)
+        r.initScene(scene)
+        shards.append(multigpu.DeviceShard(r, torch, dev))
+    mr = (H + world - 1) // world
+    for b in shards:
+        b.local_passes(0, 0, radius, req)
+    hps = []
+    for b in shards:
+        t = b.alloc(mr * W * 10)
+        b.export_hitpoints(t)
+        hps.append(t)
+    hp_all = torch.cat(hps)
+    del hps
+    total = shards[0].alloc(world * mr * W * 3)
+    part = shards[0].alloc(world * mr * W * 3)
+    for b in shards:
+        b.gather_external(hp_all, world, part)
+        total += part
+    blk = mr * W * 3
+    for k, b in enumerate(shards):
+        b.finish(total[k * blk:(k + 1) * blk].contiguous())
+    torch.cuda.synchronize()
+    blocks = [b.output_local_tensor(mr).cpu().numpy().reshape(mr, W, 3) for b in shards]
+    got = multigpu.assemble_rows(blocks, W, H, world)
+    assert np.isfinite(got).all()
+    assert rel_l2(got, o) < 1e-5, rel_l2(got, o)
+    for b in shards:
+        b.r.destroy()

@@ -269,3 +269,98 @@ def test_full_size_conference_sharded_equals_single():
     assert err < 1e-5, err
     for b in shards:
         b.r.destroy()
+
+
+def _oracle_ppm(scene, W, H, P, PH, iters, photon_map=0):
+    import oracle_lib
+
+    ora = oracle_lib.OracleRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=PH,
+                                                        photon_map=photon_map))
+    ora.init_scene(scene)
+    req = RenderRequestDetails(scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H))),
+                               scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W, H).to_abi()
+    radius = scene.initial_ppm_radius()
+    for it in range(iters):
+        ora.render_next_iteration(it, it, radius, req)
+        radius = next_ppm_radius(radius, it)
+    out = ora.output().copy()
+    ora.close()
+    return out
+
+
+@pytest.mark.parametrize("world,W,H,P,PH,photon_map,pipelined",
+                         [(4, 96, 80, 128, 128, 0, False), (8, 96, 80, 128, 128, 0, False),
+                          (8, 100, 75, 96, 101, 0, False), (4, 96, 80, 128, 128, 0, True),
+                          (8, 96, 80, 128, 128, 0, True), (4, 96, 80, 128, 128, 2, False),
+                          (8, 96, 80, 128, 128, 2, True)])
+def test_sharded_world4_world8_match_oracle(world, W, H, P, PH, photon_map, pipelined):
+    """The 4- and 8-GPU partitions of the multi-GPU bench (strong scaling: a fixed P x PH global
+    photon launch and W x H pixels dealt to the ranks by rows; PH = 101 gives uneven shares),
+    on one device with the collectives done by torch ops, against the ORACLE's single renderer
+    (OptixRenderer.cpp:569-673; the gather is linear in the photon set, so the union of the
+    shards is the reference frame up to fp32 summation order).  Covers what world >= 4 selects:
+    cell-order photon layout, the per-lane gather at eight segments, the kd-tree shard, and the
+    pipelined side-stream schedule (orx_set_ppm_pipeline)."""
+    dev = torch.device("cuda", 0)
+    scene = scenes.cornell()
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    det = RenderRequestDetails(cam, scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W, H)
+    req = det.to_abi()
+    side = torch.cuda.Stream(dev) if pipelined else None
+    shards = []
+    for rank in range(world):
+        r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=PH,
+                                              photon_map=photon_map))
+        r.initialize(0)
+        r.set_shard(rank, world)
+        r.initScene(scene)
+        b = multigpu.DeviceShard(r, torch, dev)
+        if pipelined:
+            b.enable_pipeline(side)
+        shards.append(b)
+    main = torch.cuda.current_stream(dev)
+    mr = (H + world - 1) // world
+    blk = mr * W * 3
+    nsets = 2 if pipelined else 1
+    sets = [([b.alloc(mr * W * 10) for b in shards], shards[0].alloc(world * mr * W * 10),
+             [b.alloc(world * blk) for b in shards], shards[0].alloc(world * blk)) for _ in range(nsets)]
+    radius = scene.initial_ppm_radius()
+    iters = 3
+    for it in range(iters):
+        hp_loc, hp_all, parts, total = sets[it % nsets]
+        if pipelined:
+            for b, t in zip(shards, hp_loc):
+                b.local_eye(it, it, radius, req)
+                b.export_hitpoints(t)
+            hp_all.copy_(torch.cat(hp_loc))
+            for b in shards:
+                b.local_photons()
+            with torch.cuda.stream(side):
+                side.wait_stream(main)
+                for b, part in zip(shards, parts):
+                    b.gather_external(hp_all, world, part)
+                total.copy_(torch.stack(parts).sum(0))
+                for k, b in enumerate(shards):
+                    b.finish(total[k * blk:(k + 1) * blk].contiguous())
+        else:
+            for b, t in zip(shards, hp_loc):
+                b.local_passes(it, it, radius, req)
+                b.export_hitpoints(t)
+            hp_all.copy_(torch.cat(hp_loc))
+            for b, part in zip(shards, parts):
+                b.gather_external(hp_all, world, part)
+            total.copy_(torch.stack(parts).sum(0))
+            for k, b in enumerate(shards):
+                b.finish(total[k * blk:(k + 1) * blk].contiguous())
+        radius = next_ppm_radius(radius, it)
+    torch.cuda.synchronize()
+    got = multigpu.assemble_rows([b.output_local_tensor(mr).cpu().numpy().reshape(mr, W, 3) for b in shards],
+                                 W, H, world)
+    ref = _oracle_ppm(scene, W, H, P, PH, iters, photon_map)
+    err = np.sqrt(((got.astype(np.float64) - ref) ** 2).sum() / (ref.astype(np.float64) ** 2).sum())
+    assert ref.mean() > 0 and np.isfinite(got).all()
+    assert err < 1e-5, err
+    if pipelined:
+        assert all(b.r.pipelined() for b in shards)
+    for b in shards:
+        b.r.destroy()
