@@ -94,38 +94,46 @@ PHOTON_MAPS = {"grid": 0, "hash": 1, "kd": 2}  # orx_config.photon_map
 _METHOD_NAME = {0: "PT", 1: "VCM", 2: "PPM"}
 
 
-def traffic_lookup(key, kernels):
-    """PMC-measured HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, the gfx950
-    correction of MI355X_MICROARCH.md) recorded by tools/profile_traffic.py for
-    this exact workload, or None."""
+def _table(name, key):
     try:
-        table = json.load(open(os.path.join(ROOT, "profiles", "traffic.json"))).get(key, {})
+        return json.load(open(os.path.join(ROOT, "profiles", name))).get(key, {})
     except (OSError, ValueError):
-        return None
-    vals = [table[k]["bytes_per_launch"] for k in kernels if k in table]
+        return {}
+
+
+def table_entries(table, kernels):
+    """The entries of a per-kernel profile table (keys: kernel names with template arguments,
+    tools/profile_traffic.short) that belong to the pass's kernels (base names, `k_kd_*` prefixes)."""
+    out = {}
+    for k, v in table.items():
+        base = k.split("<")[0]
+        if any(base == w or (w.endswith("*") and base.startswith(w[:-1])) for w in kernels):
+            out[k] = v
+    return out
+
+
+def traffic_lookup(key, kernels):
+    """PMC-measured HBM bytes per launch of the pass (2 x FETCH_SIZE + WRITE_SIZE, the gfx950
+    correction of MI355X_MICROARCH.md; mean over the bench's timed iterations) recorded by
+    tools/profile_traffic.py for this exact workload, or None."""
+    vals = [v["bytes_per_launch"] for v in table_entries(_table("traffic.json", key), kernels).values()]
     return int(sum(vals)) if vals else None
 
 
 def profiled_kernels(key, kernels):
-    """The pass's kernels the committed PMC profile of this workload saw dispatched (None: no profile)."""
-    try:
-        table = json.load(open(os.path.join(ROOT, "profiles", "traffic.json"))).get(key, {})
-    except (OSError, ValueError):
-        return None
-    return [k for k in kernels if k in table] or None
+    """The pass's kernels (with template arguments) the committed PMC profile of this workload saw
+    dispatched (None: no profile)."""
+    return sorted(table_entries(_table("traffic.json", key), kernels)) or None
 
 
 def bound_lookup(key, kernels):
-    """What bounds the kernel, from the committed PMC passes (profiles/bound.json, written by
+    """What bounds the pass's longest kernel, from the committed PMC passes (profiles/bound.json,
     tools/pmc_bound.py): VALU issue, the vector-memory address path (TA) or HBM."""
-    try:
-        table = json.load(open(os.path.join(ROOT, "profiles", "bound.json"))).get(key, {})
-    except (OSError, ValueError):
+    ent = table_entries(_table("bound.json", key), kernels)
+    if not ent:
         return None
-    for k in kernels:
-        if k in table:
-            return table[k]
-    return None
+    k = max(ent, key=lambda n: ent[n].get("avg_us_standalone", ent[n].get("avg_us_profiled", 0.0)))
+    return dict(ent[k], bound_kernel=k)
 
 
 def host_cpu():
@@ -167,8 +175,7 @@ def host_cpu():
 def cpu_baseline(scene, method, W, H, P, seconds, photon_map=0):
     """Oracle (oracle/liborx_oracle.so: the C/OpenMP restatement of the reference
     passes) on the host cores, same scene, resolution, photon count and seed as
-    the GPU line.  Iterations 0, 1, ... are timed (iteration 0 includes the RNG
-    initialisation and, for VCM, the light-subpath estimate launch) until
+    the GPU line.  Iteration 0 runs untimed; iterations 1, 2, ... are timed until
     `seconds` of CPU wall time are spent (at least one, at most 8); median."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
@@ -187,10 +194,14 @@ def cpu_baseline(scene, method, W, H, P, seconds, photon_map=0):
     r = oracle_lib.OracleRenderer(cfg)
     r.init_scene(scene)
     radius = scene.initial_ppm_radius()
+    # iteration 0 carries the buffer allocation, the RNG initialisation and (VCM) the light-vertex
+    # estimate launch: untimed, like the GPU line's warmup
+    r.render_next_iteration(0, 0, radius, req)
+    radius = next_ppm_radius(radius, 0)
     times = []
     t_start = time.perf_counter()
-    it = 0
-    while it < 8 and (it == 0 or (time.perf_counter() - t_start) < seconds):
+    it = 1
+    while it < 9 and (it == 1 or (time.perf_counter() - t_start) < seconds):
         t0 = time.perf_counter()
         r.render_next_iteration(it, it, radius, req)
         times.append(time.perf_counter() - t0)
@@ -205,7 +216,7 @@ def cpu_baseline(scene, method, W, H, P, seconds, photon_map=0):
             "sample": f"oracle (C/OpenMP restatement of the reference passes, {cores} threads) on the full "
                       f"workload: {scene.name} {W}x{H} {_METHOD_NAME[method]}"
                       + (f", {P * P} photons/iter" if method == 2 else "") +
-                      f"; median of {len(times)} iteration(s) from iteration 0"}
+                      f"; median of {len(times)} iteration(s) after one untimed iteration"}
 
 
 def roofline_block(pass_ms, pbytes, key, photon_map, serial_ms=None, overlapped=()):
@@ -220,7 +231,15 @@ def roofline_block(pass_ms, pbytes, key, photon_map, serial_ms=None, overlapped=
                              photon_map=photon_map, kernels=seen)
     b = bound_lookup(key, kernels)
     if b:
-        roof.update(b)
+        roof["bound"] = b.get("bound", "unmeasured")
+        roof["bound_source"] = b.get("bound_source")
+        # the compute roofline beside the HBM one: VALU issue slots of the chip's 1024 SIMD-32s
+        # (calibrated cost per instruction, profiles/valu_calib.json), achieved fp32 FLOP/s, the
+        # vector-memory address unit, and the fraction of wave time spent waiting
+        roof["compute"] = {k: b[k] for k in ("valu_issue_frac", "fp32_tflops", "fp32_frac", "ta_frac", "wait_frac",
+                                              "hbm_frac", "avg_us_standalone", "bound_kernel") if k in b}
+        roof["compute"]["peak"] = ("VALU issue: 1024 SIMD-32 x clock at 4 cycles per wave64 instruction "
+                                   "(profiles/valu_calib.json); fp32: 157.3 TFLOP/s; TA: 256 CUs x clock")
     else:
         roof["bound"] = "unmeasured"
     roof["overlapped"] = dominant in overlapped
@@ -357,11 +376,15 @@ def main():
         for k, v in serial.items():
             if k in passes:
                 passes[k]["serial_ms"] = round(v, 4)
-    if method == _abi.PROGRESSIVE_PHOTON_MAPPING:
+    if method == _abi.PROGRESSIVE_PHOTON_MAPPING and dominant == "ppm_gather":
+        # SURVEY 8(d) prices the gather as N*(64+12) + Z*8 + V*36 with V the photons in the
+        # reference's search windows; those window photons are re-read from L1/LDS, not HBM
+        # (each grid photon is loaded once per 8x8 wave tile), so the algorithmic bytes here
+        # charge each grid photon once
         visited = st.photons_visited_total / n_it
-        gms = (serial or per_pass).get("ppm_gather", 0.0)
-        roof["gather_visited_photons_per_launch"] = int(visited)
-        roof["gather_visited_photon_GBps"] = round(visited * 36 / (gms * 1e-3) / 1e9, 1) if gms > 0 else None
+        roof["bytes_model"] = ("hit points 40 B + indirect 12 B per pixel, each grid photon once (36 B), "
+                               "offsets once; departs from SURVEY 8(d)'s V x 36 B per window photon")
+        roof["window_photons_per_launch"] = int(visited)
     data = ("synthetic: seeded procedural scene (" + scene.name + "), XORWOW streams seeded 1645301512; "
             "no assets or checkpoints")
     out = {

@@ -388,9 +388,8 @@ struct orx_renderer {
     hipStream_t ext_stream = nullptr; /* caller-provided stream (orx_set_stream) */
     bool use_ext = false;
     DevBuf d_rng, d_hp, d_ind, d_dir, d_out, d_dbg;
-    DevBuf d_slots, d_vmask, d_sorted, d_perm, d_keys, d_ranks;
-    DevBuf d_hist, d_offsets, d_bbox, d_partials, d_grid, d_work;
-    DevBuf d_wray0, d_wray1, d_whit, d_wpath, d_wseg; /* wavefront photon pass queues */
+    DevBuf d_slots, d_vmask, d_sorted, d_perm, d_keys;
+    DevBuf d_offsets, d_bbox, d_grid;
     DevBuf d_pos4, d_bstable, d_bspartials, d_bspairs, d_subofs;  /* bucket-sort grid build */
     DevBuf d_hcount, d_hwin;  /* stochastic hash table */
     DevBuf d_hp2, d_dir2, d_sorted2, d_subofs2, d_offsets2, d_grid2; /* second buffer set (pipelining) */
@@ -481,11 +480,9 @@ static bool hash_config_ok(const orx_config& c) {
     return n && n <= (1ull << 31) && (n & (n - 1)) == 0 && c.max_photon_trace_depth <= 9;
 }
 
-/* the deferred gather yields to the next iteration's passes (ORX_GATHER_PRIORITY: 0 normal,
- * 1 lowest, the default; measured equal on the hall) */
+/* the deferred gather yields to the next iteration's passes (lowest priority; measured equal
+ * to normal priority on the hall) */
 static int gather_stream_priority() {
-    const char* e = getenv("ORX_GATHER_PRIORITY");
-    if (e && atoi(e) == 0) return 0;
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
     return least;
@@ -861,7 +858,6 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     const size_t nphot = (size_t)r->prows * PW;
     const size_t S = nphot * D;
     const size_t G2 = (size_t)r->cfg.photon_grid_max_size + 2;
-    const size_t nblocks = (G2 + 1023) / 1024 + 1;
     HIPCHK(r, r->d_rng.ensure(nslot_rng * 24));
     HIPCHK(r, r->d_hp.ensure(nhp * 40));
     HIPCHK(r, r->d_ind.ensure(nhp * 12));
@@ -879,17 +875,9 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_perm.ensure(S * 4 + 16));
     HIPCHK(r, hipMemsetAsync(r->d_sorted.p, 0, SP_PLANES * splane * 4, r->stream)); /* tail reads stay finite */
     HIPCHK(r, r->d_keys.ensure(S * 4));
-    HIPCHK(r, r->d_ranks.ensure(S * 4));
-    HIPCHK(r, r->d_hist.ensure(G2 * 4));
     HIPCHK(r, r->d_offsets.ensure(G2 * 4));
     HIPCHK(r, r->d_bbox.ensure(6 * BBOX_REPLICAS * 4));
-    HIPCHK(r, r->d_partials.ensure(nblocks * 4));
     HIPCHK(r, r->d_grid.ensure(sizeof(GridParams)));
-    HIPCHK(r, r->d_work.ensure(64));
-    HIPCHK(r, r->d_wray0.ensure(nphot * 32 + 32));
-    HIPCHK(r, r->d_wray1.ensure(nphot * 32 + 32));
-    HIPCHK(r, r->d_whit.ensure(nphot * 32 + 32));
-    HIPCHK(r, r->d_wpath.ensure(nphot * 32 + 32));
     /* bucket-sort grid build: at most 2048 buckets of 2^bshift virtual cells
      * (nsub sub-rows per cell row, k_bs_count) */
     /* sub-row layout on one device; a shard of world >= 2 gathers all W*H hit points against 1/N
@@ -912,10 +900,6 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
      * (ensure_second_set); the sharded pipeline (orx_set_ppm_pipeline) wants it at once */
     r->pipe_bufs = false;
     r->pend = false;
-    const size_t wnseg = (nphot + 511) / 512 + 1;
-    HIPCHK(r, r->d_wseg.ensure(2 * wnseg * 4));
-    HIPCHK(r, hipMemsetAsync(r->d_wseg.p, 0, 2 * wnseg * 4, r->stream));
-    HIPCHK(r, hipMemsetAsync(r->d_hist.p, 0, G2 * 4, r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_offsets.p, 0, G2 * 4, r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_vmask.p, 0, nphot, r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_grid.p, 0, sizeof(GridParams), r->stream));
@@ -1022,17 +1006,9 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     pb.splane = (uint32_t)splane;
     pb.perm = r->d_perm.as<uint32_t>();
     pb.keys = r->d_keys.as<uint32_t>();
-    pb.ranks = r->d_ranks.as<uint32_t>();
-    pb.hist = r->d_hist.as<uint32_t>();
     pb.offsets = r->d_offsets.as<uint32_t>();
     pb.bbox = r->d_bbox.as<uint32_t>();
-    pb.scan_partials = r->d_partials.as<uint32_t>();
     pb.grid = r->d_grid.as<GridParams>();
-    pb.work = r->d_work.as<uint32_t>();
-    pb.wray[0] = r->d_wray0.as<float4>();
-    pb.wray[1] = r->d_wray1.as<float4>();
-    pb.whit = r->d_whit.as<float4>();
-    pb.wpath = r->d_wpath.as<float4>();
     pb.pos4 = r->d_pos4.as<float4>();
     pb.bshift = bshift;
     pb.nsub = nsub;
@@ -1040,16 +1016,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     pb.bs_table = r->d_bstable.as<uint32_t>();
     pb.bs_partials = r->d_bspartials.as<uint32_t>();
     pb.bs_pairs = r->d_bspairs.as<uint2>();
-    {
-        static const int atomic_grid_env = [] {
-            const char* e = getenv("ORX_GRID_ATOMIC");
-            return e ? atoi(e) : 0;
-        }();
-        pb.subofs = atomic_grid_env ? nullptr : r->d_subofs.as<uint32_t>();
-        if (atomic_grid_env) pb.nsub = 1; /* the atomic path sorts by cell only */
-    }
-    pb.wseg = r->d_wseg.as<uint32_t>();
-    pb.wnseg = (uint32_t)wnseg;
+    pb.subofs = r->d_subofs.as<uint32_t>();
 
     /* initializeRandomStates (OptixRenderer_SpatialHash.cu:310-347) */
     uint32_t seed = r->cfg.seed;
@@ -1253,7 +1220,6 @@ static GatherIn local_gather_in(orx_renderer* r) {
     gi.W = r->W;
     gi.indirect = r->d_ind.as<float>();
     gi.dbg = r->cfg.debug_counters ? r->d_dbg.as<uint32_t>() : nullptr;
-    gi.tshape = 0;
     gi.visits = 1;
     return gi;
 }
@@ -1285,12 +1251,7 @@ static void ppm_photons_grid(orx_renderer* r, const Consts& c) {
     hipStream_t st = cur_stream(r);
     ev_begin(r, P_PHOTON);
     r->eye_chain = false;
-    static const int wavefront = [] {
-        const char* e = getenv("ORX_PHOTON_WAVEFRONT");
-        return e ? atoi(e) : 0;
-    }();
-    if (wavefront && !r->pb.hash) launch_ppm_photon_wavefront(st, r->scene, r->px, r->pb, c);
-    else launch_ppm_photon(st, r->scene, r->px, r->pb, c);
+    launch_ppm_photon(st, r->scene, r->px, r->pb, c);
     ev_end(r, P_PHOTON);
     if (r->overlap_direct) {
         /* the direct pass needs the hitpoints and the RNG states the photon pass
@@ -1316,24 +1277,17 @@ static void ppm_photons_grid(orx_renderer* r, const Consts& c) {
         ev_end(r, P_SETUP_HASH);
         return;
     }
-    /* grid build: the atomic-free bucket sort (default) or the atomic-rank
-     * counting sort (ORX_GRID_ATOMIC=1, kept for A/B) */
-    static const int atomic_grid = [] {
-        const char* e = getenv("ORX_GRID_ATOMIC");
-        return e ? atoi(e) : 0;
-    }();
+    /* grid build: the atomic-free bucket sort (an atomic-rank counting sort measured slower:
+     * one device-scope atomic per photon into a 4 MB histogram) */
     ev_begin(r, P_SETUP_HASH);
     launch_grid_setup(st, r->pb);
-    if (atomic_grid) launch_grid_hash(st, r->pb);
-    else launch_grid_bucket_count(st, r->pb);
+    launch_grid_bucket_count(st, r->pb);
     ev_end(r, P_SETUP_HASH);
     ev_begin(r, P_SCAN);
-    if (atomic_grid) launch_grid_scan(st, r->pb);
-    else launch_grid_bucket_scan(st, r->pb);
+    launch_grid_bucket_scan(st, r->pb);
     ev_end(r, P_SCAN);
     ev_begin(r, P_SCATTER);
-    if (atomic_grid) launch_grid_scatter(st, r->pb);
-    else launch_grid_bucket_place(st, r->pb);
+    launch_grid_bucket_place(st, r->pb);
     ev_end(r, P_SCATTER);
 }
 static void ppm_local_passes(orx_renderer* r, const DevCamera& cam, const Consts& c) {
@@ -1487,14 +1441,10 @@ static orx_status ppm_pipelined_iteration(orx_renderer* r, const orx_request* de
     HIPCHK(r, hipEventRecord(r->ev_grid_done, st));
     hipStream_t g = r->gstream;
     HIPCHK(r, hipStreamWaitEvent(g, r->ev_grid_done, 0));
-    static const size_t lds_pad = [] {
-        const char* e = getenv("ORX_GATHER_LDS_PAD_KB");
-        return e ? (size_t)atoi(e) * 1024 : (size_t)0;
-    }();
     ev_begin_on(r, P_GATHER, g);
     if (r->cfg.photon_map == 2) launch_ppm_gather_kd(g, local_gather_in(r), r->pb, r->kd, c);
     else if (r->pb.hash) launch_ppm_gather_hash(g, local_gather_in(r), r->pb, hash_params(r, c.ppm_radius), c);
-    else launch_ppm_gather(g, local_gather_in(r), r->pb, c, lds_pad);
+    else launch_ppm_gather(g, local_gather_in(r), r->pb, c);
     ev_end_on(r, P_GATHER, g);
     HIPCHK(r, hipStreamWaitEvent(g, r->ev_direct_done, 0));
     ev_begin_on(r, P_DIRECT, g);
@@ -1557,11 +1507,9 @@ static orx_status render_next_iteration(orx_renderer* r, uint64_t local_iteratio
         orx_status sv = vcm_iteration(r, det, ppm_radius);
         if (sv != ORX_OK) return sv;
     } else {
-        static const int overlap = [] {
-            const char* e = getenv("ORX_OVERLAP_DIRECT");
-            return e ? atoi(e) : 1;
-        }();
-        r->overlap_direct = overlap != 0;
+        /* the direct pass on the aux stream beside the grid build and the gather; the output
+         * accumulation after both */
+        r->overlap_direct = true;
         ppm_local_passes(r, cam, c);
         ev_begin(r, P_GATHER);
         if (r->pb.hash) launch_ppm_gather_hash(st, local_gather_in(r), r->pb, hash_params(r, c.ppm_radius), c);
@@ -1569,12 +1517,8 @@ static orx_status render_next_iteration(orx_renderer* r, uint64_t local_iteratio
         else launch_ppm_gather(st, local_gather_in(r), r->pb, c);
         ev_end(r, P_GATHER);
         ev_begin(r, P_DIRECT);
-        if (r->overlap_direct) {
-            HIPCHK(r, hipStreamWaitEvent(st, r->ev_direct_done, 0));
-            launch_ppm_direct_output(st, r->scene, r->px, c, 2);
-        } else {
-            launch_ppm_direct_output(st, r->scene, r->px, c, 0);
-        }
+        HIPCHK(r, hipStreamWaitEvent(st, r->ev_direct_done, 0));
+        launch_ppm_direct_output(st, r->scene, r->px, c, 2);
         ev_end(r, P_DIRECT);
         r->overlap_direct = false;
     }
@@ -1667,7 +1611,6 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hp, uint32_t seg
     gi.W = r->W;
     gi.indirect = (float*)indirect;
     gi.dbg = nullptr;
-    gi.tshape = 0;
     gi.visits = 0; /* rank-local counts are not the reference's; no per-pixel debug buffers here */
     hipStream_t st = cur_stream(r);
     if (r->last_pipelined) { /* on the side stream, after the grid build */

@@ -72,28 +72,18 @@ struct PhotonBufs {
     float* sorted;      /* grid-ordered photons, SP_PLANES float planes (SoA): x y z | dirq | dir x y z | power x y z */
     uint32_t splane;    /* plane stride in floats (multiple of 4, >= S + 4) */
     uint32_t* perm;     /* [S] grid position -> photon slot (counting-sort scatter target) */
-    uint32_t* keys;     /* [S] */
-    uint32_t* ranks;    /* [S] */
-    uint32_t* hist;     /* [gmax+2] */
+    uint32_t* keys;     /* [S] sub-cell keys (k_bs_count) */
     uint32_t* offsets;  /* [gmax+2] */
     uint32_t* bbox;     /* [6][BBOX_REPLICAS] ordered-float min xyz, max xyz */
-    uint32_t* scan_partials; /* [ceil((gmax+2)/1024)+1] */
     GridParams* grid;
-    uint32_t* work;     /* [1] persistent photon pass: next photon index (zeroed before each launch) */
-    /* wavefront photon pass (launch_ppm_photon_wavefront) */
-    float4* wray[2];    /* ping-pong ray queues [n][2]: o.xyz|tmin, d.xyz|photon index */
-    float4* whit;       /* [n][2]: t|prim|slot|b (sphere: sn.x), g|sn.y|sn.z|- */
-    float4* wpath;      /* [P][2]: power.xyz|weight, depth|numStored|mask|- */
     float4* pos4;       /* [S] deposit positions (compact copy of the records' first float4) */
     uint32_t bshift;    /* bucket sort: cells per bucket = 1 << bshift, at most BS_MAXB buckets */
     uint32_t bs_nchunk; /* slot chunks (ceil(S / BS_CHUNK)) */
     uint32_t* bs_table; /* [buckets][chunks] counts, then exclusive offsets */
     uint32_t* bs_partials; /* scan partials + grand total */
     uint2* bs_pairs;    /* [S] (sub-cell key, slot) in bucket order; sub-cell key = cell * SUBX + x slice */
-    uint32_t* subofs;   /* [SUBX nsub G + 1] first photon of each sub-cell (NULL: atomic grid path, cell offsets only) */
+    uint32_t* subofs;   /* [SUBX nsub G + 1] first photon of each sub-cell */
     uint32_t nsub;      /* sub-rows per cell row: 1 (photons in cell order) or SUBR^2 (see k_bs_count) */
-    uint32_t* wseg;     /* [2][wnseg] live entries of each queue segment */
-    uint32_t wnseg;     /* segments per queue */
     /* stochastic-hash photon map (orx_config.photon_map = 1) */
     uint32_t hash;      /* 1: deposits go to the hash table, D = slot capacity per photon */
     uint32_t Dlim;      /* deposits that end a photon path: D (uniform grid), none (hash: store_photon.h never counts) */
@@ -155,14 +145,7 @@ void launch_rng_init(hipStream_t s, RngPlanes rng, uint32_t RW, uint32_t rows, u
                      uint32_t seed);
 void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c);
 void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c);
-/* wavefront form of the photon pass: emit, then per bounce a persistent
- * trace kernel over the compacted ray queue and a shading kernel */
-void launch_ppm_photon_wavefront(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb,
-                                 const Consts& c);
 void launch_grid_setup(hipStream_t s, const PhotonBufs& pb);
-void launch_grid_hash(hipStream_t s, const PhotonBufs& pb);
-void launch_grid_scan(hipStream_t s, const PhotonBufs& pb);
-void launch_grid_scatter(hipStream_t s, const PhotonBufs& pb);
 /* atomic-free grid build: keys + bucket histogram / scan of the table /
  * bucket placement + per-bucket cells (offsets, permutation) + permute */
 void launch_grid_bucket_count(hipStream_t s, const PhotonBufs& pb);
@@ -178,7 +161,6 @@ struct GatherIn {
     uint32_t segments, seg_rows, W;
     float* indirect;    /* [segments*seg_rows*W*3] */
     uint32_t* dbg;      /* [segments*seg_rows*W*2] or NULL */
-    uint32_t tshape;    /* wave pixel tile of the union gather: 0 = 8x8, 1 = 16x4, 2 = 4x16 */
     uint32_t visits;    /* 1: count the reference's per-pixel visits (IndirectRadianceEstimation.cu:113/124)
                          * into dbg and the stats; 0 for the sharded gather, which has no per-pixel
                          * debug buffers and whose rank-local counts are not the reference's
@@ -194,9 +176,8 @@ __device__ __forceinline__ uint32_t gather_row(const GatherIn& gi, uint32_t y) {
     const uint32_t s = y % gi.segments, lj = y / gi.segments;
     return s * gi.seg_rows + lj;
 }
-/* variant 0: one thread per pixel, 8x8 wave tiles (default); 1: wave-cooperative LDS staging */
-/* lds_pad: unused dynamic LDS per block, to cap the gather's blocks per CU when it overlaps other passes */
-void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, size_t lds_pad = 0);
+/* 8x8-pixel wave tiles; the wave-union kernel, or the per-lane kernel for gathers of >= 8 segments */
+void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c);
 void launch_hash_build(hipStream_t s, const PhotonBufs& pb, const HashParams& hp);
 void launch_ppm_gather_hash(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const HashParams& hp,
                             const Consts& c);

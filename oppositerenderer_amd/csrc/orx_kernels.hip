@@ -8,10 +8,11 @@
  *                       closest-hit photon programs) fused with the photon AABB
  *                       reduction of getPhotonsBoundingBox (SpatialHash.cu:123-128)
  *   k_grid_setup        cell size / grid dims  (SpatialHash.cu:229-249), on device
- *   k_grid_hash         calculateHashCellsKernel (SpatialHash.cu:152-173) + histogram
- *   k_scan_*            exclusive_scan of the histogram (SpatialHash.cu:202-207)
- *   k_grid_scatter      sort_by_key as a counting-sort scatter (SpatialHash.cu:193-196)
- *   k_ppm_gather        PPM_INDIRECT_RADIANCE_ESTIMATION_PASS (ppm/IndirectRadianceEstimation.cu:69-227)
+ *   k_bs_*              calculateHashCellsKernel + sort_by_key + exclusive_scan
+ *                       (SpatialHash.cu:152-207) as an LDS bucket counting sort
+ *   k_grid_permute      the sorted photon array, as SoA planes
+ *   k_ppm_gather_union  PPM_INDIRECT_RADIANCE_ESTIMATION_PASS (ppm/IndirectRadianceEstimation.cu:69-227),
+ *                       wave-union form; k_ppm_gather the per-lane form (sharded gathers at N >= 8)
  *   k_ppm_direct_output PPM_DIRECT + PPM_OUTPUT (ppm/DirectRadianceEstimation.cu:29-77, ppm/Output.cu:32-37)
  *   k_pt                PT_RAYTRACE_PASS       (pt/RayGeneratorPT.cu:46-131)
  * Wave size is 64 on CDNA4; block reductions below are written for it.
@@ -301,10 +302,9 @@ __device__ __forceinline__ void photon_bbox_flush(const PhotonBufs& pb, float lo
     }
 }
 
-#ifndef ORX_PHOTON_CHUNK
-#define ORX_PHOTON_CHUNK 64 /* photons per counter fetch of a persistent wave */
-#endif
-template <bool PERSISTENT>
+/* one photon per lane: block b traces photons [64b, 64b + 64) (per-lane refill from a device
+ * counter, a wavefront pass with per-bounce queues and a direction-binned photon order were
+ * measured slower on the hall: DESIGN.md section 4) */
 __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, PhotonBufs pb, Consts c) {
     ORX_STACK_DECL;
     const StackL stk{ORX_STACK_PTR};
@@ -314,42 +314,10 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
     float hi_x = -INFINITY, hi_y = -INFINITY, hi_z = -INFINITY;
     PhotonPath P;
     Rng rs;
-    bool alive = false;
-    /* the wave's private range [next, end) of photon indices, refilled
-     * CHUNK at a time from the device counter (one atomic per chunk) */
-    constexpr uint32_t CHUNK = ORX_PHOTON_CHUNK;
-    uint32_t next = 0, end = 0;
-    for (;;) {
-        /* refill: lanes without a path take consecutive photon indices */
-        uint64_t need = __ballot(!alive);
-        if (!PERSISTENT) { /* one photon per lane: block b owns photons [64b, 64b + 64) */
-            if (end == 0) {
-                next = blockIdx.x * 64u;
-                end = next + 64u < total ? next + 64u : total;
-                if (next > end) next = end;
-            } else {
-                next = end;
-            }
-        }
-        if (PERSISTENT && need && next >= end && end < total) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(pb.work, CHUNK);
-            base = (uint32_t)__shfl((int)base, 0, 64);
-            next = base < total ? base : total;
-            end = base + CHUNK < total ? base + CHUNK : total;
-            if (base >= total) end = total, next = total;
-        }
-        if (need && next < end) {
-            const uint32_t avail = end - next;
-            const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
-            if (!alive && rank < avail) {
-                photon_emit(S, px, pb, next + rank, P, rs);
-                alive = true;
-            }
-            const uint32_t n = (uint32_t)__popcll(need);
-            next += n < avail ? n : avail;
-        }
-        if (!__ballot(alive)) break;
+    const uint32_t p = blockIdx.x * 64u + lane;
+    bool alive = p < total;
+    if (alive) photon_emit(S, px, pb, p, P, rs);
+    while (__ballot(alive)) {
         if (alive) alive = photon_bounce(S, px, pb, c, P, rs, stk, NodesG{}, lo_x, lo_y, lo_z, hi_x, hi_y, hi_z);
     }
     photon_bbox_flush(pb, lo_x, lo_y, lo_z, hi_x, hi_y, hi_z, blockIdx.x & (BBOX_REPLICAS - 1), lane);
@@ -357,304 +325,8 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
 
 void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c) {
     const uint32_t total = pb.prows * pb.PW;
-    static const int persistent = [] {
-        const char* e = getenv("ORX_PHOTON_PERSISTENT");
-        return e ? atoi(e) : 0;
-    }();
-    if (persistent) { /* per-lane refill (A/B): one-wave blocks drain the shared photon counter */
-        /* one wave per resident slot (4 per SIMD at this kernel's registers and LDS stack) */
-        static const uint32_t waves = [] {
-            const char* e = getenv("ORX_PHOTON_PERSISTENT_WAVES");
-            return e ? (uint32_t)atoi(e) : 256u * 4u * 4u;
-        }();
-        const uint32_t blocks = std::min<uint32_t>((total + 63) / 64, waves);
-        hipMemsetAsync(pb.work, 0, 4, s);
-        hipLaunchKernelGGL(k_ppm_photon<true>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, px, pb, c);
-    } else {
-        hipLaunchKernelGGL(k_ppm_photon<false>, dim3((total + 63) / 64), dim3(64), ORX_STACK_BYTES(S), s, S, px, pb, c);
-    }
-}
-
-/* ------------------------------------------------------------------ */
-/* wavefront photon pass                                               */
-/* ------------------------------------------------------------------ */
-/* The single-kernel pass above runs a wave until its longest photon path
- * has finished, and each bounce until its lane with the most node visits
- * has: PMC shows it VALU-saturated at ~1/3 useful lanes.  Here every
- * bounce is a compacted queue: k_wf_trace is a persistent traversal kernel
- * whose lanes take a new ray from the queue as soon as theirs finishes
- * (dynamic fetch), k_wf_shade runs the photon closest-hit programs over the
- * hits and appends the surviving paths to the next bounce's queue.  Every
- * path evaluates exactly the operations of k_ppm_photon in the same order
- * (RNG state stays in its slot), so the deposits are bit-identical. */
-__device__ __forceinline__ float4 u4f(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    return make_float4(__uint_as_float(a), __uint_as_float(b), __uint_as_float(c), __uint_as_float(d));
-}
-
-/* Queues are kept as WF_SEG-entry segments: segment k of a bounce's queue
- * holds the surviving paths of segment k of the previous bounce, compacted
- * in place by the shading block that owns it (an LDS prefix sum), with its
- * length in wseg[parity][k].  No queue position ever comes from a global
- * atomic: one counter for all waves serialises at the memory side (~12 ns
- * per add), which at 19 M rays per pass costs more than the tracing. */
-constexpr uint32_t WF_SEG = 512;
-
-__global__ __launch_bounds__(256) void k_wf_emit(DevScene S, PixelBufs px, PhotonBufs pb) {
-    const uint32_t total = pb.prows * pb.PW;
-    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < total; p += gridDim.x * blockDim.x) {
-        PhotonPath P;
-        Rng rs;
-        photon_emit(S, px, pb, p, P, rs);
-        rng_store(px.rng, P.slot, rs);
-        pb.wpath[2 * (size_t)p] = make_float4(P.power.x, P.power.y, P.power.z, P.weight);
-        pb.wpath[2 * (size_t)p + 1] = u4f(0u, 0u, 0u, 0u);
-        float4* r = pb.wray[0] + 2 * (size_t)p;
-        r[0] = make_float4(P.o.x, P.o.y, P.o.z, P.tmin);
-        r[1] = make_float4(P.d.x, P.d.y, P.d.z, __uint_as_float(p));
-        if (p % WF_SEG == 0) pb.wseg[p / WF_SEG] = total - p < WF_SEG ? total - p : WF_SEG;
-    }
-}
-
-/* persistent closest-hit traversal over the queue of parity `par`: wave w
- * walks segments w, w + waves, ...; a lane whose ray is done takes the next
- * ray of the wave's current segment (dynamic fetch without atomics) */
-__global__ __launch_bounds__(64) void k_wf_trace(DevScene S, PhotonBufs pb, uint32_t par, uint32_t nseg) {
-    ORX_STACK_DECL;
-    uint32_t* stk = ORX_STACK_PTR;
-    const uint32_t lane = threadIdx.x;
-    const float4* rays = pb.wray[par];
-    const uint32_t* cnt = pb.wseg + par * pb.wnseg;
-    TraceState T;
-    uint32_t ri = 0;
-    uint32_t seg = blockIdx.x, next = 0, end = 0;
-    if (seg < nseg) {
-        next = seg * WF_SEG;
-        end = next + cnt[seg];
-    }
-    bool active = false;
-    for (;;) {
-        uint64_t need = __ballot(!active);
-        while (need && next >= end && seg < nseg) { /* wave-uniform: move to the wave's next segment */
-            seg += gridDim.x;
-            if (seg < nseg) {
-                next = seg * WF_SEG;
-                end = next + cnt[seg];
-            }
-        }
-        if (need && next < end) {
-            const uint32_t avail = end - next;
-            const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
-            if (!active && rank < avail) {
-                ri = next + rank;
-                const float4 a = rays[2 * (size_t)ri], b = rays[2 * (size_t)ri + 1];
-                trace_begin(S, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), a.w, RT_DEFAULT_MAX, T);
-                active = true;
-            }
-            const uint32_t nn = (uint32_t)__popcll(need);
-            next += nn < avail ? nn : avail;
-        }
-        if (!__ballot(active)) {
-            if (next >= end && seg >= nseg) break;
-            continue;
-        }
-        if (active) {
-            if (T.ref != ORX_DONE) trace_round(S, T, stk);
-            if (T.ref == ORX_DONE) {
-                float4* h = pb.whit + 2 * (size_t)ri;
-                const bool tri = T.bp >= 0 && (uint32_t)T.bp >= S.nq + S.ns;
-                h[0] = make_float4(T.best, __int_as_float(T.bp), __uint_as_float(T.bslot), tri ? T.bb : T.sn.x);
-                h[1] = make_float4(tri ? T.bg : T.sn.y, T.sn.z, 0.f, 0.f);
-                active = false;
-            }
-        }
-    }
-}
-
-/* photon closest-hit programs (as k_ppm_photon) over the queue of parity
- * `par`; block k owns segment k and compacts its survivors into segment k of
- * the other queue */
-__global__ __launch_bounds__(256) void k_wf_shade(DevScene S, PixelBufs px, PhotonBufs pb, Consts c, uint32_t par,
-                                                  uint32_t nseg) {
-    __shared__ uint32_t wcount[4];
-    const uint32_t seg = blockIdx.x;
-    if (seg >= nseg) return;
-    const uint32_t n = pb.wseg[par * pb.wnseg + seg];
-    const float4* rays = pb.wray[par];
-    float4* out = pb.wray[par ^ 1];
-    float lo_x = INFINITY, lo_y = INFINITY, lo_z = INFINITY;
-    float hi_x = -INFINITY, hi_y = -INFINITY, hi_z = -INFINITY;
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t written = 0; /* block-uniform */
-    for (uint32_t k0 = 0; k0 < n; k0 += 256) {
-        const uint32_t k = k0 + threadIdx.x;
-        const uint32_t i = seg * WF_SEG + k;
-        bool cont = false;
-        f3 no = mk1(0.f), nd = mk1(0.f);
-        float ntmin = 0.f;
-        uint32_t p = 0;
-        if (k < n) {
-            const float4 a = rays[2 * (size_t)i], b = rays[2 * (size_t)i + 1];
-            const float4 h0 = pb.whit[2 * (size_t)i], h1 = pb.whit[2 * (size_t)i + 1];
-            p = __float_as_uint(b.w);
-            const float4 pa = pb.wpath[2 * (size_t)p], pq = pb.wpath[2 * (size_t)p + 1];
-            PhotonPath P;
-            P.o = mk(a.x, a.y, a.z);
-            P.d = mk(b.x, b.y, b.z);
-            P.tmin = a.w;
-            P.power = mk(pa.x, pa.y, pa.z);
-            P.weight = pa.w;
-            P.depth = __float_as_uint(pq.x);
-            P.numStored = __float_as_uint(pq.y);
-            P.mask = __float_as_uint(pq.z);
-            P.p_local = p;
-            const uint32_t j = p / pb.PW;
-            P.slot = (size_t)j * px.RW + (p - j * pb.PW);
-            bool done = false;
-            Hit h;
-            h.prim = __float_as_int(h0.y);
-            if (h.prim < 0) {
-                done = true;
-            } else {
-                h.t = h0.x;
-                h.slot = __float_as_uint(h0.z);
-                h.b = h0.w;
-                h.g = h1.x;
-                h.sn = mk(h0.w, h1.x, h1.y);
-                Rng rs = rng_load(px.rng, P.slot);
-                const DevMaterial& m = S.mats[prim_material(S, h)];
-                const f3 hitPoint = P.o + P.d * h.t;
-                if (m.type == MAT_DIFFUSE || m.type == MAT_GLOSSY || m.type == MAT_TEXTURE) {
-                    const bool tex = m.type == MAT_TEXTURE;
-                    const f3 N = shading_normal(S, h);
-                    if (P.depth >= 1 && P.numStored < pb.D) {
-                        const uint32_t si = P.p_local * pb.D + P.numStored;
-                        float4* rec = pb.slots + 4 * (size_t)si;
-                        rec[0] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, P.power.x);
-                        pb.pos4[si] = make_float4(hitPoint.x, hitPoint.y, hitPoint.z, 0.f);
-                        rec[1] = make_float4(P.d.x, P.d.y, P.d.z, P.power.y);
-                        rec[2].x = P.power.z;
-                        /* the hash's STORE_PHOTON (store_photon.h:19-25) counts every deposit */
-                        if (fmax3(P.power) > 0 || pb.hash) {
-                            P.mask |= 1u << P.numStored;
-                            lo_x = fminf(lo_x, hitPoint.x); lo_y = fminf(lo_y, hitPoint.y); lo_z = fminf(lo_z, hitPoint.z);
-                            hi_x = fmaxf(hi_x, hitPoint.x); hi_y = fmaxf(hi_y, hitPoint.y); hi_z = fmaxf(hi_z, hitPoint.z);
-                        }
-                        P.numStored++;
-                    }
-                    const f3 Kd = tex ? tex_color(S, m, h) : m.Kd;
-                    P.power = P.power * Kd;
-                    P.weight *= fmax3(Kd);
-                    if (P.depth >= 3) {
-                        float probContinue = favgf(Kd);
-                        float probSample = rnd(rs);
-                        if (probSample >= probContinue) done = true;
-                        else P.power = P.power / probContinue;
-                    }
-                    if (!done) {
-                        P.depth++;
-                        if (P.depth >= c.max_photon_depth || (double)P.weight < (tex ? 0.01 : 0.001) ||
-                            P.numStored >= pb.Dlim) {
-                            done = true;
-                        } else {
-                            float s0 = rnd(rs);
-                            float s1 = rnd(rs);
-                            nd = sample_hemisphere_cos(N, s0, s1);
-                            no = hitPoint;
-                            ntmin = tex ? 0.01f : 0.0001f;
-                        }
-                    }
-                } else if (m.type == MAT_EMITTER) {
-                    done = true;
-                } else if (m.type == MAT_MIRROR) {
-                    const f3 N = shading_normal(S, h);
-                    P.depth++;
-                    if (P.depth <= c.max_photon_depth) {
-                        P.power = P.power * m.Kr;
-                        nd = reflect(P.d, N);
-                        no = hitPoint;
-                        ntmin = 0.0001f;
-                    } else {
-                        done = true;
-                    }
-                } else {
-                    const f3 wsn = shading_normal(S, h);
-                    const bool outside = dot(wsn, P.d) < 0;
-                    const f3 N = outside ? wsn : -wsn;
-                    const float n1 = outside ? 1.0f : m.ior, n2 = outside ? m.ior : 1.0f;
-                    f3 refr;
-                    bool valid;
-                    const float refl = glass_reflect_factor(P.d, N, n1, n2, refr, valid);
-                    const float sample = rnd(rs);
-                    nd = (sample <= refl) ? reflect(P.d, N) : refr;
-                    P.depth++;
-                    if (P.depth <= c.max_photon_depth) {
-                        no = hitPoint;
-                        ntmin = 0.0001f;
-                    } else {
-                        done = true;
-                    }
-                }
-                rng_store(px.rng, P.slot, rs);
-            }
-            if (done) {
-                pb.vmask[p] = (uint8_t)P.mask;
-            } else {
-                cont = true;
-                pb.wpath[2 * (size_t)p] = make_float4(P.power.x, P.power.y, P.power.z, P.weight);
-                pb.wpath[2 * (size_t)p + 1] = u4f(P.depth, P.numStored, P.mask, 0u);
-            }
-        }
-        /* block-local compaction: wave ballots + LDS prefix over the 4 waves */
-        const uint64_t m = __ballot(cont);
-        if (lane == 0) wcount[wid] = (uint32_t)__popcll(m);
-        __syncthreads();
-        uint32_t before = 0, total = 0;
-        for (uint32_t w = 0; w < 4; w++) {
-            const uint32_t cw = wcount[w];
-            before += w < wid ? cw : 0u;
-            total += cw;
-        }
-        if (cont) {
-            const uint32_t o = seg * WF_SEG + written + before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            out[2 * (size_t)o] = make_float4(no.x, no.y, no.z, ntmin);
-            out[2 * (size_t)o + 1] = make_float4(nd.x, nd.y, nd.z, __uint_as_float(p));
-        }
-        written += total;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) pb.wseg[(par ^ 1) * pb.wnseg + seg] = written;
-    lo_x = wave_min(lo_x); lo_y = wave_min(lo_y); lo_z = wave_min(lo_z);
-    hi_x = wave_max(hi_x); hi_y = wave_max(hi_y); hi_z = wave_max(hi_z);
-    const uint32_t rep = (blockIdx.x * 4 + wid) & (BBOX_REPLICAS - 1);
-    if (lane < 6) {
-        float v = lane == 0 ? lo_x : lane == 1 ? lo_y : lane == 2 ? lo_z : lane == 3 ? hi_x : lane == 4 ? hi_y : hi_z;
-        if (lane < 3) {
-            if (v != INFINITY) atomicMin(&pb.bbox[lane * BBOX_REPLICAS + rep], f2ord(v));
-        } else {
-            if (v != -INFINITY) atomicMax(&pb.bbox[lane * BBOX_REPLICAS + rep], f2ord(v));
-        }
-    }
-}
-
-void launch_ppm_photon_wavefront(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb,
-                                 const Consts& c) {
-    const uint32_t total = pb.prows * pb.PW;
     if (total == 0) return;
-    const uint32_t nseg = (total + WF_SEG - 1) / WF_SEG;
-    const uint32_t eblocks = std::min<uint32_t>((total + 255) / 256, 4096u);
-    hipLaunchKernelGGL(k_wf_emit, dim3(eblocks), dim3(256), 0, s, S, px, pb);
-    /* a path traces at most max_photon_depth + 2 segments (each continuing
-     * bounce raises depth by one and continues only while depth <= max) */
-    const uint32_t rounds = c.max_photon_depth + 2;
-    /* as many one-wave blocks as the LDS stacks of one CU allow (160 KiB),
-     * at most 24 per CU (6 waves/SIMD at the kernel's ~75 VGPRs), 256 CUs */
-    const size_t lds = ORX_STACK_BYTES(S);
-    const uint32_t per_cu = lds ? (uint32_t)std::min<size_t>(24, (160u * 1024u) / lds) : 24u;
-    const uint32_t tblocks = std::min<uint32_t>(256u * per_cu, nseg);
-    for (uint32_t r = 0; r < rounds; r++) {
-        hipLaunchKernelGGL(k_wf_trace, dim3(tblocks), dim3(64), lds, s, S, pb, r & 1u, nseg);
-        hipLaunchKernelGGL(k_wf_shade, dim3(nseg), dim3(256), 0, s, S, px, pb, c, r & 1u, nseg);
-    }
+    hipLaunchKernelGGL(k_ppm_photon, dim3((total + 63) / 64), dim3(64), ORX_STACK_BYTES(S), s, S, px, pb, c);
 }
 
 /* ------------------------------------------------------------------ */
@@ -727,66 +399,7 @@ void launch_grid_setup(hipStream_t s, const PhotonBufs& pb) {
 }
 
 /* ------------------------------------------------------------------ */
-/* hash + histogram (atomic rank = position inside the cell)           */
-/* ------------------------------------------------------------------ */
-/* calculateHashCellsKernel + histogram (OptixRenderer_SpatialHash.cu:152-173):
- * four slots per thread per step, their loads and the rank-returning
- * histogram atomics issued back to back (memory-level parallelism). */
-__global__ __launch_bounds__(256) void k_grid_hash(PhotonBufs pb) {
-    const GridParams g = *pb.grid;
-    const uint32_t invalid = g.G + 1;
-    const float inv = 1.f / g.cell;
-    const uint32_t T = gridDim.x * blockDim.x;
-    for (uint32_t s0 = blockIdx.x * blockDim.x + threadIdx.x; s0 < pb.S; s0 += 4 * T) {
-        uint32_t key[4], rank[4];
-        bool v[4];
-        float4 a[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t s = s0 + q * T;
-            key[q] = invalid;
-            rank[q] = 0;
-            v[q] = false;
-            if (s < pb.S && g.G) {
-                const uint32_t p = s / pb.D, k = s - p * pb.D;
-                v[q] = (pb.vmask[p] >> k) & 1u;
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            if (v[q]) a[q] = pb.slots[4 * (size_t)(s0 + q * T)];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            if (v[q]) {
-                const f3 pp = (mk(a[q].x, a[q].y, a[q].z) - mk(g.ox, g.oy, g.oz)) * inv;
-                const uint32_t cx = orx_f2u_sat(orx_floorf(pp.x));
-                const uint32_t cy = orx_f2u_sat(orx_floorf(pp.y));
-                const uint32_t cz = orx_f2u_sat(orx_floorf(pp.z));
-                uint32_t kk = cx + cy * g.gx + cz * g.gx * g.gy;
-                key[q] = kk > g.G ? g.G : kk;
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            if (v[q]) rank[q] = atomicAdd(&pb.hist[key[q]], 1u);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t s = s0 + q * T;
-            if (s < pb.S) {
-                pb.keys[s] = key[q];
-                pb.ranks[s] = rank[q];
-            }
-        }
-    }
-}
-void launch_grid_hash(hipStream_t s, const PhotonBufs& pb) {
-    unsigned blocks = (pb.S + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(k_grid_hash, dim3(blocks), dim3(256), 0, s, pb);
-}
-
-/* ------------------------------------------------------------------ */
-/* exclusive scan of hist[0..G] -> offsets[0..G]; zeroes hist          */
+/* block-wide exclusive scan (the bucket sort's table scan)             */
 /* ------------------------------------------------------------------ */
 constexpr int SCAN_BLOCK = 1024; /* elements per block: 256 threads x 4 */
 
@@ -807,88 +420,6 @@ __device__ __forceinline__ uint32_t block_exclusive_scan_256(uint32_t v, uint32_
     return pre + x - v;
 }
 
-__global__ __launch_bounds__(256) void k_scan_reduce(PhotonBufs pb) {
-    const uint32_t n = pb.grid->G + 1;
-    uint32_t base = blockIdx.x * SCAN_BLOCK + threadIdx.x * 4;
-    uint32_t sum = 0;
-    if (blockIdx.x * SCAN_BLOCK < n) {
-        for (int k = 0; k < 4; k++)
-            if (base + k < n) sum += pb.hist[base + k];
-    }
-    uint32_t total;
-    (void)block_exclusive_scan_256(sum, &total);
-    if (threadIdx.x == 0) pb.scan_partials[blockIdx.x] = total;
-}
-__global__ __launch_bounds__(256) void k_scan_partials(PhotonBufs pb, uint32_t nblocks) {
-    /* single block: exclusive scan of the per-block totals */
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < nblocks; base += 256) {
-        uint32_t i = base + threadIdx.x;
-        uint32_t v = i < nblocks ? pb.scan_partials[i] : 0;
-        uint32_t total;
-        uint32_t ex = block_exclusive_scan_256(v, &total);
-        if (i < nblocks) pb.scan_partials[i] = carry + ex;
-        carry += total;
-        __syncthreads();
-    }
-}
-__global__ __launch_bounds__(256) void k_scan_apply(PhotonBufs pb) {
-    const uint32_t G = pb.grid->G;
-    const uint32_t n = G + 1;
-    if (blockIdx.x * SCAN_BLOCK >= n) return;
-    uint32_t base = blockIdx.x * SCAN_BLOCK + threadIdx.x * 4;
-    uint32_t v[4];
-    uint32_t sum = 0;
-    for (int k = 0; k < 4; k++) {
-        v[k] = (base + k < n) ? pb.hist[base + k] : 0;
-        sum += v[k];
-    }
-    uint32_t total;
-    uint32_t ex = block_exclusive_scan_256(sum, &total) + pb.scan_partials[blockIdx.x];
-    for (int k = 0; k < 4; k++) {
-        if (base + k < n) {
-            pb.offsets[base + k] = ex;
-            pb.hist[base + k] = 0; /* consumed: ready for the next iteration */
-            if (base + k == G) {
-                pb.grid->valid = ex;
-                pb.grid->valid_total += ex;
-            }
-        }
-        ex += v[k];
-    }
-}
-void launch_grid_scan(hipStream_t s, const PhotonBufs& pb) {
-    uint32_t nblocks = (pb.gmax + 2 + SCAN_BLOCK - 1) / SCAN_BLOCK;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(nblocks), dim3(256), 0, s, pb);
-    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(256), 0, s, pb, nblocks);
-    hipLaunchKernelGGL(k_scan_apply, dim3(nblocks), dim3(256), 0, s, pb);
-}
-
-/* ------------------------------------------------------------------ */
-/* scatter photons into cell order                                     */
-/* ------------------------------------------------------------------ */
-/* sort_by_key as a counting-sort scatter (SpatialHash.cu:193-196): the
- * destination of slot s is offsets[key] + rank; this writes the permutation,
- * k_grid_permute then moves the photons destination-major. */
-__global__ __launch_bounds__(256) void k_grid_scatter(PhotonBufs pb) {
-    const uint32_t G = pb.grid->G;
-    const uint32_t T = gridDim.x * blockDim.x;
-    for (uint32_t s0 = blockIdx.x * blockDim.x + threadIdx.x; s0 < pb.S; s0 += 4 * T) {
-        uint32_t key[4], rank[4], off[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t s = s0 + q * T;
-            key[q] = s < pb.S ? pb.keys[s] : G + 1;
-            rank[q] = s < pb.S ? pb.ranks[s] : 0;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            if (key[q] <= G) off[q] = pb.offsets[key[q]];
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            if (key[q] <= G) pb.perm[off[q] + rank[q]] = s0 + q * T;
-    }
-}
 /* Direction prefilter word of a grid photon (sorted plane SP_DIRQ): the
  * direction as three int8 snorm bytes q = rint(127 d).  The gather's facing
  * test dot(d, n) <= 0 is decided from v_dot4_i32_i8(q, qn) (qn the same
@@ -1026,7 +557,7 @@ __global__ __launch_bounds__(BS_THREADS) void k_bs_count(PhotonBufs pb) {
     for (uint32_t b = threadIdx.x; b < nb; b += BS_THREADS) pb.bs_table[(size_t)b * pb.bs_nchunk + blockIdx.x] = hist[b];
 }
 
-/* exclusive scan of n = nb * nchunk table entries in place (three kernels, as k_scan_*) */
+/* exclusive scan of n = nb * nchunk table entries in place (three kernels) */
 __global__ __launch_bounds__(256) void k_bs_scan_reduce(PhotonBufs pb) {
     const uint32_t nb = (pb.grid->G * pb.nsub + (1u << pb.bshift) - 1) >> pb.bshift;
     const uint32_t n = nb * pb.bs_nchunk;
@@ -1224,13 +755,6 @@ void launch_grid_bucket_place(hipStream_t s, const PhotonBufs& pb) {
     hipLaunchKernelGGL(k_grid_permute, dim3(blocks), dim3(256), 0, s, pb);
 }
 
-void launch_grid_scatter(hipStream_t s, const PhotonBufs& pb) {
-    unsigned blocks = (pb.S + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(k_grid_scatter, dim3(blocks), dim3(256), 0, s, pb);
-    hipLaunchKernelGGL(k_grid_permute, dim3(blocks), dim3(256), 0, s, pb);
-}
-
 /* ------------------------------------------------------------------ */
 /* indirect radiance estimate: uniform-grid gather                     */
 /* ------------------------------------------------------------------ */
@@ -1318,10 +842,8 @@ __device__ __forceinline__ void window_visits(const uint32_t* __restrict__ offse
 
 constexpr uint32_t GQ = 8; /* chord ranges per lane per phase A (LDS: GQ * 8 B per lane) */
 
-/* NSUB: sub-rows per cell row (SUBR^2, or 1 for the cell-order layout);
- * SUBOFS: sub-cell offsets present (bucket-sort grid) or cell offsets only
- * (atomic-rank grid, ORX_GRID_ATOMIC=1) */
-template <uint32_t NSUB, bool SUBOFS>
+/* NSUB: sub-rows per cell row (SUBR^2, or 1 for the cell-order layout) */
+template <uint32_t NSUB>
 #ifndef ORX_GATHER_LANE_WAVES
 #define ORX_GATHER_LANE_WAVES 6 /* waves per SIMD the per-lane gather is register-capped for (no spills) */
 #endif
@@ -1407,7 +929,6 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
             const uint32_t zq = t / ny;
             const uint32_t z = z_lo + zq, yy = y_lo + (t - zq * ny);
             t++;
-            const uint32_t row = yy * g.gx + z * g.gx * g.gy;
             uint32_t offs[NSUB], ends[NSUB];
 #pragma unroll
             for (uint32_t sr = 0; sr < NSUB; sr++) {
@@ -1425,20 +946,16 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
                 const uint32_t xl = cxl > (int32_t)x_lo ? (uint32_t)cxl : x_lo;
                 const uint32_t xh = cxh < (int32_t)x_hi ? (uint32_t)cxh : x_hi;
                 if (cxh < 0 || xl > xh) continue;
-                if (SUBOFS) { /* x-quarter trimming of the chord's end cells */
-                    const float sx = invCellSize * (float)SUBX;
-                    const int32_t q0 = orx_f2i_sat(orx_floorf((np.x - rx) * sx));
-                    const int32_t q1 = orx_f2i_sat(orx_floorf((np.x + rx) * sx));
-                    const uint32_t a0 = q0 > (int32_t)(SUBX * xl) ? (uint32_t)q0 : SUBX * xl;
-                    const uint32_t a1 = q1 < (int32_t)(SUBX * xh + SUBX - 1) ? (uint32_t)q1 : SUBX * xh + SUBX - 1;
-                    if (q1 < 0 || a0 > a1) continue;
-                    const uint32_t* so = pb.subofs + ((size_t)(yy + z * g.gy) * NSUB + sr) * g.gx * SUBX;
-                    offs[sr] = so[a0];
-                    ends[sr] = so[a1 + 1];
-                } else {
-                    offs[sr] = pb.offsets[xl + row];
-                    ends[sr] = pb.offsets[xh + row + 1];
-                }
+                /* x-quarter trimming of the chord's end cells */
+                const float sx = invCellSize * (float)SUBX;
+                const int32_t q0 = orx_f2i_sat(orx_floorf((np.x - rx) * sx));
+                const int32_t q1 = orx_f2i_sat(orx_floorf((np.x + rx) * sx));
+                const uint32_t a0 = q0 > (int32_t)(SUBX * xl) ? (uint32_t)q0 : SUBX * xl;
+                const uint32_t a1 = q1 < (int32_t)(SUBX * xh + SUBX - 1) ? (uint32_t)q1 : SUBX * xh + SUBX - 1;
+                if (q1 < 0 || a0 > a1) continue;
+                const uint32_t* so = pb.subofs + ((size_t)(yy + z * g.gy) * NSUB + sr) * g.gx * SUBX;
+                offs[sr] = so[a0];
+                ends[sr] = so[a1 + 1];
             }
 #pragma unroll
             for (uint32_t sr = 0; sr < NSUB; sr++)
@@ -1602,19 +1119,6 @@ __device__ __forceinline__ UChunk uload_chunk(const float* __restrict__ SX, cons
     b.WZ = SPZ[k];
     return b;
 }
-/* photons e..e+3 of a chunk to every lane (uniform e): four v_readlane into SGPRs */
-__device__ __forceinline__ f4u bcast4(float v, uint32_t e) {
-    return f4u{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)e)),
-               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)e + 1)),
-               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)e + 2)),
-               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)e + 3))};
-}
-__device__ __forceinline__ u4v bcast4u(uint32_t v, uint32_t e) {
-    return u4v{(uint32_t)__builtin_amdgcn_readlane((int)v, (int)e), (uint32_t)__builtin_amdgcn_readlane((int)v, (int)e + 1),
-               (uint32_t)__builtin_amdgcn_readlane((int)v, (int)e + 2),
-               (uint32_t)__builtin_amdgcn_readlane((int)v, (int)e + 3)};
-}
-
 /* The union kernel's per-batch constants and accumulators (LDS-broadcast form) */
 struct UAcc {
     v2f accx, accy, accz;
@@ -1703,33 +1207,22 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
     }
 }
 
-/* BC: photon broadcast form — 0: v_readlane from the chunk registers; 1: the wave's LDS
- * image (union_chunk_lds) with the chord test dropped on sub-rows where no lane's chord is
- * cut by its window */
-template <uint32_t NSUB, bool SORTED, int BC>
+/* Photons are broadcast through the wave's LDS image (union_chunk_lds), with the chord test
+ * dropped on sub-rows where no lane's chord is cut by its window.  (A v_readlane broadcast from
+ * the chunk registers measured 2.81 ms against 1.91 on the serial hall gather, 16x4 and 4x16
+ * wave tiles slower than 8x8.)  Block = 16x16 pixels, four 8x8 wave tiles; blocks are dealt
+ * XCD-major (block b runs on XCD b % 8 and takes the tiles [k per, (k+1) per) of XCD k). */
+template <uint32_t NSUB>
 __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
-                                                          uint32_t ntiles, const uint32_t* __restrict__ order,
-                                                          uint32_t norder) {
-    __shared__ float ulds[BC == 1 ? 4 : 1][BC == 1 ? 7 * 64 : 1];
+                                                          uint32_t ntiles) {
+    __shared__ float ulds[4][7 * 64];
     const uint32_t tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-    uint32_t x = 0, j = 0;
-    bool live;
-    if (SORTED) {
-        const uint32_t g = (blockIdx.x * 4 + w) * 64 + l;
-        live = g < norder;
-        const uint32_t pix = live ? order[g] : 0u;
-        j = pix / gi.W;
-        x = pix - j * gi.W;
-    } else {
-        const uint32_t per = (ntiles + 7) / 8;
-        const uint32_t tile = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
-        const uint32_t ox = gi.tshape == 0 ? (w & 1) * 8 + (l & 7) : gi.tshape == 1 ? (l & 15) : w * 4 + (l & 3);
-        const uint32_t oy = gi.tshape == 0 ? (w >> 1) * 8 + (l >> 3) : gi.tshape == 1 ? w * 4 + (l >> 4) : (l >> 2);
-        x = (tile % ntx) * 16 + ox;
-        const uint32_t y = (tile / ntx) * 16 + oy;
-        j = gather_row(gi, y);
-        live = tile < ntiles && x < gi.W && y < gi.segments * gi.seg_rows;
-    }
+    const uint32_t per = (ntiles + 7) / 8;
+    const uint32_t tile = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    const uint32_t x = (tile % ntx) * 16 + (w & 1) * 8 + (l & 7);
+    const uint32_t y = (tile / ntx) * 16 + (w >> 1) * 8 + (l >> 3);
+    const uint32_t j = gather_row(gi, y);
+    const bool live = tile < ntiles && x < gi.W && y < gi.segments * gi.seg_rows;
     const GridParams g = *pb.grid;
     uint32_t dC = 0, dP = 0;
     ORX_TS_DECL;
@@ -1795,12 +1288,8 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
     const float m = g.cell * 1e-3f;
     constexpr uint32_t HS = NSUB > 1 ? SUBR : 1u;
     const float hc = g.cell / (float)HS;
-    UConst UK;
-    UAcc UA;
-    if (BC == 1) {
-        UK = UConst{px2, py2, pz2, nx2, ny2, nz2, kx2, wc6, wc5, wc4, wc3, wc2, wc1, wc0, nq, SDX, SDY, SDZ};
-        UA = UAcc{accx, accy, accz};
-    }
+    const UConst UK{px2, py2, pz2, nx2, ny2, nz2, kx2, wc6, wc5, wc4, wc3, wc2, wc1, wc0, nq, SDX, SDY, SDZ};
+    UAcc UA{accx, accy, accz};
     /* the union of the lanes' windows (rows) */
     const uint32_t UZ0 = wave_min_u32(act ? z_lo : 0xffffffffu), UZ1 = wave_max_u32(act ? z_hi : 0u);
     const uint32_t UY0 = wave_min_u32(act ? y_lo : 0xffffffffu), UY1 = wave_max_u32(act ? y_hi : 0u);
@@ -1848,14 +1337,14 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
                 const uint32_t* so = pb.subofs + ((size_t)rowc * NSUB + sr) * g.gx * SUBX;
                 const uint32_t U0 = so[A0], U1 = so[A1 + 1]; /* uniform: scalar loads */
                 if (U0 >= U1) continue;
-                /* this lane's candidates: [lo, lo + len); the LDS-broadcast form needs them
-                 * only on sub-rows where some lane's chord is cut (two scattered loads) */
+                /* this lane's candidates [lo, lo + len): needed only on sub-rows where some lane's
+                 * chord is cut (two scattered loads) */
 #ifdef ORX_TRAV_STATS
                 constexpr bool need_all = true;
 #else
-                constexpr bool need_all = BC != 1;
+                constexpr bool need_all = false;
 #endif
-                const bool range = BC == 1 ? wave_any(cut) : true;
+                const bool range = wave_any(cut);
                 uint32_t lo = 0, len = 0;
                 if ((need_all || range) && a0 <= a1) {
                     lo = so[a0];
@@ -1864,112 +1353,36 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
                 ORX_TS_INC(ts_nodes, len);              /* trav stats: lane candidate photons */
                 if (l == 0) ORX_TS_INC(ts_wn, U1 - U0); /* union photons of the wave */
                 ORX_TS_INC(ts_leaves, 1);
-                if (BC == 1) {
-                    /* a lane without a chord here accepts nothing (its window excludes the
-                     * sub-row, or its sphere misses it) */
-                    const float r2 = a0 <= a1 ? radius2 : -1.f;
-                    float* L = ulds[w];
-                    uint32_t cc = U0;
-                    UChunk cur = uload_chunk(SX, SY, SZ, SQ, SPX, SPY, SPZ, cc + l);
-                    while (cc < U1) {
-                        const uint32_t cn = cc + 64;
-                        const UChunk nxt = uload_chunk(SX, SY, SZ, SQ, SPX, SPY, SPZ, (cn < U1 ? cn : cc) + l);
-                        const uint32_t ce = U1 - cc < 64 ? U1 - cc : 64;
-                        L[l] = cc + l < U1 ? cur.X : INFINITY;
-                        L[64 + l] = cur.Y;
-                        L[128 + l] = cur.Z;
-                        L[192 + l] = __uint_as_float(cur.Q);
-                        L[256 + l] = cur.WX;
-                        L[320 + l] = cur.WY;
-                        L[384 + l] = cur.WZ;
-                        __builtin_amdgcn_wave_barrier();
-                        if (range) union_chunk_lds<true>(L, cc, ce, lo, len, r2, UK, UA);
-                        else union_chunk_lds<false>(L, cc, ce, lo, len, r2, UK, UA);
-                        __builtin_amdgcn_wave_barrier();
-                        cur = nxt;
-                        cc = cn;
-                    }
-                    continue;
-                }
-                /* chunks of 64 photons: lane k loads photon c + k of every plane it needs (one
-                 * coalesced dwordx4 per plane and 16 lanes... per chunk, the next chunk's loads
-                 * in flight while this one is evaluated), then batches of four are broadcast to
-                 * all lanes with v_readlane into SGPR operands */
-                uint32_t c = U0;
-                UChunk cur = uload_chunk(SX, SY, SZ, SQ, SPX, SPY, SPZ, c + l);
-                while (c < U1) {
-                    const uint32_t cn = c + 64;
-                    const UChunk nxt = uload_chunk(SX, SY, SZ, SQ, SPX, SPY, SPZ, (cn < U1 ? cn : c) + l);
-                    const uint32_t ce = U1 - c < 64 ? U1 - c : 64;
-                    for (uint32_t e = 0; e < ce; e += 4) {
-                        const uint32_t kb = c + e;
-                        const f4u X = bcast4(cur.X, e), Y = bcast4(cur.Y, e), Z = bcast4(cur.Z, e);
-                        const uint32_t t = kb - lo;
-                        const v2f dx0 = px2 - lo2(X), dx1 = px2 - hi2(X);
-                        const v2f dy0 = py2 - lo2(Y), dy1 = py2 - hi2(Y);
-                        const v2f dz0 = pz2 - lo2(Z), dz1 = pz2 - hi2(Z);
-                        const v2f d20 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
-                        const v2f d21 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
-                        bool in0 = t < len && d20.x <= radius2;
-                        bool in1 = t + 1 < len && d20.y <= radius2;
-                        bool in2 = t + 2 < len && d21.x <= radius2;
-                        bool in3 = t + 3 < len && d21.y <= radius2;
-                        if (!wave_any(in0 | in1 | in2 | in3)) continue;
-                        const u4v Q = bcast4u(cur.Q, e);
-                        const int32_t q0 = __builtin_amdgcn_sdot4((int32_t)Q.x, nq, 0, false);
-                        const int32_t q1 = __builtin_amdgcn_sdot4((int32_t)Q.y, nq, 0, false);
-                        const int32_t q2 = __builtin_amdgcn_sdot4((int32_t)Q.z, nq, 0, false);
-                        const int32_t q3 = __builtin_amdgcn_sdot4((int32_t)Q.w, nq, 0, false);
-                        in0 = in0 && q0 <= DIRQ_BAND;
-                        in1 = in1 && q1 <= DIRQ_BAND;
-                        in2 = in2 && q2 <= DIRQ_BAND;
-                        in3 = in3 && q3 <= DIRQ_BAND;
-                        const bool u0 = in0 && q0 >= -DIRQ_BAND, u1 = in1 && q1 >= -DIRQ_BAND;
-                        const bool u2 = in2 && q2 >= -DIRQ_BAND, u3 = in3 && q3 >= -DIRQ_BAND;
-                        if (wave_any(u0 | u1 | u2 | u3)) { /* inside the band: the exact test (rare) */
-                            const uint32_t ku = (uint32_t)__builtin_amdgcn_readfirstlane((int)kb);
-                            const f4u DX = sload4(SDX, ku), DY = sload4(SDY, ku), DZ = sload4(SDZ, ku);
-                            const v2f nd0 = (lo2(DX) * nx2 + lo2(DY) * ny2) + lo2(DZ) * nz2;
-                            const v2f nd1 = (hi2(DX) * nx2 + hi2(DY) * ny2) + hi2(DZ) * nz2;
-                            in0 = in0 && (!u0 || nd0.x <= 0.f);
-                            in1 = in1 && (!u1 || nd0.y <= 0.f);
-                            in2 = in2 && (!u2 || nd1.x <= 0.f);
-                            in3 = in3 && (!u3 || nd1.y <= 0.f);
-                        }
-                        if (!wave_any(in0 | in1 | in2 | in3)) continue;
-                        const f4u WX = bcast4(cur.WX, e), WY = bcast4(cur.WY, e), WZ = bcast4(cur.WZ, e);
-                        const v2f x0 = d20 * kx2;
-                        const v2f x1 = d21 * kx2;
-                        v2f p0 = wc6, p1 = wc6;
-                        p0 = __builtin_elementwise_fma(p0, x0, wc5); p1 = __builtin_elementwise_fma(p1, x1, wc5);
-                        p0 = __builtin_elementwise_fma(p0, x0, wc4); p1 = __builtin_elementwise_fma(p1, x1, wc4);
-                        p0 = __builtin_elementwise_fma(p0, x0, wc3); p1 = __builtin_elementwise_fma(p1, x1, wc3);
-                        p0 = __builtin_elementwise_fma(p0, x0, wc2); p1 = __builtin_elementwise_fma(p1, x1, wc2);
-                        p0 = __builtin_elementwise_fma(p0, x0, wc1); p1 = __builtin_elementwise_fma(p1, x1, wc1);
-                        v2f w0 = __builtin_elementwise_fma(p0, x0, wc0), w1 = __builtin_elementwise_fma(p1, x1, wc0);
-                        w0.x = in0 ? w0.x : 0.f;
-                        w0.y = in1 ? w0.y : 0.f;
-                        w1.x = in2 ? w1.x : 0.f;
-                        w1.y = in3 ? w1.y : 0.f;
-                        ORX_TS_INC(ts_tris, (uint32_t)in0 + (uint32_t)in1 + (uint32_t)in2 + (uint32_t)in3);
-                        accx = __builtin_elementwise_fma(lo2(WX), w0, accx);
-                        accy = __builtin_elementwise_fma(lo2(WY), w0, accy);
-                        accz = __builtin_elementwise_fma(lo2(WZ), w0, accz);
-                        accx = __builtin_elementwise_fma(hi2(WX), w1, accx);
-                        accy = __builtin_elementwise_fma(hi2(WY), w1, accy);
-                        accz = __builtin_elementwise_fma(hi2(WZ), w1, accz);
-                    }
+                /* a lane without a chord here accepts nothing (its window excludes the
+                 * sub-row, or its sphere misses it) */
+                const float r2 = a0 <= a1 ? radius2 : -1.f;
+                float* L = ulds[w];
+                uint32_t cc = U0;
+                UChunk cur = uload_chunk(SX, SY, SZ, SQ, SPX, SPY, SPZ, cc + l);
+                while (cc < U1) {
+                    const uint32_t cn = cc + 64;
+                    const UChunk nxt = uload_chunk(SX, SY, SZ, SQ, SPX, SPY, SPZ, (cn < U1 ? cn : cc) + l);
+                    const uint32_t ce = U1 - cc < 64 ? U1 - cc : 64;
+                    L[l] = cc + l < U1 ? cur.X : INFINITY;
+                    L[64 + l] = cur.Y;
+                    L[128 + l] = cur.Z;
+                    L[192 + l] = __uint_as_float(cur.Q);
+                    L[256 + l] = cur.WX;
+                    L[320 + l] = cur.WY;
+                    L[384 + l] = cur.WZ;
+                    __builtin_amdgcn_wave_barrier();
+                    if (range) union_chunk_lds<true>(L, cc, ce, lo, len, r2, UK, UA);
+                    else union_chunk_lds<false>(L, cc, ce, lo, len, r2, UK, UA);
+                    __builtin_amdgcn_wave_barrier();
                     cur = nxt;
-                    c = cn;
+                    cc = cn;
                 }
             }
         }
     }
-    if (BC == 1) {
-        accx = UA.accx;
-        accy = UA.accy;
-        accz = UA.accz;
-    }
+    accx = UA.accx;
+    accy = UA.accy;
+    accz = UA.accz;
 #ifdef ORX_TRAV_STATS
     atomicAdd((unsigned long long*)&pb.grid->st_lane_batches, (unsigned long long)ts_nodes);
     atomicAdd((unsigned long long*)&pb.grid->st_wave_batches, (unsigned long long)ts_wn);
@@ -1999,53 +1412,22 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
     }
 }
 
-void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, size_t lds_pad) {
+void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c) {
     const uint32_t rows = gi.segments * gi.seg_rows;
     const uint32_t ntx = (gi.W + 15) / 16, nty = (rows + 15) / 16, ntiles = ntx * nty;
     const dim3 grid(8 * ((ntiles + 7) / 8));
-    /* ORX_GATHER_UNION: 2 (default) the union kernel with LDS-broadcast batches; 1 the union
-     * kernel with v_readlane broadcasts; 0 the per-lane kernel.  Measured (serial hall gather /
-     * pipelined hall frame / 4K conference frame): 0: 2.5 ms / 7.9 ms / 120 ms;
-     * 1: 2.81 / 7.68 / 77.2; 2: 1.91 / 7.02 / 53.3 */
-    static const int union_env = [] {
-        const char* e = getenv("ORX_GATHER_UNION");
-        return e ? atoi(e) : -1;
-    }();
     /* The sharded gather (segments = ranks, cell-order layout, no visit counters) meets 1/N of
      * the photons: at N >= 8 the wave union's per-row work outweighs the photons it shares, and
      * the per-lane kernel is faster (hall 1080p, tools/shard_model.py, per-rank gather union /
-     * per-lane: N=2 1.29 / 1.56 ms, N=4 0.73 / 0.80, N=8 0.47 / 0.43) */
-    const int union_gather = union_env >= 0 ? union_env : (gi.segments >= 8 ? 0 : 2);
-    static const uint32_t tshape = [] {
-        const char* e = getenv("ORX_GATHER_TILE");
-        return e ? (uint32_t)atoi(e) % 3u : 0u;
-    }();
-    GatherIn gt = gi;
-    gt.tshape = tshape;
-    if (union_gather == 2 && pb.subofs) {
-        if (pb.nsub == 1)
-            hipLaunchKernelGGL((k_ppm_gather_union<1, false, 1>), grid, dim3(256), lds_pad, s, gt, pb, c, ntx, ntiles,
-                               nullptr, 0u);
-        else
-            hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR, false, 1>), grid, dim3(256), lds_pad, s, gt, pb, c,
-                               ntx, ntiles, nullptr, 0u);
+     * per-lane: N=2 1.29 / 1.56 ms, N=4 0.73 / 0.80, N=8 0.47 / 0.43).  Measured on one device
+     * (serial hall gather / 4K conference frame): per-lane 2.5 ms / 120 ms, union 1.91 / 53.3. */
+    if (gi.segments >= 8) {
+        if (pb.nsub == 1) hipLaunchKernelGGL((k_ppm_gather<1>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
+        else hipLaunchKernelGGL((k_ppm_gather<SUBR * SUBR>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
         return;
     }
-    if (union_gather && pb.subofs) {
-        if (pb.nsub == 1)
-            hipLaunchKernelGGL((k_ppm_gather_union<1, false, 0>), grid, dim3(256), lds_pad, s, gt, pb, c, ntx, ntiles,
-                               nullptr, 0u);
-        else
-            hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR, false, 0>), grid, dim3(256), lds_pad, s, gt, pb, c,
-                               ntx, ntiles, nullptr, 0u);
-        return;
-    }
-    if (!pb.subofs)
-        hipLaunchKernelGGL((k_ppm_gather<1, false>), grid, dim3(256), lds_pad, s, gt, pb, c, ntx, ntiles);
-    else if (pb.nsub == 1)
-        hipLaunchKernelGGL((k_ppm_gather<1, true>), grid, dim3(256), lds_pad, s, gt, pb, c, ntx, ntiles);
-    else
-        hipLaunchKernelGGL((k_ppm_gather<SUBR * SUBR, true>), grid, dim3(256), lds_pad, s, gt, pb, c, ntx, ntiles);
+    if (pb.nsub == 1) hipLaunchKernelGGL((k_ppm_gather_union<1>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
+    else hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
 }
 
 /* ------------------------------------------------------------------ */

@@ -20,8 +20,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 KERNELS_OF_PASS = {
     "ppm_eye": ["k_ppm_eye"],
     "ppm_photon": ["k_ppm_photon"],
-    # default bucket-sort grid build; the atomic path (ORX_GRID_ATOMIC=1) is
-    # k_grid_hash / k_scan_* / k_grid_scatter with the same pass split
+    # the bucket-sort grid build
     "grid_hash": ["k_grid_setup", "k_bs_count"],
     "grid_scan": ["k_bs_scan_reduce", "k_bs_scan_partials", "k_bs_scan_apply"],
     "grid_scatter": ["k_bs_place", "k_bs_cells", "k_grid_coarse_offsets", "k_grid_permute"],
@@ -37,7 +36,7 @@ KERNELS_OF_PASS = {
 # the other photon maps (orx_config.photon_map): the grid passes' event slots time their build and gather
 KERNELS_OF_PASS_MAP = {
     1: {"grid_hash": ["k_hash_build"], "ppm_gather": ["k_ppm_gather_hash"]},
-    2: {"grid_hash": ["k_kd_*", "k_rs_*"], "ppm_gather": ["k_ppm_gather_kd"]},
+    2: {"grid_hash": ["k_kd_*", "k_rs_*"], "ppm_gather": ["k_ppm_gather_kd_wave"]},
 }
 
 

@@ -8,7 +8,9 @@ W*H hit points against the local photons, and the finish (direct + output of the
 The full-image hit points come from a second, unsharded renderer's eye pass on the
 same camera and radius, rearranged into the ranks' row-interleaved segments (what the
 all-gather delivers).  The collectives are not run; their volumes are printed so the exchange
-over xGMI can be added by hand.  Usage: shard_model.py [N ...]  (default 1 2 4 8), hall 1080p, 2048^2."""
+over xGMI can be added by hand.  Usage: shard_model.py [--config 2|4] [N ...]  (default 1 2 4 8):
+configs[2] hall 1080p with a 2048^2 photon launch (default), configs[4] conference 3840x2160
+with 4096^2."""
 import os
 import sys
 
@@ -23,9 +25,9 @@ from oppositerenderer_amd.renderer import OptixRenderer, RenderRequestDetails, n
 SEED = 1645301512
 
 
-def run(world, W=1920, H=1080, P=2048, iters=6, warm=2):
+def run(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None):
     dev = torch.device("cuda", 0)
-    scene = synthetic.synthetic_hall()
+    scene = scene or synthetic.synthetic_hall()
     cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
     det = RenderRequestDetails(cam, scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W, H)
     req = det.to_abi()
@@ -97,8 +99,15 @@ def run(world, W=1920, H=1080, P=2048, iters=6, warm=2):
 
 
 if __name__ == "__main__":
-    worlds = [int(v) for v in sys.argv[1:]] or [1, 2, 4, 8]
+    args = sys.argv[1:]
+    conf = 2
+    if args[:1] == ["--config"]:
+        conf, args = int(args[1]), args[2:]
+    worlds = [int(v) for v in args] or [1, 2, 4, 8]
+    kw = (dict(W=3840, H=2160, P=4096, iters=4, warm=1, scene=synthetic.synthetic_conference()) if conf == 4
+          else {})
+    print(f"configs[{conf}]: " + ("conference 3840x2160, 4096^2 photons" if conf == 4 else "hall 1920x1080, 2048^2"))
     for n in worlds:
-        ms, passes, ag, rs = run(n)
+        ms, passes, ag, rs = run(n, **kw)
         print(f"N={n}: per-rank serial {sum(ms.values()):.3f} ms {ms} | all-gather {ag:.0f} MB, "
               f"reduce-scatter {rs:.0f} MB | passes {passes}", flush=True)

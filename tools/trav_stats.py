@@ -39,14 +39,9 @@ for it in range(3):
               f"  leaf {v[b + 2] / max(1, 64 * wl):5.3f}")
     print(f"it{it} closest node visits in the top BVH4 levels (index < 21/85/341/1365): "
           + " ".join(f"{v[17 + q] / max(1, v[1]):5.3f}" for q in range(4)))
-    if method == 2 and os.environ.get("ORX_GATHER_UNION", "0") != "0":
+    if method == 2:  # the union gather (single device)
         lc, up, nr = v[12], v[13], v[14]
         print(f"it{it} union    lane candidates/px {lc / (W * H):8.1f}  union photons/px {64 * up / (W * H):8.1f}"
               f"  union factor {64 * up / max(1, lc):5.2f}  accepted/px {v[16] / (W * H):7.1f}"
               f"  lane sub-rows/px {nr / (W * H):6.1f}")
-    elif method == 2:
-        lb, wb, lr, wr = v[12:16]
-        print(f"it{it} gather   batches/px {lb / (W * H):8.1f}  SIMT batch {lb / max(1, 64 * wb):5.3f}"
-              f"  rows/px {lr / (W * H):6.1f}  SIMT row {lr / max(1, 64 * wr):5.3f}"
-              f"  accepted/px {v[16] / (W * H):7.1f} ({v[16] / max(1, 4 * lb):5.3f} of slots)")
 print("bvh stack entries", r.stats().bvh_stack_entries)
