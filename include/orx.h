@@ -146,6 +146,10 @@ typedef struct {
     const float* bitangents;         /* n_vertices * 3 or NULL */
     uint32_t n_textures;
     const orx_texture* textures;
+    /* participating media (AABInstance + ParticipatingMedium(sigma_s, sigma_a), Scene.cpp:337-350):
+     * at most one axis-aligned box; used when orx_config.enable_media is set */
+    uint32_t n_media;
+    const float* media;              /* n_media * 8: box min xyz, box max xyz, sigma_s, sigma_a */
 } orx_scene;
 
 /* Compile-time constants of config.h / OptixRenderer.cpp:38-61 as runtime config. */
@@ -173,7 +177,13 @@ typedef struct {
                                          2 kd-tree (ACCELERATION_STRUCTURE_KD_TREE_CPU:
                                          OptixRenderer_CPUKdTree.cpp, IndirectRadianceEstimation.cu:164-209;
                                          built on the device here) */
-    uint32_t reserved[5];
+    uint32_t enable_media;            /* ENABLE_PARTICIPATING_MEDIA (config.h:29): the scene's medium box
+                                         (orx_scene.media) scatters photons and eye rays gather its volumetric
+                                         photons (ParticipatingMedium.cu, VolumetricPhotonSphere*.cu); the PPM
+                                         direct pass takes no shadow samples (DirectRadianceEstimation.cu:54).
+                                         PPM on one device only (other methods / world > 1: ORX_ERR_UNSUPPORTED) */
+    uint32_t volumetric_photons;      /* NUM_VOLUMETRIC_PHOTONS = 200000 (config.h:35): volumetric photon table */
+    uint32_t reserved[3];
 } orx_config;
 
 void orx_default_config(orx_config* cfg);
@@ -318,6 +328,42 @@ orx_status orx_ppm_finish(orx_renderer* r, const void* indirect_device, size_t i
  * buffer reuse; the caller makes `side_stream` wait for the hitpoint all-gather before the
  * gather.  enable = 0 restores the serial phases. */
 orx_status orx_set_ppm_pipeline(orx_renderer* r, void* side_stream, int enable);
+
+/* Spatial photon partition of the sharded gather ("slab mode", uniform grid only; call before the
+ * first iteration, like orx_set_shard).  Rank g gathers against the photons of ALL ranks that lie
+ * in its slab of one axis of the scene AABB, and only the hit points whose sphere reaches them, so
+ * the gather's per-pixel work also divides by N (the row partition above gathers all W*H hit
+ * points on every rank).  One PPM iteration:
+ *   orx_ppm_local_eye + orx_ppm_local_photon_trace   (or orx_ppm_local_trace: both)  eye pass,
+ *                            photon pass of the own rows; no grid yet
+ *   orx_ppm_slab_histogram   per-bin counts [2][3][nbins] (uint32): the own valid deposits and the
+ *                            own non-specular hit points, per axis, nbins bins over the scene AABB;
+ *                            then 6 more words: the AABB of the own deposits as order-preserving
+ *                            integers (f >= 0: bits | 2^31, f < 0: ~bits; empty: lo 0xffffffff, hi 0)
+ *   (caller all-gathers the histograms and plans on the host: one axis and a bin -> rank table, the
+ *    same on every rank; photons from rank s to rank d = the sum of s's photon bins mapped to d)
+ *   orx_ppm_slab_pack        the own valid deposits, rank-major into the caller's send buffer: at
+ *                            dest_base[d] + k for the k-th photon sent to d (9 floats each:
+ *                            position, direction, power); host arrays bin_dest[nbins], dest_base[world]
+ *   (caller all-to-alls the photon records)
+ *   orx_ppm_slab_import      the received records become this rank's photon set; grid build over
+ *                            photon_box (host, 6 words as above: the min/max over ranks of the
+ *                            histograms' AABBs, so every rank's grid has the single-device grid's
+ *                            origin and cell size; NULL: the AABB of the imported photons)
+ *   orx_export_hitpoints / orx_ppm_gather_external / orx_ppm_finish as above (the gather skips hit
+ *   points whose sphere misses this rank's photon grid)
+ * The sum over ranks of the partial gathers is again the single-GPU gather up to fp32 order: every
+ * photon is in exactly one rank's grid.  Capacity: the import takes up to the global photon launch's
+ * deposit slots (PW * PH * max deposits) per rank. */
+orx_status orx_set_slab_partition(orx_renderer* r, int enable);
+orx_status orx_ppm_local_trace(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
+                               float ppm_radius, const orx_request* details);
+orx_status orx_ppm_local_photon_trace(orx_renderer* r);
+orx_status orx_ppm_slab_histogram(orx_renderer* r, uint32_t* hist_device /* 6*nbins + 6 */, uint32_t nbins);
+orx_status orx_ppm_slab_pack(orx_renderer* r, const uint8_t* bin_dest, uint32_t nbins, uint32_t axis,
+                             const uint32_t* dest_base, uint64_t send_records, void* send_device);
+orx_status orx_ppm_slab_import(orx_renderer* r, const void* recv_device, uint64_t n_records,
+                               const uint32_t* photon_box);
 
 /* One VCM iteration of a sharded renderer (OptixRenderer.cpp:675-795 split at
  * the light-tracing splats).  Light subpath i pairs with camera pixel i

@@ -102,6 +102,7 @@ class OrxScene(C.Structure):
         ("texcoords", C.POINTER(C.c_float)), ("tangents", C.POINTER(C.c_float)),
         ("bitangents", C.POINTER(C.c_float)),
         ("n_textures", C.c_uint32), ("textures", C.POINTER(OrxTexture)),
+        ("n_media", C.c_uint32), ("media", C.POINTER(C.c_float)),
     ]
 
 
@@ -111,7 +112,7 @@ class OrxConfig(C.Structure):
                 ("max_photon_trace_depth", C.c_uint32), ("max_radiance_trace_depth", C.c_uint32),
                 ("vcm_max_path_length", C.c_uint32), ("seed", C.c_uint32),
                 ("debug_counters", C.c_uint32), ("gather_variant", C.c_uint32), ("photon_map", C.c_uint32),
-                ("reserved", C.c_uint32 * 5)]
+                ("enable_media", C.c_uint32), ("volumetric_photons", C.c_uint32), ("reserved", C.c_uint32 * 3)]
 
 
 class OrxStats(C.Structure):
@@ -139,6 +140,7 @@ def default_config(**overrides):
     c.vcm_max_path_length = 10
     c.seed = 0
     c.debug_counters = 1
+    c.volumetric_photons = 200000  # NUM_VOLUMETRIC_PHOTONS (config.h:35)
     for k, v in overrides.items():
         setattr(c, k, v)
     return c

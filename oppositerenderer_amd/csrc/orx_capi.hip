@@ -370,6 +370,10 @@ struct orx_renderer {
     bool pipe_bufs = false, pend = false, last_pipelined = false;
     /* sharded PPM pipelining (orx_set_ppm_pipeline): gather + finish on the caller's side stream */
     bool shard_pipe = false;
+    /* slab mode (orx_set_slab_partition): photon buffers sized for the imported slab photons */
+    bool slab = false;
+    size_t S_cap = 0;
+    DevBuf d_slabtab, d_slabcur;
     int pipe_mode = -1; /* orx_set_iteration_pipelining: -1 = ORX_PIPELINE env */
     hipStream_t side = nullptr;
     uint32_t pp = 0;
@@ -857,6 +861,9 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     const size_t nslot_rng = (size_t)r->rng_rows * r->RW;
     const size_t nphot = (size_t)r->prows * PW;
     const size_t S = nphot * D;
+    /* slab mode: room for every deposit slot of the global launch (the photons this rank imports) */
+    const size_t S_cap = r->slab ? std::max(S, (size_t)PW * PH * D) : S;
+    r->S_cap = S_cap;
     const size_t G2 = (size_t)r->cfg.photon_grid_max_size + 2;
     HIPCHK(r, r->d_rng.ensure(nslot_rng * 24));
     HIPCHK(r, r->d_hp.ensure(nhp * 40));
@@ -864,17 +871,17 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_dir.ensure(nhp * 12));
     HIPCHK(r, r->d_out.ensure(nhp * 12));
     HIPCHK(r, r->d_dbg.ensure(nhp * 8));
-    HIPCHK(r, r->d_slots.ensure(S * 64));
-    HIPCHK(r, r->d_vmask.ensure(nphot));
+    HIPCHK(r, r->d_slots.ensure(S_cap * 64));
+    HIPCHK(r, r->d_vmask.ensure(S_cap / D + 1));
     /* 64 photons of tail padding per plane: the union gather loads whole 64-photon chunks (and
      * prefetches the next one) up to index U1 + 63 of the last plane */
-    const size_t splane = ((S + 64) + 3) & ~(size_t)3;
+    const size_t splane = ((S_cap + 64) + 3) & ~(size_t)3;
     if ((size_t)SP_PLANES * splane * 4 > 0xffffff00ull) /* the gather addresses the planes with 32-bit buffer offsets */
         return set_err(r, ORX_ERR_UNSUPPORTED, "photon slots per device exceed the 4 GiB sorted-photon window");
     HIPCHK(r, r->d_sorted.ensure(SP_PLANES * splane * 4));
-    HIPCHK(r, r->d_perm.ensure(S * 4 + 16));
+    HIPCHK(r, r->d_perm.ensure(S_cap * 4 + 16));
     HIPCHK(r, hipMemsetAsync(r->d_sorted.p, 0, SP_PLANES * splane * 4, r->stream)); /* tail reads stay finite */
-    HIPCHK(r, r->d_keys.ensure(S * 4));
+    HIPCHK(r, r->d_keys.ensure(S_cap * 4));
     HIPCHK(r, r->d_offsets.ensure(G2 * 4));
     HIPCHK(r, r->d_bbox.ensure(6 * BBOX_REPLICAS * 4));
     HIPCHK(r, r->d_grid.ensure(sizeof(GridParams)));
@@ -889,19 +896,20 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     uint32_t bshift = 10;
     while (((vmax + (1u << bshift) - 1) >> bshift) > 2048) bshift++;
     const size_t bs_nchunk = (S + 16383) / 16384;
+    const size_t bs_nchunk_cap = (S_cap + 16383) / 16384;
     const size_t bs_nbmax = (vmax + (1u << bshift) - 1) >> bshift;
-    const size_t bs_nscan = (bs_nbmax * bs_nchunk + 1023) / 1024;
-    HIPCHK(r, r->d_pos4.ensure(S * 16 + 16));
-    HIPCHK(r, r->d_bstable.ensure(bs_nbmax * bs_nchunk * 4 + 16));
+    const size_t bs_nscan = (bs_nbmax * bs_nchunk_cap + 1023) / 1024;
+    HIPCHK(r, r->d_pos4.ensure(S_cap * 16 + 16));
+    HIPCHK(r, r->d_bstable.ensure(bs_nbmax * bs_nchunk_cap * 4 + 16));
     HIPCHK(r, r->d_bspartials.ensure((bs_nscan + 2) * 4));
-    HIPCHK(r, r->d_bspairs.ensure(S * 8 + 16));
+    HIPCHK(r, r->d_bspairs.ensure(S_cap * 8 + 16));
     HIPCHK(r, r->d_subofs.ensure(G2 * 4 * SUBX * nsub + 16));
     /* the second buffer set of PPM pipelining is allocated on the first pipelined iteration
      * (ensure_second_set); the sharded pipeline (orx_set_ppm_pipeline) wants it at once */
     r->pipe_bufs = false;
     r->pend = false;
     HIPCHK(r, hipMemsetAsync(r->d_offsets.p, 0, G2 * 4, r->stream));
-    HIPCHK(r, hipMemsetAsync(r->d_vmask.p, 0, nphot, r->stream));
+    HIPCHK(r, hipMemsetAsync(r->d_vmask.p, 0, S_cap / D + 1, r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_grid.p, 0, sizeof(GridParams), r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_out.p, 0, nhp * 12, r->stream));
     HIPCHK(r, hipMemsetAsync(r->d_hp.p, 0, nhp * 40, r->stream)); /* pad rows: flags 0 */
@@ -1220,6 +1228,7 @@ static GatherIn local_gather_in(orx_renderer* r) {
     gi.W = r->W;
     gi.indirect = r->d_ind.as<float>();
     gi.dbg = r->cfg.debug_counters ? r->d_dbg.as<uint32_t>() : nullptr;
+    gi.cull = 0;
     gi.visits = 1;
     return gi;
 }
@@ -1247,7 +1256,10 @@ static HashParams hash_params(const orx_renderer* r, float ppm_radius) {
     hp.mask = r->pb.hnum - 1u;
     return hp;
 }
-static void ppm_photons_grid(orx_renderer* r, const Consts& c) {
+static void ppm_grid_build(orx_renderer* r, const PhotonBufs& pb, const GridBox& gb = GridBox{});
+/* photon pass (+ the overlapped direct pass), then the photon map (build_map: false in slab
+ * mode, whose grid is built over the imported photons by orx_ppm_slab_import) */
+static void ppm_photons_grid(orx_renderer* r, const Consts& c, bool build_map = true) {
     hipStream_t st = cur_stream(r);
     ev_begin(r, P_PHOTON);
     r->eye_chain = false;
@@ -1265,6 +1277,7 @@ static void ppm_photons_grid(orx_renderer* r, const Consts& c) {
         ev_end_on(r, P_DIRECT, r->aux);
         hipEventRecord(r->ev_direct_done, r->aux);
     }
+    if (!build_map) return;
     if (r->pb.hash) {
         ev_begin(r, P_SETUP_HASH);
         launch_hash_build(st, r->pb, hash_params(r, c.ppm_radius));
@@ -1277,17 +1290,21 @@ static void ppm_photons_grid(orx_renderer* r, const Consts& c) {
         ev_end(r, P_SETUP_HASH);
         return;
     }
-    /* grid build: the atomic-free bucket sort (an atomic-rank counting sort measured slower:
-     * one device-scope atomic per photon into a 4 MB histogram) */
+    ppm_grid_build(r, r->pb);
+}
+/* grid build: the atomic-free bucket sort (an atomic-rank counting sort measured slower:
+ * one device-scope atomic per photon into a 4 MB histogram) */
+static void ppm_grid_build(orx_renderer* r, const PhotonBufs& pb, const GridBox& gb) {
+    hipStream_t st = cur_stream(r);
     ev_begin(r, P_SETUP_HASH);
-    launch_grid_setup(st, r->pb);
-    launch_grid_bucket_count(st, r->pb);
+    launch_grid_setup(st, pb, gb);
+    launch_grid_bucket_count(st, pb);
     ev_end(r, P_SETUP_HASH);
     ev_begin(r, P_SCAN);
-    launch_grid_bucket_scan(st, r->pb);
+    launch_grid_bucket_scan(st, pb);
     ev_end(r, P_SCAN);
     ev_begin(r, P_SCATTER);
-    launch_grid_bucket_place(st, r->pb);
+    launch_grid_bucket_place(st, pb);
     ev_end(r, P_SCATTER);
 }
 static void ppm_local_passes(orx_renderer* r, const DevCamera& cam, const Consts& c) {
@@ -1587,6 +1604,125 @@ orx_status orx_ppm_local_photons(orx_renderer* r) {
     return ORX_OK;
 }
 
+orx_status orx_set_slab_partition(orx_renderer* r, int enable) {
+    if (!r) return ORX_ERR_INVALID_ARGUMENT;
+    if (enable && r->cfg.photon_map != 0)
+        return set_err(r, ORX_ERR_UNSUPPORTED, "the slab partition needs the uniform-grid photon map");
+    HIPCHK(r, hipSetDevice(r->device));
+    orx_status s0 = sync_all(r);
+    if (s0 != ORX_OK) return s0;
+    r->slab = enable != 0;
+    r->rng_ready = false; /* re-allocate the photon buffers for the imported photons */
+    return ORX_OK;
+}
+
+orx_status orx_ppm_local_trace(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
+                               float ppm_radius, const orx_request* det) {
+    (void)iteration_number;
+    if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
+    if (det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
+        return set_err(r, ORX_ERR_INVALID_ARGUMENT, "orx_ppm_local_trace needs a PPM request");
+    if (!r->slab) return set_err(r, ORX_ERR_STATE, "orx_ppm_local_trace is the slab mode's first phase");
+    r->last_pipelined = false;
+    orx_status s0 = begin_iteration(r, local_iteration_number, det);
+    if (s0 != ORX_OK) return s0;
+    DevCamera cam = camera_setup(det->camera);
+    Consts c = make_consts(r, ppm_radius, local_iteration_number);
+    ppm_eye(r, cam, c);
+    ppm_photons_grid(r, c, false);
+    HIPCHK(r, hipGetLastError());
+    r->last_method = (uint64_t)det->method;
+    r->last_consts = c;
+    return ORX_OK;
+}
+
+orx_status orx_ppm_local_photon_trace(orx_renderer* r) {
+    if (!r) return ORX_ERR_INVALID_ARGUMENT;
+    if (!r->rng_ready) return set_err(r, ORX_ERR_STATE, "orx_ppm_local_eye first");
+    if (!r->slab) return set_err(r, ORX_ERR_STATE, "orx_ppm_local_photon_trace is a slab-mode phase");
+    HIPCHK(r, hipSetDevice(r->device));
+    r->overlap_direct = r->last_pipelined; /* direct pass on the aux stream right after the photons */
+    ppm_photons_grid(r, r->last_consts, false);
+    r->overlap_direct = false;
+    HIPCHK(r, hipGetLastError());
+    return ORX_OK;
+}
+
+static SlabBins slab_bins(const orx_renderer* r, uint32_t nb) {
+    SlabBins sb;
+    const float lo[3] = {r->aabb_lo.x, r->aabb_lo.y, r->aabb_lo.z}, hi[3] = {r->aabb_hi.x, r->aabb_hi.y, r->aabb_hi.z};
+    for (int a = 0; a < 3; a++) {
+        const float ext = hi[a] - lo[a];
+        sb.lo[a] = lo[a];
+        sb.inv[a] = ext > 0.f ? (float)nb / ext : 0.f;
+    }
+    sb.nb = nb;
+    return sb;
+}
+
+orx_status orx_ppm_slab_histogram(orx_renderer* r, uint32_t* hist, uint32_t nb) {
+    if (!r || !hist || nb == 0 || nb > 8192) return ORX_ERR_INVALID_ARGUMENT;
+    if (!r->slab || !r->rng_ready) return set_err(r, ORX_ERR_STATE, "orx_ppm_slab_histogram: slab mode, after the photon pass");
+    HIPCHK(r, hipSetDevice(r->device));
+    hipStream_t st = cur_stream(r);
+    HIPCHK(r, hipMemsetAsync(hist, 0, (size_t)6 * nb * 4, st));
+    launch_slab_hist(st, r->pb, r->px, slab_bins(r, nb), hist);
+    launch_slab_bbox(st, r->pb, hist + 6 * (size_t)nb);
+    HIPCHK(r, hipGetLastError());
+    return ORX_OK;
+}
+
+orx_status orx_ppm_slab_pack(orx_renderer* r, const uint8_t* bin_dest, uint32_t nb, uint32_t axis,
+                             const uint32_t* dest_base, uint64_t send_records, void* send) {
+    if (!r || !bin_dest || !dest_base || !send || nb == 0 || nb > 8192 || axis > 2) return ORX_ERR_INVALID_ARGUMENT;
+    if (!r->slab || !r->rng_ready) return set_err(r, ORX_ERR_STATE, "orx_ppm_slab_pack: slab mode, after the photon pass");
+    if (r->world > 64) return set_err(r, ORX_ERR_UNSUPPORTED, "slab mode supports at most 64 ranks");
+    for (uint32_t b = 0; b < nb; b++)
+        if (bin_dest[b] >= r->world) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "bin_dest names a rank >= world");
+    /* the run of each rank must lie inside the send buffer; the plan's counts come from the
+     * histogram of the same photons, so the runs are exactly filled */
+    for (uint32_t d = 0; d < r->world; d++)
+        if (dest_base[d] > send_records || (d && dest_base[d] < dest_base[d - 1]))
+            return set_err(r, ORX_ERR_INVALID_ARGUMENT, "dest_base must be ascending and inside the send buffer");
+    if (send_records > 0xffffffffull) return set_err(r, ORX_ERR_UNSUPPORTED, "send buffer beyond 2^32 records");
+    HIPCHK(r, hipSetDevice(r->device));
+    hipStream_t st = cur_stream(r);
+    HIPCHK(r, r->d_slabtab.ensure(8192));
+    HIPCHK(r, r->d_slabcur.ensure(64 * 4));
+    HIPCHK(r, hipMemcpyAsync(r->d_slabtab.p, bin_dest, nb, hipMemcpyHostToDevice, st));
+    HIPCHK(r, hipMemcpyAsync(r->d_slabcur.p, dest_base, (size_t)r->world * 4, hipMemcpyHostToDevice, st));
+    launch_slab_pack(st, r->pb, slab_bins(r, nb), axis, r->d_slabtab.as<uint8_t>(), r->world,
+                     r->d_slabcur.as<uint32_t>(), (uint32_t)send_records, (float*)send);
+    HIPCHK(r, hipGetLastError());
+    return ORX_OK;
+}
+
+orx_status orx_ppm_slab_import(orx_renderer* r, const void* recv, uint64_t n, const uint32_t* photon_box) {
+    if (!r || (!recv && n)) return ORX_ERR_INVALID_ARGUMENT;
+    if (!r->slab || !r->rng_ready) return set_err(r, ORX_ERR_STATE, "orx_ppm_slab_import: slab mode, after the photon pass");
+    if (n > r->S_cap) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "more photons than the slab import capacity");
+    HIPCHK(r, hipSetDevice(r->device));
+    hipStream_t st = cur_stream(r);
+    /* the photon AABB replicas hold the own photon pass's deposits: reset, then the imported ones */
+    HIPCHK(r, hipMemsetAsync(r->d_bbox.p, 0xff, 3 * BBOX_REPLICAS * 4, st));
+    HIPCHK(r, hipMemsetAsync(r->d_bbox.as<uint32_t>() + 3 * BBOX_REPLICAS, 0, 3 * BBOX_REPLICAS * 4, st));
+    PhotonBufs pbi = r->pb;
+    const size_t groups = n ? (n + pbi.D - 1) / pbi.D : 1; /* an empty import: one group with no deposit */
+    pbi.S = (uint32_t)(groups * pbi.D);
+    pbi.bs_nchunk = (pbi.S + 16383) / 16384;
+    if (n == 0) HIPCHK(r, hipMemsetAsync(r->d_vmask.p, 0, 1, st));
+    else launch_slab_import(st, pbi, (const float*)recv, (uint32_t)n);
+    GridBox gb{};
+    if (photon_box) {
+        gb.on = 1;
+        for (int k = 0; k < 6; k++) gb.b[k] = photon_box[k];
+    }
+    ppm_grid_build(r, pbi, gb);
+    if (r->last_pipelined) HIPCHK(r, hipEventRecord(r->ev_grid_done, st));
+    HIPCHK(r, hipGetLastError());
+    return ORX_OK;
+}
+
 orx_status orx_export_hitpoints(orx_renderer* r, void* dst, size_t bytes) {
     if (!r || !dst) return ORX_ERR_INVALID_ARGUMENT;
     size_t need = (size_t)r->max_rows * r->W * 40;
@@ -1611,6 +1747,7 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hp, uint32_t seg
     gi.W = r->W;
     gi.indirect = (float*)indirect;
     gi.dbg = nullptr;
+    gi.cull = r->slab ? 1u : 0u;
     gi.visits = 0; /* rank-local counts are not the reference's; no per-pixel debug buffers here */
     hipStream_t st = cur_stream(r);
     if (r->last_pipelined) { /* on the side stream, after the grid build */

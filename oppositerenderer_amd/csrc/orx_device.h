@@ -669,105 +669,6 @@ __device__ __forceinline__ bool trace_closest(const DevScene& S, f3 o, f3 d, flo
                                               uint32_t* stk) {
     return trace_closest_t(S, o, d, tmin, tmax, h, StackL{stk}, NodesG{});
 }
-/* Resumable closest-hit traversal for the wavefront passes: the same
- * computation as trace_closest, split so that a persistent kernel can run one
- * while-while round per lane and hand a lane whose ray finished a new ray
- * (Aila & Laine 2009, "dynamic fetch").  Results are identical to
- * trace_closest: the hit is fixed by the exact triangle tests and the
- * (t, primitive id) tie rule, not by the visiting order. */
-struct TraceState {
-    RayBox rb;
-    f3 d;
-    float tmin, best, bb, bg;
-    int32_t bp;
-    uint32_t bslot, ref;
-    int32_t sp;
-    f3 sn;
-};
-__device__ __forceinline__ void trace_begin(const DevScene& S, f3 o, f3 d, float tmin, float tmax, TraceState& T) {
-    float best = tmax, t;
-    int32_t bp = -1;
-    for (uint32_t i = 0; i < S.nq; i++) {
-        if (isect_quad(S.quads[i], o, d, tmin, best, t)) {
-            best = t;
-            bp = (int32_t)i;
-        }
-    }
-    f3 sn = mk1(0);
-    for (uint32_t i = 0; i < S.ns; i++) {
-        f3 n;
-        if (isect_sphere(S.spheres[i], o, d, tmin, best, t, n)) {
-            best = t;
-            bp = (int32_t)(S.nq + i);
-            sn = n;
-        }
-    }
-    T.rb = ray_box(o, d);
-    T.d = d;
-    T.tmin = tmin;
-    T.best = best;
-    T.bp = bp;
-    T.bslot = 0;
-    T.bb = 0.f;
-    T.bg = 0.f;
-    T.sn = sn;
-    T.sp = 0;
-    T.ref = S.nt ? 0u : ORX_DONE;
-}
-/* one round: inner nodes until a leaf (or the end), then leaves until the
- * next entry is an inner node */
-__device__ __forceinline__ void trace_round(const DevScene& S, TraceState& T, uint32_t* stk) {
-    const uint32_t base = S.nq + S.ns;
-    const f3 o = T.rb.o;
-    uint32_t ref = T.ref;
-    int32_t sp = T.sp;
-    uint32_t lf = 0;
-    while (!(ref & ORX_LEAF) && ref != ORX_DONE) {
-        float ct[4];
-        uint32_t cc[4];
-        node_test(S.bvh4, ref, T.rb, T.tmin, T.best, ct, cc);
-        cswap(ct[0], cc[0], ct[1], cc[1]);
-        cswap(ct[2], cc[2], ct[3], cc[3]);
-        cswap(ct[0], cc[0], ct[2], cc[2]);
-        cswap(ct[1], cc[1], ct[3], cc[3]);
-        cswap(ct[1], cc[1], ct[2], cc[2]);
-        if (ct[0] != INFINITY) {
-            if (ct[3] != INFINITY) stk[(sp++) * 64] = cc[3];
-            if (ct[2] != INFINITY) stk[(sp++) * 64] = cc[2];
-            if (ct[1] != INFINITY) stk[(sp++) * 64] = cc[1];
-            ref = cc[0];
-        } else {
-            ref = sp ? stk[(--sp) * 64] : ORX_DONE;
-        }
-        if ((ref & ORX_LEAF) && !(lf & ORX_LEAF)) {
-            lf = ref;
-            ref = sp ? stk[(--sp) * 64] : ORX_DONE;
-        }
-        if (!__ballot(!(lf & ORX_LEAF))) break;
-    }
-    while (lf & ORX_LEAF) {
-        const uint32_t first = (lf & 0x7fffffffu) >> 3, cnt = (lf & 7u) + 1u;
-        for (uint32_t k = first; k < first + cnt; k++) {
-            const float4 v0 = S.tri_v[3 * k], v1 = S.tri_v[3 * k + 1], v2 = S.tri_v[3 * k + 2];
-            const int32_t gid = (int32_t)(base + __float_as_uint(v0.w));
-            float t, b, g;
-            float lim = T.bp >= 0 ? orx_as_float(orx_as_uint(T.best) + 1u) : T.best;
-            if (isect_tri(ld_f3(v0), ld_f3(v1), ld_f3(v2), o, T.d, T.tmin, lim, t, b, g) &&
-                (t < T.best || gid < T.bp)) {
-                T.best = t;
-                T.bp = gid;
-                T.bslot = k;
-                T.bb = b;
-                T.bg = g;
-            }
-        }
-        lf = ref;
-        if (ref & ORX_LEAF) ref = sp ? stk[(--sp) * 64] : ORX_DONE;
-    }
-    T.ref = ref;
-    T.sp = sp;
-}
-
 /* any hit in (tmin,tmax): every material's RayType::SHADOW any-hit is
  * gatherAnyHitOnNonEmitter (Material.cpp:18-26, DirectRadianceEstimation.cu:79-83) */
 template <class STK, class NODES>

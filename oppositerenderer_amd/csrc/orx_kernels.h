@@ -30,6 +30,13 @@ struct GridParams {
     uint64_t union_photons_total; /* reserved (stats ABI: gather_staged_total, always 0) */
     uint64_t st_lane_batches, st_wave_batches, st_lane_rows, st_wave_rows; /* ORX_TRAV_STATS builds: gather SIMT */
     uint64_t st_accepted;   /* ORX_TRAV_STATS builds: gather photons within r and facing the normal */
+    float clo[3], chi[3];   /* the AABB of the photons in the grid (slab mode's gather cull; empty: +inf/-inf) */
+};
+/* grid bounds from the caller (slab mode: the AABB of ALL ranks' photons, ordered-int bits as the
+ * bbox replicas hold them), so every rank's grid has the single-device grid's origin and cells */
+struct GridBox {
+    uint32_t on;
+    uint32_t b[6]; /* f2ord(lo xyz), f2ord(hi xyz) */
 };
 
 /* Per-frame pixel state. Pixel (x,y) of rank r is stored at local row
@@ -145,7 +152,7 @@ void launch_rng_init(hipStream_t s, RngPlanes rng, uint32_t RW, uint32_t rows, u
                      uint32_t seed);
 void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c);
 void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c);
-void launch_grid_setup(hipStream_t s, const PhotonBufs& pb);
+void launch_grid_setup(hipStream_t s, const PhotonBufs& pb, const GridBox& gb = GridBox{});
 /* atomic-free grid build: keys + bucket histogram / scan of the table /
  * bucket placement + per-bucket cells (offsets, permutation) + permute */
 void launch_grid_bucket_count(hipStream_t s, const PhotonBufs& pb);
@@ -161,6 +168,8 @@ struct GatherIn {
     uint32_t segments, seg_rows, W;
     float* indirect;    /* [segments*seg_rows*W*3] */
     uint32_t* dbg;      /* [segments*seg_rows*W*2] or NULL */
+    uint32_t cull;      /* 1 (slab mode): a hit point whose sphere misses the AABB of the grid's photons
+                         * gathers nothing (its window would only clamp onto cells without them) */
     uint32_t visits;    /* 1: count the reference's per-pixel visits (IndirectRadianceEstimation.cu:113/124)
                          * into dbg and the stats; 0 for the sharded gather, which has no per-pixel
                          * debug buffers and whose rank-local counts are not the reference's
@@ -178,6 +187,18 @@ __device__ __forceinline__ uint32_t gather_row(const GatherIn& gi, uint32_t y) {
 }
 /* 8x8-pixel wave tiles; the wave-union kernel, or the per-lane kernel for gathers of >= 8 segments */
 void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c);
+/* slab mode (sharded PPM with a spatial photon partition): nb bins per axis over the scene AABB */
+struct SlabBins {
+    float lo[3];
+    float inv[3]; /* nb / extent */
+    uint32_t nb;
+};
+void launch_slab_hist(hipStream_t s, const PhotonBufs& pb, const PixelBufs& px, const SlabBins& sb, uint32_t* hist);
+void launch_slab_pack(hipStream_t s, const PhotonBufs& pb, const SlabBins& sb, uint32_t axis, const uint8_t* bin_dest,
+                      uint32_t world, uint32_t* cursor, uint32_t cap, float* send);
+void launch_slab_import(hipStream_t s, const PhotonBufs& pb, const float* recv, uint32_t n);
+/* the own photon pass's AABB (folded bbox replicas, ordered-int bits) -> out[6] */
+void launch_slab_bbox(hipStream_t s, const PhotonBufs& pb, uint32_t* out);
 void launch_hash_build(hipStream_t s, const PhotonBufs& pb, const HashParams& hp);
 void launch_ppm_gather_hash(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const HashParams& hp,
                             const Consts& c);

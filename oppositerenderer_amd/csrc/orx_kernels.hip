@@ -332,7 +332,7 @@ void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, co
 /* ------------------------------------------------------------------ */
 /* grid setup: createUniformGridPhotonMap host math, on one thread     */
 /* ------------------------------------------------------------------ */
-__global__ void k_grid_setup(PhotonBufs pb) {
+__global__ void k_grid_setup(PhotonBufs pb, GridBox gb) {
     /* lanes k*64..: fold the replicas, then reset them for the next photon pass */
     __shared__ uint32_t red[6];
     const uint32_t lane = threadIdx.x;
@@ -348,7 +348,14 @@ __global__ void k_grid_setup(PhotonBufs pb) {
     __syncthreads();
     if (lane != 0) return;
     uint32_t b[6];
-    for (int k = 0; k < 6; k++) b[k] = red[k];
+    GridParams* g = pb.grid;
+    /* the photons' own AABB: the slab gather's cull box */
+    const bool own = red[0] != 0xffffffffu;
+    for (int k = 0; k < 3; k++) {
+        g->clo[k] = own ? ord2f(red[k]) : INFINITY;
+        g->chi[k] = own ? ord2f(red[k + 3]) : -INFINITY;
+    }
+    for (int k = 0; k < 6; k++) b[k] = gb.on ? gb.b[k] : red[k];
     bool any = b[0] != 0xffffffffu; /* min initialised to ord(+max) */
     f3 lo, hi;
     if (any) {
@@ -379,7 +386,6 @@ __global__ void k_grid_setup(PhotonBufs pb) {
     gy = gy < 1 ? 1 : gy;
     gz = gz < 1 ? 1 : gz;
     uint64_t G = (uint64_t)gx * gy * gz;
-    GridParams* g = pb.grid;
     g->ox = lo.x; g->oy = lo.y; g->oz = lo.z;
     g->cell = cellSize;
     g->gx = gx; g->gy = gy; g->gz = gz;
@@ -394,8 +400,8 @@ __global__ void k_grid_setup(PhotonBufs pb) {
         g->G = (uint32_t)G;
     }
 }
-void launch_grid_setup(hipStream_t s, const PhotonBufs& pb) {
-    hipLaunchKernelGGL(k_grid_setup, dim3(1), dim3(64), 0, s, pb);
+void launch_grid_setup(hipStream_t s, const PhotonBufs& pb, const GridBox& gb) {
+    hipLaunchKernelGGL(k_grid_setup, dim3(1), dim3(64), 0, s, pb, gb);
 }
 
 /* ------------------------------------------------------------------ */
@@ -842,6 +848,14 @@ __device__ __forceinline__ void window_visits(const uint32_t* __restrict__ offse
 
 constexpr uint32_t GQ = 8; /* chord ranges per lane per phase A (LDS: GQ * 8 B per lane) */
 
+/* slab mode: the hit point's sphere (grown by a margin far above the rounding of the distance
+ * test) misses the AABB of this rank's photons (the grid spans all ranks' photons) */
+__device__ __forceinline__ bool sphere_misses_grid(const GridParams& g, f3 pos, float r) {
+    const float m = r * 1e-3f + g.cell * 1e-3f, rr = r + m;
+    return pos.x + rr < g.clo[0] || pos.x - rr > g.chi[0] || pos.y + rr < g.clo[1] || pos.y - rr > g.chi[1] ||
+           pos.z + rr < g.clo[2] || pos.z - rr > g.chi[2];
+}
+
 /* NSUB: sub-rows per cell row (SUBR^2, or 1 for the cell-order layout) */
 template <uint32_t NSUB>
 #ifndef ORX_GATHER_LANE_WAVES
@@ -879,7 +893,7 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
     const float invCellSize = 1.f / g.cell;
     const f3 np = pos - mk(g.ox, g.oy, g.oz);
     uint32_t x_lo = 0, x_hi = 0, y_lo = 0, z_lo = 0, ny = 0, nrows = 0;
-    if (live && (flags & PRD_HIT_NON_SPECULAR) && g.G) {
+    if (live && (flags & PRD_HIT_NON_SPECULAR) && g.G && !(gi.cull && sphere_misses_grid(g, pos, radius))) {
         const int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
         const int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
         const int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
@@ -1244,7 +1258,7 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
     const f3 np = pos - mk(g.ox, g.oy, g.oz);
     uint32_t x_lo = 1, x_hi = 0, y_lo = 1, y_hi = 0, z_lo = 1, z_hi = 0;
     bool act = false;
-    if (live && (flags & PRD_HIT_NON_SPECULAR) && g.G) {
+    if (live && (flags & PRD_HIT_NON_SPECULAR) && g.G && !(gi.cull && sphere_misses_grid(g, pos, radius))) {
         const int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
         const int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
         const int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
@@ -1428,6 +1442,160 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
     }
     if (pb.nsub == 1) hipLaunchKernelGGL((k_ppm_gather_union<1>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
     else hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
+}
+
+/* ------------------------------------------------------------------ */
+/* spatial photon partition of the sharded gather (slab mode)          */
+/* ------------------------------------------------------------------ */
+/* Rank g of N receives every photon whose position falls in its slab of one axis of the scene
+ * AABB, and gathers only the hit points whose sphere reaches its photons; the bins and the
+ * bin -> rank table are the host's plan (multigpu.slab_plan) over the all-gathered histograms.
+ * The bin of a position is computed by the one function below in the histogram and in the
+ * pack, so the host's per-rank counts are exact. */
+__device__ __forceinline__ uint32_t slab_bin(const SlabBins& sb, float v, uint32_t a) {
+    const int32_t b = orx_f2i_sat(orx_floorf((v - sb.lo[a]) * sb.inv[a]));
+    return b < 0 ? 0u : (b >= (int32_t)sb.nb ? sb.nb - 1u : (uint32_t)b);
+}
+__device__ __forceinline__ bool slot_valid(const PhotonBufs& pb, uint32_t s) {
+    const uint32_t p = s / pb.D, k = s - p * pb.D;
+    return (pb.vmask[p] >> k) & 1u;
+}
+/* [2][3][nb] counts: the valid deposits of the own photon pass, the own rows' non-specular hit
+ * points (LDS histograms, one global add per non-empty bin and block) */
+__global__ __launch_bounds__(256) void k_slab_hist(PhotonBufs pb, PixelBufs px, SlabBins sb, uint32_t* hist) {
+    extern __shared__ uint32_t lh[]; /* [2][3][nb] */
+    const uint32_t n6 = 6 * sb.nb;
+    for (uint32_t k = threadIdx.x; k < n6; k += blockDim.x) lh[k] = 0;
+    __syncthreads();
+    const uint32_t T = gridDim.x * blockDim.x;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < pb.S; s += T) {
+        if (!slot_valid(pb, s)) continue;
+        const float4 q = pb.pos4[s];
+        atomicAdd(&lh[0 * sb.nb + slab_bin(sb, q.x, 0)], 1u);
+        atomicAdd(&lh[1 * sb.nb + slab_bin(sb, q.y, 1)], 1u);
+        atomicAdd(&lh[2 * sb.nb + slab_bin(sb, q.z, 2)], 1u);
+    }
+    const uint32_t npx = px.rows * px.W;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += T) {
+        const float4 A = px.hpA[i];
+        if (!(__float_as_uint(A.w) & PRD_HIT_NON_SPECULAR)) continue;
+        atomicAdd(&lh[3 * sb.nb + slab_bin(sb, A.x, 0)], 1u);
+        atomicAdd(&lh[4 * sb.nb + slab_bin(sb, A.y, 1)], 1u);
+        atomicAdd(&lh[5 * sb.nb + slab_bin(sb, A.z, 2)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < n6; k += blockDim.x)
+        if (lh[k]) atomicAdd(&hist[k], lh[k]);
+}
+void launch_slab_hist(hipStream_t s, const PhotonBufs& pb, const PixelBufs& px, const SlabBins& sb, uint32_t* hist) {
+    const uint32_t n = pb.S > px.rows * px.W ? pb.S : px.rows * px.W;
+    uint32_t blocks = (n + 4095) / 4096;
+    blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+    hipLaunchKernelGGL(k_slab_hist, dim3(blocks), dim3(256), 6 * sb.nb * 4, s, pb, px, sb, hist);
+}
+
+/* valid deposits -> the send buffer, rank-major: photon record (9 floats: position, direction,
+ * power) at cursor[rank]++.  A block takes SLAB_CHUNK slots: counts per destination in LDS,
+ * one device atomic per destination reserves the block's run, then every photon takes its
+ * place in it (the order inside a run is not the slot order: it only changes the gather's
+ * fp32 summation order on the receiving rank) */
+constexpr uint32_t SLAB_CHUNK = 4096;
+constexpr uint32_t SLAB_MAX_RANKS = 64;
+__global__ __launch_bounds__(256) void k_slab_pack(PhotonBufs pb, SlabBins sb, uint32_t axis,
+                                                   const uint8_t* __restrict__ bin_dest, uint32_t world,
+                                                   uint32_t* cursor, uint32_t cap, float* __restrict__ send) {
+    __shared__ uint32_t cnt[SLAB_MAX_RANKS], base[SLAB_MAX_RANKS];
+    for (uint32_t c0 = blockIdx.x * SLAB_CHUNK; c0 < pb.S; c0 += gridDim.x * SLAB_CHUNK) {
+        const uint32_t c1 = c0 + SLAB_CHUNK < pb.S ? c0 + SLAB_CHUNK : pb.S;
+        if (threadIdx.x < SLAB_MAX_RANKS) cnt[threadIdx.x] = 0;
+        __syncthreads();
+        for (uint32_t s = c0 + threadIdx.x; s < c1; s += blockDim.x) {
+            if (!slot_valid(pb, s)) continue;
+            const float4 q = pb.pos4[s];
+            const float v = axis == 0 ? q.x : axis == 1 ? q.y : q.z;
+            atomicAdd(&cnt[bin_dest[slab_bin(sb, v, axis)]], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < world) {
+            const uint32_t n = cnt[threadIdx.x];
+            base[threadIdx.x] = n ? atomicAdd(&cursor[threadIdx.x], n) : 0u;
+            cnt[threadIdx.x] = 0;
+        }
+        __syncthreads();
+        for (uint32_t s = c0 + threadIdx.x; s < c1; s += blockDim.x) {
+            if (!slot_valid(pb, s)) continue;
+            const float4* rec = pb.slots + 4 * (size_t)s;
+            const float4 a = rec[0], b = rec[1];
+            const float pz = rec[2].x;
+            const float v = axis == 0 ? a.x : axis == 1 ? a.y : a.z;
+            const uint32_t d = bin_dest[slab_bin(sb, v, axis)];
+            const uint32_t o = base[d] + atomicAdd(&cnt[d], 1u);
+            if (o >= cap) continue; /* a plan whose counts disagree with the photons: never write past */
+            float* w = send + 9 * (size_t)o;
+            w[0] = a.x; w[1] = a.y; w[2] = a.z;
+            w[3] = b.x; w[4] = b.y; w[5] = b.z;
+            w[6] = a.w; w[7] = b.w; w[8] = pz;
+        }
+        __syncthreads();
+    }
+}
+void launch_slab_pack(hipStream_t s, const PhotonBufs& pb, const SlabBins& sb, uint32_t axis, const uint8_t* bin_dest,
+                      uint32_t world, uint32_t* cursor, uint32_t cap, float* send) {
+    uint32_t blocks = (pb.S + SLAB_CHUNK - 1) / SLAB_CHUNK;
+    blocks = blocks < 1 ? 1 : (blocks > 4096 ? 4096 : blocks);
+    hipLaunchKernelGGL(k_slab_pack, dim3(blocks), dim3(256), 0, s, pb, sb, axis, bin_dest, world, cursor, cap, send);
+}
+
+/* received photon records -> this rank's deposit records: record i is slot i of photon group
+ * i / D (deposit mask bit i % D), with its compact position and the photon AABB of the grid
+ * setup (the replicas k_grid_setup folds; reset beforehand) */
+__global__ __launch_bounds__(256) void k_slab_import(PhotonBufs pb, const float* __restrict__ recv, uint32_t n) {
+    float lo_x = INFINITY, lo_y = INFINITY, lo_z = INFINITY;
+    float hi_x = -INFINITY, hi_y = -INFINITY, hi_z = -INFINITY;
+    const uint32_t groups = (n + pb.D - 1) / pb.D;
+    const uint32_t T = gridDim.x * blockDim.x;
+    const uint32_t g_end = ((groups + T - 1) / T) * T; /* every lane runs the same trip count */
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < g_end; g += T) {
+        if (g >= groups) continue;
+        uint32_t mask = 0;
+        for (uint32_t k = 0; k < pb.D; k++) {
+            const uint32_t i = g * pb.D + k;
+            if (i >= n) break;
+            const float* w = recv + 9 * (size_t)i;
+            const float x = w[0], y = w[1], z = w[2];
+            float4* rec = pb.slots + 4 * (size_t)i;
+            rec[0] = make_float4(x, y, z, w[6]);
+            rec[1] = make_float4(w[3], w[4], w[5], w[7]);
+            rec[2].x = w[8];
+            pb.pos4[i] = make_float4(x, y, z, 0.f);
+            mask |= 1u << k;
+            lo_x = fminf(lo_x, x); lo_y = fminf(lo_y, y); lo_z = fminf(lo_z, z);
+            hi_x = fmaxf(hi_x, x); hi_y = fmaxf(hi_y, y); hi_z = fmaxf(hi_z, z);
+        }
+        pb.vmask[g] = (uint8_t)mask;
+    }
+    photon_bbox_flush(pb, lo_x, lo_y, lo_z, hi_x, hi_y, hi_z, (blockIdx.x * 4 + (threadIdx.x >> 6)) & (BBOX_REPLICAS - 1),
+                      threadIdx.x & 63);
+}
+__global__ void k_slab_bbox(PhotonBufs pb, uint32_t* out) {
+    const uint32_t lane = threadIdx.x;
+    for (int k = 0; k < 6; k++) {
+        uint32_t v = pb.bbox[k * BBOX_REPLICAS + lane];
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t w = (uint32_t)__shfl_xor((int)v, o, 64);
+            v = k < 3 ? min(v, w) : max(v, w);
+        }
+        if (lane == 0) out[k] = v;
+    }
+}
+void launch_slab_bbox(hipStream_t s, const PhotonBufs& pb, uint32_t* out) {
+    hipLaunchKernelGGL(k_slab_bbox, dim3(1), dim3(64), 0, s, pb, out);
+}
+void launch_slab_import(hipStream_t s, const PhotonBufs& pb, const float* recv, uint32_t n) {
+    const uint32_t groups = (n + pb.D - 1) / pb.D;
+    uint32_t blocks = (groups + 255) / 256;
+    blocks = blocks < 1 ? 1 : (blocks > 4096 ? 4096 : blocks);
+    hipLaunchKernelGGL(k_slab_import, dim3(blocks), dim3(256), 0, s, pb, recv, n);
 }
 
 /* ------------------------------------------------------------------ */

@@ -38,6 +38,60 @@ def local_rows(H, rank, world):
     return (H - rank + world - 1) // world if H > rank else 0
 
 
+SLAB_BINS = 1024
+
+
+def slab_hist_words(nb):
+    """uint32 words of one rank's orx_ppm_slab_histogram output: [2][3][nb] counts + its AABB"""
+    return 6 * nb + 6
+
+
+def split_slab_hists(words, world, nb):
+    """all-gathered histogram words -> (counts uint32[world][2][3][nb], the AABB of every rank's
+    photons: uint32[6] ordered words, include/orx.h orx_ppm_slab_import's photon_box)"""
+    w = np.ascontiguousarray(words).view(np.uint32).reshape(world, 6 * nb + 6)
+    box = np.concatenate([w[:, 6 * nb:6 * nb + 3].min(0), w[:, 6 * nb + 3:].max(0)]).astype(np.uint32)
+    return w[:, :6 * nb].reshape(world, 2, 3, nb), box
+
+
+def slab_plan(hists, world, w_gather=0.6, w_photon=0.25, w_pixel=0.15):
+    """The slab partition of one iteration (include/orx.h orx_set_slab_partition), computed on
+    every rank from the all-gathered histograms, identically (float64 numpy on identical inputs).
+
+    hists: [world][2][3][nb] counts (uint32): each rank's valid deposits and own non-specular hit
+    points per bin of each axis of the scene AABB.  The cost of a bin mixes the gather (hit points
+    x photons: a hit point gathers the photons near it), the grid build (photons) and the per-pixel
+    work (hit points), each normalised to sum 1.  On each axis every bin goes to the rank whose
+    share of the cumulative cost holds the bin's midpoint (contiguous slabs, ascending ranks); the
+    axis with the smallest largest-slab cost wins (ties: the lower axis).
+    Returns (axis, bin_dest uint8[nb], counts int64[world][world]: photons rank s sends to rank d)."""
+    h = np.asarray(hists, dtype=np.float64).reshape(world, 2, 3, -1)
+    nb = h.shape[-1]
+    ph, hp = h[:, 0].sum(0), h[:, 1].sum(0)
+    best = None
+    for a in range(3):
+        g = ph[a] * hp[a]
+        w = np.zeros(nb)
+        for part, weight in ((g, w_gather), (ph[a], w_photon), (hp[a], w_pixel)):
+            tot = part.sum()
+            if tot > 0:
+                w += weight * part / tot
+        total = w.sum()
+        if total > 0:
+            mid = np.cumsum(w) - 0.5 * w
+            dest = np.minimum(np.floor(mid * world / total), world - 1).astype(np.int64)
+        else:
+            dest = np.minimum(np.arange(nb) * world // nb, world - 1)
+        cost = np.bincount(dest, weights=w, minlength=world).max() if total > 0 else 0.0
+        if best is None or cost < best[0]:
+            best = (cost, a, dest)
+    _, axis, dest = best
+    counts = np.zeros((world, world), np.int64)
+    for src in range(world):
+        counts[src] = np.bincount(dest, weights=h[src, 0, axis], minlength=world).astype(np.int64)
+    return axis, dest.astype(np.uint8), counts
+
+
 def assemble_rows(blocks, W, H, world):
     """blocks[g]: [max_rows, W, 3] of rank g (local row j = global row g + j*world)."""
     img = np.zeros((H, W, 3), np.float32)
@@ -51,11 +105,22 @@ class ShardedPPM:
     """Runs the 5-step sharded iteration for any backend exposing
     local_passes / export_hitpoints / gather_external / finish / alloc."""
 
-    def __init__(self, backend, dist, world, rank, W, H, pipeline=False):
+    def __init__(self, backend, dist, world, rank, W, H, pipeline=False, slab=False):
         self.b, self.dist, self.world, self.rank, self.W, self.H = backend, dist, world, rank, W, H
         self.max_rows = (H + world - 1) // world
         self.gloo = dist.get_backend() == "gloo"
         self.pipe = pipeline and not self.gloo and hasattr(backend, "enable_pipeline")
+        self.slab = slab
+        if slab:
+            # spatial photon partition: each rank gathers against the photons of its slab
+            backend.enable_slab()
+            s_local, s_global = backend.slot_capacity()
+            self.nb = SLAB_BINS
+            self.hist = backend.alloc_i32(slab_hist_words(self.nb))
+            self.hists = backend.alloc_i32(world * slab_hist_words(self.nb))
+            self.send = backend.alloc(9 * s_local + 9)
+            self.recv = backend.alloc(9 * s_global + 9)
+            self.last_plan = None
         nsets = 2 if self.pipe else 1
         self.sets = [(backend.alloc(self.max_rows * W * 10),             # own hitpoints, 40 B/px as float32
                       backend.alloc(world * self.max_rows * W * 10),     # all hitpoints
@@ -67,8 +132,29 @@ class ShardedPPM:
         if self.pipe:
             backend.enable_pipeline()
 
+    def slab_exchange(self):
+        """histograms -> plan (host) -> pack -> all-to-all of the photon records -> import + grid"""
+        b, d, world, rank = self.b, self.dist, self.world, self.rank
+        b.slab_histogram(self.hist, self.nb)
+        if self.gloo:
+            d.all_gather(list(self.hists.chunk(world)), self.hist)
+        else:
+            d.all_gather_into_tensor(self.hists, self.hist)
+        hists, box = split_slab_hists(self.hists.cpu().numpy(), world, self.nb)
+        axis, bin_dest, counts = slab_plan(hists, world)
+        send_n, recv_n = counts[rank], counts[:, rank]
+        base = np.concatenate([[0], np.cumsum(send_n)[:-1]]).astype(np.uint32)
+        ns, nr = int(send_n.sum()), int(recv_n.sum())
+        b.slab_pack(bin_dest, self.nb, axis, base, ns, self.send)
+        recv = self.recv[:9 * nr]
+        d.all_to_all_single(recv, self.send[:9 * ns], (9 * recv_n).tolist(), (9 * send_n).tolist())
+        b.slab_import(recv, nr, box)
+        self.last_plan = (axis, bin_dest, counts)
+
     def iteration(self, it, local_it, radius, request):
         d = self.dist
+        if self.slab:
+            return self._iteration_slab(it, local_it, radius, request)
         if self.pipe:
             # iteration i's gather, reduce-scatter and output on the side stream while the next
             # iteration's eye, photon and grid passes run on the compute stream (buffer sets
@@ -103,6 +189,38 @@ class ShardedPPM:
             work.wait()
         self.b.gather_external(self.hp_all, self.world, self.ind_partial)
         if self.gloo:  # gloo has no reduce_scatter: all_reduce + own block
+            d.all_reduce(self.ind_partial)
+            blk = self.max_rows * self.W * 3
+            self.ind_local.copy_(self.ind_partial[self.rank * blk:(self.rank + 1) * blk])
+        else:
+            d.reduce_scatter_tensor(self.ind_local, self.ind_partial)
+        self.b.finish(self.ind_local)
+
+    def _iteration_slab(self, it, local_it, radius, request):
+        d = self.dist
+        if self.pipe:
+            hp_local, hp_all, ind_partial, ind_local = self.sets[self.k]
+            self.k ^= 1
+            self.b.local_eye(it, local_it, radius, request)
+            self.b.export_hitpoints(hp_local)
+            work = d.all_gather_into_tensor(hp_all, hp_local, async_op=True)
+            self.b.local_photon_trace()
+            self.slab_exchange()
+            with self.b.torch.cuda.stream(self.b.side):
+                work.wait()
+                self.b.gather_external(hp_all, self.world, ind_partial)
+                d.reduce_scatter_tensor(ind_local, ind_partial)
+                self.b.finish(ind_local)
+            return
+        self.b.local_trace(it, local_it, radius, request)
+        self.b.export_hitpoints(self.hp_local)
+        if self.gloo:
+            d.all_gather(list(self.hp_all.chunk(self.world)), self.hp_local)
+        else:
+            d.all_gather_into_tensor(self.hp_all, self.hp_local)
+        self.slab_exchange()
+        self.b.gather_external(self.hp_all, self.world, self.ind_partial)
+        if self.gloo:
             d.all_reduce(self.ind_partial)
             blk = self.max_rows * self.W * 3
             self.ind_local.copy_(self.ind_partial[self.rank * blk:(self.rank + 1) * blk])
@@ -168,8 +286,9 @@ class ShardedPT:
 class DeviceShard:
     """liborx.so backend: buffers are torch device tensors, kernels run on torch's current stream."""
 
-    def __init__(self, renderer, torch, device):
+    def __init__(self, renderer, torch, device, rank_world=(0, 1)):
         self.r, self.torch, self.device = renderer, torch, device
+        self.rank_world = rank_world
         lib = renderer._lib
         for name, args, res in (
             ("orx_set_stream", [C.c_void_p, C.c_void_p, C.c_int], C.c_int),
@@ -183,6 +302,13 @@ class DeviceShard:
             ("orx_vcm_local_light", [C.c_void_p, C.c_uint64, C.c_uint64, C.c_float, C.c_void_p], C.c_int),
             ("orx_export_vcm_splats", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
             ("orx_vcm_finish", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
+            ("orx_set_slab_partition", [C.c_void_p, C.c_int], C.c_int),
+            ("orx_ppm_local_trace", [C.c_void_p, C.c_uint64, C.c_uint64, C.c_float, C.c_void_p], C.c_int),
+            ("orx_ppm_local_photon_trace", [C.c_void_p], C.c_int),
+            ("orx_ppm_slab_histogram", [C.c_void_p, C.c_void_p, C.c_uint32], C.c_int),
+            ("orx_ppm_slab_pack", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64,
+                                   C.c_void_p], C.c_int),
+            ("orx_ppm_slab_import", [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p], C.c_int),
         ):
             f = getattr(lib, name)
             f.argtypes, f.restype = args, res
@@ -206,8 +332,43 @@ class DeviceShard:
     def alloc(self, nfloat):
         return self.torch.zeros(nfloat, dtype=self.torch.float32, device=self.device)
 
+    def alloc_i32(self, n):
+        return self.torch.zeros(n, dtype=self.torch.int32, device=self.device)
+
     def local_passes(self, it, local_it, radius, request):
         self.r._check(self.lib.orx_ppm_local_passes(self.r._h, it, local_it, radius, C.byref(request)))
+
+    # -- slab mode (orx_set_slab_partition) --
+    def enable_slab(self):
+        self.r._check(self.lib.orx_set_slab_partition(self.r._h, 1))
+
+    def slot_capacity(self):
+        """(own deposit slots, global deposit slots): the send and receive capacities in photons"""
+        cfg = self.r._cfg
+        rank, world = self.rank_world
+        prows = local_rows(cfg.photon_launch_height, rank, world)
+        return (cfg.photon_launch_width * prows * cfg.max_photon_deposits,
+                cfg.photon_launch_width * cfg.photon_launch_height * cfg.max_photon_deposits)
+
+    def local_trace(self, it, local_it, radius, request):
+        self.r._check(self.lib.orx_ppm_local_trace(self.r._h, it, local_it, radius, C.byref(request)))
+
+    def local_photon_trace(self):
+        self.r._check(self.lib.orx_ppm_local_photon_trace(self.r._h))
+
+    def slab_histogram(self, hist, nb):
+        self.r._check(self.lib.orx_ppm_slab_histogram(self.r._h, C.c_void_p(hist.data_ptr()), nb))
+
+    def slab_pack(self, bin_dest, nb, axis, base, n_records, send):
+        bd = np.ascontiguousarray(bin_dest, np.uint8)
+        bs = np.ascontiguousarray(base, np.uint32)
+        self.r._check(self.lib.orx_ppm_slab_pack(self.r._h, bd.ctypes.data, nb, axis, bs.ctypes.data, n_records,
+                                                 C.c_void_p(send.data_ptr())))
+
+    def slab_import(self, recv, n_records, box=None):
+        bx = None if box is None else np.ascontiguousarray(box, np.uint32)
+        self.r._check(self.lib.orx_ppm_slab_import(self.r._h, C.c_void_p(recv.data_ptr()), n_records,
+                                                   None if bx is None else bx.ctypes.data))
 
     def local_eye(self, it, local_it, radius, request):
         self.r._check(self.lib.orx_ppm_local_eye(self.r._h, it, local_it, radius, C.byref(request)))
@@ -255,7 +416,7 @@ def device_shard_factory(cfg, rank, world, local_rank, scene):
     r.initialize(local_rank)
     r.set_shard(rank, world)
     r.initScene(scene)
-    return DeviceShard(r, torch, torch.device("cuda", local_rank))
+    return DeviceShard(r, torch, torch.device("cuda", local_rank), (rank, world))
 
 
 def _resolve_factory():
@@ -322,7 +483,9 @@ def bench_main(args, metric, cpu_baseline=None):
     if vcm or pt:
         sharded = (ShardedVCM if vcm else ShardedPT)(backend, dist, world, rank, W, H)
     else:
-        sharded = ShardedPPM(backend, dist, world, rank, W, H, pipeline=os.environ.get("ORX_PIPELINE", "1") != "0")
+        slab = getattr(args, "partition", "slab") == "slab" and world > 1
+        sharded = ShardedPPM(backend, dist, world, rank, W, H, pipeline=os.environ.get("ORX_PIPELINE", "1") != "0",
+                             slab=slab)
     it = 0
     for _ in range(max(1, args.warmup)):
         sharded.iteration(it, it, radius, req)
@@ -394,8 +557,11 @@ def bench_main(args, metric, cpu_baseline=None):
                         "baseline_config": getattr(args, "config", None),
                         "scene": scene.name, "width": W, "height": H, "photons_per_iteration": P * PH,
                         "paths_per_iteration": paths,
-                        "parallelism": f"row-interleaved RNG/pixel/photon ownership x{world}, "
-                                       "RCCL all_gather(hitpoints) + reduce_scatter(indirect)"}),
+                        "parallelism": (f"row-interleaved RNG/pixel/photon ownership x{world}; "
+                                        + ("spatial photon slabs: RCCL all_gather(hitpoints, histograms) + "
+                                           "all_to_all(photons) + reduce_scatter(indirect)"
+                                           if getattr(sharded, "slab", False) else
+                                           "RCCL all_gather(hitpoints) + reduce_scatter(indirect)"))}),
             "roofline": roof,
             "passes": {k: round(v, 4) for k, v in per_pass.items()},
             "dominant_pass": dominant,

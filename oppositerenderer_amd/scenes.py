@@ -193,6 +193,7 @@ class Scene:
         self.aabb_min = _v(0, 0, 0)
         self.aabb_max = _v(0, 0, 0)
         self.default_camera: Camera | None = None
+        self.media: list[np.ndarray] = []  # [min xyz, max xyz, sigma_s, sigma_a] per medium box
         self._keep = []
 
     def add_material(self, m: Material) -> int:
@@ -217,6 +218,12 @@ class Scene:
         self.texcoords = f(texcoords)
         self.tangents = f(tangents)
         self.bitangents = f(bitangents)
+
+    def add_medium_box(self, box_min, box_max, sigma_s, sigma_a):
+        """AABInstance(ParticipatingMedium(sigma_s, sigma_a), AAB(min, max)) (Scene.cpp:337-350,
+        Cornell.cpp:167-172): rendered when orx_config.enable_media is set."""
+        self.media.append(np.array([*np.float32(box_min), *np.float32(box_max), f32(sigma_s), f32(sigma_a)],
+                                   dtype=np.float32))
 
     def add_texture(self, rgba, normal_rgba=None) -> int:
         chk = lambda a: None if a is None else np.ascontiguousarray(a, dtype=np.uint8).reshape(
@@ -282,6 +289,9 @@ class Scene:
         keep.append(texs)
         s.n_textures = len(self.textures)
         s.textures = C.cast(texs, C.POINTER(_abi.OrxTexture))
+        med = np.array(self.media, dtype=np.float32).reshape(-1, 8)
+        s.n_media = len(med)
+        s.media = arr(med, C.c_float)
         self._keep = keep
         return s
 
@@ -304,6 +314,21 @@ def cornell() -> Scene:
     emitter = sc.add_material(DiffuseEmitter(light.power, 1.0, light.inverse_area))
     sc.add_parallelogram(light.position, light.v1, light.v2, emitter)
     sc.default_camera = Camera(_v(278.0, 273.0, -850.0), _v(278.0, 273.0, 0.0), _v(0.0, 1.0, 0.0), 35.0, 35.0, 0.0)
+    return sc
+
+
+def cornell_medium(sigma_s=0.001, sigma_a=0.0, glass_sphere=True) -> Scene:
+    """Cornell with a participating-medium box: the test block of Cornell.cpp:165-173 (compiled
+    in under ENABLE_PARTICIPATING_MEDIA): ParticipatingMedium(0.001, 0.00) on
+    AAB(Vector3(-1), Vector3(556.0f, 548.85f, 559.2f) - 1) and a glass sphere Sphere((250, 370, 250), 50)
+    of Glass(1.5, 1) (Cornell.cpp:161).  The camera (z = -850) looks in through the box's open
+    front, the light (y = 548.7999) sits just above its top face (547.85)."""
+    sc = cornell()
+    sc.name = "CornellMedium"
+    sc.add_medium_box((-1.0, -1.0, -1.0), (555.0, f32(548.85) - f32(1.0), f32(559.2) - f32(1.0)), sigma_s, sigma_a)
+    if glass_sphere:
+        glass = sc.add_material(Glass(1.5, 1.0, 1.0))
+        sc.add_sphere((250.0, 370.0, 250.0), 50.0, glass)
     return sc
 
 
@@ -414,6 +439,7 @@ def scene_by_name(name: str) -> Scene:
     K = CornellSmallConfig
     table = {
         "Cornell": lambda: cornell(),
+        "CornellMedium": lambda: cornell_medium(),
         "CornellSmall": lambda: cornell_small(K.Default, "CornellSmall"),
         "CornellSmallNoBlocks": lambda: cornell_small(K.LightArea, "CornellSmallNoBlocks"),
         "CornellSmallLargeSphere": lambda: cornell_small(

@@ -1226,19 +1226,47 @@ static float smallest_possible_cell_size(v3 ext, uint32_t maxGridSize) {
 }
 
 /* createUniformGridPhotonMap (OptixRenderer_SpatialHash.cu:209-282) */
+static orx_status ppm_build_grid_n(orc_renderer* r, size_t S, const uint32_t* box);
 static orx_status ppm_build_grid(orc_renderer* r) {
-    const size_t S = (size_t)r->cfg.photon_launch_width * r->prows * r->cfg.max_photon_deposits;
-    photon_t* ph = r->photons;
-    /* getPhotonsBoundingBox: transform_reduce over valid photons (:123-128) */
-    int any = 0;
-    v3 lo = ph[0].position, hi = ph[0].position;
+    return ppm_build_grid_n(r, (size_t)r->cfg.photon_launch_width * r->prows * r->cfg.max_photon_deposits, NULL);
+}
+/* order-preserving float <-> uint32 (the slab mode's AABB words, include/orx.h) */
+static inline uint32_t f2ord(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+static inline float ord2f(uint32_t u) {
+    uint32_t v = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+    float f;
+    memcpy(&f, &v, 4);
+    return f;
+}
+/* AABB of the valid photons among the first S entries, as ordered words (empty: ~0, 0) */
+static void photon_box_words(const photon_t* ph, size_t S, uint32_t w[6]) {
+    w[0] = w[1] = w[2] = 0xffffffffu;
+    w[3] = w[4] = w[5] = 0u;
     for (size_t i = 0; i < S; i++) {
-        if (fmax3(ph[i].power) > 0) {
-            if (!any) { lo = hi = ph[i].position; any = 1; }
-            else { lo = vmin(lo, ph[i].position); hi = vmax(hi, ph[i].position); }
+        if (!(fmax3(ph[i].power) > 0)) continue;
+        const float c[3] = {ph[i].position.x, ph[i].position.y, ph[i].position.z};
+        for (int k = 0; k < 3; k++) {
+            const uint32_t o = f2ord(c[k]);
+            if (o < w[k]) w[k] = o;
+            if (o > w[k + 3]) w[k + 3] = o;
         }
     }
-    if (!any) { lo = mk1(0); hi = mk1(0); }
+}
+/* over the first S entries of r->photons; box: the grid bounds as ordered words (slab mode: all
+ * ranks' photons), NULL: the AABB of these photons */
+static orx_status ppm_build_grid_n(orc_renderer* r, size_t S, const uint32_t* box) {
+    photon_t* ph = r->photons;
+    /* getPhotonsBoundingBox: transform_reduce over valid photons (:123-128) */
+    uint32_t w[6];
+    if (box) memcpy(w, box, sizeof w);
+    else photon_box_words(ph, S, w);
+    const int any = w[0] != 0xffffffffu;
+    v3 lo = any ? mk(ord2f(w[0]), ord2f(w[1]), ord2f(w[2])) : mk1(0);
+    v3 hi = any ? mk(ord2f(w[3]), ord2f(w[4]), ord2f(w[5])) : mk1(0);
     /* padAABB (:135-141) */
     lo = sub_s(lo, 0.0000001f);
     hi = mk(hi.x + 0.0000001f, hi.y + 0.0000001f, hi.z + 0.0000001f);
@@ -1895,6 +1923,89 @@ orx_status orc_ppm_local_passes(orc_renderer* r, uint64_t iter, uint64_t local, 
     r->last_local = local;
     return ORX_OK;
 }
+/* Slab mode of the sharded gather (include/orx.h orx_set_slab_partition): the same phases on the
+ * oracle's photon array.  A photon is valid if fmaxf(power) > 0 (the grid's own test). */
+orx_status orc_ppm_local_trace(orc_renderer* r, uint64_t iter, uint64_t local, float ppmRadius, const orx_request* det) {
+    (void)iter;
+    if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
+    orx_status s0 = begin_iteration(r, local, det);
+    if (s0 != ORX_OK) return s0;
+    cam_t cam = camera_setup(&det->camera);
+    ppm_eye_pass(r, &cam);
+    ppm_photon_pass(r);
+    r->last_radius = ppmRadius;
+    r->last_radius2 = ppmRadius * ppmRadius;
+    r->last_local = local;
+    return ORX_OK;
+}
+static inline uint32_t slab_bin(const orc_renderer* r, v3 p, uint32_t a, uint32_t nb) {
+    const float lo = a == 0 ? r->aabb_min.x : a == 1 ? r->aabb_min.y : r->aabb_min.z;
+    const float hi = a == 0 ? r->aabb_max.x : a == 1 ? r->aabb_max.y : r->aabb_max.z;
+    const float ext = hi - lo, inv = ext > 0.f ? (float)nb / ext : 0.f;
+    const float v = a == 0 ? p.x : a == 1 ? p.y : p.z;
+    const int32_t b = orx_f2i_sat(orx_floorf((v - lo) * inv));
+    return b < 0 ? 0u : (b >= (int32_t)nb ? nb - 1u : (uint32_t)b);
+}
+static size_t local_slots(const orc_renderer* r) {
+    return (size_t)r->cfg.photon_launch_width * r->prows * r->cfg.max_photon_deposits;
+}
+orx_status orc_ppm_slab_histogram(orc_renderer* r, uint32_t* hist, uint32_t nb) {
+    if (!r || !hist || nb == 0) return ORX_ERR_INVALID_ARGUMENT;
+    memset(hist, 0, (size_t)6 * nb * 4);
+    const size_t S = local_slots(r);
+    photon_box_words(r->photons, S, hist + 6 * (size_t)nb);
+    for (size_t i = 0; i < S; i++) {
+        if (!(fmax3(r->photons[i].power) > 0)) continue;
+        for (uint32_t a = 0; a < 3; a++) hist[a * nb + slab_bin(r, r->photons[i].position, a, nb)]++;
+    }
+    for (size_t i = 0; i < (size_t)r->rows * r->W; i++) {
+        if (!(r->hp[i].flags & PRD_HIT_NON_SPECULAR)) continue;
+        for (uint32_t a = 0; a < 3; a++) hist[(3 + a) * nb + slab_bin(r, r->hp[i].position, a, nb)]++;
+    }
+    return ORX_OK;
+}
+orx_status orc_ppm_slab_pack(orc_renderer* r, const uint8_t* bin_dest, uint32_t nb, uint32_t axis,
+                             const uint32_t* dest_base, uint64_t send_records, float* send) {
+    if (!r || !bin_dest || !dest_base || !send || nb == 0 || axis > 2) return ORX_ERR_INVALID_ARGUMENT;
+    uint32_t cur[256];
+    if (r->world > 256) return ORX_ERR_UNSUPPORTED;
+    memcpy(cur, dest_base, (size_t)r->world * 4);
+    const size_t S = local_slots(r);
+    for (size_t i = 0; i < S; i++) {
+        const photon_t* p = &r->photons[i];
+        if (!(fmax3(p->power) > 0)) continue;
+        const uint32_t d = bin_dest[slab_bin(r, p->position, axis, nb)];
+        if (d >= r->world || cur[d] >= send_records) return fail(r, ORX_ERR_INVALID_ARGUMENT, "slab plan overflows the send buffer");
+        float* w = send + 9 * (size_t)cur[d]++;
+        w[0] = p->position.x; w[1] = p->position.y; w[2] = p->position.z;
+        w[3] = p->direction.x; w[4] = p->direction.y; w[5] = p->direction.z;
+        w[6] = p->power.x; w[7] = p->power.y; w[8] = p->power.z;
+    }
+    return ORX_OK;
+}
+orx_status orc_ppm_slab_import(orc_renderer* r, const float* recv, uint64_t n, const uint32_t* box) {
+    if (!r || (!recv && n)) return ORX_ERR_INVALID_ARGUMENT;
+    const size_t S = local_slots(r);
+    const size_t need = n > S ? n : S;
+    if (need > S) { /* realloc keeps the contents; the own photon pass uses the first S entries */
+        photon_t* a = (photon_t*)realloc(r->photons, need * sizeof(photon_t));
+        if (a) r->photons = a;
+        photon_t* b = (photon_t*)realloc(r->sort_tmp, need * sizeof(photon_t));
+        if (b) r->sort_tmp = b;
+        uint32_t* k = (uint32_t*)realloc(r->keys, need * 4);
+        if (k) r->keys = k;
+        if (!a || !b || !k) return fail(r, ORX_ERR_OUT_OF_MEMORY, "oracle: out of memory");
+    }
+    for (size_t i = 0; i < n; i++) {
+        const float* w = recv + 9 * i;
+        photon_t* p = &r->photons[i];
+        p->position = mk(w[0], w[1], w[2]);
+        p->direction = mk(w[3], w[4], w[5]);
+        p->power = mk(w[6], w[7], w[8]);
+    }
+    return ppm_build_grid_n(r, (size_t)n, box);
+}
+
 orx_status orc_export_hitpoints(orc_renderer* r, void* dst, size_t bytes) {
     const size_t plane = (size_t)r->max_rows * r->W;
     if (!dst || bytes < plane * 40) return ORX_ERR_INVALID_ARGUMENT;

@@ -111,6 +111,11 @@ class OracleShard:
             ("orc_vcm_local_light", [C.c_void_p, C.c_uint64, C.c_uint64, C.c_float, C.c_void_p], C.c_int),
             ("orc_export_vcm_splats", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
             ("orc_vcm_finish", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
+            ("orc_ppm_local_trace", [C.c_void_p, C.c_uint64, C.c_uint64, C.c_float, C.c_void_p], C.c_int),
+            ("orc_ppm_slab_histogram", [C.c_void_p, C.c_void_p, C.c_uint32], C.c_int),
+            ("orc_ppm_slab_pack", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64,
+                                   C.c_void_p], C.c_int),
+            ("orc_ppm_slab_import", [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p], C.c_int),
         ):
             f = getattr(lib, name)
             f.argtypes, f.restype = args, res
@@ -118,6 +123,39 @@ class OracleShard:
 
     def set_shard(self, rank, world):
         self.r._check(self.lib.orc_set_shard(self.r.h, rank, world))
+        self.rank_world = (rank, world)
+
+    # -- slab mode (orx_set_slab_partition's phases on the oracle) --
+    def enable_slab(self):
+        pass
+
+    def slot_capacity(self):
+        cfg = self.r.cfg
+        rank, world = self.rank_world
+        prows = (cfg.photon_launch_height - rank + world - 1) // world if cfg.photon_launch_height > rank else 0
+        return (cfg.photon_launch_width * prows * cfg.max_photon_deposits,
+                cfg.photon_launch_width * cfg.photon_launch_height * cfg.max_photon_deposits)
+
+    def alloc_i32(self, n):
+        return self.torch.zeros(n, dtype=self.torch.int32)
+
+    def local_trace(self, it, local_it, radius, request):
+        self.r.width, self.r.height = request.width, request.height
+        self.r._check(self.lib.orc_ppm_local_trace(self.r.h, it, local_it, radius, C.byref(request)))
+
+    def slab_histogram(self, hist, nb):
+        self.r._check(self.lib.orc_ppm_slab_histogram(self.r.h, C.c_void_p(hist.data_ptr()), nb))
+
+    def slab_pack(self, bin_dest, nb, axis, base, n_records, send):
+        bd = np.ascontiguousarray(bin_dest, np.uint8)
+        bs = np.ascontiguousarray(base, np.uint32)
+        self.r._check(self.lib.orc_ppm_slab_pack(self.r.h, bd.ctypes.data, nb, axis, bs.ctypes.data, n_records,
+                                                 C.c_void_p(send.data_ptr())))
+
+    def slab_import(self, recv, n_records, box=None):
+        bx = None if box is None else np.ascontiguousarray(box, np.uint32)
+        self.r._check(self.lib.orc_ppm_slab_import(self.r.h, C.c_void_p(recv.data_ptr()), n_records,
+                                                   None if bx is None else bx.ctypes.data))
 
     def alloc(self, nfloat):
         return self.torch.zeros(nfloat, dtype=self.torch.float32)

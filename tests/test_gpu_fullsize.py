@@ -171,8 +171,10 @@ def test_configs4_conference4k_ppm_single_and_8_shards():
        per-cell photon multisets, direct, visit counters bit-exact; indirect rel-L2 <= 1e-5).
     2. The same frame through eight row-interleaved shards in the 8-GPU bench's strong-scaling
        partition (each shard: 1/8 of the pixel rows, photon launch rows and RNG rows; cell-order
-       photon layout and the per-lane gather that world >= 8 selects), exchanging hit points and
-       partial indirect through torch ops, against the oracle's output: rel-L2 <= 1e-5."""
+       photon layout and the per-lane gather that world >= 8 selects), exchanging hit points,
+       photons (slab mode, the bench's default) and partial indirect through torch ops
+       (tests/shard_emul.py), against the oracle's output: rel-L2 <= 1e-5, with spatial photon
+       slabs and with the row partition."""
     import torch
 
     from oppositerenderer_amd import multigpu
@@ -193,38 +195,16 @@ def test_configs4_conference4k_ppm_single_and_8_shards():
     del g
     torch.cuda.empty_cache()
 
+    import shard_emul
+
     world = 8
-    dev = torch.device("cuda", 0)
     req = det.to_abi()
-    shards = []
-    for rank in range(world):
-        r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P))
-        r.initialize(0)
-        r.set_shard(rank, world)
-        r.initScene(scene)
-        shards.append(multigpu.DeviceShard(r, torch, dev))
-    mr = (H + world - 1) // world
-    for b in shards:
-        b.local_passes(0, 0, radius, req)
-    hps = []
-    for b in shards:
-        t = b.alloc(mr * W * 10)
-        b.export_hitpoints(t)
-        hps.append(t)
-    hp_all = torch.cat(hps)
-    del hps
-    total = shards[0].alloc(world * mr * W * 3)
-    part = shards[0].alloc(world * mr * W * 3)
-    for b in shards:
-        b.gather_external(hp_all, world, part)
-        total += part
-    blk = mr * W * 3
-    for k, b in enumerate(shards):
-        b.finish(total[k * blk:(k + 1) * blk].contiguous())
-    torch.cuda.synchronize()
-    blocks = [b.output_local_tensor(mr).cpu().numpy().reshape(mr, W, 3) for b in shards]
-    got = multigpu.assemble_rows(blocks, W, H, world)
-    assert np.isfinite(got).all()
-    assert rel_l2(got, o) < 1e-5, rel_l2(got, o)
-    for b in shards:
-        b.r.destroy()
+    for slab in (True, False):  # the bench's default spatial slabs, and the row partition
+        shards = shard_emul.make_shards(scene, world, P, P, slab=slab)
+        got, plans = shard_emul.run_iterations(shards, scene, W, H, req, 1, slab=slab)
+        assert np.isfinite(got).all()
+        assert rel_l2(got, o) < 1e-5, (slab, rel_l2(got, o))
+        for b in shards:
+            b.r.destroy()
+        del shards, got
+        torch.cuda.empty_cache()

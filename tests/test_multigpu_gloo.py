@@ -39,7 +39,7 @@ def request(scene, W, H, method=_abi.PROGRESSIVE_PHOTON_MAPPING):
 
 
 def worker(rank, world, port, out_path, W, H, P, iters, method=_abi.PROGRESSIVE_PHOTON_MAPPING, photon_map=0,
-           PH=None):
+           PH=None, slab=False):
     """PH: global photon launch height (default P * world: every rank a full P x P batch)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -54,7 +54,7 @@ def worker(rank, world, port, out_path, W, H, P, iters, method=_abi.PROGRESSIVE_
     b.set_shard(rank, world)
     cls = {_abi.VCM_BIDIRECTIONAL_PATH_TRACING: multigpu.ShardedVCM,
            _abi.PATH_TRACING: multigpu.ShardedPT}.get(method, multigpu.ShardedPPM)
-    sh = cls(b, dist, world, rank, W, H)
+    sh = cls(b, dist, world, rank, W, H, slab=slab) if slab else cls(b, dist, world, rank, W, H)
     req = request(scene, W, H, method)
     radius = scene.initial_ppm_radius()
     for it in range(iters):
@@ -94,6 +94,52 @@ def test_sharded_ppm_matches_single(world, W, H, photon_map, scaling):
     err = np.sqrt(((got.astype(np.float64) - ref) ** 2).sum() / (ref.astype(np.float64) ** 2).sum())
     assert err < 1e-5, err
     assert got.mean() > 0
+
+
+@pytest.mark.parametrize("world,W,H,PH", [(2, 48, 40, 41), (3, 40, 37, 48), (4, 40, 37, 41)])
+def test_sharded_ppm_slab_partition_matches_single(world, W, H, PH):
+    """Slab mode (include/orx.h orx_set_slab_partition): every rank traces its launch rows, the
+    photons are redistributed by a spatial slab of one scene axis (histograms all-gathered, the
+    plan of multigpu.slab_plan, photon records all-to-all), each rank grids its slab's photons
+    and gathers every hit point against them; the sum is the single renderer's image."""
+    P, iters = 48, 2
+    out = os.path.join(tempfile.mkdtemp(), "img.npy")
+    mp.spawn(worker, args=(world, free_port(), out, W, H, P, iters, _abi.PROGRESSIVE_PHOTON_MAPPING, 0, PH, True),
+             nprocs=world, join=True)
+    got = np.load(out)
+    scene = scenes.cornell()
+    r = oracle_lib.OracleRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=PH))
+    r.init_scene(scene)
+    req = request(scene, W, H)
+    radius = scene.initial_ppm_radius()
+    for it in range(iters):
+        r.render_next_iteration(it, it, radius, req)
+        radius = next_ppm_radius(radius, it)
+    ref = r.output()
+    err = np.sqrt(((got.astype(np.float64) - ref) ** 2).sum() / (ref.astype(np.float64) ** 2).sum())
+    assert err < 1e-5, err
+    assert got.mean() > 0
+
+
+def test_slab_plan_properties():
+    """slab_plan: contiguous ascending slabs, identical on every rank, counts = the photon bins
+    each rank sends, and the chosen axis balances the cost better than the others."""
+    rng = np.random.default_rng(7)
+    world, nb = 4, 64
+    hists = rng.integers(0, 50, size=(world, 2, 3, nb)).astype(np.uint32)
+    hists[:, :, 1, :] = 0
+    hists[:, :, 1, 10] = 1000  # axis 1: everything in one bin, a poor axis to split
+    axis, dest, counts = multigpu.slab_plan(hists, world)
+    assert axis != 1
+    assert np.all(np.diff(dest.astype(int)) >= 0) and dest.max() < world
+    for src in range(world):
+        for d in range(world):
+            assert counts[src, d] == hists[src, 0, axis][dest == d].sum()
+    a2, d2, c2 = multigpu.slab_plan(hists.copy(), world)
+    assert a2 == axis and np.array_equal(d2, dest) and np.array_equal(c2, counts)
+    empty = np.zeros((2, 2, 3, 8), np.uint32)
+    a0, d0, c0 = multigpu.slab_plan(empty, 2)
+    assert c0.sum() == 0 and d0.max() < 2
 
 
 @pytest.mark.parametrize("world,W,H", [(2, 40, 32), (3, 36, 29)])

@@ -32,7 +32,10 @@ def run(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None):
     det = RenderRequestDetails(cam, scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W, H)
     req = det.to_abi()
     gv = int(os.environ.get("MODEL_GATHER_VARIANT", "0"))  # 1: whole cell rows (no sub-rows)
-    r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P, gather_variant=gv))
+    # MODEL_GMAX_DIV=1: the rank's grid gets PHOTON_GRID_MAX_SIZE / N cells (1/N of the photons)
+    gmax = 1000000 // world if os.environ.get("MODEL_GMAX_DIV", "0") != "0" else 1000000
+    r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P, gather_variant=gv,
+                                          photon_grid_max_size=gmax))
     r.initialize(0)
     r.set_shard(0, world)
     r.initScene(scene)
@@ -98,15 +101,111 @@ def run(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None):
     return ms, passes, allgather_mb, rs_mb
 
 
+def run_slab(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None, nb=multigpu.SLAB_BINS):
+    """Slab mode (orx_set_slab_partition): all N shards on the one GPU, each phase of each rank
+    timed on its own (the shards run one after another), the collectives by torch ops and not
+    timed (their volumes are returned).  Per-rank serial time = the slowest rank's sum of phases."""
+    dev = torch.device("cuda", 0)
+    scene = scene or synthetic.synthetic_hall()
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    req = RenderRequestDetails(cam, scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W, H).to_abi()
+    shards = []
+    for rank in range(world):
+        r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P))
+        r.initialize(0)
+        r.set_shard(rank, world)
+        r.initScene(scene)
+        b = multigpu.DeviceShard(r, torch, dev, (rank, world))
+        b.enable_slab()
+        shards.append(b)
+    mr = (H + world - 1) // world
+    hps = [b.alloc(mr * W * 10) for b in shards]
+    hp_all = shards[0].alloc(world * mr * W * 10)
+    part = shards[0].alloc(world * mr * W * 3)
+    names = ("local", "hist_pack", "import_grid", "gather", "finish")
+    tot = [dict.fromkeys(names, 0.0) for _ in range(world)]
+    a2a_mb = 0.0
+    radius = scene.initial_ppm_radius()
+
+    def timed(fn):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1)
+
+    diag = []
+    for it in range(iters):
+        ms = [dict.fromkeys(names, 0.0) for _ in range(world)]
+        hists = []
+        for k, b in enumerate(shards):
+            ms[k]["local"] += timed(lambda: (b.local_trace(it, it, radius, req), b.export_hitpoints(hps[k])))
+            h = b.alloc_i32(multigpu.slab_hist_words(nb))
+            ms[k]["hist_pack"] += timed(lambda: b.slab_histogram(h, nb))
+            hists.append(h)
+        hp_all.copy_(torch.cat(hps))
+        Hh, box = multigpu.split_slab_hists(torch.stack(hists).cpu().numpy(), world, nb)
+        axis, bin_dest, counts = multigpu.slab_plan(Hh, world)
+        sends = []
+        for k, b in enumerate(shards):
+            n = counts[k]
+            base = np.concatenate([[0], np.cumsum(n)[:-1]]).astype(np.uint32)
+            send = b.alloc(9 * int(n.sum()) + 9)
+            ms[k]["hist_pack"] += timed(lambda: b.slab_pack(bin_dest, nb, axis, base, int(n.sum()), send))
+            sends.append((send, base, n))
+        for d, b in enumerate(shards):
+            recv = torch.cat([s_[9 * int(bs[d]):9 * int(bs[d] + n_[d])] for s_, bs, n_ in sends]).contiguous()
+            ms[d]["import_grid"] += timed(lambda: b.slab_import(recv, int(counts[:, d].sum()), box))
+            ms[d]["gather"] += timed(lambda: b.gather_external(hp_all, world, part))
+            if it == iters - 1:
+                # diagnostic: the non-specular hit points whose sphere reaches this rank's photons
+                pr = recv.view(-1, 9)[:, :3]
+                lo, hi = pr.min(0).values, pr.max(0).values
+                A = hp_all.view(world, -1)[:, :mr * W * 4].reshape(-1, 4)
+                ns = (A[:, 3].view(torch.int32) & (1 << 27)) != 0
+                q = A[:, :3]
+                hit = ns & ((q + radius >= lo) & (q - radius <= hi)).all(1)
+                diag.append((d, int(ns.sum()), int(hit.sum()), int(pr.shape[0])))
+            ms[d]["finish"] += timed(lambda: b.finish(part[:mr * W * 3].contiguous()))
+        if it >= warm:
+            for k in range(world):
+                for n_ in names:
+                    tot[k][n_] += ms[k][n_]
+            a2a_mb = (counts.sum() - np.trace(counts)) * 36 / 1e6
+        radius = next_ppm_radius(radius, it)
+    n = iters - warm
+    per_rank = [{k: round(v / n, 3) for k, v in t.items()} for t in tot]
+    slowest = max(range(world), key=lambda k: sum(per_rank[k].values()))
+    for b in shards:
+        b.r.destroy()
+    print("  (rank, NS hit points, gathered, photons):", diag, flush=True)
+    return per_rank, slowest, a2a_mb, int(axis), counts
+
+
 if __name__ == "__main__":
     args = sys.argv[1:]
     conf = 2
+    slab = "--slab" in args
+    args = [a for a in args if a != "--slab"]
     if args[:1] == ["--config"]:
         conf, args = int(args[1]), args[2:]
     worlds = [int(v) for v in args] or [1, 2, 4, 8]
     kw = (dict(W=3840, H=2160, P=4096, iters=4, warm=1, scene=synthetic.synthetic_conference()) if conf == 4
           else {})
     print(f"configs[{conf}]: " + ("conference 3840x2160, 4096^2 photons" if conf == 4 else "hall 1920x1080, 2048^2"))
+    if slab:
+        for n in worlds:
+            if n == 1:
+                ms, passes, ag, rs = run(1, **kw)
+                print(f"N=1: per-rank serial {sum(ms.values()):.3f} ms {ms}", flush=True)
+                continue
+            per_rank, slowest, a2a, axis, counts = run_slab(n, **kw)
+            pr = per_rank[slowest]
+            print(f"N={n} slab: per-rank serial {sum(pr.values()):.3f} ms (slowest rank {slowest}: {pr}) | "
+                  f"rank sums {[round(sum(p.values()), 3) for p in per_rank]} | axis {axis}, photons per rank "
+                  f"{counts.sum(0).tolist()}, all-to-all {a2a:.0f} MB", flush=True)
+        sys.exit(0)
     for n in worlds:
         ms, passes, ag, rs = run(n, **kw)
         print(f"N={n}: per-rank serial {sum(ms.values()):.3f} ms {ms} | all-gather {ag:.0f} MB, "
