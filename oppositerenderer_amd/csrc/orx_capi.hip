@@ -374,6 +374,7 @@ struct orx_renderer {
     bool slab = false;
     size_t S_cap = 0;
     DevBuf d_slabtab, d_slabcur;
+    DevBuf d_tiles; /* slab gather: tile list, count, flags */
     int pipe_mode = -1; /* orx_set_iteration_pipelining: -1 = ORX_PIPELINE env */
     hipStream_t side = nullptr;
     uint32_t pp = 0;
@@ -887,10 +888,13 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_grid.ensure(sizeof(GridParams)));
     /* bucket-sort grid build: at most 2048 buckets of 2^bshift virtual cells
      * (nsub sub-rows per cell row, k_bs_count) */
-    /* sub-row layout on one device; a shard of world >= 2 gathers all W*H hit points against 1/N
-     * of the photons and runs faster on whole cell rows (tools/shard_model.py, hall 1080p:
-     * per-rank gather N=2 1.40 -> 1.32 ms, N=8 0.96 -> 0.90 ms, grid build shorter too) */
-    const bool cell_order = r->cfg.gather_variant == 1 || (r->cfg.gather_variant == 0 && r->world >= 2);
+    /* sub-row layout on one device; a row-partition shard of world >= 2 gathers all W*H hit points
+     * against 1/N of the photons and runs faster on whole cell rows (tools/shard_model.py, hall
+     * 1080p: per-rank gather N=2 1.40 -> 1.32 ms, N=8 0.96 -> 0.90 ms, grid build shorter too);
+     * a slab shard holds the single-device photon density in its cells: sub-rows (configs[4]
+     * N=2 rank 0: 47 ms gather in cell order) */
+    const bool cell_order =
+        r->cfg.gather_variant == 1 || (r->cfg.gather_variant == 0 && r->world >= 2 && !r->slab);
     const uint32_t nsub = cell_order ? 1u : SUBR * SUBR;
     const size_t vmax = (size_t)r->cfg.photon_grid_max_size * nsub;
     uint32_t bshift = 10;
@@ -1755,6 +1759,16 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hp, uint32_t seg
         HIPCHK(r, hipStreamWaitEvent(st, r->ev_grid_done, 0));
     }
     ev_begin_on(r, P_GATHER, st);
+    if (r->slab && r->cfg.photon_map == 0) { /* the tiles with hit points that reach this rank's photons */
+        const size_t ntiles = (size_t)((r->W + 15) / 16) * ((segments * r->max_rows + 15) / 16);
+        HIPCHK(r, r->d_tiles.ensure(ntiles * 5 + 64));
+        uint32_t* list = r->d_tiles.as<uint32_t>();
+        uint32_t* count = list + ntiles;
+        uint8_t* flags = (uint8_t*)(count + 4);
+        launch_gather_tiles(st, gi, r->pb, r->last_consts, flags, list, count);
+        gi.tile_list = list;
+        gi.tile_count = count;
+    }
     if (r->cfg.photon_map == 2) launch_ppm_gather_kd(st, gi, r->pb, r->kd, r->last_consts);
     else launch_ppm_gather(st, gi, r->pb, r->last_consts);
     ev_end_on(r, P_GATHER, st);

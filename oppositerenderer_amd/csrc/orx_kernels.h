@@ -170,6 +170,10 @@ struct GatherIn {
     uint32_t* dbg;      /* [segments*seg_rows*W*2] or NULL */
     uint32_t cull;      /* 1 (slab mode): a hit point whose sphere misses the AABB of the grid's photons
                          * gathers nothing (its window would only clamp onto cells without them) */
+    /* slab mode: the 16x16-pixel tiles that gather here, ascending (tile_list[0..*tile_count)),
+     * dealt to the XCDs in contiguous bands; NULL: every tile */
+    const uint32_t* tile_list = nullptr;
+    const uint32_t* tile_count = nullptr;
     uint32_t visits;    /* 1: count the reference's per-pixel visits (IndirectRadianceEstimation.cu:113/124)
                          * into dbg and the stats; 0 for the sharded gather, which has no per-pixel
                          * debug buffers and whose rank-local counts are not the reference's
@@ -187,6 +191,10 @@ __device__ __forceinline__ uint32_t gather_row(const GatherIn& gi, uint32_t y) {
 }
 /* 8x8-pixel wave tiles; the wave-union kernel, or the per-lane kernel for gathers of >= 8 segments */
 void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c);
+/* slab mode: flags[tile] / the ascending list of the tiles with a hit point that gathers here
+ * (the others' indirect is zeroed here); ntiles of the gather's 16x16 tiling */
+void launch_gather_tiles(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, uint8_t* flags,
+                         uint32_t* list, uint32_t* count);
 /* slab mode (sharded PPM with a spatial photon partition): nb bins per axis over the scene AABB */
 struct SlabBins {
     float lo[3];

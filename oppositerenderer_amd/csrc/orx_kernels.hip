@@ -782,6 +782,23 @@ __device__ __forceinline__ HpRef hp_ref(const GatherIn& gi, uint32_t j, uint32_t
     return r;
 }
 
+/* XCD-aware tile order: block b runs on XCD b % 8; XCD k takes tiles [k per, (k+1) per) of the
+ * image's tiles, or of the slab mode's list of tiles that gather here (a band of the image
+ * would otherwise leave most XCDs idle when the rank's hit points cluster in the image).
+ * false: no tile for this block. */
+__device__ __forceinline__ bool gather_tile(const GatherIn& gi, uint32_t ntiles, uint32_t& tile) {
+    if (!gi.tile_list) {
+        const uint32_t per = (ntiles + 7) / 8;
+        tile = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+        return true;
+    }
+    const uint32_t n = *gi.tile_count, per = (n + 7) / 8;
+    const uint32_t i = blockIdx.x >> 3, k = (blockIdx.x & 7u) * per + i;
+    if (i >= per || k >= n) return false;
+    tile = gi.tile_list[k];
+    return true;
+}
+
 /* Per-pixel gather, packed fp32: one lane per pixel, four 8x8 wave tiles per
  * 256-thread block (neighbouring lanes share photons in L1), tiles dealt to
  * the eight XCDs in contiguous bands (neighbouring tiles share one L2).
@@ -865,9 +882,8 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
                                                     uint32_t ntiles) {
     __shared__ uint2 rq[GQ][256];
     const uint32_t tid = threadIdx.x;
-    /* XCD-aware tile order: block b runs on XCD b % 8; XCD k takes tiles [k per, (k+1) per) */
-    const uint32_t per = (ntiles + 7) / 8;
-    const uint32_t tile = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    uint32_t tile;
+    if (!gather_tile(gi, ntiles, tile)) return; /* block-uniform */
     const uint32_t w = tid >> 6, l = tid & 63;
     const uint32_t x = (tile % ntx) * 16 + (w & 1) * 8 + (l & 7);
     const uint32_t y = (tile / ntx) * 16 + (w >> 1) * 8 + (l >> 3);
@@ -1231,8 +1247,8 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
                                                           uint32_t ntiles) {
     __shared__ float ulds[4][7 * 64];
     const uint32_t tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-    const uint32_t per = (ntiles + 7) / 8;
-    const uint32_t tile = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    uint32_t tile;
+    if (!gather_tile(gi, ntiles, tile)) return; /* block-uniform */
     const uint32_t x = (tile % ntx) * 16 + (w & 1) * 8 + (l & 7);
     const uint32_t y = (tile / ntx) * 16 + (w >> 1) * 8 + (l >> 3);
     const uint32_t j = gather_row(gi, y);
@@ -1426,6 +1442,66 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
     }
 }
 
+__global__ __launch_bounds__(256) void k_gather_tiles(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
+                                                      uint8_t* flags) {
+    const uint32_t tile = blockIdx.x, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    const uint32_t x = (tile % ntx) * 16 + (w & 1) * 8 + (l & 7);
+    const uint32_t y = (tile / ntx) * 16 + (w >> 1) * 8 + (l >> 3);
+    const uint32_t j = gather_row(gi, y);
+    const bool live = x < gi.W && y < gi.segments * gi.seg_rows;
+    const GridParams g = *pb.grid;
+    bool act = false;
+    if (live) {
+        const HpRef hr = hp_ref(gi, j, x);
+        const float4 A = hr.A[hr.li];
+        act = (__float_as_uint(A.w) & PRD_HIT_NON_SPECULAR) && g.G &&
+              !sphere_misses_grid(g, mk(A.x, A.y, A.z), c.ppm_radius);
+    }
+    const int any = __syncthreads_or(act);
+    if (tid == 0) flags[tile] = (uint8_t)(any != 0);
+    if (!any && live) {
+        const size_t i = (size_t)j * gi.W + x;
+        gi.indirect[3 * i + 0] = 0.f;
+        gi.indirect[3 * i + 1] = 0.f;
+        gi.indirect[3 * i + 2] = 0.f;
+    }
+}
+/* one block: the flagged tiles in ascending order */
+__global__ __launch_bounds__(1024) void k_tile_compact(const uint8_t* flags, uint32_t ntiles, uint32_t* list,
+                                                       uint32_t* count) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t base;
+    const uint32_t tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    if (tid == 0) base = 0;
+    __syncthreads();
+    for (uint32_t t0 = 0; t0 < ntiles; t0 += 1024) {
+        const uint32_t t = t0 + tid;
+        const bool f = t < ntiles && flags[t];
+        const uint64_t m = __ballot(f);
+        const uint32_t pre = (uint32_t)__popcll(m & ((1ull << l) - 1ull));
+        if (l == 0) wsum[w] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t off = base;
+        for (uint32_t k = 0; k < w; k++) off += wsum[k];
+        if (f) list[off + pre] = t;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t tot = 0;
+            for (uint32_t k = 0; k < 16; k++) tot += wsum[k];
+            base += tot;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) *count = base;
+}
+void launch_gather_tiles(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, uint8_t* flags,
+                         uint32_t* list, uint32_t* count) {
+    const uint32_t rows = gi.segments * gi.seg_rows;
+    const uint32_t ntx = (gi.W + 15) / 16, nty = (rows + 15) / 16, ntiles = ntx * nty;
+    hipLaunchKernelGGL(k_gather_tiles, dim3(ntiles), dim3(256), 0, s, gi, pb, c, ntx, flags);
+    hipLaunchKernelGGL(k_tile_compact, dim3(1), dim3(1024), 0, s, flags, ntiles, list, count);
+}
+
 void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c) {
     const uint32_t rows = gi.segments * gi.seg_rows;
     const uint32_t ntx = (gi.W + 15) / 16, nty = (rows + 15) / 16, ntiles = ntx * nty;
@@ -1435,7 +1511,7 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
      * the per-lane kernel is faster (hall 1080p, tools/shard_model.py, per-rank gather union /
      * per-lane: N=2 1.29 / 1.56 ms, N=4 0.73 / 0.80, N=8 0.47 / 0.43).  Measured on one device
      * (serial hall gather / 4K conference frame): per-lane 2.5 ms / 120 ms, union 1.91 / 53.3. */
-    if (gi.segments >= 8) {
+    if (gi.segments >= 8 && !gi.cull) { /* a slab shard meets the single-device density: union */
         if (pb.nsub == 1) hipLaunchKernelGGL((k_ppm_gather<1>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
         else hipLaunchKernelGGL((k_ppm_gather<SUBR * SUBR>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
         return;

@@ -161,12 +161,15 @@ def run_slab(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None, nb=mult
             if it == iters - 1:
                 # diagnostic: the non-specular hit points whose sphere reaches this rank's photons
                 pr = recv.view(-1, 9)[:, :3]
-                lo, hi = pr.min(0).values, pr.max(0).values
-                A = hp_all.view(world, -1)[:, :mr * W * 4].reshape(-1, 4)
-                ns = (A[:, 3].view(torch.int32) & (1 << 27)) != 0
-                q = A[:, :3]
-                hit = ns & ((q + radius >= lo) & (q - radius <= hi)).all(1)
-                diag.append((d, int(ns.sum()), int(hit.sum()), int(pr.shape[0])))
+                if pr.shape[0] == 0:
+                    diag.append((d, 0, 0, 0))
+                else:
+                    lo, hi = pr.min(0).values, pr.max(0).values
+                    A = hp_all.view(world, -1)[:, :mr * W * 4].reshape(-1, 4)
+                    ns = (A[:, 3].view(torch.int32) & (1 << 27)) != 0
+                    q = A[:, :3]
+                    hit = ns & ((q + radius >= lo) & (q - radius <= hi)).all(1)
+                    diag.append((d, int(ns.sum()), int(hit.sum()), int(pr.shape[0])))
             ms[d]["finish"] += timed(lambda: b.finish(part[:mr * W * 3].contiguous()))
         if it >= warm:
             for k in range(world):
@@ -187,7 +190,7 @@ if __name__ == "__main__":
     args = sys.argv[1:]
     conf = 2
     slab = "--slab" in args
-    args = [a for a in args if a != "--slab"]
+    args = [a for a in args if a not in ("--slab", "--slab1")]
     if args[:1] == ["--config"]:
         conf, args = int(args[1]), args[2:]
     worlds = [int(v) for v in args] or [1, 2, 4, 8]
@@ -196,7 +199,7 @@ if __name__ == "__main__":
     print(f"configs[{conf}]: " + ("conference 3840x2160, 4096^2 photons" if conf == 4 else "hall 1920x1080, 2048^2"))
     if slab:
         for n in worlds:
-            if n == 1:
+            if n == 1 and "--slab1" not in sys.argv:
                 ms, passes, ag, rs = run(1, **kw)
                 print(f"N=1: per-rank serial {sum(ms.values()):.3f} ms {ms}", flush=True)
                 continue
