@@ -337,9 +337,12 @@ orx_status orx_set_ppm_pipeline(orx_renderer* r, void* side_stream, int enable);
  *   orx_ppm_local_eye + orx_ppm_local_photon_trace   (or orx_ppm_local_trace: both)  eye pass,
  *                            photon pass of the own rows; no grid yet
  *   orx_ppm_slab_histogram   per-bin counts [2][3][nbins] (uint32): the own valid deposits and the
- *                            own non-specular hit points, per axis, nbins bins over the scene AABB;
- *                            then 6 more words: the AABB of the own deposits as order-preserving
- *                            integers (f >= 0: bits | 2^31, f < 0: ~bits; empty: lo 0xffffffff, hi 0)
+ *                            own non-specular hit points, per axis, nbins bins over the scene AABB
+ *                            (nbins a multiple of ORX_SLAB_VOXELS, at most 1024); then 6 words: the
+ *                            AABB of the own deposits as order-preserving integers (f >= 0:
+ *                            bits | 2^31, f < 0: ~bits; empty: lo 0xffffffff, hi 0); then
+ *                            [2][V^3] counts of both over V = ORX_SLAB_VOXELS voxels per axis of
+ *                            the scene AABB (x + V (y + V z)): orx_slab_histogram_words(nbins) words
  *   (caller all-gathers the histograms and plans on the host: one axis and a bin -> rank table, the
  *    same on every rank; photons from rank s to rank d = the sum of s's photon bins mapped to d)
  *   orx_ppm_slab_pack        the own valid deposits, rank-major into the caller's send buffer: at
@@ -355,11 +358,16 @@ orx_status orx_set_ppm_pipeline(orx_renderer* r, void* side_stream, int enable);
  * The sum over ranks of the partial gathers is again the single-GPU gather up to fp32 order: every
  * photon is in exactly one rank's grid.  Capacity: the import takes up to the global photon launch's
  * deposit slots (PW * PH * max deposits) per rank. */
+#define ORX_SLAB_VOXELS 32u
+static inline size_t orx_slab_histogram_words(uint32_t nbins) {
+    return (size_t)6 * nbins + 6 + (size_t)2 * ORX_SLAB_VOXELS * ORX_SLAB_VOXELS * ORX_SLAB_VOXELS;
+}
 orx_status orx_set_slab_partition(orx_renderer* r, int enable);
 orx_status orx_ppm_local_trace(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
                                float ppm_radius, const orx_request* details);
 orx_status orx_ppm_local_photon_trace(orx_renderer* r);
-orx_status orx_ppm_slab_histogram(orx_renderer* r, uint32_t* hist_device /* 6*nbins + 6 */, uint32_t nbins);
+orx_status orx_ppm_slab_histogram(orx_renderer* r, uint32_t* hist_device /* orx_slab_histogram_words */,
+                                  uint32_t nbins);
 orx_status orx_ppm_slab_pack(orx_renderer* r, const uint8_t* bin_dest, uint32_t nbins, uint32_t axis,
                              const uint32_t* dest_base, uint64_t send_records, void* send_device);
 orx_status orx_ppm_slab_import(orx_renderer* r, const void* recv_device, uint64_t n_records,

@@ -298,6 +298,13 @@ static inline ORX_HD double orx_exp_d(double x) {
     if (kk < -1000) { scale = orx_as_double(((uint64_t)(1023 - 1000)) << 52); kk += 1000; }
     return p * orx_as_double(((uint64_t)(kk + 1023)) << 52) * scale;
 }
+/* logf(x) through the double log (ParticipatingMedium.cu:138's scatter distance); log(0) = -inf */
+static inline ORX_HD float orx_logf(float x) {
+    if (x == 0.0f) return -orx_as_float(0x7f800000u);
+    if (!(x > 0.0f)) return orx_as_float(0x7fc00000u);
+    if (x == orx_as_float(0x7f800000u)) return x;
+    return (float)orx_log_d((double)x);
+}
 static inline ORX_HD float orx_powf(float x, float y) {
     if (y == 0.0f) return 1.0f;
     if (x == 1.0f) return 1.0f;

@@ -1652,6 +1652,7 @@ orx_status orx_ppm_local_photon_trace(orx_renderer* r) {
     return ORX_OK;
 }
 
+static_assert(SLAB_VOX == ORX_SLAB_VOXELS, "slab voxel grid: kernels and ABI disagree");
 static SlabBins slab_bins(const orx_renderer* r, uint32_t nb) {
     SlabBins sb;
     const float lo[3] = {r->aabb_lo.x, r->aabb_lo.y, r->aabb_lo.z}, hi[3] = {r->aabb_hi.x, r->aabb_hi.y, r->aabb_hi.z};
@@ -1665,12 +1666,12 @@ static SlabBins slab_bins(const orx_renderer* r, uint32_t nb) {
 }
 
 orx_status orx_ppm_slab_histogram(orx_renderer* r, uint32_t* hist, uint32_t nb) {
-    if (!r || !hist || nb == 0 || nb > 8192) return ORX_ERR_INVALID_ARGUMENT;
+    if (!r || !hist || nb < ORX_SLAB_VOXELS || nb > 1024 || nb % ORX_SLAB_VOXELS) return ORX_ERR_INVALID_ARGUMENT;
     if (!r->slab || !r->rng_ready) return set_err(r, ORX_ERR_STATE, "orx_ppm_slab_histogram: slab mode, after the photon pass");
     HIPCHK(r, hipSetDevice(r->device));
     hipStream_t st = cur_stream(r);
-    HIPCHK(r, hipMemsetAsync(hist, 0, (size_t)6 * nb * 4, st));
-    launch_slab_hist(st, r->pb, r->px, slab_bins(r, nb), hist);
+    HIPCHK(r, hipMemsetAsync(hist, 0, orx_slab_histogram_words(nb) * 4, st));
+    launch_slab_hist(st, r->pb, r->px, slab_bins(r, nb), slab_bins(r, ORX_SLAB_VOXELS), hist);
     launch_slab_bbox(st, r->pb, hist + 6 * (size_t)nb);
     HIPCHK(r, hipGetLastError());
     return ORX_OK;
@@ -1678,7 +1679,7 @@ orx_status orx_ppm_slab_histogram(orx_renderer* r, uint32_t* hist, uint32_t nb) 
 
 orx_status orx_ppm_slab_pack(orx_renderer* r, const uint8_t* bin_dest, uint32_t nb, uint32_t axis,
                              const uint32_t* dest_base, uint64_t send_records, void* send) {
-    if (!r || !bin_dest || !dest_base || !send || nb == 0 || nb > 8192 || axis > 2) return ORX_ERR_INVALID_ARGUMENT;
+    if (!r || !bin_dest || !dest_base || !send || nb == 0 || nb > 1024 || axis > 2) return ORX_ERR_INVALID_ARGUMENT;
     if (!r->slab || !r->rng_ready) return set_err(r, ORX_ERR_STATE, "orx_ppm_slab_pack: slab mode, after the photon pass");
     if (r->world > 64) return set_err(r, ORX_ERR_UNSUPPORTED, "slab mode supports at most 64 ranks");
     for (uint32_t b = 0; b < nb; b++)

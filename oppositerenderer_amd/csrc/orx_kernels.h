@@ -201,7 +201,9 @@ struct SlabBins {
     float inv[3]; /* nb / extent */
     uint32_t nb;
 };
-void launch_slab_hist(hipStream_t s, const PhotonBufs& pb, const PixelBufs& px, const SlabBins& sb, uint32_t* hist);
+constexpr uint32_t SLAB_VOX = 32; /* coarse voxels per axis of the slab histogram (include/orx.h) */
+void launch_slab_hist(hipStream_t s, const PhotonBufs& pb, const PixelBufs& px, const SlabBins& sb,
+                      const SlabBins& vb, uint32_t* hist);
 void launch_slab_pack(hipStream_t s, const PhotonBufs& pb, const SlabBins& sb, uint32_t axis, const uint8_t* bin_dest,
                       uint32_t world, uint32_t* cursor, uint32_t cap, float* send);
 void launch_slab_import(hipStream_t s, const PhotonBufs& pb, const float* recv, uint32_t n);

@@ -1536,38 +1536,58 @@ __device__ __forceinline__ bool slot_valid(const PhotonBufs& pb, uint32_t s) {
     const uint32_t p = s / pb.D, k = s - p * pb.D;
     return (pb.vmask[p] >> k) & 1u;
 }
-/* [2][3][nb] counts: the valid deposits of the own photon pass, the own rows' non-specular hit
- * points (LDS histograms, one global add per non-empty bin and block) */
-__global__ __launch_bounds__(256) void k_slab_hist(PhotonBufs pb, PixelBufs px, SlabBins sb, uint32_t* hist) {
-    extern __shared__ uint32_t lh[]; /* [2][3][nb] */
-    const uint32_t n6 = 6 * sb.nb;
+/* [2][3][nb] counts: the valid deposits of the own photon pass and the own rows' non-specular
+ * hit points per bin of each axis; then [2][SLAB_VOX^3] counts of both over a coarse voxel grid
+ * of the scene AABB (voxel x + V (y + V z)), which the plan uses to weigh each hit point by the
+ * photon density around it.  LDS histograms, one global add per non-empty bin and block; the
+ * voxel counters are 16-bit halves of one word (photons low, hit points high), so a block takes
+ * a contiguous chunk of at most 65535 slots and 65535 pixels. */
+constexpr uint32_t SLAB_MAX_BINS = 1024;
+__global__ __launch_bounds__(256) void k_slab_hist(PhotonBufs pb, PixelBufs px, SlabBins sb, SlabBins vb,
+                                                   uint32_t cs, uint32_t cp, uint32_t* hist) {
+    __shared__ uint32_t lh[6 * SLAB_MAX_BINS];
+    __shared__ uint32_t lv[SLAB_VOX * SLAB_VOX * SLAB_VOX];
+    const uint32_t n6 = 6 * sb.nb, NV = SLAB_VOX * SLAB_VOX * SLAB_VOX;
     for (uint32_t k = threadIdx.x; k < n6; k += blockDim.x) lh[k] = 0;
+    for (uint32_t k = threadIdx.x; k < NV; k += blockDim.x) lv[k] = 0;
     __syncthreads();
-    const uint32_t T = gridDim.x * blockDim.x;
-    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < pb.S; s += T) {
+    const uint32_t s0 = blockIdx.x * cs, s1 = s0 + cs < pb.S ? s0 + cs : pb.S;
+    for (uint32_t s = s0 + threadIdx.x; s < s1; s += blockDim.x) {
         if (!slot_valid(pb, s)) continue;
         const float4 q = pb.pos4[s];
         atomicAdd(&lh[0 * sb.nb + slab_bin(sb, q.x, 0)], 1u);
         atomicAdd(&lh[1 * sb.nb + slab_bin(sb, q.y, 1)], 1u);
         atomicAdd(&lh[2 * sb.nb + slab_bin(sb, q.z, 2)], 1u);
+        atomicAdd(&lv[slab_bin(vb, q.x, 0) + SLAB_VOX * (slab_bin(vb, q.y, 1) + SLAB_VOX * slab_bin(vb, q.z, 2))], 1u);
     }
     const uint32_t npx = px.rows * px.W;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += T) {
+    const uint32_t p0 = blockIdx.x * cp, p1 = p0 + cp < npx ? p0 + cp : npx;
+    for (uint32_t i = p0 + threadIdx.x; i < p1; i += blockDim.x) {
         const float4 A = px.hpA[i];
         if (!(__float_as_uint(A.w) & PRD_HIT_NON_SPECULAR)) continue;
         atomicAdd(&lh[3 * sb.nb + slab_bin(sb, A.x, 0)], 1u);
         atomicAdd(&lh[4 * sb.nb + slab_bin(sb, A.y, 1)], 1u);
         atomicAdd(&lh[5 * sb.nb + slab_bin(sb, A.z, 2)], 1u);
+        atomicAdd(&lv[slab_bin(vb, A.x, 0) + SLAB_VOX * (slab_bin(vb, A.y, 1) + SLAB_VOX * slab_bin(vb, A.z, 2))],
+                  1u << 16);
     }
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < n6; k += blockDim.x)
         if (lh[k]) atomicAdd(&hist[k], lh[k]);
+    uint32_t* hv = hist + n6 + 6; /* past the photon AABB words (k_slab_bbox) */
+    for (uint32_t k = threadIdx.x; k < NV; k += blockDim.x) {
+        const uint32_t v = lv[k];
+        if (v & 0xffffu) atomicAdd(&hv[k], v & 0xffffu);
+        if (v >> 16) atomicAdd(&hv[NV + k], v >> 16);
+    }
 }
-void launch_slab_hist(hipStream_t s, const PhotonBufs& pb, const PixelBufs& px, const SlabBins& sb, uint32_t* hist) {
-    const uint32_t n = pb.S > px.rows * px.W ? pb.S : px.rows * px.W;
-    uint32_t blocks = (n + 4095) / 4096;
-    blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
-    hipLaunchKernelGGL(k_slab_hist, dim3(blocks), dim3(256), 6 * sb.nb * 4, s, pb, px, sb, hist);
+void launch_slab_hist(hipStream_t s, const PhotonBufs& pb, const PixelBufs& px, const SlabBins& sb,
+                      const SlabBins& vb, uint32_t* hist) {
+    const uint32_t npx = px.rows * px.W;
+    uint32_t blocks = std::max((pb.S + 65534) / 65535, (npx + 65534) / 65535);
+    blocks = std::max(blocks, 64u);
+    const uint32_t cs = (pb.S + blocks - 1) / blocks, cp = (npx + blocks - 1) / blocks;
+    hipLaunchKernelGGL(k_slab_hist, dim3(blocks), dim3(256), 0, s, pb, px, sb, vb, cs, cp, hist);
 }
 
 /* valid deposits -> the send buffer, rank-major: photon record (9 floats: position, direction,

@@ -39,38 +39,57 @@ def local_rows(H, rank, world):
 
 
 SLAB_BINS = 1024
+SLAB_VOXELS = 32  # ORX_SLAB_VOXELS (include/orx.h)
 
 
 def slab_hist_words(nb):
-    """uint32 words of one rank's orx_ppm_slab_histogram output: [2][3][nb] counts + its AABB"""
-    return 6 * nb + 6
+    """uint32 words of one rank's orx_ppm_slab_histogram output (orx_slab_histogram_words):
+    [2][3][nb] counts, the AABB of its photons, [2][V^3] voxel counts"""
+    return 6 * nb + 6 + 2 * SLAB_VOXELS ** 3
 
 
 def split_slab_hists(words, world, nb):
-    """all-gathered histogram words -> (counts uint32[world][2][3][nb], the AABB of every rank's
+    """all-gathered histogram words -> (counts uint32[world][2][3][nb], voxel counts
+    uint32[world][2][V^3] (photons, hit points; voxel x + V (y + V z)), the AABB of every rank's
     photons: uint32[6] ordered words, include/orx.h orx_ppm_slab_import's photon_box)"""
-    w = np.ascontiguousarray(words).view(np.uint32).reshape(world, 6 * nb + 6)
-    box = np.concatenate([w[:, 6 * nb:6 * nb + 3].min(0), w[:, 6 * nb + 3:].max(0)]).astype(np.uint32)
-    return w[:, :6 * nb].reshape(world, 2, 3, nb), box
+    w = np.ascontiguousarray(words).view(np.uint32).reshape(world, slab_hist_words(nb))
+    box = np.concatenate([w[:, 6 * nb:6 * nb + 3].min(0), w[:, 6 * nb + 3:6 * nb + 6].max(0)]).astype(np.uint32)
+    vox = w[:, 6 * nb + 6:].reshape(world, 2, SLAB_VOXELS ** 3)
+    return w[:, :6 * nb].reshape(world, 2, 3, nb), vox, box
 
 
-def slab_plan(hists, world, w_gather=0.6, w_photon=0.25, w_pixel=0.15):
+def slab_plan(hists, world, vox=None, w_gather=0.8, w_photon=0.15, w_pixel=0.05):
     """The slab partition of one iteration (include/orx.h orx_set_slab_partition), computed on
     every rank from the all-gathered histograms, identically (float64 numpy on identical inputs).
 
     hists: [world][2][3][nb] counts (uint32): each rank's valid deposits and own non-specular hit
-    points per bin of each axis of the scene AABB.  The cost of a bin mixes the gather (hit points
-    x photons: a hit point gathers the photons near it), the grid build (photons) and the per-pixel
-    work (hit points), each normalised to sum 1.  On each axis every bin goes to the rank whose
-    share of the cumulative cost holds the bin's midpoint (contiguous slabs, ascending ranks); the
-    axis with the smallest largest-slab cost wins (ties: the lower axis).
+    points per bin of each axis of the scene AABB; vox: [world][2][V^3] the same over V^3 voxels.
+    A bin's cost mixes the gather (its hit points, each weighted by the photon count of its voxel:
+    a hit point gathers the photons near it; spread over the bins of a voxel layer by their hit
+    points), the import and grid build (photons) and the per-pixel work (hit points), each
+    normalised to sum 1.  Without vox the gather term is photons x hit points per bin.  On each
+    axis every bin goes to the rank whose share of the cumulative cost holds the bin's midpoint
+    (contiguous slabs, ascending ranks); the axis with the smallest largest-slab cost wins (ties:
+    the lower axis).
     Returns (axis, bin_dest uint8[nb], counts int64[world][world]: photons rank s sends to rank d)."""
     h = np.asarray(hists, dtype=np.float64).reshape(world, 2, 3, -1)
     nb = h.shape[-1]
     ph, hp = h[:, 0].sum(0), h[:, 1].sum(0)
+    if vox is not None:
+        V = SLAB_VOXELS
+        v = np.asarray(vox, dtype=np.float64).reshape(world, 2, V, V, V).sum(0)  # [2][z][y][x]
+        cost = v[0] * v[1]  # hit points x photons in the same voxel
+        layer = nb // V
     best = None
     for a in range(3):
-        g = ph[a] * hp[a]
+        if vox is not None:
+            ax = (2, 1, 0)[a]  # numpy axis of voxel coordinate a
+            other = tuple(k for k in range(3) if k != ax)
+            lc, lh = cost.sum(axis=other), v[1].sum(axis=other)  # per voxel layer
+            per_hp = np.divide(lc, lh, out=np.zeros_like(lc), where=lh > 0)
+            g = hp[a] * np.repeat(per_hp, layer)
+        else:
+            g = ph[a] * hp[a]
         w = np.zeros(nb)
         for part, weight in ((g, w_gather), (ph[a], w_photon), (hp[a], w_pixel)):
             tot = part.sum()
@@ -82,9 +101,9 @@ def slab_plan(hists, world, w_gather=0.6, w_photon=0.25, w_pixel=0.15):
             dest = np.minimum(np.floor(mid * world / total), world - 1).astype(np.int64)
         else:
             dest = np.minimum(np.arange(nb) * world // nb, world - 1)
-        cost = np.bincount(dest, weights=w, minlength=world).max() if total > 0 else 0.0
-        if best is None or cost < best[0]:
-            best = (cost, a, dest)
+        cost_a = np.bincount(dest, weights=w, minlength=world).max() if total > 0 else 0.0
+        if best is None or cost_a < best[0]:
+            best = (cost_a, a, dest)
     _, axis, dest = best
     counts = np.zeros((world, world), np.int64)
     for src in range(world):
@@ -140,8 +159,8 @@ class ShardedPPM:
             d.all_gather(list(self.hists.chunk(world)), self.hist)
         else:
             d.all_gather_into_tensor(self.hists, self.hist)
-        hists, box = split_slab_hists(self.hists.cpu().numpy(), world, self.nb)
-        axis, bin_dest, counts = slab_plan(hists, world)
+        hists, vox, box = split_slab_hists(self.hists.cpu().numpy(), world, self.nb)
+        axis, bin_dest, counts = slab_plan(hists, world, vox)
         send_n, recv_n = counts[rank], counts[:, rank]
         base = np.concatenate([[0], np.cumsum(send_n)[:-1]]).astype(np.uint32)
         ns, nr = int(send_n.sum()), int(recv_n.sum())

@@ -259,6 +259,19 @@ struct orc_renderer {
     uint32_t* vcount; float* vverts; v3* vsplat; v3* vcam;
     v3* vkd; /* [9][lpx] texel colour of Texture light vertices */
     void* vcm_ctx; /* vcm_ctx_t of the pending sharded light pass */
+    /* participating medium (cfg.enable_media, ENABLE_PARTICIPATING_MEDIA): one box
+     * (geometry_instance/AAB.cu) with ParticipatingMedium's programs; the volumetric photon
+     * table (NUM_VOLUMETRIC_PHOTONS slots: power, position, numDeposits) of the last photon pass,
+     * gathered by the next eye pass with that iteration's radius */
+    int med_on;
+    v3 med_lo, med_hi;
+    float sig_s, sig_a;
+    uint32_t nvol;
+    v3* vpow; v3* vpos; uint32_t* vcnt;
+    int vol_ready;
+    float vol_R;
+    uint32_t* ev_n; v3* ev_pos; v3* ev_pow; /* per emitted photon: scatter events, the last one */
+    v3* volR;                               /* per pixel: Hitpoint::volumetricRadiance */
 };
 
 static orx_status fail(orc_renderer* r, orx_status s, const char* msg) {
@@ -300,6 +313,8 @@ static void free_scene(orc_renderer* r) {
     r->tex = NULL; r->ntex = 0; r->has_tex = 0; r->uv = NULL; r->tang = NULL; r->btan = NULL;
     r->quads = NULL; r->qmat = NULL; r->sph = NULL; r->smat = NULL; r->verts = NULL;
     r->vnorm = NULL; r->tris = NULL; r->tmat = NULL; r->mats = NULL; r->lights = NULL;
+    free(r->vpow); free(r->vpos); free(r->vcnt);
+    r->vpow = NULL; r->vpos = NULL; r->vcnt = NULL; r->med_on = 0; r->vol_ready = 0;
 }
 static void free_frame(orc_renderer* r) {
     free(r->rng); free(r->hp); free(r->photons); free(r->keys); free(r->sort_tmp);
@@ -313,6 +328,9 @@ static void free_frame(orc_renderer* r) {
     r->ndep = NULL; r->hcount = NULL; r->hwin = NULL;
     free(r->kdwork); free(r->kdtree);
     r->kdwork = NULL; r->kdtree = NULL; r->kdsize = 0;
+    free(r->ev_n); free(r->ev_pos); free(r->ev_pow); free(r->volR);
+    r->ev_n = NULL; r->ev_pos = NULL; r->ev_pow = NULL; r->volR = NULL;
+    r->vol_ready = 0;
 }
 void orc_destroy(orc_renderer* r) {
     if (!r) return;
@@ -443,7 +461,29 @@ orx_status orc_init_scene(orc_renderer* r, const orx_scene* s) {
         if (s->materials[i].type == ORX_MAT_TEXTURE &&
             (s->materials[i].texture < 0 || (uint32_t)s->materials[i].texture >= s->n_textures))
             return fail(r, ORX_ERR_INVALID_ARGUMENT, "Texture material without a texture image");
+    const int med = r->cfg.enable_media && s->n_media;
+    if (med) {
+        if (s->n_media != 1 || !s->media)
+            return fail(r, ORX_ERR_UNSUPPORTED, "participating media: one medium box per scene");
+        const float* m = s->media;
+        if (!(m[0] < m[3] && m[1] < m[4] && m[2] < m[5]) || !(m[6] >= 0 && m[7] >= 0 && m[6] + m[7] > 0))
+            return fail(r, ORX_ERR_INVALID_ARGUMENT, "medium box: min < max and sigma_s + sigma_a > 0");
+        if (r->cfg.volumetric_photons == 0)
+            return fail(r, ORX_ERR_INVALID_ARGUMENT, "volumetric_photons must be > 0 with media");
+    }
     free_scene(r);
+    if (med) {
+        r->med_lo = ld3(s->media);
+        r->med_hi = ld3(s->media + 3);
+        r->sig_s = s->media[6];
+        r->sig_a = s->media[7];
+        r->nvol = r->cfg.volumetric_photons;
+        r->vpow = (v3*)calloc(r->nvol, sizeof(v3));
+        r->vpos = (v3*)calloc(r->nvol, sizeof(v3));
+        r->vcnt = (uint32_t*)calloc(r->nvol, 4);
+        if (!r->vpow || !r->vpos || !r->vcnt) return fail(r, ORX_ERR_OUT_OF_MEMORY, "oracle: out of memory");
+        r->med_on = 1;
+    }
     r->nq = s->n_quads; r->ns = s->n_spheres; r->nt = s->n_triangles; r->nv = s->n_vertices;
     r->nm = s->n_materials; r->nl = s->n_lights;
     r->quads = (quadp_t*)calloc(r->nq + 1, sizeof(quadp_t));
@@ -770,6 +810,88 @@ static int trace_any(const orc_renderer* r, v3 o, v3 d, float tmin, float tmax) 
     return 0;
 }
 
+/* The medium box (geometry_instance/AAB.cu:24-157): slab test with the near and far axes; a ray
+ * starting inside (tNear < 0.01, tFar > 0) reports t = 0.000115 on the far axis with the normal
+ * against the ray for RADIANCE/PHOTON rays (so the medium program starts its walk right there),
+ * and the exit t = tFar with the normal along the ray for the IN_PARTICIPATING_MEDIUM types. */
+#define MED_PRIM 0x7ffffff0
+static inline int isect_medium(const orc_renderer* r, v3 o, v3 d, float tmin, float tmax, int in_medium, float* tout,
+                               v3* nout) {
+    int axn = 0, axf = 0;
+    float tn, tf;
+    const float divx = 1 / d.x;
+    if (divx >= 0) { tn = (r->med_lo.x - o.x) * divx; tf = (r->med_hi.x - o.x) * divx; }
+    else { tn = (r->med_hi.x - o.x) * divx; tf = (r->med_lo.x - o.x) * divx; }
+    if (tf < tn) return 0;
+    const float divy = 1 / d.y;
+    float tyn, tyf;
+    if (divy >= 0) { tyn = (r->med_lo.y - o.y) * divy; tyf = (r->med_hi.y - o.y) * divy; }
+    else { tyn = (r->med_hi.y - o.y) * divy; tyf = (r->med_lo.y - o.y) * divy; }
+    if (tyn > tn) { tn = tyn; axn = 1; }
+    if (tyf < tf) { tf = tyf; axf = 1; }
+    if (tf < tn) return 0;
+    const float divz = 1 / d.z;
+    float tzn, tzf;
+    if (divz >= 0) { tzn = (r->med_lo.z - o.z) * divz; tzf = (r->med_hi.z - o.z) * divz; }
+    else { tzn = (r->med_hi.z - o.z) * divz; tzf = (r->med_lo.z - o.z) * divz; }
+    if (tzn > tn) { tn = tzn; axn = 2; }
+    if (tzf < tf) { tf = tzf; axf = 2; }
+    if (tf < tn) return 0;
+    float t = tn, nvr = -1;
+    int ax = axn;
+    if (tn < 0.01f && tf > 0.0f) {
+        ax = axf;
+        if (!in_medium) t = (float)0.000115;
+        else { t = tf; nvr = 1; }
+    }
+    if (!(t > tmin && t < tmax)) return 0;
+    const float dc = ax == 0 ? d.x : ax == 1 ? d.y : d.z;
+    const float nc = dc >= 0 ? nvr : -nvr;
+    *nout = mk(ax == 0 ? nc : 0.f, ax == 1 ? nc : 0.f, ax == 2 ? nc : 0.f);
+    *tout = t;
+    return 1;
+}
+/* closest hit with the medium as the last primitive (a surface at the same t wins) */
+static int trace_closest_m(const orc_renderer* r, v3 o, v3 d, float tmin, float tmax, int in_medium, hit_t* h) {
+    const int hit = trace_closest(r, o, d, tmin, tmax, h);
+    if (!r->med_on) return hit;
+    float t;
+    v3 n;
+    if (isect_medium(r, o, d, tmin, hit ? h->t : tmax, in_medium, &t, &n)) {
+        h->t = t;
+        h->prim = MED_PRIM;
+        h->gn = h->sn = n;
+        h->b = h->g = 0.f;
+        return 1;
+    }
+    return hit;
+}
+/* VolumetricPhotonSphere.cu:24-59 + VolumetricPhotonSphereRadiance.cu:24-34 over the table in
+ * slot order: each root of the photon's sphere inside (tmin, tmax) reports an intersection whose
+ * any-hit adds the photon when its projection on the ray is inside (tmin, tmax) and then ignores
+ * it, so a photon with both roots inside counts twice */
+static v3 vol_gather(const orc_renderer* r, v3 o, v3 d, float tmin, float tmax, float sig_t) {
+    v3 acc = mk1(0.f);
+    if (!r->vol_ready) return acc;
+    const float R = r->vol_R, R2 = R * R;
+    const float coef = 1 / (ORX_PI_F * R * R), k4 = 1.f / (4.f * ORX_PI_F);
+    for (uint32_t s = 0; s < r->nvol; s++) {
+        if (!r->vcnt[s] || !(fmax3(r->vpow[s]) > 0)) continue;
+        const v3 pos = r->vpos[s];
+        const v3 O = sub(o, pos);
+        const float b = dot(O, d), c = dot(O, O) - R2, disc = b * b - c;
+        if (!(disc > 0.0f)) continue;
+        const float sd = sqrtf(disc), r1 = -b - sd, r2 = -b + sd;
+        const float t = dot(sub(pos, o), d);
+        if (!(t < tmax && t > tmin)) continue;
+        const v3 pw = scl(r->vpow[s], (float)r->vcnt[s]);
+        const v3 add1 = scl(scl(scl(pw, coef), orx_expf(-sig_t * t)), k4);
+        if (r1 > tmin && r1 < tmax) acc = add(acc, add1);
+        if (r2 > tmin && r2 < tmax) acc = add(acc, add1);
+    }
+    return acc;
+}
+
 int32_t orc_trace_closest(orc_renderer* r, const float o[3], const float d[3], float tmin, float tmax, float* t_out) {
     hit_t h;
     if (!trace_closest(r, ld3(o), ld3(d), tmin, tmax, &h)) return -1;
@@ -854,20 +976,72 @@ typedef struct {
 } rprd_t;
 
 /* Iterative form of the recursive rtTrace(RADIANCE) chain: Mirror/Glass
- * closest-hit programs tail-recurse (Mirror.cu:50-63, Glass.cu:90-143). */
-static void trace_radiance(const orc_renderer* r, v3 o, v3 d, float tmin, rprd_t* prd) {
+ * closest-hit programs tail-recurse (Mirror.cu:50-63, Glass.cu:90-143).
+ *
+ * With a medium (volR != NULL): ParticipatingMedium.cu:53-104.  A RADIANCE ray that enters the
+ * box opens a frame: attenSaved = (attenuation + 0.1f) - 0.1f, then the rest of the path runs on
+ * an IN_PARTICIPATING_MEDIUM ray from the entry point (tmin 0.01); when it returns, the frame's
+ * distance is the radiancePrd.lastTHit left by that ray's first hit (every closest-hit program
+ * writes its own tHit after its recursion; a miss and a back-facing emitter write nothing, so the
+ * value is the PRD's initial one, 0 here; the medium program's own write goes through double,
+ * tHit + 0.1 - 0.1), T = exp(-distance sigma_t), V = the volumetric gather on (entry, tmin 1e-7,
+ * tmax distance), and volumetricRadiance = volumetricRadiance*T + attenSaved*V,
+ * attenuation *= T.  Frames nest along the path; unrolled, the path's
+ *   volumetricRadiance = sum_k attenSaved_k V_k prod_{j<k} T_j,  attenuation = (...) prod_k T_k,
+ * accumulated here in path order (the nested evaluation's fp32 rounding order differs).  A ray
+ * hitting the box from inside (leaving it) continues as RADIANCE from the exit point (tmin 0.01).
+ * Glass rays travelling inside the glass are IN_PARTICIPATING_MEDIUM rays (Glass.cu:126-131). */
+static void trace_radiance(const orc_renderer* r, v3 o, v3 d, float tmin, rprd_t* prd, v3* volR) {
     const uint32_t maxd = r->cfg.max_radiance_trace_depth;
+    const int med = r->med_on && volR;
+    const float sig_t = r->sig_a + r->sig_s;
+    int inmed = 0, frame = 0;
+    v3 fa = mk1(0.f), fh = mk1(0.f), fd = mk1(0.f);
+    float P = 1.f;
     for (;;) {
         hit_t h;
-        if (!trace_closest(r, o, d, tmin, ORC_RT_DEFAULT_MAX, &h)) {
+        const int hit = med ? trace_closest_m(r, o, d, tmin, ORC_RT_DEFAULT_MAX, inmed, &h)
+                            : trace_closest(r, o, d, tmin, ORC_RT_DEFAULT_MAX, &h);
+        if (frame) { /* the open frame's inner ray has its first hit: close the frame */
+            frame = 0;
+            float dist = 0.f;
+            if (hit) {
+                if (h.prim == MED_PRIM) {
+                    dist = (float)(((double)h.t + 0.1) - 0.1);
+                } else {
+                    const mat_t* fm = &r->mats[prim_material(r, h.prim)];
+                    if (fm->type != ORX_MAT_DIFFUSE_EMITTER || !(dot(normalize(h.sn), neg(d)) < 0.f)) dist = h.t;
+                }
+            }
+            const float T = orx_expf(-dist * sig_t);
+            const v3 V = vol_gather(r, fh, fd, (float)0.0000001, dist, sig_t);
+            *volR = add(*volR, scl(mul(fa, V), P));
+            P = P * T;
+        }
+        if (!hit) {
             /* miss (RayGeneratorPPM.cu:72-77, RayGeneratorPT.cu:144-150) */
             prd->flags = PRD_MISS;
             prd->attenuation = mk1(0.f);
             prd->radiance = mk1(0.f);
-            return;
+            break;
+        }
+        v3 hitPoint = add(o, scl(d, h.t));
+        if (h.prim == MED_PRIM) {
+            const v3 N = normalize(h.sn);
+            if (dot(N, d) < 0) { /* entering: open a frame */
+                frame = 1;
+                fa = sub_s(add(prd->attenuation, mk1(0.1f)), 0.1f);
+                fh = hitPoint;
+                fd = d;
+                inmed = 1;
+            } else {
+                inmed = 0;
+            }
+            o = hitPoint;
+            tmin = 0.01f;
+            continue;
         }
         const mat_t* m = &r->mats[prim_material(r, h.prim)];
-        v3 hitPoint = add(o, scl(d, h.t));
         if (m->type == ORX_MAT_DIFFUSE || m->type == ORX_MAT_GLOSSY) {
             /* Diffuse.cu:71-87, Glossy.cu:74-90 */
             v3 N = normalize(h.sn);
@@ -881,7 +1055,7 @@ static void trace_radiance(const orc_renderer* r, v3 o, v3 d, float tmin, rprd_t
                 float s1 = orc_uniform(prd->rs);
                 prd->newdir = sample_hemisphere_cos(N, s0, s1);
             }
-            return;
+            break;
         } else if (m->type == ORX_MAT_TEXTURE) {
             /* Texture.cu:83-110: normal-mapped normal, no depth++ */
             v3 wsn = normalize(h.sn);
@@ -894,15 +1068,15 @@ static void trace_radiance(const orc_renderer* r, v3 o, v3 d, float tmin, rprd_t
                 prd->newdir = sample_hemisphere_cos(wsn, s0, s1);
             }
             prd->attenuation = mul(prd->attenuation, tex_color(r, m, &h));
-            return;
+            break;
         } else if (m->type == ORX_MAT_DIFFUSE_EMITTER) {
             /* DiffuseEmitter.cu:40-51 */
             v3 N = normalize(h.sn);
             prd->flags |= PRD_HIT_EMITTER;
-            if (dot(N, neg(d)) < 0.f) return;
+            if (dot(N, neg(d)) < 0.f) break;
             v3 Le = divs(m->powerPerArea, ORX_PI_F);
             prd->radiance = add(prd->radiance, mul(prd->attenuation, Le));
-            return;
+            break;
         } else if (m->type == ORX_MAT_MIRROR) {
             /* Mirror.cu:50-63 */
             v3 N = normalize(h.sn);
@@ -912,9 +1086,10 @@ static void trace_radiance(const orc_renderer* r, v3 o, v3 d, float tmin, rprd_t
                 d = reflect(d, N);
                 o = hitPoint;
                 tmin = 0.0001f;
+                inmed = 0;
                 continue;
             }
-            return;
+            break;
         } else { /* ORX_MAT_GLASS, Glass.cu:90-143 */
             v3 wsn = normalize(h.sn);
             int outside = dot(wsn, d) < 0;
@@ -943,12 +1118,14 @@ static void trace_radiance(const orc_renderer* r, v3 o, v3 d, float tmin, rprd_t
             prd->depth++;
             if (prd->depth <= maxd) {
                 o = hitPoint; d = nd; tmin = 0.0001f;
+                inmed = (outside && !isReflected) || (!outside && isReflected);
                 continue;
             }
             prd->attenuation = scl(prd->attenuation, 0.f);
-            return;
+            break;
         }
     }
+    if (med) prd->attenuation = scl(prd->attenuation, P);
 }
 
 /* ------------------------------------------------------------------ */
@@ -996,6 +1173,14 @@ static orx_status resize(orc_renderer* r, uint32_t W, uint32_t H) {
     r->direct = (v3*)calloc(npx, sizeof(v3));
     r->output = (v3*)calloc(npx, sizeof(v3));
     r->dbg = (uint32_t*)calloc(npx * 2, 4);
+    if (r->med_on) {
+        const size_t np = (size_t)PW * r->prows + 1;
+        r->ev_n = (uint32_t*)calloc(np, 4);
+        r->ev_pos = (v3*)calloc(np, sizeof(v3));
+        r->ev_pow = (v3*)calloc(np, sizeof(v3));
+        r->volR = (v3*)calloc(npx + 1, sizeof(v3));
+        if (!r->ev_n || !r->ev_pos || !r->ev_pow || !r->volR) return fail(r, ORX_ERR_OUT_OF_MEMORY, "oracle: out of memory");
+    }
     if (!r->rng || !r->hp || !r->photons || !r->sort_tmp || !r->keys || !r->offsets || !r->hist ||
         !r->indirect || !r->direct || !r->output || !r->dbg)
         return fail(r, ORX_ERR_OUT_OF_MEMORY, "oracle: out of memory");
@@ -1028,7 +1213,9 @@ static void ppm_eye_pass(orc_renderer* r, const cam_t* cam) {
             prd.rs = rs;
             v3 o, d;
             primary_ray(cam, x, y, W, H, rs, &o, &d);
-            trace_radiance(r, o, d, 0.001f, &prd);
+            v3 vr = mk1(0.f); /* RayGeneratorPPM.cu:39-41 */
+            trace_radiance(r, o, d, 0.001f, &prd, r->med_on ? &vr : NULL);
+            if (r->med_on) r->volR[(size_t)j * W + x] = vr;
             hitpoint_t* h = &r->hp[(size_t)j * W + x];
             h->position = prd.position;
             h->normal = prd.normal;
@@ -1041,114 +1228,160 @@ static void ppm_eye_pass(orc_renderer* r, const cam_t* cam) {
 }
 
 /* Photon closest-hit chain (Diffuse.cu:92-135, Mirror.cu:65-77, Glass.cu:164-205,
- * DiffuseEmitter.cu:56-59) in iterative form. */
+ * DiffuseEmitter.cu:56-59) in iterative form.
+ *
+ * With a medium (ev != NULL): ParticipatingMedium.cu:110-201.  Every medium hit counts a depth.
+ * An IN_PARTICIPATING_MEDIUM ray leaving the box continues as PHOTON from hit + 0.0001 d (tmin
+ * 0.001); any other medium hit samples scatterT = -log(1 - u)/sigma_t and probes [0.001, scatterT]
+ * with an IN_PARTICIPATING_MEDIUM ray.  The probe's frame scatters when the photon depth came
+ * back unchanged: the probe met nothing (miss), an emitter (no program for that ray type), or a
+ * diffuse/texture surface whose Russian roulette ended the path after its deposit (the scatter
+ * position then lies beyond that surface, as in the reference).  A scatter survives with
+ * probability sigma_s/sigma_t, is recorded as this photon's latest volumetric event and, below
+ * the depth limit, continues as PHOTON in a uniform direction from the scatter position (tmin
+ * 0.001).  Glass rays travelling inside the glass are IN_PARTICIPATING_MEDIUM rays. */
+typedef struct { uint32_t n; v3 pos, pow; } vev_t;
 static void trace_photon(const orc_renderer* r, v3 o, v3 d, v3 power, uint32_t pm_index, uint32_t* rs,
-                         uint8_t* ndep) {
+                         uint8_t* ndep, vev_t* ev) {
     /* uniform grid: at most maxDeposits, then the path ends (Diffuse.cu:97, :128-131); stochastic
      * hash: STORE_PHOTON never counts (store_photon.h:19-25), every hit at depth >= 1 deposits */
     const int hash = r->cfg.photon_map == 1;
     const uint32_t maxDeposits = hash ? r->dslot : r->cfg.max_photon_deposits;
     const uint32_t depositLimit = hash ? 0xffffffffu : maxDeposits;
     const uint32_t maxDepth = r->cfg.max_photon_trace_depth;
+    const int med = r->med_on && ev;
+    const float sig_t = r->sig_a + r->sig_s;
     uint32_t numStored = 0, depth = 0;
     float weight = 1.0f;
-    float tmin = 0.0001f;
+    float tmin = 0.0001f, tmax = ORC_RT_DEFAULT_MAX;
+    int inmed = 0, probe = 0;
+    uint32_t pdepth = 0;
+    v3 spos = mk1(0.f);
     for (;;) {
         hit_t h;
-        if (!trace_closest(r, o, d, tmin, ORC_RT_DEFAULT_MAX, &h)) return; /* PhotonGenerator.cu:132-135 */
-        const mat_t* m = &r->mats[prim_material(r, h.prim)];
-        v3 hitPoint = add(o, scl(d, h.t));
-        if (m->type == ORX_MAT_DIFFUSE || m->type == ORX_MAT_GLOSSY) {
-            v3 N = normalize(h.sn);
-            if (depth >= 1 && numStored < maxDeposits) {
-                photon_t* p = &r->photons[pm_index + numStored];
-                p->power = power;
-                p->position = hitPoint;
-                p->direction = d;
-                numStored++;
-                if (ndep) *ndep = (uint8_t)numStored;
-            }
-            power = mul(power, m->Kd);
-            weight *= fmax3(m->Kd);
-            if (depth >= 3) { /* PHOTON_TRACING_RR_START_DEPTH */
-                float probContinue = favgf(m->Kd);
-                float probSample = orc_uniform(rs);
-                if (probSample >= probContinue) return;
-                power = divs(power, probContinue);
-            }
+        const int had_probe = probe;
+        probe = 0;
+        int end = 0;
+        const int hit = med ? trace_closest_m(r, o, d, tmin, tmax, inmed, &h)
+                            : trace_closest(r, o, d, tmin, ORC_RT_DEFAULT_MAX, &h);
+        if (!hit) {
+            end = 1; /* PhotonGenerator.cu:132-135 */
+        } else if (h.prim == MED_PRIM) {
             depth++;
-            if (depth >= maxDepth || (double)weight < 0.001) return;
-            if (numStored >= depositLimit) return;
-            float s0 = orc_uniform(rs);
-            float s1 = orc_uniform(rs);
-            d = sample_hemisphere_cos(N, s0, s1);
-            o = hitPoint;
-            tmin = 0.0001f;
-        } else if (m->type == ORX_MAT_TEXTURE) {
-            /* Texture.cu:116-175: weight cutoff 0.01, new ray tmin 0.01 */
-            v3 N = normalize(h.sn);
-            if (depth >= 1 && numStored < maxDeposits) {
-                photon_t* p = &r->photons[pm_index + numStored];
-                p->power = power;
-                p->position = hitPoint;
-                p->direction = d;
-                numStored++;
-                if (ndep) *ndep = (uint8_t)numStored;
-            }
-            const v3 kd = tex_color(r, m, &h);
-            power = mul(power, kd);
-            weight *= fmax3(kd);
-            if (depth >= 3) {
-                float probContinue = favgf(kd);
-                float probSample = orc_uniform(rs);
-                if (probSample >= probContinue) return;
-                power = divs(power, probContinue);
-            }
-            depth++;
-            if (depth >= maxDepth || (double)weight < 0.01) return;
-            if (numStored >= depositLimit) return;
-            float s0 = orc_uniform(rs);
-            float s1 = orc_uniform(rs);
-            d = sample_hemisphere_cos(N, s0, s1);
-            o = hitPoint;
-            tmin = 0.01f;
-        } else if (m->type == ORX_MAT_DIFFUSE_EMITTER) {
-            return; /* depth++ only */
-        } else if (m->type == ORX_MAT_MIRROR) {
-            v3 N = normalize(h.sn);
-            depth++;
-            if (depth <= maxDepth) {
-                power = mul(power, m->Kr);
-                d = reflect(d, N);
+            const v3 N = normalize(h.sn);
+            const v3 hitPoint = add(o, scl(d, h.t));
+            if (dot(N, d) > 0 && inmed) { /* leaving the box */
+                o = add(hitPoint, scl(d, 0.0001f));
+                tmin = 0.001f;
+                tmax = ORC_RT_DEFAULT_MAX;
+                inmed = 0;
+            } else {
+                const float sample = orc_uniform(rs);
+                const float st = -orx_logf(1 - sample) / sig_t;
+                spos = add(hitPoint, scl(d, st));
+                probe = 1;
+                pdepth = depth;
                 o = hitPoint;
-                tmin = 0.0001f;
-                continue;
+                tmin = 0.001f;
+                tmax = st;
+                inmed = 1;
             }
-            return;
-        } else { /* glass */
-            v3 wsn = normalize(h.sn);
-            int outside = dot(wsn, d) < 0;
-            v3 N = outside ? wsn : neg(wsn);
-            float n1 = outside ? 1.0f : m->ior, n2 = outside ? m->ior : 1.0f;
-            v3 refr;
-            int valid = refract(&refr, d, N, n2 / n1);
-            float cosI = -dot(d, N);
-            float cosT = -dot(refr, N);
-            float refl = 1.f;
-            if (valid) {
-                float rp = (n2 * cosI - n1 * cosT) / (n2 * cosI + n1 * cosT);
-                float rsv = (n1 * cosI - n2 * cosT) / (n1 * cosI + n2 * cosT);
-                refl = (rp * rp + rsv * rsv) / 2.f;
+        } else {
+            const mat_t* m = &r->mats[prim_material(r, h.prim)];
+            v3 hitPoint = add(o, scl(d, h.t));
+            tmax = ORC_RT_DEFAULT_MAX;
+            if (m->type == ORX_MAT_DIFFUSE || m->type == ORX_MAT_GLOSSY || m->type == ORX_MAT_TEXTURE) {
+                /* Texture.cu:116-175 differs only in Kd = texel colour, the weight cutoff (0.01)
+                 * and the new ray's tmin (0.01) */
+                const int tex = m->type == ORX_MAT_TEXTURE;
+                v3 N = normalize(h.sn);
+                if (depth >= 1 && numStored < maxDeposits) {
+                    photon_t* p = &r->photons[pm_index + numStored];
+                    p->power = power;
+                    p->position = hitPoint;
+                    p->direction = d;
+                    numStored++;
+                    if (ndep) *ndep = (uint8_t)numStored;
+                }
+                const v3 kd = tex ? tex_color(r, m, &h) : m->Kd;
+                power = mul(power, kd);
+                weight *= fmax3(kd);
+                if (depth >= 3) { /* PHOTON_TRACING_RR_START_DEPTH */
+                    float probContinue = favgf(kd);
+                    float probSample = orc_uniform(rs);
+                    if (probSample >= probContinue) end = 1;
+                    else power = divs(power, probContinue);
+                }
+                if (!end) {
+                    depth++;
+                    if (depth >= maxDepth || (double)weight < (tex ? 0.01 : 0.001)) end = 1;
+                    else if (numStored >= depositLimit) end = 1;
+                    else {
+                        float s0 = orc_uniform(rs);
+                        float s1 = orc_uniform(rs);
+                        d = sample_hemisphere_cos(N, s0, s1);
+                        o = hitPoint;
+                        tmin = tex ? 0.01f : 0.0001f;
+                        inmed = 0;
+                    }
+                }
+            } else if (m->type == ORX_MAT_DIFFUSE_EMITTER) {
+                if (!inmed) depth++; /* closestHitPhoton is the PHOTON program only */
+                end = 1;
+            } else if (m->type == ORX_MAT_MIRROR) {
+                v3 N = normalize(h.sn);
+                depth++;
+                if (depth <= maxDepth) {
+                    power = mul(power, m->Kr);
+                    d = reflect(d, N);
+                    o = hitPoint;
+                    tmin = 0.0001f;
+                    inmed = 0;
+                } else {
+                    end = 1;
+                }
+            } else { /* glass */
+                v3 wsn = normalize(h.sn);
+                int outside = dot(wsn, d) < 0;
+                v3 N = outside ? wsn : neg(wsn);
+                float n1 = outside ? 1.0f : m->ior, n2 = outside ? m->ior : 1.0f;
+                v3 refr;
+                int valid = refract(&refr, d, N, n2 / n1);
+                float cosI = -dot(d, N);
+                float cosT = -dot(refr, N);
+                float refl = 1.f;
+                if (valid) {
+                    float rp = (n2 * cosI - n1 * cosT) / (n2 * cosI + n1 * cosT);
+                    float rsv = (n1 * cosI - n2 * cosT) / (n1 * cosI + n2 * cosT);
+                    refl = (rp * rp + rsv * rsv) / 2.f;
+                }
+                float sample = orc_uniform(rs);
+                const int isReflected = sample <= refl;
+                v3 nd = isReflected ? reflect(d, N) : refr;
+                depth++;
+                if (depth <= maxDepth) {
+                    o = hitPoint; d = nd; tmin = 0.0001f;
+                    inmed = (outside && !isReflected) || (!outside && isReflected);
+                } else {
+                    end = 1;
+                }
             }
-            float sample = orc_uniform(rs);
-            v3 nd = (sample <= refl) ? reflect(d, N) : refr;
-            depth++;
-            if (depth <= maxDepth) {
-                o = hitPoint; d = nd; tmin = 0.0001f;
-                continue;
-            }
-            return;
         }
+        if (had_probe && depth == pdepth) { /* scatter at the probe's end */
+            if (orc_uniform(rs) >= r->sig_s / sig_t) return;
+            ev->n++;
+            ev->pos = spos;
+            ev->pow = power;
+            if (depth >= maxDepth) return;
+            const float s0 = orc_uniform(rs), s1 = orc_uniform(rs);
+            d = sample_unit_sphere(s0, s1);
+            o = spos;
+            tmin = 0.001f;
+            tmax = ORC_RT_DEFAULT_MAX;
+            inmed = 0;
+            continue;
+        }
+        if (end) return;
     }
 }
 
@@ -1206,10 +1439,40 @@ static void ppm_photon_pass(orc_renderer* r) {
             }
             uint8_t* nd = r->ndep ? &r->ndep[(size_t)j * PW + x] : NULL;
             if (nd) *nd = 0;
-            trace_photon(r, origin, dir, power, pm_index, rs, nd);
+            vev_t ev = {0, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+            trace_photon(r, origin, dir, power, pm_index, rs, nd, r->med_on ? &ev : NULL);
+            if (r->med_on) {
+                const size_t pi = (size_t)j * PW + x;
+                r->ev_n[pi] = ev.n;
+                r->ev_pos[pi] = ev.pos;
+                r->ev_pow[pi] = ev.pow;
+            }
             memcpy(g, rs, 24);
         }
     }
+}
+
+/* The volumetric photon table of this photon pass (VolumetricPhotonInitialize.cu:19-24 clears it,
+ * ParticipatingMedium.cu:170-177 stores): photon p's scatter events all land in slot
+ * pm_index % NUM_VOLUMETRIC_PHOTONS (pm_index = p * maxPhotonDepositsPerEmitted) and bump its
+ * numDeposits; the reference's racing stores leave an arbitrary event's power and position in
+ * the slot, here the last event of the highest photon index (the device's atomicMax).  The
+ * table and this iteration's radius (volumetricRadius = PPMRadius, OptixRenderer.cpp:592-593)
+ * serve the next eye pass. */
+static void vol_resolve(orc_renderer* r, float ppmRadius) {
+    memset(r->vcnt, 0, (size_t)r->nvol * 4);
+    memset(r->vpow, 0, (size_t)r->nvol * sizeof(v3));
+    memset(r->vpos, 0, (size_t)r->nvol * sizeof(v3));
+    const size_t np = (size_t)r->cfg.photon_launch_width * r->prows;
+    for (size_t p = 0; p < np; p++) {
+        if (!r->ev_n[p]) continue;
+        const uint32_t slot = (uint32_t)((uint32_t)p * r->dslot) % r->nvol;
+        r->vcnt[slot] += r->ev_n[p];
+        r->vpow[slot] = r->ev_pow[p];
+        r->vpos[slot] = r->ev_pos[p];
+    }
+    r->vol_R = ppmRadius;
+    r->vol_ready = 1;
 }
 
 /* OptixRenderer_SpatialHash.cu:62-71 (host code: glibc-free detmath pow) */
@@ -1751,6 +2014,10 @@ static void ppm_direct(orc_renderer* r) {
                     r->direct[px] = rec.radiance;
                 continue;
             }
+            if (r->med_on) { /* numShadowSamples = ENABLE_PARTICIPATING_MEDIA ? 0 : 4 (:54) */
+                r->direct[px] = mk1(0.f);
+                continue;
+            }
             uint32_t* rs = r->rng + 6 * ((size_t)y * r->RW + x);
             v3 avg = mk1(0.f);
             for (int s = 0; s < 4; s++) {
@@ -1796,7 +2063,7 @@ static void pt_pass(orc_renderer* r, const cam_t* cam, uint64_t local) {
             v3 fin = mk1(0);
             for (int i = 0; i < 5; i++) {
                 prd.flags = PRD_PATH_TRACING;
-                trace_radiance(r, o, d, 0.001f, &prd);
+                trace_radiance(r, o, d, 0.001f, &prd, NULL);
                 if (prd.flags & PRD_HIT_EMITTER) {
                     if ((prd.flags & PRD_HIT_SPECULAR) || i == 0) fin = prd.radiance;
                     break;
@@ -1860,6 +2127,10 @@ orx_status orc_render_next_iteration(orc_renderer* r, uint64_t iter, uint64_t lo
     if (det->method != ORX_METHOD_PATH_TRACING && det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING &&
         det->method != ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING)
         return fail(r, ORX_ERR_UNSUPPORTED, "oracle: method not implemented");
+    if (r->med_on && det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
+        return fail(r, ORX_ERR_UNSUPPORTED, "participating media: progressive photon mapping only");
+    if (r->med_on && r->cfg.photon_map == 1)
+        return fail(r, ORX_ERR_UNSUPPORTED, "participating media: uniform grid or kd-tree photon map");
     orx_status s0 = begin_iteration(r, local, det);
     if (s0 != ORX_OK) return s0;
     cam_t cam = camera_setup(&det->camera);
@@ -1871,6 +2142,7 @@ orx_status orc_render_next_iteration(orc_renderer* r, uint64_t iter, uint64_t lo
         ppm_eye_pass(r, &cam);
         const float ppmRadiusSquared = ppmRadius * ppmRadius;
         ppm_photon_pass(r);
+        if (r->med_on) vol_resolve(r, ppmRadius);
         float emittedF = (float)(r->cfg.photon_launch_width * r->cfg.photon_launch_height);
         if (r->cfg.photon_map == 1) {
             ppm_build_hash(r, ppmRadius);
@@ -1884,6 +2156,8 @@ orx_status orc_render_next_iteration(orc_renderer* r, uint64_t iter, uint64_t lo
             if (s != ORX_OK) return s;
             ppm_gather(r, ppmRadius, ppmRadiusSquared, emittedF);
         }
+        if (r->med_on) /* IndirectRadianceEstimation.cu:215-218 */
+            for (size_t i = 0; i < (size_t)r->W * r->rows; i++) r->indirect[i] = add(r->indirect[i], divs(r->volR[i], emittedF));
         ppm_direct(r);
         ppm_output(r, local);
     }
@@ -1893,6 +2167,8 @@ orx_status orc_render_next_iteration(orc_renderer* r, uint64_t iter, uint64_t lo
 /* ---- sharded phase API (mirrors orx_ppm_* in include/orx.h) ---- */
 orx_status orc_set_shard(orc_renderer* r, uint32_t rank, uint32_t world) {
     if (!r || world == 0 || rank >= world) return ORX_ERR_INVALID_ARGUMENT;
+    if (world > 1 && r->cfg.enable_media)
+        return fail(r, ORX_ERR_UNSUPPORTED, "participating media are single-device");
     if (world > 1 && r->cfg.photon_map == 1)
         return fail(r, ORX_ERR_UNSUPPORTED, "the stochastic hash photon map is single-device");
     r->rank = rank;
@@ -1949,18 +2225,26 @@ static inline uint32_t slab_bin(const orc_renderer* r, v3 p, uint32_t a, uint32_
 static size_t local_slots(const orc_renderer* r) {
     return (size_t)r->cfg.photon_launch_width * r->prows * r->cfg.max_photon_deposits;
 }
+static inline uint32_t slab_voxel(const orc_renderer* r, v3 p) {
+    const uint32_t V = ORX_SLAB_VOXELS;
+    return slab_bin(r, p, 0, V) + V * (slab_bin(r, p, 1, V) + V * slab_bin(r, p, 2, V));
+}
 orx_status orc_ppm_slab_histogram(orc_renderer* r, uint32_t* hist, uint32_t nb) {
-    if (!r || !hist || nb == 0) return ORX_ERR_INVALID_ARGUMENT;
-    memset(hist, 0, (size_t)6 * nb * 4);
+    if (!r || !hist || nb < ORX_SLAB_VOXELS || nb > 1024 || nb % ORX_SLAB_VOXELS) return ORX_ERR_INVALID_ARGUMENT;
+    memset(hist, 0, orx_slab_histogram_words(nb) * 4);
     const size_t S = local_slots(r);
+    const size_t NV = (size_t)ORX_SLAB_VOXELS * ORX_SLAB_VOXELS * ORX_SLAB_VOXELS;
+    uint32_t* hv = hist + 6 * (size_t)nb + 6;
     photon_box_words(r->photons, S, hist + 6 * (size_t)nb);
     for (size_t i = 0; i < S; i++) {
         if (!(fmax3(r->photons[i].power) > 0)) continue;
         for (uint32_t a = 0; a < 3; a++) hist[a * nb + slab_bin(r, r->photons[i].position, a, nb)]++;
+        hv[slab_voxel(r, r->photons[i].position)]++;
     }
     for (size_t i = 0; i < (size_t)r->rows * r->W; i++) {
         if (!(r->hp[i].flags & PRD_HIT_NON_SPECULAR)) continue;
         for (uint32_t a = 0; a < 3; a++) hist[(3 + a) * nb + slab_bin(r, r->hp[i].position, a, nb)]++;
+        hv[NV + slab_voxel(r, r->hp[i].position)]++;
     }
     return ORX_OK;
 }
@@ -2141,4 +2425,5 @@ void orc_default_config(orx_config* c) {
     c->vcm_max_path_length = 10;
     c->seed = 0;
     c->debug_counters = 1;
+    c->volumetric_photons = 200000; /* NUM_VOLUMETRIC_PHOTONS (config.h:35) */
 }

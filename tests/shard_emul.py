@@ -37,8 +37,8 @@ def slab_exchange(shards, world, nb=multigpu.SLAB_BINS):
         h = b.alloc_i32(multigpu.slab_hist_words(nb))
         b.slab_histogram(h, nb)
         hists.append(h)
-    H, box = multigpu.split_slab_hists(torch.stack(hists).cpu().numpy(), world, nb)
-    axis, bin_dest, counts = multigpu.slab_plan(H, world)
+    H, vox, box = multigpu.split_slab_hists(torch.stack(hists).cpu().numpy(), world, nb)
+    axis, bin_dest, counts = multigpu.slab_plan(H, world, vox)
     sends = []
     for rank, b in enumerate(shards):
         n = counts[rank]

@@ -142,6 +142,33 @@ def test_slab_plan_properties():
     assert c0.sum() == 0 and d0.max() < 2
 
 
+def test_slab_plan_voxel_weights():
+    """With voxel counts the gather term weighs a hit point by the photons of its voxel: hit points
+    spread evenly along x, photons all in the voxel layer of the first x-quarter -> the first rank
+    gets a thin slab of that layer, and the split follows the voxel cost, not the hit-point count."""
+    V, nb, world = multigpu.SLAB_VOXELS, 256, 4
+    hists = np.zeros((world, 2, 3, nb), np.uint32)
+    vox = np.zeros((world, 2, V, V, V), np.uint32)  # [z][y][x]
+    hists[:, 1, 0, :] = 10                           # hit points: uniform in x
+    hists[:, 1, 1, nb // 2] = 10 * nb                # ... all in one y and one z bin
+    hists[:, 1, 2, nb // 2] = 10 * nb
+    vox[:, 1, V // 2, V // 2, :] = 10 * (nb // V)
+    hists[:, 0, 0, 0:nb // V] = 100                  # photons in the first x voxel layer
+    hists[:, 0, 1, nb // 2] = 100 * (nb // V)
+    hists[:, 0, 2, nb // 2] = 100 * (nb // V)
+    vox[:, 0, V // 2, V // 2, 0] = 100 * (nb // V)
+    axis, dest, counts = multigpu.slab_plan(hists, world, vox.reshape(world, 2, -1))
+    assert axis == 0
+    assert np.all(np.diff(dest.astype(int)) >= 0)
+    # the first layer's bins (the whole gather cost) are split over the ranks, not one rank's
+    assert len(set(dest[:nb // V].tolist())) >= 3
+    w = multigpu.slab_hist_words(nb)
+    words = np.arange(world * w, dtype=np.uint32).reshape(world, w)
+    h2, v2, box = multigpu.split_slab_hists(words.view(np.int32), world, nb)
+    assert h2.shape == (world, 2, 3, nb) and v2.shape == (world, 2, V ** 3)
+    assert box[0] == words[:, 6 * nb].min() and box[5] == words[:, 6 * nb + 5].max()
+
+
 @pytest.mark.parametrize("world,W,H", [(2, 40, 32), (3, 36, 29)])
 def test_sharded_vcm_matches_single(world, W, H):
     """VCM row sharding: own-row light + camera subpaths, splats reduce-scattered."""

@@ -145,8 +145,8 @@ def run_slab(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None, nb=mult
             ms[k]["hist_pack"] += timed(lambda: b.slab_histogram(h, nb))
             hists.append(h)
         hp_all.copy_(torch.cat(hps))
-        Hh, box = multigpu.split_slab_hists(torch.stack(hists).cpu().numpy(), world, nb)
-        axis, bin_dest, counts = multigpu.slab_plan(Hh, world)
+        Hh, vox, box = multigpu.split_slab_hists(torch.stack(hists).cpu().numpy(), world, nb)
+        axis, bin_dest, counts = multigpu.slab_plan(Hh, world, vox)
         sends = []
         for k, b in enumerate(shards):
             n = counts[k]
