@@ -227,7 +227,11 @@ typedef enum {
        node i's children at 2i+1, 2i+2; per node power3 position3 direction3 axis(uint32 bits: PPM_X 1, PPM_Y 2,
        PPM_Z 4, PPM_LEAF 8, PPM_NULL 16, config.h:12-16).  Only nodes reachable from the root are defined (the
        reference never clears the buffer; a NULL node defines axis and power only). */
-    ORX_BUF_KD_TREE = 13
+    ORX_BUF_KD_TREE = 13,
+    /* participating medium (orx_config.enable_media) */
+    ORX_BUF_VOLUMETRIC = 14,        /* float [W*H][3]: the last eye pass's Hitpoint::volumetricRadiance */
+    ORX_BUF_VOLUMETRIC_PHOTONS = 15 /* float [volumetric_photons][7]: the last photon pass's volumetric photon
+                                       table, power3 position3 numDeposits(uint32 bits); 0 when empty */
 } orx_buffer_id;
 /* Copies buffer `id` to host; returns the byte size through *out_bytes
  * (call with dst=NULL to query). */

@@ -50,6 +50,8 @@ BUF_VCM_VERTICES = 10
 BUF_VCM_SPLAT = 11
 BUF_VCM_CAMERA = 12
 BUF_KD_TREE = 13
+BUF_VOLUMETRIC = 14
+BUF_VOLUMETRIC_PHOTONS = 15
 
 # RadiancePRD.h:30-35 flag bits
 PRD_HIT_EMITTER = 1 << 31

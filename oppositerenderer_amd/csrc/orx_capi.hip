@@ -425,6 +425,12 @@ struct orx_renderer {
     VcmConsts vcm_c{};
     DevBuf d_vcount, d_vverts, d_vsplat, d_vcam, d_vkd, d_vshq, d_vwork, d_tstats;
     std::vector<DevLight> host_lights;
+    /* participating medium (cfg.enable_media with a medium box): the box, this frame's per-pixel
+     * volumetricRadiance and per-photon last events, the volumetric table of the last photon pass */
+    bool media = false;
+    VolMap vm{};
+    DevBuf d_volR, d_ev_a, d_ev_b;
+    DevBuf d_vcnt, d_vwin, d_vA, d_vB, d_vkeys, d_vvals, d_vkeys2, d_vvals2, d_vsort, d_vstart, d_vrec;
 };
 
 static orx_status set_err(orx_renderer* r, orx_status s, const std::string& m) {
@@ -475,6 +481,7 @@ void orx_default_config(orx_config* c) {
     c->vcm_max_path_length = 10;
     c->seed = 0;
     c->debug_counters = 1;
+    c->volumetric_photons = 200000; /* NUM_VOLUMETRIC_PHOTONS (config.h:35) */
 }
 
 /* stochastic hash: photonsSize = NUM_PHOTONS must be a power of two (getHashValue masks with
@@ -555,6 +562,8 @@ void* orx_stream(orx_renderer* r) { return r ? (void*)r->stream : nullptr; }
 
 orx_status orx_set_shard(orx_renderer* r, uint32_t rank, uint32_t world) {
     if (!r || world == 0 || rank >= world) return ORX_ERR_INVALID_ARGUMENT;
+    if (world > 1 && r->cfg.enable_media)
+        return set_err(r, ORX_ERR_UNSUPPORTED, "participating media are single-device");
     if (world > 1 && r->cfg.photon_map == 1)
         return set_err(r, ORX_ERR_UNSUPPORTED, "the stochastic hash photon map is single-device (one table per iteration)");
     r->rank = rank;
@@ -587,6 +596,37 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
         if (s->materials[i].type == ORX_MAT_TEXTURE &&
             (s->materials[i].texture < 0 || (uint32_t)s->materials[i].texture >= s->n_textures))
             return set_err(r, ORX_ERR_INVALID_ARGUMENT, "Texture material without a texture image");
+    const bool media = r->cfg.enable_media && s->n_media;
+    if (media) {
+        if (s->n_media != 1 || !s->media)
+            return set_err(r, ORX_ERR_UNSUPPORTED, "participating media: one medium box per scene");
+        const float* m = s->media;
+        if (!(m[0] < m[3] && m[1] < m[4] && m[2] < m[5]) || !(m[6] >= 0 && m[7] >= 0 && m[6] + m[7] > 0))
+            return set_err(r, ORX_ERR_INVALID_ARGUMENT, "medium box: min < max and sigma_s + sigma_a > 0");
+        if (r->cfg.volumetric_photons == 0)
+            return set_err(r, ORX_ERR_INVALID_ARGUMENT, "volumetric_photons must be > 0 with media");
+        if (r->world > 1) return set_err(r, ORX_ERR_UNSUPPORTED, "participating media are single-device");
+    }
+    r->media = media;
+    r->vm = VolMap{};
+    if (media) {
+        r->vm.on = 1;
+        r->vm.lo = mk(s->media[0], s->media[1], s->media[2]);
+        r->vm.hi = mk(s->media[3], s->media[4], s->media[5]);
+        r->vm.sig_s = s->media[6];
+        r->vm.sig_a = s->media[7];
+        const uint32_t NV = r->cfg.volumetric_photons;
+        HIPCHK(r, r->d_vcnt.ensure((size_t)NV * 4));
+        HIPCHK(r, r->d_vwin.ensure((size_t)NV * 4));
+        HIPCHK(r, r->d_vA.ensure((size_t)NV * 16));
+        HIPCHK(r, r->d_vB.ensure((size_t)NV * 16));
+        HIPCHK(r, r->d_vkeys.ensure((size_t)NV * 4));
+        HIPCHK(r, r->d_vvals.ensure((size_t)NV * 4));
+        HIPCHK(r, r->d_vkeys2.ensure((size_t)NV * 4));
+        HIPCHK(r, r->d_vvals2.ensure((size_t)NV * 4));
+        HIPCHK(r, r->d_vsort.ensure(vol_sort_tmp_bytes(NV) + 256));
+        HIPCHK(r, r->d_vrec.ensure((size_t)NV * 32 + 32));
+    }
     for (uint32_t i = 0; i < nt; i++) {
         if (s->triangle_material[i] >= nm) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "triangle material out of range");
         for (int k = 0; k < 3; k++)
@@ -872,6 +912,13 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     HIPCHK(r, r->d_dir.ensure(nhp * 12));
     HIPCHK(r, r->d_out.ensure(nhp * 12));
     HIPCHK(r, r->d_dbg.ensure(nhp * 8));
+    if (r->media) { /* volumetricRadiance per pixel, last volumetric event per photon */
+        HIPCHK(r, r->d_volR.ensure(nhp * 12));
+        HIPCHK(r, r->d_ev_a.ensure(nphot * 16 + 16));
+        HIPCHK(r, r->d_ev_b.ensure(nphot * 16 + 16));
+        HIPCHK(r, hipMemsetAsync(r->d_volR.p, 0, nhp * 12, r->stream));
+        r->vm.valid = 0;
+    }
     HIPCHK(r, r->d_slots.ensure(S_cap * 64));
     HIPCHK(r, r->d_vmask.ensure(S_cap / D + 1));
     /* 64 photons of tail padding per plane: the union gather loads whole 64-photon chunks (and
@@ -1194,7 +1241,63 @@ static Consts make_consts(orx_renderer* r, float ppm_radius, uint64_t local_iter
     /* emittedPhotonsPerIterationFloat: global launch (all ranks) */
     c.emitted_f = (float)(r->cfg.photon_launch_width * r->cfg.photon_launch_height);
     c.local_iteration = (uint32_t)(local_iteration_number != 0);
+    c.media = r->media ? 1u : 0u;
     return c;
+}
+
+/* The volumetric table's grid for radius R (host): the box padded by 2R, cells >= 1.01 R and at
+ * least the cube root of (volume / table slots), at most 1024 per axis (orx_device.h VolMap) */
+static void vol_grid(orx_renderer* r, float R) {
+    VolMap& vm = r->vm;
+    vm.R = R;
+    const f3 pad = mk1(2.f * R);
+    vm.glo = vm.lo - pad;
+    const f3 ext = (vm.hi + pad) - vm.glo;
+    double cell = std::max((double)R * 1.01, std::cbrt((double)ext.x * ext.y * ext.z / (double)r->cfg.volumetric_photons));
+    cell = std::max(cell, (double)std::max(ext.x, std::max(ext.y, ext.z)) / 1024.0);
+    vm.cell = (float)cell * 1.0001f;
+    const float e[3] = {ext.x, ext.y, ext.z};
+    for (int k = 0; k < 3; k++) vm.n[k] = std::min(1024u, std::max(1u, (uint32_t)std::ceil(e[k] / vm.cell)));
+    vm.G = vm.n[0] * vm.n[1] * vm.n[2];
+    vm.ilo = vm.lo - mk1(R);
+    vm.ihi = vm.hi + mk1(R);
+}
+static MediaBufs media_bufs(orx_renderer* r) {
+    MediaBufs mb;
+    mb.vm = r->vm;
+    mb.vm.start = r->d_vstart.as<uint32_t>();
+    mb.vm.rec = r->d_vrec.as<float4>();
+    mb.volR = r->d_volR.as<float>();
+    mb.ev_a = r->d_ev_a.as<float4>();
+    mb.ev_b = r->d_ev_b.as<float4>();
+    return mb;
+}
+/* after the photon pass: this pass's volumetric table, gathered by the next eye pass with this
+ * iteration's radius (volumetricRadius = PPMRadius after the eye pass, OptixRenderer.cpp:592-593) */
+static orx_status vol_build(orx_renderer* r, hipStream_t st, float R) {
+    vol_grid(r, R);
+    HIPCHK(r, r->d_vstart.ensure(((size_t)r->vm.G + 2) * 4));
+    VolBuild vb;
+    vb.ev_a = r->d_ev_a.as<float4>();
+    vb.ev_b = r->d_ev_b.as<float4>();
+    vb.nphot = r->prows * r->cfg.photon_launch_width;
+    vb.D = r->cfg.max_photon_deposits;
+    vb.NV = r->cfg.volumetric_photons;
+    vb.vcnt = r->d_vcnt.as<uint32_t>();
+    vb.vwin = r->d_vwin.as<uint32_t>();
+    vb.vA = r->d_vA.as<float4>();
+    vb.vB = r->d_vB.as<float4>();
+    vb.keys = r->d_vkeys.as<uint32_t>();
+    vb.vals = r->d_vvals.as<uint32_t>();
+    vb.keys_sorted = r->d_vkeys2.as<uint32_t>();
+    vb.vals_sorted = r->d_vvals2.as<uint32_t>();
+    vb.sort_tmp = r->d_vsort.p;
+    vb.sort_tmp_bytes = vol_sort_tmp_bytes(vb.NV);
+    vb.start = r->d_vstart.as<uint32_t>();
+    vb.rec = r->d_vrec.as<float4>();
+    launch_vol_build(st, vb, r->vm);
+    r->vm.valid = 1;
+    return ORX_OK;
 }
 
 /* resize / RNG init / output clear common to every method (OptixRenderer.cpp:531-557) */
@@ -1239,7 +1342,12 @@ static GatherIn local_gather_in(orx_renderer* r) {
 
 static void ppm_eye(orx_renderer* r, const DevCamera& cam, const Consts& c) {
     ev_begin(r, P_EYE);
-    launch_ppm_eye(cur_stream(r), r->scene, cam, r->px, c);
+    if (r->media) {
+        const MediaBufs mb = media_bufs(r);
+        launch_ppm_eye(cur_stream(r), r->scene, cam, r->px, c, &mb);
+    } else {
+        launch_ppm_eye(cur_stream(r), r->scene, cam, r->px, c);
+    }
     ev_end(r, P_EYE);
 }
 /* initializeStochasticHashPhotonMap (OptixRenderer_SpatialHash.cu:286-302): the scene AABB padded
@@ -1267,7 +1375,13 @@ static void ppm_photons_grid(orx_renderer* r, const Consts& c, bool build_map = 
     hipStream_t st = cur_stream(r);
     ev_begin(r, P_PHOTON);
     r->eye_chain = false;
-    launch_ppm_photon(st, r->scene, r->px, r->pb, c);
+    if (r->media) {
+        const MediaBufs mb = media_bufs(r);
+        launch_ppm_photon(st, r->scene, r->px, r->pb, c, &mb);
+        vol_build(r, st, c.ppm_radius);
+    } else {
+        launch_ppm_photon(st, r->scene, r->px, r->pb, c);
+    }
     ev_end(r, P_PHOTON);
     if (r->overlap_direct) {
         /* the direct pass needs the hitpoints and the RNG states the photon pass
@@ -1504,13 +1618,17 @@ static orx_status render_next_iteration(orx_renderer* r, uint64_t local_iteratio
         return ORX_ERR_UNSUPPORTED;
     if (det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world > 1)
         return set_err(r, ORX_ERR_STATE, "sharded PPM runs through orx_ppm_local_passes/_gather_external/_finish");
+    if (r->media && det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
+        return set_err(r, ORX_ERR_UNSUPPORTED, "participating media: progressive photon mapping only");
+    if (r->media && r->cfg.photon_map == 1)
+        return set_err(r, ORX_ERR_UNSUPPORTED, "participating media: uniform grid or kd-tree photon map");
     static const int pipeline_env = [] {
         const char* e = getenv("ORX_PIPELINE");
         return e ? atoi(e) : 1;
     }();
     const int pipe_on = r->pipe_mode >= 0 ? r->pipe_mode : pipeline_env;
     const bool pipelined = pipe_on && det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world == 1 &&
-                           !r->use_ext;
+                           !r->use_ext && !r->media;
     orx_status s0 = begin_iteration(r, local_iteration_number, det, pipelined);
     if (s0 != ORX_OK) return s0;
     if (pipelined && (s0 = ensure_second_set(r)) != ORX_OK) return s0;
@@ -1536,6 +1654,7 @@ static orx_status render_next_iteration(orx_renderer* r, uint64_t local_iteratio
         if (r->pb.hash) launch_ppm_gather_hash(st, local_gather_in(r), r->pb, hash_params(r, c.ppm_radius), c);
         else if (r->cfg.photon_map == 2) launch_ppm_gather_kd(st, local_gather_in(r), r->pb, r->kd, c);
         else launch_ppm_gather(st, local_gather_in(r), r->pb, c);
+        if (r->media) launch_vol_indirect(st, r->px, r->d_volR.as<float>(), c.emitted_f);
         ev_end(r, P_GATHER);
         ev_begin(r, P_DIRECT);
         HIPCHK(r, hipStreamWaitEvent(st, r->ev_direct_done, 0));
@@ -1553,6 +1672,7 @@ orx_status orx_ppm_local_passes(orx_renderer* r, uint64_t iteration_number, uint
                                 float ppm_radius, const orx_request* det) {
     (void)iteration_number;
     if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
+    if (r->media) return set_err(r, ORX_ERR_UNSUPPORTED, "participating media run through orx_render_next_iteration");
     if (det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
         return set_err(r, ORX_ERR_INVALID_ARGUMENT, "orx_ppm_local_passes needs a PPM request");
     r->last_pipelined = false;
@@ -1571,6 +1691,7 @@ orx_status orx_ppm_local_eye(orx_renderer* r, uint64_t iteration_number, uint64_
                              float ppm_radius, const orx_request* det) {
     (void)iteration_number;
     if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
+    if (r->media) return set_err(r, ORX_ERR_UNSUPPORTED, "participating media run through orx_render_next_iteration");
     if (det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
         return set_err(r, ORX_ERR_INVALID_ARGUMENT, "orx_ppm_local_eye needs a PPM request");
     orx_status s0 = begin_iteration(r, local_iteration_number, det, r->shard_pipe);
@@ -1624,6 +1745,7 @@ orx_status orx_ppm_local_trace(orx_renderer* r, uint64_t iteration_number, uint6
                                float ppm_radius, const orx_request* det) {
     (void)iteration_number;
     if (!r || !det) return ORX_ERR_INVALID_ARGUMENT;
+    if (r->media) return set_err(r, ORX_ERR_UNSUPPORTED, "participating media run through orx_render_next_iteration");
     if (det->method != ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING)
         return set_err(r, ORX_ERR_INVALID_ARGUMENT, "orx_ppm_local_trace needs a PPM request");
     if (!r->slab) return set_err(r, ORX_ERR_STATE, "orx_ppm_local_trace is the slab mode's first phase");
@@ -1944,6 +2066,8 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
     case ORX_BUF_VCM_VERTEX_COUNT: need = r->vcm_npx * 4; break;
     case ORX_BUF_VCM_VERTICES: need = r->vcm_npx * VCM_MAX_VERTS * 64; break;
     case ORX_BUF_VCM_SPLAT: case ORX_BUF_VCM_CAMERA: need = r->vcm_npx * 12; break;
+    case ORX_BUF_VOLUMETRIC: need = r->media ? npx * 12 : 0; break;
+    case ORX_BUF_VOLUMETRIC_PHOTONS: need = r->media ? (size_t)r->cfg.volumetric_photons * 28 : 0; break;
     default: return set_err(r, ORX_ERR_INVALID_ARGUMENT, "unknown buffer id");
     }
     if (out_bytes) *out_bytes = need;
@@ -2061,6 +2185,26 @@ orx_status orx_read_buffer(orx_renderer* r, int32_t id, void* dst, size_t bytes,
     }
     case ORX_BUF_GRID_OFFSETS: HIPCHK(r, d2h(dst, r->pb.hash ? r->d_hcount.p : r->d_offsets.p, need)); break;
     case ORX_BUF_INDIRECT: HIPCHK(r, d2h(dst, r->d_ind.p, need)); break;
+    case ORX_BUF_VOLUMETRIC: if (need) HIPCHK(r, d2h(dst, r->d_volR.p, need)); break;
+    case ORX_BUF_VOLUMETRIC_PHOTONS: {
+        if (!need) break;
+        const size_t NV = r->cfg.volumetric_photons;
+        std::vector<uint32_t> cnt(NV);
+        std::vector<float4> A(NV), B(NV);
+        HIPCHK(r, d2h(cnt.data(), r->d_vcnt.p, NV * 4));
+        HIPCHK(r, d2h(A.data(), r->d_vA.p, NV * 16));
+        HIPCHK(r, d2h(B.data(), r->d_vB.p, NV * 16));
+        float* o = (float*)dst;
+        for (size_t i = 0; i < NV; i++) {
+            const bool on = r->vm.valid && cnt[i];
+            float v[7] = {on ? B[i].x : 0.f, on ? B[i].y : 0.f, on ? B[i].z : 0.f,
+                          on ? A[i].x : 0.f, on ? A[i].y : 0.f, on ? A[i].z : 0.f, 0.f};
+            const uint32_t c = on ? cnt[i] : 0u;
+            std::memcpy(&v[6], &c, 4);
+            std::memcpy(o + 7 * i, v, sizeof v);
+        }
+        break;
+    }
     case ORX_BUF_DIRECT: HIPCHK(r, d2h(dst, r->d_dir.p, need)); break;
     case ORX_BUF_OUTPUT: HIPCHK(r, d2h(dst, r->d_out.p, need)); break;
     case ORX_BUF_DEBUG_VISITED: HIPCHK(r, d2h(dst, r->d_dbg.p, need)); break;

@@ -965,6 +965,281 @@ __device__ inline void trace_radiance(const DevScene& S, uint32_t maxd, f3 o, f3
     }
 }
 
+/* ------------------------------------------------------------------ */
+/* participating medium (cfg.enable_media, ENABLE_PARTICIPATING_MEDIA) */
+/* ------------------------------------------------------------------ */
+constexpr int32_t MED_PRIM = 0x7ffffff0; /* Hit::prim of the medium box (after every surface) */
+/* The medium box and the volumetric photon table of the last photon pass: a uniform grid of
+ * cells >= 1.01 R over the box padded by 2R (records of the cells in cell order, slot order
+ * inside a cell, then the photons outside that box), read by the next eye pass. */
+struct VolMap {
+    uint32_t on;              /* media enabled */
+    f3 lo, hi;                /* the box */
+    float sig_s, sig_a;
+    uint32_t valid;           /* a photon pass has filled the table (else it gathers nothing) */
+    float R;                  /* volumetricRadius of the table */
+    f3 glo;                   /* grid origin (box - 2R) */
+    float cell;
+    uint32_t n[3], G;         /* cells per axis, G = n0 n1 n2; bucket G: outside the grid */
+    f3 ilo, ihi;              /* box +- R: a segment with both ends inside uses the grid */
+    const uint32_t* start;    /* [G + 2]: start[c] first record of cell c, start[G + 1] = total */
+    const float4* rec;        /* [total][2]: pos.xyz, pw.x | pw.y, pw.z (pw = power * numDeposits) */
+};
+
+/* geometry_instance/AAB.cu:24-157: slab test with the near/far axes; inside the box (tNear < 0.01,
+ * tFar > 0) RADIANCE/PHOTON rays report t = 0.000115 with the far axis' normal against the ray,
+ * the IN_PARTICIPATING_MEDIUM types report tFar with the normal along it */
+__device__ __forceinline__ bool isect_medium(const VolMap& vm, f3 o, f3 d, float tmin, float tmax, bool in_medium,
+                                             float& tout, f3& nout) {
+    int axn = 0, axf = 0;
+    float tn, tf;
+    const float divx = 1 / d.x;
+    if (divx >= 0) { tn = (vm.lo.x - o.x) * divx; tf = (vm.hi.x - o.x) * divx; }
+    else { tn = (vm.hi.x - o.x) * divx; tf = (vm.lo.x - o.x) * divx; }
+    if (tf < tn) return false;
+    const float divy = 1 / d.y;
+    float tyn, tyf;
+    if (divy >= 0) { tyn = (vm.lo.y - o.y) * divy; tyf = (vm.hi.y - o.y) * divy; }
+    else { tyn = (vm.hi.y - o.y) * divy; tyf = (vm.lo.y - o.y) * divy; }
+    if (tyn > tn) { tn = tyn; axn = 1; }
+    if (tyf < tf) { tf = tyf; axf = 1; }
+    if (tf < tn) return false;
+    const float divz = 1 / d.z;
+    float tzn, tzf;
+    if (divz >= 0) { tzn = (vm.lo.z - o.z) * divz; tzf = (vm.hi.z - o.z) * divz; }
+    else { tzn = (vm.hi.z - o.z) * divz; tzf = (vm.lo.z - o.z) * divz; }
+    if (tzn > tn) { tn = tzn; axn = 2; }
+    if (tzf < tf) { tf = tzf; axf = 2; }
+    if (tf < tn) return false;
+    float t = tn, nvr = -1;
+    int ax = axn;
+    if (tn < 0.01f && tf > 0.0f) {
+        ax = axf;
+        if (!in_medium) t = (float)0.000115;
+        else { t = tf; nvr = 1; }
+    }
+    if (!(t > tmin && t < tmax)) return false;
+    const float dc = ax == 0 ? d.x : ax == 1 ? d.y : d.z;
+    const float nc = dc >= 0 ? nvr : -nvr;
+    nout = mk(ax == 0 ? nc : 0.f, ax == 1 ? nc : 0.f, ax == 2 ? nc : 0.f);
+    tout = t;
+    return true;
+}
+/* closest hit with the medium box as the last primitive (a surface at the same t wins) */
+template <class STK, class NODES>
+__device__ __forceinline__ bool trace_closest_m(const DevScene& S, const VolMap& vm, f3 o, f3 d, float tmin, float tmax,
+                                                bool in_medium, Hit& h, const STK& stk, const NODES& nodes) {
+    const bool hit = trace_closest_t(S, o, d, tmin, tmax, h, stk, nodes);
+    float t;
+    f3 n;
+    if (isect_medium(vm, o, d, tmin, hit ? h.t : tmax, in_medium, t, n)) {
+        h.t = t;
+        h.prim = MED_PRIM;
+        h.sn = n;
+        h.b = h.g = 0.f;
+        return true;
+    }
+    return hit;
+}
+
+/* The volumetric gather of one segment (VolumetricPhotonSphere.cu:24-59 +
+ * VolumetricPhotonSphereRadiance.cu:24-34): every root of a photon's sphere inside (tmin, tmax)
+ * adds the photon when its projection on the ray lies inside (tmin, tmax) (a photon with both
+ * roots inside counts twice).  The photons are found by walking the grid cells of the segment
+ * (3D DDA) and testing the 3x3x3 neighbourhood of each: cells are >= 1.01 R, so a photon within
+ * R of a segment point lies in the neighbourhood of that point's cell, and the neighbourhoods
+ * of consecutive cells differ by one 3x3 face, which is all a step visits (the walk is monotone
+ * per axis, so no cell is visited twice).  A segment not inside box +- R (it can leave the box
+ * only through a grazing corner) tests every record. */
+__device__ __forceinline__ void vol_test(const VolMap& vm, uint32_t i, f3 o, f3 d, float tmin, float tmax, float R2,
+                                         float coef, float sig_t, f3& acc) {
+    const float4 A = vm.rec[2 * i], B = vm.rec[2 * i + 1];
+    const f3 pos = mk(A.x, A.y, A.z);
+    const f3 O = o - pos;
+    const float b = dot(O, d), c = dot(O, O) - R2, disc = b * b - c;
+    if (!(disc > 0.0f)) return;
+    const float sd = sqrtf(disc), r1 = -b - sd, r2 = -b + sd;
+    const float t = dot(pos - o, d);
+    if (!(t < tmax && t > tmin)) return;
+    const f3 pw = mk(A.w, B.x, B.y);
+    const f3 add1 = ((pw * coef) * orx_expf(-sig_t * t)) * (1.f / (4.f * ORX_PI_F));
+    if (r1 > tmin && r1 < tmax) acc = acc + add1;
+    if (r2 > tmin && r2 < tmax) acc = acc + add1;
+}
+__device__ __forceinline__ void vol_cell(const VolMap& vm, int x, int y, int z, f3 o, f3 d, float tmin, float tmax,
+                                         float R2, float coef, float sig_t, f3& acc) {
+    if (x < 0 || y < 0 || z < 0 || x >= (int)vm.n[0] || y >= (int)vm.n[1] || z >= (int)vm.n[2]) return;
+    const uint32_t c = (uint32_t)x + vm.n[0] * ((uint32_t)y + vm.n[1] * (uint32_t)z);
+    const uint32_t e = vm.start[c + 1];
+    for (uint32_t i = vm.start[c]; i < e; i++) vol_test(vm, i, o, d, tmin, tmax, R2, coef, sig_t, acc);
+}
+__device__ inline f3 vol_gather(const VolMap& vm, f3 o, f3 d, float tmin, float tmax, float sig_t) {
+    f3 acc = mk1(0.f);
+    if (!vm.valid || !(tmax > tmin)) return acc;
+    const float R = vm.R, R2 = R * R, coef = 1 / (ORX_PI_F * R * R);
+    const f3 p0 = o + d * tmin, p1 = o + d * tmax;
+    const bool in0 = p0.x >= vm.ilo.x && p0.y >= vm.ilo.y && p0.z >= vm.ilo.z && p0.x <= vm.ihi.x &&
+                     p0.y <= vm.ihi.y && p0.z <= vm.ihi.z;
+    const bool in1 = p1.x >= vm.ilo.x && p1.y >= vm.ilo.y && p1.z >= vm.ilo.z && p1.x <= vm.ihi.x &&
+                     p1.y <= vm.ihi.y && p1.z <= vm.ihi.z;
+    if (!(in0 && in1)) {
+        const uint32_t total = vm.start[vm.G + 1];
+        for (uint32_t i = 0; i < total; i++) vol_test(vm, i, o, d, tmin, tmax, R2, coef, sig_t, acc);
+        return acc;
+    }
+    const float inv = 1.f / vm.cell;
+    const float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z}, pp[3] = {p0.x, p0.y, p0.z};
+    const float gl[3] = {vm.glo.x, vm.glo.y, vm.glo.z};
+    int c[3], st[3];
+    float tn[3];
+    for (int k = 0; k < 3; k++) {
+        int ck = (int)orx_floorf((pp[k] - gl[k]) * inv);
+        ck = ck < 0 ? 0 : (ck >= (int)vm.n[k] ? (int)vm.n[k] - 1 : ck);
+        c[k] = ck;
+        st[k] = dd[k] > 0.f ? 1 : (dd[k] < 0.f ? -1 : 0);
+        tn[k] = st[k] ? (gl[k] + (float)(ck + (st[k] > 0)) * vm.cell - oo[k]) / dd[k] : INFINITY;
+    }
+    for (int dz = -1; dz <= 1; dz++)
+        for (int dy = -1; dy <= 1; dy++)
+            for (int dx = -1; dx <= 1; dx++)
+                vol_cell(vm, c[0] + dx, c[1] + dy, c[2] + dz, o, d, tmin, tmax, R2, coef, sig_t, acc);
+    const int maxsteps = (int)(vm.n[0] + vm.n[1] + vm.n[2]) + 3;
+    for (int s = 0; s < maxsteps; s++) {
+        const int k = tn[0] <= tn[1] ? (tn[0] <= tn[2] ? 0 : 2) : (tn[1] <= tn[2] ? 1 : 2);
+        if (!(tn[k] <= tmax)) break;
+        c[k] += st[k];
+        if (c[k] < 0 || c[k] >= (int)vm.n[k]) break;
+        tn[k] = (gl[k] + (float)(c[k] + (st[k] > 0)) * vm.cell - oo[k]) / dd[k];
+        const int f = c[k] + st[k]; /* the neighbourhood's new face */
+        const int u = (k + 1) % 3, v = (k + 2) % 3;
+        for (int a = -1; a <= 1; a++)
+            for (int b2 = -1; b2 <= 1; b2++) {
+                int q[3];
+                q[k] = f;
+                q[u] = c[u] + a;
+                q[v] = c[v] + b2;
+                vol_cell(vm, q[0], q[1], q[2], o, d, tmin, tmax, R2, coef, sig_t, acc);
+            }
+    }
+    return acc;
+}
+
+/* trace_radiance with the medium (ParticipatingMedium.cu:53-104; the frames and their unrolled
+ * accumulation are described at the oracle's trace_radiance): volR = the path's
+ * Hitpoint::volumetricRadiance, the attenuation leaves multiplied by every frame's T. */
+__device__ inline void trace_radiance_vol(const DevScene& S, const VolMap& vm, uint32_t maxd, f3 o, f3 d, float tmin,
+                                          RadiancePRD& prd, Rng& rs, uint32_t* stk, f3& volR) {
+    const float sig_t = vm.sig_a + vm.sig_s;
+    bool inmed = false, frame = false;
+    f3 fa = mk1(0.f), fh = mk1(0.f), fd = mk1(0.f);
+    float P = 1.f;
+    volR = mk1(0.f);
+    for (;;) {
+        Hit h;
+        const bool hit = trace_closest_m(S, vm, o, d, tmin, RT_DEFAULT_MAX, inmed, h, StackL{stk}, NodesG{});
+        if (frame) {
+            frame = false;
+            float dist = 0.f;
+            if (hit) {
+                if (h.prim == MED_PRIM) {
+                    dist = (float)(((double)h.t + 0.1) - 0.1);
+                } else {
+                    const DevMaterial& fm = S.mats[prim_material(S, h)];
+                    if (fm.type != MAT_EMITTER || !(dot(shading_normal(S, h), -d) < 0.f)) dist = h.t;
+                }
+            }
+            const float T = orx_expf(-dist * sig_t);
+            const f3 V = vol_gather(vm, fh, fd, (float)0.0000001, dist, sig_t);
+            volR = volR + (fa * V) * P;
+            P = P * T;
+        }
+        if (!hit) {
+            prd.flags = PRD_MISS;
+            prd.attenuation = mk1(0.f);
+            prd.radiance = mk1(0.f);
+            break;
+        }
+        const f3 hitPoint = o + d * h.t;
+        if (h.prim == MED_PRIM) {
+            const f3 N = normalize(h.sn);
+            if (dot(N, d) < 0) {
+                frame = true;
+                fa = (prd.attenuation + mk1(0.1f)) - mk1(0.1f);
+                fh = hitPoint;
+                fd = d;
+                inmed = true;
+            } else {
+                inmed = false;
+            }
+            o = hitPoint;
+            tmin = 0.01f;
+            continue;
+        }
+        const DevMaterial& m = S.mats[prim_material(S, h)];
+        const f3 N = shading_normal(S, h);
+        if (m.type == MAT_DIFFUSE || m.type == MAT_GLOSSY) {
+            prd.flags |= PRD_HIT_NON_SPECULAR;
+            prd.attenuation = prd.attenuation * m.Kd;
+            prd.normal = N;
+            prd.position = hitPoint;
+            prd.depth++;
+            break;
+        } else if (m.type == MAT_TEXTURE) {
+            prd.flags |= PRD_HIT_NON_SPECULAR;
+            prd.normal = tex_normal(S, m, h, N);
+            prd.position = hitPoint;
+            prd.attenuation = prd.attenuation * tex_color(S, m, h);
+            break;
+        } else if (m.type == MAT_EMITTER) {
+            prd.flags |= PRD_HIT_EMITTER;
+            if (dot(N, -d) < 0.f) break;
+            const f3 Le = m.powerPerArea / ORX_PI_F;
+            prd.radiance = prd.radiance + prd.attenuation * Le;
+            break;
+        } else if (m.type == MAT_MIRROR) {
+            prd.depth++;
+            if (prd.depth <= maxd) {
+                prd.attenuation = prd.attenuation * m.Kr;
+                d = reflect(d, N);
+                o = hitPoint;
+                tmin = 0.0001f;
+                inmed = false;
+                continue;
+            }
+            break;
+        } else { /* glass */
+            const bool outside = dot(N, d) < 0;
+            const f3 Nn = outside ? N : -N;
+            const float n1 = outside ? 1.0f : m.ior, n2 = outside ? m.ior : 1.0f;
+            f3 refr;
+            bool valid;
+            const float refl = glass_reflect_factor(d, Nn, n1, n2, refr, valid);
+            const float sample = rnd(rs);
+            const bool reflected = sample <= refl;
+            f3 nd;
+            if (reflected) {
+                nd = reflect(d, Nn);
+            } else {
+                nd = refr;
+                prd.attenuation = prd.attenuation * ((n2 * n2) / (n1 * n1));
+            }
+            prd.flags |= PRD_HIT_SPECULAR;
+            prd.flags &= ~PRD_HIT_NON_SPECULAR;
+            prd.depth++;
+            if (prd.depth <= maxd) {
+                o = hitPoint;
+                d = nd;
+                tmin = 0.0001f;
+                inmed = (outside && !reflected) || (!outside && reflected);
+                continue;
+            }
+            prd.attenuation = prd.attenuation * 0.f;
+            break;
+        }
+    }
+    prd.attenuation = prd.attenuation * P;
+}
+
 /* getLightContribution (helpers/light.h:29-87) */
 __device__ inline f3 light_contribution(const DevScene& S, const DevLight& light, f3 pos, f3 normal, Rng& rs,
                                         uint32_t* stk) {

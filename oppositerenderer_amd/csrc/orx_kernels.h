@@ -141,7 +141,40 @@ struct Consts {
     float ppm_radius2;
     float emitted_f;    /* emittedPhotonsPerIterationFloat (global count) */
     uint32_t local_iteration;
+    uint32_t media;     /* participating medium on: no shadow samples in the direct pass */
 };
+
+/* participating medium: the box + volumetric table (VolMap, orx_device.h), the eye pass's
+ * per-pixel volumetricRadiance and the photon pass's per-photon last volumetric event */
+struct MediaBufs {
+    VolMap vm;
+    float* volR;   /* [rows*W*3] */
+    float4* ev_a;  /* [photons]: last event position, event count bits */
+    float4* ev_b;  /* [photons]: its power */
+};
+/* the volumetric photon table of one photon pass and its grid (orx_media.hip) */
+struct VolBuild {
+    const float4* ev_a;
+    const float4* ev_b;
+    uint32_t nphot, D, NV;          /* photons, max deposits (pm_index stride), table slots */
+    uint32_t* vcnt;                 /* [NV] numDeposits */
+    uint32_t* vwin;                 /* [NV] winning photon + 1 */
+    float4* vA;                     /* [NV] position */
+    float4* vB;                     /* [NV] power */
+    uint32_t* keys;                 /* [NV] cell, G (outside the grid) or G + 1 (empty) */
+    uint32_t* vals;                 /* [NV] slot */
+    uint32_t* keys_sorted;
+    uint32_t* vals_sorted;
+    void* sort_tmp;
+    size_t sort_tmp_bytes;
+    uint32_t* start;                /* [G + 2] */
+    float4* rec;                    /* [NV][2] */
+};
+size_t vol_sort_tmp_bytes(uint32_t NV);
+/* clear + resolve + grid + sort + records; vm: the grid parameters (host) */
+void launch_vol_build(hipStream_t s, const VolBuild& vb, const VolMap& vm);
+/* indirect += volR / emitted (IndirectRadianceEstimation.cu:215-218) */
+void launch_vol_indirect(hipStream_t s, const PixelBufs& px, const float* volR, float emitted_f);
 
 /* on-device BVH build (orx_bvh.hip): V float3 [n_vertices], I uint3 [nt] on the
  * device; writes out4 (capacity cap4 nodes) and leaf_order [nt] */
@@ -150,8 +183,10 @@ hipError_t device_build_bvh4(hipStream_t s, const float* V, const uint32_t* I, u
                              uint32_t* stack_bound, uint32_t* max_depth, bool* ok);
 void launch_rng_init(hipStream_t s, RngPlanes rng, uint32_t RW, uint32_t rows, uint32_t rank, uint32_t world,
                      uint32_t seed);
-void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c);
-void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c);
+void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c,
+                    const MediaBufs* mb = nullptr);
+void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c,
+                       const MediaBufs* mb = nullptr);
 void launch_grid_setup(hipStream_t s, const PhotonBufs& pb, const GridBox& gb = GridBox{});
 /* atomic-free grid build: keys + bucket histogram / scan of the table /
  * bucket placement + per-bucket cells (offsets, permutation) + permute */

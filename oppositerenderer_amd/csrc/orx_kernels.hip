@@ -94,7 +94,9 @@ static dim3 pix_grid(const PixelBufs& px) {
 /* ------------------------------------------------------------------ */
 /* PPM eye pass                                                        */
 /* ------------------------------------------------------------------ */
-__global__ __launch_bounds__(64) void k_ppm_eye(DevScene S, DevCamera cam, PixelBufs px, Consts c) {
+template <bool MEDIA>
+__global__ __launch_bounds__(64) void k_ppm_eye(DevScene S, DevCamera cam, PixelBufs px, Consts c, VolMap vm,
+                                                float* volR) {
     ORX_STACK_DECL;
     uint32_t x, j;
     pix_tile(px, x, j);
@@ -112,13 +114,24 @@ __global__ __launch_bounds__(64) void k_ppm_eye(DevScene S, DevCamera cam, Pixel
     prd.newdir = mk1(0.f);
     f3 o, d;
     primary_ray(cam, x, y, px.W, px.H, rs, o, d);
-    trace_radiance(S, c.max_radiance_depth, o, d, 0.001f, prd, rs, ORX_STACK_PTR);
+    if (MEDIA) {
+        f3 vr;
+        trace_radiance_vol(S, vm, c.max_radiance_depth, o, d, 0.001f, prd, rs, ORX_STACK_PTR, vr);
+        const size_t i = (size_t)j * px.W + x;
+        volR[3 * i + 0] = vr.x;
+        volR[3 * i + 1] = vr.y;
+        volR[3 * i + 2] = vr.z;
+    } else {
+        trace_radiance(S, c.max_radiance_depth, o, d, 0.001f, prd, rs, ORX_STACK_PTR);
+    }
     store_hitpoint(px, (size_t)j * px.W + x, prd);
     rng_store(px.rng, slot, rs);
 }
-void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c) {
+void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c,
+                    const MediaBufs* mb) {
     const dim3 grid = pix_grid(px);
-    hipLaunchKernelGGL(k_ppm_eye, grid, dim3(64), ORX_STACK_BYTES(S), s, S, cam, px, c);
+    if (mb) hipLaunchKernelGGL((k_ppm_eye<true>), grid, dim3(64), ORX_STACK_BYTES(S), s, S, cam, px, c, mb->vm, mb->volR);
+    else hipLaunchKernelGGL((k_ppm_eye<false>), grid, dim3(64), ORX_STACK_BYTES(S), s, S, cam, px, c, VolMap{}, nullptr);
 }
 
 /* ------------------------------------------------------------------ */
@@ -136,6 +149,14 @@ struct PhotonPath {
     float weight, tmin;
     uint32_t p_local, depth, numStored, mask;
     size_t slot;
+};
+/* the medium's extra photon state (ParticipatingMedium.cu:110-201): ray type and tmax, the open
+ * scatter probe (depth at its start, scatter position) and the volumetric events so far */
+struct PhotonMedia {
+    float tmax;
+    bool inmed, probe;
+    uint32_t pdepth, nev;
+    f3 spos, ev_pos, ev_pow;
 };
 __device__ __forceinline__ void photon_emit(const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, uint32_t p,
                                             PhotonPath& P, Rng& rs) {
@@ -192,16 +213,48 @@ __device__ __forceinline__ void photon_emit(const DevScene& S, const PixelBufs& 
 /* One bounce of a photon path (Diffuse.cu:92-135, Glossy.cu:94-137, Mirror.cu:65-77,
  * Glass.cu:164-205, DiffuseEmitter.cu:56-59); false once the path has ended (its
  * deposit mask and RNG state are then stored). */
-template <class STK, class NODES>
+template <bool MEDIA, class STK, class NODES>
 __device__ __forceinline__ bool photon_bounce(const DevScene& S, const PixelBufs& px, const PhotonBufs& pb,
                                               const Consts& c, PhotonPath& P, Rng& rs, const STK& stk,
                                               const NODES& nodes, float& lo_x, float& lo_y, float& lo_z,
-                                              float& hi_x, float& hi_y, float& hi_z) {
+                                              float& hi_x, float& hi_y, float& hi_z, const VolMap& vm,
+                                              PhotonMedia& M, const MediaBufs& mb) {
     bool done = false;
     Hit h;
-    if (!trace_closest_t(S, P.o, P.d, P.tmin, RT_DEFAULT_MAX, h, stk, nodes)) {
-        done = true;
+    bool had_probe = false;
+    bool hit;
+    if (MEDIA) {
+        had_probe = M.probe;
+        M.probe = false;
+        hit = trace_closest_m(S, vm, P.o, P.d, P.tmin, M.tmax, M.inmed, h, stk, nodes);
     } else {
+        hit = trace_closest_t(S, P.o, P.d, P.tmin, RT_DEFAULT_MAX, h, stk, nodes);
+    }
+    if (!hit) {
+        done = true;
+    } else if (MEDIA && h.prim == MED_PRIM) {
+        P.depth++;
+        const f3 N = normalize(h.sn);
+        const f3 hitPoint = P.o + P.d * h.t;
+        if (dot(N, P.d) > 0 && M.inmed) { /* leaving the box */
+            P.o = hitPoint + P.d * 0.0001f;
+            P.tmin = 0.001f;
+            M.tmax = RT_DEFAULT_MAX;
+            M.inmed = false;
+        } else { /* sample the scatter distance, probe [0.001, scatterT] */
+            const float sig_t = vm.sig_a + vm.sig_s;
+            const float sample = rnd(rs);
+            const float st = -orx_logf(1 - sample) / sig_t;
+            M.spos = hitPoint + P.d * st;
+            M.probe = true;
+            M.pdepth = P.depth;
+            P.o = hitPoint;
+            P.tmin = 0.001f;
+            M.tmax = st;
+            M.inmed = true;
+        }
+    } else {
+        if (MEDIA) M.tmax = RT_DEFAULT_MAX;
         const DevMaterial& m = S.mats[prim_material(S, h)];
         const f3 hitPoint = P.o + P.d * h.t;
         if (m.type == MAT_DIFFUSE || m.type == MAT_GLOSSY || m.type == MAT_TEXTURE) {
@@ -244,9 +297,11 @@ __device__ __forceinline__ bool photon_bounce(const DevScene& S, const PixelBufs
                     P.d = sample_hemisphere_cos(N, s0, s1);
                     P.o = hitPoint;
                     P.tmin = tex ? 0.01f : 0.0001f;
+                    if (MEDIA) M.inmed = false;
                 }
             }
         } else if (m.type == MAT_EMITTER) {
+            if (MEDIA && !M.inmed) P.depth++; /* closestHitPhoton is the PHOTON program only */
             done = true;
         } else if (m.type == MAT_MIRROR) {
             const f3 N = shading_normal(S, h);
@@ -256,6 +311,7 @@ __device__ __forceinline__ bool photon_bounce(const DevScene& S, const PixelBufs
                 P.d = reflect(P.d, N);
                 P.o = hitPoint;
                 P.tmin = 0.0001f;
+                if (MEDIA) M.inmed = false;
             } else {
                 done = true;
             }
@@ -268,20 +324,43 @@ __device__ __forceinline__ bool photon_bounce(const DevScene& S, const PixelBufs
             bool valid;
             const float refl = glass_reflect_factor(P.d, N, n1, n2, refr, valid);
             const float sample = rnd(rs);
-            const f3 nd = (sample <= refl) ? reflect(P.d, N) : refr;
+            const bool reflected = sample <= refl;
+            const f3 nd = reflected ? reflect(P.d, N) : refr;
             P.depth++;
             if (P.depth <= c.max_photon_depth) {
                 P.o = hitPoint;
                 P.d = nd;
                 P.tmin = 0.0001f;
+                if (MEDIA) M.inmed = (outside && !reflected) || (!outside && reflected);
             } else {
                 done = true;
+            }
+        }
+    }
+    if (MEDIA && had_probe && P.depth == M.pdepth) { /* the probe met nothing that took the path over */
+        done = true;
+        if (rnd(rs) < vm.sig_s / (vm.sig_a + vm.sig_s)) {
+            M.nev++;
+            M.ev_pos = M.spos;
+            M.ev_pow = P.power;
+            if (P.depth < c.max_photon_depth) {
+                const float s0 = rnd(rs), s1 = rnd(rs);
+                P.d = sample_unit_sphere(s0, s1);
+                P.o = M.spos;
+                P.tmin = 0.001f;
+                M.tmax = RT_DEFAULT_MAX;
+                M.inmed = false;
+                done = false;
             }
         }
     }
     if (done) {
         pb.vmask[P.p_local] = (uint8_t)P.mask;
         rng_store(px.rng, P.slot, rs);
+        if (MEDIA) {
+            mb.ev_a[P.p_local] = make_float4(M.ev_pos.x, M.ev_pos.y, M.ev_pos.z, __uint_as_float(M.nev));
+            mb.ev_b[P.p_local] = make_float4(M.ev_pow.x, M.ev_pow.y, M.ev_pow.z, 0.f);
+        }
         return false;
     }
     return true;
@@ -305,7 +384,8 @@ __device__ __forceinline__ void photon_bbox_flush(const PhotonBufs& pb, float lo
 /* one photon per lane: block b traces photons [64b, 64b + 64) (per-lane refill from a device
  * counter, a wavefront pass with per-bounce queues and a direction-binned photon order were
  * measured slower on the hall: DESIGN.md section 4) */
-__global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, PhotonBufs pb, Consts c) {
+template <bool MEDIA>
+__global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, PhotonBufs pb, Consts c, MediaBufs mb) {
     ORX_STACK_DECL;
     const StackL stk{ORX_STACK_PTR};
     const uint32_t lane = threadIdx.x;
@@ -313,20 +393,33 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
     float lo_x = INFINITY, lo_y = INFINITY, lo_z = INFINITY;
     float hi_x = -INFINITY, hi_y = -INFINITY, hi_z = -INFINITY;
     PhotonPath P;
+    PhotonMedia M;
+    M.tmax = RT_DEFAULT_MAX;
+    M.inmed = M.probe = false;
+    M.pdepth = M.nev = 0;
+    M.spos = M.ev_pos = M.ev_pow = mk1(0.f);
     Rng rs;
     const uint32_t p = blockIdx.x * 64u + lane;
     bool alive = p < total;
     if (alive) photon_emit(S, px, pb, p, P, rs);
     while (__ballot(alive)) {
-        if (alive) alive = photon_bounce(S, px, pb, c, P, rs, stk, NodesG{}, lo_x, lo_y, lo_z, hi_x, hi_y, hi_z);
+        if (alive)
+            alive = photon_bounce<MEDIA>(S, px, pb, c, P, rs, stk, NodesG{}, lo_x, lo_y, lo_z, hi_x, hi_y, hi_z, mb.vm,
+                                         M, mb);
     }
     photon_bbox_flush(pb, lo_x, lo_y, lo_z, hi_x, hi_y, hi_z, blockIdx.x & (BBOX_REPLICAS - 1), lane);
 }
 
-void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c) {
+void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c,
+                       const MediaBufs* mb) {
     const uint32_t total = pb.prows * pb.PW;
     if (total == 0) return;
-    hipLaunchKernelGGL(k_ppm_photon, dim3((total + 63) / 64), dim3(64), ORX_STACK_BYTES(S), s, S, px, pb, c);
+    if (mb)
+        hipLaunchKernelGGL((k_ppm_photon<true>), dim3((total + 63) / 64), dim3(64), ORX_STACK_BYTES(S), s, S, px, pb, c,
+                           *mb);
+    else
+        hipLaunchKernelGGL((k_ppm_photon<false>), dim3((total + 63) / 64), dim3(64), ORX_STACK_BYTES(S), s, S, px, pb,
+                           c, MediaBufs{});
 }
 
 /* ------------------------------------------------------------------ */
@@ -1871,6 +1964,8 @@ __global__ __launch_bounds__(64) void k_ppm_direct_output(DevScene S, PixelBufs 
             direct = mk(fminf(rad.x, 1.f), fminf(rad.y, 1.f), fminf(rad.z, 1.f));
         else
             direct = rad;
+    } else if (c.media) { /* numShadowSamples = ENABLE_PARTICIPATING_MEDIA ? 0 : 4 (DirectRadianceEstimation.cu:54) */
+        direct = mk1(0.f);
     } else {
         const size_t slot = (size_t)j * px.RW + x;
         Rng rs = rng_load(px.rng, slot);

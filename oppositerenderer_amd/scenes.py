@@ -225,6 +225,13 @@ class Scene:
         self.media.append(np.array([*np.float32(box_min), *np.float32(box_max), f32(sigma_s), f32(sigma_a)],
                                    dtype=np.float32))
 
+    def add_scene_fog(self, sigma_s=0.05, sigma_a=0.01):
+        """The loaded-scene medium of Scene.cpp:337-350: ParticipatingMedium(0.05, 0.01) on the scene
+        AABB with AAB::addPadding(0.01) (min -= 0.01, max += 0.01 in float, math/AAB.h:21-25)."""
+        lo = (np.float32(self.aabb_min) - np.float32(0.01)).astype(np.float32)
+        hi = (np.float32(self.aabb_max) + np.float32(0.01)).astype(np.float32)
+        self.add_medium_box(lo, hi, sigma_s, sigma_a)
+
     def add_texture(self, rgba, normal_rgba=None) -> int:
         chk = lambda a: None if a is None else np.ascontiguousarray(a, dtype=np.uint8).reshape(
             np.shape(a)[0], np.shape(a)[1], 4)

@@ -2348,6 +2348,8 @@ orx_status orc_read_buffer(orc_renderer* r, int32_t id, void* dst, size_t bytes,
     case ORX_BUF_VCM_SPLAT: case ORX_BUF_VCM_CAMERA: need = r->vcm_npx * 12; break; /* own rows */
     case ORX_BUF_KD_TREE: need = r->kdsize * 40; break;
     case ORX_BUF_PHOTON_SLOTS: need = (size_t)r->cfg.photon_launch_width * r->prows * r->dslot * 36; break;
+    case ORX_BUF_VOLUMETRIC: need = r->med_on ? npx * 12 : 0; break;
+    case ORX_BUF_VOLUMETRIC_PHOTONS: need = r->med_on ? (size_t)r->nvol * 28 : 0; break;
     default: return fail(r, ORX_ERR_INVALID_ARGUMENT, "unknown buffer id");
     }
     if (out_bytes) *out_bytes = need;
@@ -2390,6 +2392,19 @@ orx_status orc_read_buffer(orc_renderer* r, int32_t id, void* dst, size_t bytes,
     case ORX_BUF_PHOTON_SLOTS: /* slot order: the grid build swapped the unsorted slots into sort_tmp */
         memcpy(dst, (r->cfg.photon_map == 0 && r->ncells) ? r->sort_tmp : r->photons, need);
         break;
+    case ORX_BUF_VOLUMETRIC: if (need) memcpy(dst, r->volR, need); break;
+    case ORX_BUF_VOLUMETRIC_PHOTONS: {
+        float* f = (float*)dst;
+        for (size_t i = 0; need && i < r->nvol; i++) {
+            const int on = r->vol_ready && r->vcnt[i];
+            float v[7] = {on ? r->vpow[i].x : 0.f, on ? r->vpow[i].y : 0.f, on ? r->vpow[i].z : 0.f,
+                          on ? r->vpos[i].x : 0.f, on ? r->vpos[i].y : 0.f, on ? r->vpos[i].z : 0.f, 0.f};
+            const uint32_t c = on ? r->vcnt[i] : 0u;
+            memcpy(&v[6], &c, 4);
+            memcpy(f + 7 * i, v, sizeof v);
+        }
+        break;
+    }
     case ORX_BUF_KD_TREE: {
         float* f = (float*)dst;
         for (size_t i = 0; i < r->kdsize; i++) {
