@@ -67,10 +67,11 @@ def parse(argv=None):
     p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                    help="multi-GPU PPM: strong = fixed global photon launch split by rows over the ranks "
                         "(the default); weak = a full photon launch per rank")
-    p.add_argument("--partition", choices=["slab", "rows"], default="slab",
-                   help="multi-GPU PPM gather: slab = each rank gathers against the photons of its spatial slab "
-                        "(all-to-all of the photons, the default); rows = every rank gathers all hit points "
-                        "against its own photons")
+    p.add_argument("--partition", choices=["slab", "rows"], default="rows",
+                   help="multi-GPU PPM gather: rows = every rank gathers all hit points against its own photons "
+                        "(the default: per-rank hall frame at N=8 1.43 ms against 2.92 ms for slab, "
+                        "tools/shard_model.py); slab = each rank gathers the hit points that reach the photons "
+                        "of its spatial slab (all-to-all of the photons; on par with rows at 4K)")
     p.add_argument("--force-sharded", action="store_true",
                    help="run the torch.distributed/RCCL sharded path even with one rank (tests the N>1 code)")
     p.add_argument("--no-serial-pass-times", action="store_true",
