@@ -363,9 +363,8 @@ orx_status orx_set_ppm_pipeline(orx_renderer* r, void* side_stream, int enable);
  * photon is in exactly one rank's grid.  Capacity: the import takes up to the global photon launch's
  * deposit slots (PW * PH * max deposits) per rank. */
 #define ORX_SLAB_VOXELS 32u
-static inline size_t orx_slab_histogram_words(uint32_t nbins) {
-    return (size_t)6 * nbins + 6 + (size_t)2 * ORX_SLAB_VOXELS * ORX_SLAB_VOXELS * ORX_SLAB_VOXELS;
-}
+/* 6 nbins + 6 + 2 ORX_SLAB_VOXELS^3 */
+size_t orx_slab_histogram_words(uint32_t nbins);
 orx_status orx_set_slab_partition(orx_renderer* r, int enable);
 orx_status orx_ppm_local_trace(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
                                float ppm_radius, const orx_request* details);

@@ -1775,6 +1775,9 @@ orx_status orx_ppm_local_photon_trace(orx_renderer* r) {
 }
 
 static_assert(SLAB_VOX == ORX_SLAB_VOXELS, "slab voxel grid: kernels and ABI disagree");
+size_t orx_slab_histogram_words(uint32_t nb) {
+    return (size_t)6 * nb + 6 + (size_t)2 * ORX_SLAB_VOXELS * ORX_SLAB_VOXELS * ORX_SLAB_VOXELS;
+}
 static SlabBins slab_bins(const orx_renderer* r, uint32_t nb) {
     SlabBins sb;
     const float lo[3] = {r->aabb_lo.x, r->aabb_lo.y, r->aabb_lo.z}, hi[3] = {r->aabb_hi.x, r->aabb_hi.y, r->aabb_hi.z};

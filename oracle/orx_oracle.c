@@ -2231,7 +2231,7 @@ static inline uint32_t slab_voxel(const orc_renderer* r, v3 p) {
 }
 orx_status orc_ppm_slab_histogram(orc_renderer* r, uint32_t* hist, uint32_t nb) {
     if (!r || !hist || nb < ORX_SLAB_VOXELS || nb > 1024 || nb % ORX_SLAB_VOXELS) return ORX_ERR_INVALID_ARGUMENT;
-    memset(hist, 0, orx_slab_histogram_words(nb) * 4);
+    memset(hist, 0, ((size_t)6 * nb + 6 + 2 * (size_t)ORX_SLAB_VOXELS * ORX_SLAB_VOXELS * ORX_SLAB_VOXELS) * 4);
     const size_t S = local_slots(r);
     const size_t NV = (size_t)ORX_SLAB_VOXELS * ORX_SLAB_VOXELS * ORX_SLAB_VOXELS;
     uint32_t* hv = hist + 6 * (size_t)nb + 6;
