@@ -334,10 +334,11 @@ orx_status orx_ppm_finish(orx_renderer* r, const void* indirect_device, size_t i
 orx_status orx_set_ppm_pipeline(orx_renderer* r, void* side_stream, int enable);
 
 /* Spatial photon partition of the sharded gather ("slab mode", uniform grid only; call before the
- * first iteration, like orx_set_shard).  Rank g gathers against the photons of ALL ranks that lie
- * in its slab of one axis of the scene AABB, and only the hit points whose sphere reaches them, so
- * the gather's per-pixel work also divides by N (the row partition above gathers all W*H hit
- * points on every rank).  One PPM iteration:
+ * first iteration, like orx_set_shard).  Rank g owns a slab of bins of one axis of the scene AABB:
+ * it receives the photons of ALL ranks in its slab plus those within halo_bins bins of it, and
+ * gathers exactly the non-specular hit points whose position lies in its slab, so every hit point
+ * is gathered once, with its complete window, and the gather's per-pixel work divides by N (the
+ * row partition above gathers all W*H hit points on every rank).  One PPM iteration:
  *   orx_ppm_local_eye + orx_ppm_local_photon_trace   (or orx_ppm_local_trace: both)  eye pass,
  *                            photon pass of the own rows; no grid yet
  *   orx_ppm_slab_histogram   per-bin counts [2][3][nbins] (uint32): the own valid deposits and the
@@ -349,19 +350,25 @@ orx_status orx_set_ppm_pipeline(orx_renderer* r, void* side_stream, int enable);
  *                            the scene AABB (x + V (y + V z)): orx_slab_histogram_words(nbins) words
  *   (caller all-gathers the histograms and plans on the host: one axis and a bin -> rank table, the
  *    same on every rank; photons from rank s to rank d = the sum of s's photon bins mapped to d)
- *   orx_ppm_slab_pack        the own valid deposits, rank-major into the caller's send buffer: at
- *                            dest_base[d] + k for the k-th photon sent to d (9 floats each:
- *                            position, direction, power); host arrays bin_dest[nbins], dest_base[world]
+ *   orx_ppm_slab_pack        the own valid deposits, rank-major into the caller's send buffer: a
+ *                            photon in bin b goes to every rank from bin_dest[b - halo_bins] to
+ *                            bin_dest[b + halo_bins] (clamped; bin_dest ascending), at dest_base[d] + k
+ *                            for the k-th photon sent to d (9 floats each: position, direction,
+ *                            power); host arrays bin_dest[nbins], dest_base[world].  halo_bins >=
+ *                            floor(r / bin width) + 2 makes every photon within r of a hit point
+ *                            reach the hit point's owner
  *   (caller all-to-alls the photon records)
  *   orx_ppm_slab_import      the received records become this rank's photon set; grid build over
  *                            photon_box (host, 6 words as above: the min/max over ranks of the
  *                            histograms' AABBs, so every rank's grid has the single-device grid's
- *                            origin and cell size; NULL: the AABB of the imported photons)
+ *                            origin and cell size; NULL: the AABB of the imported photons); the
+ *                            rank owns the hit points whose bin on `axis` lies in [own_lo, own_hi]
+ *                            (own_lo > own_hi: none)
  *   orx_export_hitpoints / orx_ppm_gather_external / orx_ppm_finish as above (the gather skips hit
  *   points whose sphere misses this rank's photon grid)
- * The sum over ranks of the partial gathers is again the single-GPU gather up to fp32 order: every
- * photon is in exactly one rank's grid.  Capacity: the import takes up to the global photon launch's
- * deposit slots (PW * PH * max deposits) per rank. */
+ * Each hit point's indirect comes whole from its owner (the others write 0), so the reduce-scatter
+ * sum is the single-GPU gather of that pixel up to fp32 order inside its window.  Capacity: the
+ * import takes up to the global photon launch's deposit slots (PW * PH * max deposits) per rank. */
 #define ORX_SLAB_VOXELS 32u
 /* 6 nbins + 6 + 2 ORX_SLAB_VOXELS^3 */
 size_t orx_slab_histogram_words(uint32_t nbins);
@@ -371,10 +378,14 @@ orx_status orx_ppm_local_trace(orx_renderer* r, uint64_t iteration_number, uint6
 orx_status orx_ppm_local_photon_trace(orx_renderer* r);
 orx_status orx_ppm_slab_histogram(orx_renderer* r, uint32_t* hist_device /* orx_slab_histogram_words */,
                                   uint32_t nbins);
+/* the halo for radius r: floor(r * nbins / extent of the scene AABB on axis) + 2 bins */
+uint32_t orx_ppm_slab_halo(const orx_renderer* r, uint32_t nbins, uint32_t axis, float radius);
 orx_status orx_ppm_slab_pack(orx_renderer* r, const uint8_t* bin_dest, uint32_t nbins, uint32_t axis,
-                             const uint32_t* dest_base, uint64_t send_records, void* send_device);
+                             uint32_t halo_bins, const uint32_t* dest_base, uint64_t send_records,
+                             void* send_device);
 orx_status orx_ppm_slab_import(orx_renderer* r, const void* recv_device, uint64_t n_records,
-                               const uint32_t* photon_box);
+                               const uint32_t* photon_box, uint32_t axis, uint32_t nbins, uint32_t own_lo,
+                               uint32_t own_hi);
 
 /* One VCM iteration of a sharded renderer (OptixRenderer.cpp:675-795 split at
  * the light-tracing splats).  Light subpath i pairs with camera pixel i

@@ -375,6 +375,7 @@ struct orx_renderer {
     size_t S_cap = 0;
     DevBuf d_slabtab, d_slabcur;
     DevBuf d_tiles; /* slab gather: tile list, count, flags */
+    uint32_t own_axis = 0, own_nb = 0, own_lo = 1, own_hi = 0; /* slab gather: the bins this rank owns */
     int pipe_mode = -1; /* orx_set_iteration_pipelining: -1 = ORX_PIPELINE env */
     hipStream_t side = nullptr;
     uint32_t pp = 0;
@@ -1790,6 +1791,12 @@ static SlabBins slab_bins(const orx_renderer* r, uint32_t nb) {
     return sb;
 }
 
+uint32_t orx_ppm_slab_halo(const orx_renderer* r, uint32_t nb, uint32_t axis, float radius) {
+    if (!r || axis > 2 || nb == 0) return 2u;
+    const SlabBins sb = slab_bins(r, nb);
+    const float h = orx_floorf(radius * sb.inv[axis]);
+    return (h >= 0.f && h < 1e6f ? (uint32_t)h : 0u) + 2u;
+}
 orx_status orx_ppm_slab_histogram(orx_renderer* r, uint32_t* hist, uint32_t nb) {
     if (!r || !hist || nb < ORX_SLAB_VOXELS || nb > 1024 || nb % ORX_SLAB_VOXELS) return ORX_ERR_INVALID_ARGUMENT;
     if (!r->slab || !r->rng_ready) return set_err(r, ORX_ERR_STATE, "orx_ppm_slab_histogram: slab mode, after the photon pass");
@@ -1802,13 +1809,14 @@ orx_status orx_ppm_slab_histogram(orx_renderer* r, uint32_t* hist, uint32_t nb) 
     return ORX_OK;
 }
 
-orx_status orx_ppm_slab_pack(orx_renderer* r, const uint8_t* bin_dest, uint32_t nb, uint32_t axis,
+orx_status orx_ppm_slab_pack(orx_renderer* r, const uint8_t* bin_dest, uint32_t nb, uint32_t axis, uint32_t halo_bins,
                              const uint32_t* dest_base, uint64_t send_records, void* send) {
     if (!r || !bin_dest || !dest_base || !send || nb == 0 || nb > 1024 || axis > 2) return ORX_ERR_INVALID_ARGUMENT;
     if (!r->slab || !r->rng_ready) return set_err(r, ORX_ERR_STATE, "orx_ppm_slab_pack: slab mode, after the photon pass");
     if (r->world > 64) return set_err(r, ORX_ERR_UNSUPPORTED, "slab mode supports at most 64 ranks");
     for (uint32_t b = 0; b < nb; b++)
-        if (bin_dest[b] >= r->world) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "bin_dest names a rank >= world");
+        if (bin_dest[b] >= r->world || (b && bin_dest[b] < bin_dest[b - 1]))
+            return set_err(r, ORX_ERR_INVALID_ARGUMENT, "bin_dest must be ascending ranks < world");
     /* the run of each rank must lie inside the send buffer; the plan's counts come from the
      * histogram of the same photons, so the runs are exactly filled */
     for (uint32_t d = 0; d < r->world; d++)
@@ -1821,14 +1829,15 @@ orx_status orx_ppm_slab_pack(orx_renderer* r, const uint8_t* bin_dest, uint32_t 
     HIPCHK(r, r->d_slabcur.ensure(64 * 4));
     HIPCHK(r, hipMemcpyAsync(r->d_slabtab.p, bin_dest, nb, hipMemcpyHostToDevice, st));
     HIPCHK(r, hipMemcpyAsync(r->d_slabcur.p, dest_base, (size_t)r->world * 4, hipMemcpyHostToDevice, st));
-    launch_slab_pack(st, r->pb, slab_bins(r, nb), axis, r->d_slabtab.as<uint8_t>(), r->world,
+    launch_slab_pack(st, r->pb, slab_bins(r, nb), axis, halo_bins, r->d_slabtab.as<uint8_t>(), r->world,
                      r->d_slabcur.as<uint32_t>(), (uint32_t)send_records, (float*)send);
     HIPCHK(r, hipGetLastError());
     return ORX_OK;
 }
 
-orx_status orx_ppm_slab_import(orx_renderer* r, const void* recv, uint64_t n, const uint32_t* photon_box) {
-    if (!r || (!recv && n)) return ORX_ERR_INVALID_ARGUMENT;
+orx_status orx_ppm_slab_import(orx_renderer* r, const void* recv, uint64_t n, const uint32_t* photon_box,
+                               uint32_t axis, uint32_t nb, uint32_t own_lo, uint32_t own_hi) {
+    if (!r || (!recv && n) || axis > 2 || nb == 0 || nb > 1024) return ORX_ERR_INVALID_ARGUMENT;
     if (!r->slab || !r->rng_ready) return set_err(r, ORX_ERR_STATE, "orx_ppm_slab_import: slab mode, after the photon pass");
     if (n > r->S_cap) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "more photons than the slab import capacity");
     HIPCHK(r, hipSetDevice(r->device));
@@ -1848,6 +1857,10 @@ orx_status orx_ppm_slab_import(orx_renderer* r, const void* recv, uint64_t n, co
         for (int k = 0; k < 6; k++) gb.b[k] = photon_box[k];
     }
     ppm_grid_build(r, pbi, gb);
+    r->own_axis = axis;
+    r->own_nb = nb;
+    r->own_lo = own_lo;
+    r->own_hi = own_hi;
     if (r->last_pipelined) HIPCHK(r, hipEventRecord(r->ev_grid_done, st));
     HIPCHK(r, hipGetLastError());
     return ORX_OK;
@@ -1877,7 +1890,11 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hp, uint32_t seg
     gi.W = r->W;
     gi.indirect = (float*)indirect;
     gi.dbg = nullptr;
-    gi.cull = r->slab ? 1u : 0u;
+    gi.cull = r->slab ? 2u : 0u;
+    gi.own_axis = r->own_axis;
+    gi.own_lo = r->own_lo;
+    gi.own_hi = r->own_hi;
+    if (r->slab) gi.own_sb = slab_bins(r, r->own_nb);
     gi.visits = 0; /* rank-local counts are not the reference's; no per-pixel debug buffers here */
     hipStream_t st = cur_stream(r);
     if (r->last_pipelined) { /* on the side stream, after the grid build */

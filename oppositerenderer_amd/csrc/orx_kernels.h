@@ -193,6 +193,18 @@ void launch_grid_setup(hipStream_t s, const PhotonBufs& pb, const GridBox& gb = 
 void launch_grid_bucket_count(hipStream_t s, const PhotonBufs& pb);
 void launch_grid_bucket_scan(hipStream_t s, const PhotonBufs& pb);
 void launch_grid_bucket_place(hipStream_t s, const PhotonBufs& pb);
+/* slab mode (sharded PPM with a spatial photon partition): nb bins per axis over the scene AABB */
+struct SlabBins {
+    float lo[3];
+    float inv[3]; /* nb / extent */
+    uint32_t nb;
+};
+/* the bin of coordinate v on axis a; one function for histogram, pack and ownership, so the
+ * host plan's counts and the ranks' ownership agree exactly */
+__device__ __forceinline__ uint32_t slab_bin(const SlabBins& sb, float v, uint32_t a) {
+    const int32_t b = orx_f2i_sat(orx_floorf((v - sb.lo[a]) * sb.inv[a]));
+    return b < 0 ? 0u : (b >= (int32_t)sb.nb ? sb.nb - 1u : (uint32_t)b);
+}
 /* gathers `rows` pixel rows whose hitpoints are in hp{A,B,C} against the
  * local photon grid; writes indirect (and debug counters) */
 /* Hitpoints to gather: `segments` segments of seg_rows x W pixels, each in the
@@ -203,8 +215,12 @@ struct GatherIn {
     uint32_t segments, seg_rows, W;
     float* indirect;    /* [segments*seg_rows*W*3] */
     uint32_t* dbg;      /* [segments*seg_rows*W*2] or NULL */
-    uint32_t cull;      /* 1 (slab mode): a hit point whose sphere misses the AABB of the grid's photons
-                         * gathers nothing (its window would only clamp onto cells without them) */
+    uint32_t cull;      /* 1: a hit point whose sphere misses the AABB of the grid's photons gathers
+                         * nothing (its window would only clamp onto cells without them); 2 (slab
+                         * mode): only the hit points this rank owns gather (bin of own_axis in
+                         * [own_lo, own_hi] over own_bins), the others get 0 */
+    uint32_t own_axis, own_lo, own_hi;
+    SlabBins own_sb;
     /* slab mode: the 16x16-pixel tiles that gather here, ascending (tile_list[0..*tile_count)),
      * dealt to the XCDs in contiguous bands; NULL: every tile */
     const uint32_t* tile_list = nullptr;
@@ -230,17 +246,11 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
  * (the others' indirect is zeroed here); ntiles of the gather's 16x16 tiling */
 void launch_gather_tiles(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, uint8_t* flags,
                          uint32_t* list, uint32_t* count);
-/* slab mode (sharded PPM with a spatial photon partition): nb bins per axis over the scene AABB */
-struct SlabBins {
-    float lo[3];
-    float inv[3]; /* nb / extent */
-    uint32_t nb;
-};
 constexpr uint32_t SLAB_VOX = 32; /* coarse voxels per axis of the slab histogram (include/orx.h) */
 void launch_slab_hist(hipStream_t s, const PhotonBufs& pb, const PixelBufs& px, const SlabBins& sb,
                       const SlabBins& vb, uint32_t* hist);
-void launch_slab_pack(hipStream_t s, const PhotonBufs& pb, const SlabBins& sb, uint32_t axis, const uint8_t* bin_dest,
-                      uint32_t world, uint32_t* cursor, uint32_t cap, float* send);
+void launch_slab_pack(hipStream_t s, const PhotonBufs& pb, const SlabBins& sb, uint32_t axis, uint32_t halo,
+                      const uint8_t* bin_dest, uint32_t world, uint32_t* cursor, uint32_t cap, float* send);
 void launch_slab_import(hipStream_t s, const PhotonBufs& pb, const float* recv, uint32_t n);
 /* the own photon pass's AABB (folded bbox replicas, ordered-int bits) -> out[6] */
 void launch_slab_bbox(hipStream_t s, const PhotonBufs& pb, uint32_t* out);

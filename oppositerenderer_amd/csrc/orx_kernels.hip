@@ -958,12 +958,23 @@ __device__ __forceinline__ void window_visits(const uint32_t* __restrict__ offse
 
 constexpr uint32_t GQ = 8; /* chord ranges per lane per phase A (LDS: GQ * 8 B per lane) */
 
-/* slab mode: the hit point's sphere (grown by a margin far above the rounding of the distance
- * test) misses the AABB of this rank's photons (the grid spans all ranks' photons) */
+/* the hit point's sphere (grown by a margin far above the rounding of the distance test) misses
+ * the AABB of this rank's photons */
 __device__ __forceinline__ bool sphere_misses_grid(const GridParams& g, f3 pos, float r) {
     const float m = r * 1e-3f + g.cell * 1e-3f, rr = r + m;
     return pos.x + rr < g.clo[0] || pos.x - rr > g.chi[0] || pos.y + rr < g.clo[1] || pos.y - rr > g.chi[1] ||
            pos.z + rr < g.clo[2] || pos.z - rr > g.chi[2];
+}
+/* a hit point this rank does not gather: cull 1, its sphere misses the rank's photons; cull 2
+ * (slab mode), its position's bin on the slab axis is another rank's (every photon within r of
+ * an owned hit point was sent here with the halo, so owners gather complete windows) */
+__device__ __forceinline__ bool gather_skips(const GatherIn& gi, const GridParams& g, f3 pos, float r) {
+    if (gi.cull == 2) {
+        const float v = gi.own_axis == 0 ? pos.x : gi.own_axis == 1 ? pos.y : pos.z;
+        const uint32_t b = slab_bin(gi.own_sb, v, gi.own_axis);
+        return b < gi.own_lo || b > gi.own_hi;
+    }
+    return gi.cull == 1 && sphere_misses_grid(g, pos, r);
 }
 
 /* NSUB: sub-rows per cell row (SUBR^2, or 1 for the cell-order layout) */
@@ -1002,7 +1013,7 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
     const float invCellSize = 1.f / g.cell;
     const f3 np = pos - mk(g.ox, g.oy, g.oz);
     uint32_t x_lo = 0, x_hi = 0, y_lo = 0, z_lo = 0, ny = 0, nrows = 0;
-    if (live && (flags & PRD_HIT_NON_SPECULAR) && g.G && !(gi.cull && sphere_misses_grid(g, pos, radius))) {
+    if (live && (flags & PRD_HIT_NON_SPECULAR) && g.G && !gather_skips(gi, g, pos, radius)) {
         const int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
         const int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
         const int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
@@ -1367,7 +1378,7 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
     const f3 np = pos - mk(g.ox, g.oy, g.oz);
     uint32_t x_lo = 1, x_hi = 0, y_lo = 1, y_hi = 0, z_lo = 1, z_hi = 0;
     bool act = false;
-    if (live && (flags & PRD_HIT_NON_SPECULAR) && g.G && !(gi.cull && sphere_misses_grid(g, pos, radius))) {
+    if (live && (flags & PRD_HIT_NON_SPECULAR) && g.G && !gather_skips(gi, g, pos, radius)) {
         const int32_t ixl = orx_f2i_sat((np.x - radius) * invCellSize);
         const int32_t iyl = orx_f2i_sat((np.y - radius) * invCellSize);
         const int32_t izl = orx_f2i_sat((np.z - radius) * invCellSize);
@@ -1548,7 +1559,7 @@ __global__ __launch_bounds__(256) void k_gather_tiles(GatherIn gi, PhotonBufs pb
         const HpRef hr = hp_ref(gi, j, x);
         const float4 A = hr.A[hr.li];
         act = (__float_as_uint(A.w) & PRD_HIT_NON_SPECULAR) && g.G &&
-              !sphere_misses_grid(g, mk(A.x, A.y, A.z), c.ppm_radius);
+              !gather_skips(gi, g, mk(A.x, A.y, A.z), c.ppm_radius);
     }
     const int any = __syncthreads_or(act);
     if (tid == 0) flags[tile] = (uint8_t)(any != 0);
@@ -1621,10 +1632,6 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
  * bin -> rank table are the host's plan (multigpu.slab_plan) over the all-gathered histograms.
  * The bin of a position is computed by the one function below in the histogram and in the
  * pack, so the host's per-rank counts are exact. */
-__device__ __forceinline__ uint32_t slab_bin(const SlabBins& sb, float v, uint32_t a) {
-    const int32_t b = orx_f2i_sat(orx_floorf((v - sb.lo[a]) * sb.inv[a]));
-    return b < 0 ? 0u : (b >= (int32_t)sb.nb ? sb.nb - 1u : (uint32_t)b);
-}
 __device__ __forceinline__ bool slot_valid(const PhotonBufs& pb, uint32_t s) {
     const uint32_t p = s / pb.D, k = s - p * pb.D;
     return (pb.vmask[p] >> k) & 1u;
@@ -1690,7 +1697,7 @@ void launch_slab_hist(hipStream_t s, const PhotonBufs& pb, const PixelBufs& px, 
  * fp32 summation order on the receiving rank) */
 constexpr uint32_t SLAB_CHUNK = 4096;
 constexpr uint32_t SLAB_MAX_RANKS = 64;
-__global__ __launch_bounds__(256) void k_slab_pack(PhotonBufs pb, SlabBins sb, uint32_t axis,
+__global__ __launch_bounds__(256) void k_slab_pack(PhotonBufs pb, SlabBins sb, uint32_t axis, uint32_t halo,
                                                    const uint8_t* __restrict__ bin_dest, uint32_t world,
                                                    uint32_t* cursor, uint32_t cap, float* __restrict__ send) {
     __shared__ uint32_t cnt[SLAB_MAX_RANKS], base[SLAB_MAX_RANKS];
@@ -1702,7 +1709,10 @@ __global__ __launch_bounds__(256) void k_slab_pack(PhotonBufs pb, SlabBins sb, u
             if (!slot_valid(pb, s)) continue;
             const float4 q = pb.pos4[s];
             const float v = axis == 0 ? q.x : axis == 1 ? q.y : q.z;
-            atomicAdd(&cnt[bin_dest[slab_bin(sb, v, axis)]], 1u);
+            const uint32_t b = slab_bin(sb, v, axis);
+            const uint32_t d0 = bin_dest[b > halo ? b - halo : 0u];
+            const uint32_t d1 = bin_dest[b + halo < sb.nb ? b + halo : sb.nb - 1u];
+            for (uint32_t d = d0; d <= d1; d++) atomicAdd(&cnt[d], 1u);
         }
         __syncthreads();
         if (threadIdx.x < world) {
@@ -1717,22 +1727,27 @@ __global__ __launch_bounds__(256) void k_slab_pack(PhotonBufs pb, SlabBins sb, u
             const float4 a = rec[0], b = rec[1];
             const float pz = rec[2].x;
             const float v = axis == 0 ? a.x : axis == 1 ? a.y : a.z;
-            const uint32_t d = bin_dest[slab_bin(sb, v, axis)];
-            const uint32_t o = base[d] + atomicAdd(&cnt[d], 1u);
-            if (o >= cap) continue; /* a plan whose counts disagree with the photons: never write past */
-            float* w = send + 9 * (size_t)o;
-            w[0] = a.x; w[1] = a.y; w[2] = a.z;
-            w[3] = b.x; w[4] = b.y; w[5] = b.z;
-            w[6] = a.w; w[7] = b.w; w[8] = pz;
+            const uint32_t bn = slab_bin(sb, v, axis);
+            const uint32_t d0 = bin_dest[bn > halo ? bn - halo : 0u];
+            const uint32_t d1 = bin_dest[bn + halo < sb.nb ? bn + halo : sb.nb - 1u];
+            for (uint32_t d = d0; d <= d1; d++) { /* the owner and the ranks within the halo */
+                const uint32_t o = base[d] + atomicAdd(&cnt[d], 1u);
+                if (o >= cap) continue; /* a plan whose counts disagree with the photons: never write past */
+                float* w = send + 9 * (size_t)o;
+                w[0] = a.x; w[1] = a.y; w[2] = a.z;
+                w[3] = b.x; w[4] = b.y; w[5] = b.z;
+                w[6] = a.w; w[7] = b.w; w[8] = pz;
+            }
         }
         __syncthreads();
     }
 }
-void launch_slab_pack(hipStream_t s, const PhotonBufs& pb, const SlabBins& sb, uint32_t axis, const uint8_t* bin_dest,
-                      uint32_t world, uint32_t* cursor, uint32_t cap, float* send) {
+void launch_slab_pack(hipStream_t s, const PhotonBufs& pb, const SlabBins& sb, uint32_t axis, uint32_t halo,
+                      const uint8_t* bin_dest, uint32_t world, uint32_t* cursor, uint32_t cap, float* send) {
     uint32_t blocks = (pb.S + SLAB_CHUNK - 1) / SLAB_CHUNK;
     blocks = blocks < 1 ? 1 : (blocks > 4096 ? 4096 : blocks);
-    hipLaunchKernelGGL(k_slab_pack, dim3(blocks), dim3(256), 0, s, pb, sb, axis, bin_dest, world, cursor, cap, send);
+    hipLaunchKernelGGL(k_slab_pack, dim3(blocks), dim3(256), 0, s, pb, sb, axis, halo, bin_dest, world, cursor, cap,
+                       send);
 }
 
 /* received photon records -> this rank's deposit records: record i is slot i of photon group

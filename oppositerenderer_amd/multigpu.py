@@ -58,7 +58,7 @@ def split_slab_hists(words, world, nb):
     return w[:, :6 * nb].reshape(world, 2, 3, nb), vox, box
 
 
-def slab_plan(hists, world, vox=None, w_gather=0.8, w_photon=0.15, w_pixel=0.05):
+def slab_plan(hists, world, vox=None, halo=0, w_gather=0.8, w_photon=0.15, w_pixel=0.05):
     """The slab partition of one iteration (include/orx.h orx_set_slab_partition), computed on
     every rank from the all-gathered histograms, identically (float64 numpy on identical inputs).
 
@@ -70,7 +70,8 @@ def slab_plan(hists, world, vox=None, w_gather=0.8, w_photon=0.15, w_pixel=0.05)
     normalised to sum 1.  Without vox the gather term is photons x hit points per bin.  On each
     axis every bin goes to the rank whose share of the cumulative cost holds the bin's midpoint
     (contiguous slabs, ascending ranks); the axis with the smallest largest-slab cost wins (ties:
-    the lower axis).
+    the lower axis).  halo: bins (one int, or one per axis, include/orx.h orx_ppm_slab_halo): a
+    photon in bin b also goes to the ranks of bins b - halo .. b + halo.
     Returns (axis, bin_dest uint8[nb], counts int64[world][world]: photons rank s sends to rank d)."""
     h = np.asarray(hists, dtype=np.float64).reshape(world, 2, 3, -1)
     nb = h.shape[-1]
@@ -105,10 +106,30 @@ def slab_plan(hists, world, vox=None, w_gather=0.8, w_photon=0.15, w_pixel=0.05)
         if best is None or cost_a < best[0]:
             best = (cost_a, a, dest)
     _, axis, dest = best
-    counts = np.zeros((world, world), np.int64)
-    for src in range(world):
-        counts[src] = np.bincount(dest, weights=h[src, 0, axis], minlength=world).astype(np.int64)
-    return axis, dest.astype(np.uint8), counts
+    return axis, dest.astype(np.uint8), slab_counts(h[:, 0, axis], dest, world, halo_of(halo, axis))
+
+
+def halo_of(halo, axis):
+    return int(halo[axis]) if np.ndim(halo) else int(halo)
+
+
+def slab_counts(ph, dest, world, halo):
+    """photons rank s sends to rank d (orx_ppm_slab_pack): ph[s][b] photon counts per bin, a photon
+    in bin b going to every rank from dest[b - halo] to dest[b + halo] (clamped; dest ascending)"""
+    ph = np.asarray(ph, dtype=np.float64)
+    nb = len(dest)
+    b = np.arange(nb)
+    d0 = np.asarray(dest)[np.maximum(b - halo, 0)]
+    d1 = np.asarray(dest)[np.minimum(b + halo, nb - 1)]
+    r = np.arange(world)
+    m = ((r[None, :] >= d0[:, None]) & (r[None, :] <= d1[:, None])).astype(np.float64)  # [nb][world]
+    return np.rint(ph @ m).astype(np.int64)
+
+
+def slab_owned(dest, rank):
+    """(own_lo, own_hi): the bins rank owns (own_lo > own_hi: none), include/orx.h orx_ppm_slab_import"""
+    idx = np.nonzero(np.asarray(dest) == rank)[0]
+    return (int(idx[0]), int(idx[-1])) if len(idx) else (1, 0)
 
 
 def assemble_rows(blocks, W, H, world):
@@ -151,7 +172,7 @@ class ShardedPPM:
         if self.pipe:
             backend.enable_pipeline()
 
-    def slab_exchange(self):
+    def slab_exchange(self, radius):
         """histograms -> plan (host) -> pack -> all-to-all of the photon records -> import + grid"""
         b, d, world, rank = self.b, self.dist, self.world, self.rank
         b.slab_histogram(self.hist, self.nb)
@@ -160,14 +181,18 @@ class ShardedPPM:
         else:
             d.all_gather_into_tensor(self.hists, self.hist)
         hists, vox, box = split_slab_hists(self.hists.cpu().numpy(), world, self.nb)
-        axis, bin_dest, counts = slab_plan(hists, world, vox)
+        halo = [b.slab_halo(self.nb, a, radius) for a in range(3)]
+        axis, bin_dest, counts = slab_plan(hists, world, vox, halo)
         send_n, recv_n = counts[rank], counts[:, rank]
         base = np.concatenate([[0], np.cumsum(send_n)[:-1]]).astype(np.uint32)
         ns, nr = int(send_n.sum()), int(recv_n.sum())
-        b.slab_pack(bin_dest, self.nb, axis, base, ns, self.send)
+        if 9 * ns + 9 > self.send.numel():  # halo copies: more records than own photons
+            self.send = b.alloc(9 * ns + 9)
+        b.slab_pack(bin_dest, self.nb, axis, halo[axis], base, ns, self.send)
         recv = self.recv[:9 * nr]
         d.all_to_all_single(recv, self.send[:9 * ns], (9 * recv_n).tolist(), (9 * send_n).tolist())
-        b.slab_import(recv, nr, box)
+        own = slab_owned(bin_dest, rank)
+        b.slab_import(recv, nr, box, axis, self.nb, own)
         self.last_plan = (axis, bin_dest, counts)
 
     def iteration(self, it, local_it, radius, request):
@@ -224,7 +249,7 @@ class ShardedPPM:
             self.b.export_hitpoints(hp_local)
             work = d.all_gather_into_tensor(hp_all, hp_local, async_op=True)
             self.b.local_photon_trace()
-            self.slab_exchange()
+            self.slab_exchange(radius)
             with self.b.torch.cuda.stream(self.b.side):
                 work.wait()
                 self.b.gather_external(hp_all, self.world, ind_partial)
@@ -237,7 +262,7 @@ class ShardedPPM:
             d.all_gather(list(self.hp_all.chunk(self.world)), self.hp_local)
         else:
             d.all_gather_into_tensor(self.hp_all, self.hp_local)
-        self.slab_exchange()
+        self.slab_exchange(radius)
         self.b.gather_external(self.hp_all, self.world, self.ind_partial)
         if self.gloo:
             d.all_reduce(self.ind_partial)
@@ -325,9 +350,11 @@ class DeviceShard:
             ("orx_ppm_local_trace", [C.c_void_p, C.c_uint64, C.c_uint64, C.c_float, C.c_void_p], C.c_int),
             ("orx_ppm_local_photon_trace", [C.c_void_p], C.c_int),
             ("orx_ppm_slab_histogram", [C.c_void_p, C.c_void_p, C.c_uint32], C.c_int),
-            ("orx_ppm_slab_pack", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64,
-                                   C.c_void_p], C.c_int),
-            ("orx_ppm_slab_import", [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p], C.c_int),
+            ("orx_ppm_slab_pack", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                                   C.c_uint64, C.c_void_p], C.c_int),
+            ("orx_ppm_slab_import", [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_uint32,
+                                     C.c_uint32, C.c_uint32], C.c_int),
+            ("orx_ppm_slab_halo", [C.c_void_p, C.c_uint32, C.c_uint32, C.c_float], C.c_uint32),
         ):
             f = getattr(lib, name)
             f.argtypes, f.restype = args, res
@@ -378,16 +405,20 @@ class DeviceShard:
     def slab_histogram(self, hist, nb):
         self.r._check(self.lib.orx_ppm_slab_histogram(self.r._h, C.c_void_p(hist.data_ptr()), nb))
 
-    def slab_pack(self, bin_dest, nb, axis, base, n_records, send):
+    def slab_halo(self, nb, axis, radius):
+        return int(self.lib.orx_ppm_slab_halo(self.r._h, nb, axis, radius))
+
+    def slab_pack(self, bin_dest, nb, axis, halo, base, n_records, send):
         bd = np.ascontiguousarray(bin_dest, np.uint8)
         bs = np.ascontiguousarray(base, np.uint32)
-        self.r._check(self.lib.orx_ppm_slab_pack(self.r._h, bd.ctypes.data, nb, axis, bs.ctypes.data, n_records,
-                                                 C.c_void_p(send.data_ptr())))
+        self.r._check(self.lib.orx_ppm_slab_pack(self.r._h, bd.ctypes.data, nb, axis, halo, bs.ctypes.data,
+                                                 n_records, C.c_void_p(send.data_ptr())))
 
-    def slab_import(self, recv, n_records, box=None):
+    def slab_import(self, recv, n_records, box, axis, nb, own):
         bx = None if box is None else np.ascontiguousarray(box, np.uint32)
         self.r._check(self.lib.orx_ppm_slab_import(self.r._h, C.c_void_p(recv.data_ptr()), n_records,
-                                                   None if bx is None else bx.ctypes.data))
+                                                   None if bx is None else bx.ctypes.data, axis, nb, own[0],
+                                                   own[1]))
 
     def local_eye(self, it, local_it, radius, request):
         self.r._check(self.lib.orx_ppm_local_eye(self.r._h, it, local_it, radius, C.byref(request)))

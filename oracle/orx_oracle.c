@@ -255,6 +255,9 @@ struct orc_renderer {
     /* VCM: pixelSizeFactor (OptixRenderer.cpp:306, :846), LVC-estimated flag (:83, :461, :847) */
     float psf_x, psf_y;
     int vcm_estimated, vcm_pending;
+    /* slab mode: the bins on own_axis whose hit points this rank gathers (orc_ppm_slab_import) */
+    int own_on;
+    uint32_t own_axis, own_nb, own_lo, own_hi;
     size_t vcm_npx, vcm_spx;
     uint32_t* vcount; float* vverts; v3* vsplat; v3* vcam;
     v3* vkd; /* [9][lpx] texel colour of Texture light vertices */
@@ -1703,6 +1706,13 @@ static hitpoint_t hp_fetch(const orc_renderer* r, const hp_src* src, size_t px) 
 }
 
 /* IndirectRadianceEstimation.cu:54-67, :69-129, :211-221 */
+static inline uint32_t slab_bin(const orc_renderer* r, v3 p, uint32_t a, uint32_t nb);
+/* slab mode: a hit point outside this rank's bins is gathered by its owner */
+static inline int hit_owned(const orc_renderer* r, v3 p) {
+    if (!r->own_on) return 1;
+    const uint32_t b = slab_bin(r, p, r->own_axis, r->own_nb);
+    return b >= r->own_lo && b <= r->own_hi;
+}
 static void ppm_gather_src(orc_renderer* r, const hp_src* src, uint32_t rows_total, v3* out, uint32_t* dbg,
                            float ppmRadius, float ppmRadiusSquared, float emittedF) {
     const uint32_t W = r->W, H = rows_total;
@@ -1717,7 +1727,7 @@ static void ppm_gather_src(orc_renderer* r, const hp_src* src, uint32_t rows_tot
             const hitpoint_t rec = hp_fetch(r, src, px);
             v3 acc = mk1(0.0f);
             uint32_t dP = 0, dC = 0;
-            if (rec.flags & PRD_HIT_NON_SPECULAR) {
+            if ((rec.flags & PRD_HIT_NON_SPECULAR) && hit_owned(r, rec.position)) {
                 float radius2 = ppmRadiusSquared;
                 float radius = ppmRadius;
                 float invCellSize = 1.f / cell;
@@ -2222,6 +2232,14 @@ static inline uint32_t slab_bin(const orc_renderer* r, v3 p, uint32_t a, uint32_
     const int32_t b = orx_f2i_sat(orx_floorf((v - lo) * inv));
     return b < 0 ? 0u : (b >= (int32_t)nb ? nb - 1u : (uint32_t)b);
 }
+uint32_t orc_ppm_slab_halo(const orc_renderer* r, uint32_t nb, uint32_t axis, float radius) {
+    if (!r || axis > 2 || nb == 0) return 2u;
+    const float lo = axis == 0 ? r->aabb_min.x : axis == 1 ? r->aabb_min.y : r->aabb_min.z;
+    const float hi = axis == 0 ? r->aabb_max.x : axis == 1 ? r->aabb_max.y : r->aabb_max.z;
+    const float ext = hi - lo, inv = ext > 0.f ? (float)nb / ext : 0.f;
+    const float h = orx_floorf(radius * inv);
+    return (h >= 0.f && h < 1e6f ? (uint32_t)h : 0u) + 2u;
+}
 static size_t local_slots(const orc_renderer* r) {
     return (size_t)r->cfg.photon_launch_width * r->prows * r->cfg.max_photon_deposits;
 }
@@ -2248,7 +2266,7 @@ orx_status orc_ppm_slab_histogram(orc_renderer* r, uint32_t* hist, uint32_t nb) 
     }
     return ORX_OK;
 }
-orx_status orc_ppm_slab_pack(orc_renderer* r, const uint8_t* bin_dest, uint32_t nb, uint32_t axis,
+orx_status orc_ppm_slab_pack(orc_renderer* r, const uint8_t* bin_dest, uint32_t nb, uint32_t axis, uint32_t halo,
                              const uint32_t* dest_base, uint64_t send_records, float* send) {
     if (!r || !bin_dest || !dest_base || !send || nb == 0 || axis > 2) return ORX_ERR_INVALID_ARGUMENT;
     uint32_t cur[256];
@@ -2258,17 +2276,27 @@ orx_status orc_ppm_slab_pack(orc_renderer* r, const uint8_t* bin_dest, uint32_t 
     for (size_t i = 0; i < S; i++) {
         const photon_t* p = &r->photons[i];
         if (!(fmax3(p->power) > 0)) continue;
-        const uint32_t d = bin_dest[slab_bin(r, p->position, axis, nb)];
-        if (d >= r->world || cur[d] >= send_records) return fail(r, ORX_ERR_INVALID_ARGUMENT, "slab plan overflows the send buffer");
-        float* w = send + 9 * (size_t)cur[d]++;
-        w[0] = p->position.x; w[1] = p->position.y; w[2] = p->position.z;
-        w[3] = p->direction.x; w[4] = p->direction.y; w[5] = p->direction.z;
-        w[6] = p->power.x; w[7] = p->power.y; w[8] = p->power.z;
+        const uint32_t b = slab_bin(r, p->position, axis, nb);
+        const uint32_t d0 = bin_dest[b > halo ? b - halo : 0u], d1 = bin_dest[b + halo < nb ? b + halo : nb - 1u];
+        for (uint32_t d = d0; d <= d1; d++) { /* the owner and the ranks within the halo */
+            if (d >= r->world || cur[d] >= send_records)
+                return fail(r, ORX_ERR_INVALID_ARGUMENT, "slab plan overflows the send buffer");
+            float* w = send + 9 * (size_t)cur[d]++;
+            w[0] = p->position.x; w[1] = p->position.y; w[2] = p->position.z;
+            w[3] = p->direction.x; w[4] = p->direction.y; w[5] = p->direction.z;
+            w[6] = p->power.x; w[7] = p->power.y; w[8] = p->power.z;
+        }
     }
     return ORX_OK;
 }
-orx_status orc_ppm_slab_import(orc_renderer* r, const float* recv, uint64_t n, const uint32_t* box) {
-    if (!r || (!recv && n)) return ORX_ERR_INVALID_ARGUMENT;
+orx_status orc_ppm_slab_import(orc_renderer* r, const float* recv, uint64_t n, const uint32_t* box, uint32_t axis,
+                               uint32_t nb, uint32_t own_lo, uint32_t own_hi) {
+    if (!r || (!recv && n) || axis > 2 || nb == 0) return ORX_ERR_INVALID_ARGUMENT;
+    r->own_on = 1;
+    r->own_axis = axis;
+    r->own_nb = nb;
+    r->own_lo = own_lo;
+    r->own_hi = own_hi;
     const size_t S = local_slots(r);
     const size_t need = n > S ? n : S;
     if (need > S) { /* realloc keeps the contents; the own photon pass uses the first S entries */

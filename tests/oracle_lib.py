@@ -113,9 +113,11 @@ class OracleShard:
             ("orc_vcm_finish", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
             ("orc_ppm_local_trace", [C.c_void_p, C.c_uint64, C.c_uint64, C.c_float, C.c_void_p], C.c_int),
             ("orc_ppm_slab_histogram", [C.c_void_p, C.c_void_p, C.c_uint32], C.c_int),
-            ("orc_ppm_slab_pack", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64,
-                                   C.c_void_p], C.c_int),
-            ("orc_ppm_slab_import", [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p], C.c_int),
+            ("orc_ppm_slab_pack", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                                   C.c_uint64, C.c_void_p], C.c_int),
+            ("orc_ppm_slab_import", [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_uint32,
+                                     C.c_uint32, C.c_uint32], C.c_int),
+            ("orc_ppm_slab_halo", [C.c_void_p, C.c_uint32, C.c_uint32, C.c_float], C.c_uint32),
         ):
             f = getattr(lib, name)
             f.argtypes, f.restype = args, res
@@ -146,16 +148,20 @@ class OracleShard:
     def slab_histogram(self, hist, nb):
         self.r._check(self.lib.orc_ppm_slab_histogram(self.r.h, C.c_void_p(hist.data_ptr()), nb))
 
-    def slab_pack(self, bin_dest, nb, axis, base, n_records, send):
+    def slab_halo(self, nb, axis, radius):
+        return int(self.lib.orc_ppm_slab_halo(self.r.h, nb, axis, radius))
+
+    def slab_pack(self, bin_dest, nb, axis, halo, base, n_records, send):
         bd = np.ascontiguousarray(bin_dest, np.uint8)
         bs = np.ascontiguousarray(base, np.uint32)
-        self.r._check(self.lib.orc_ppm_slab_pack(self.r.h, bd.ctypes.data, nb, axis, bs.ctypes.data, n_records,
-                                                 C.c_void_p(send.data_ptr())))
+        self.r._check(self.lib.orc_ppm_slab_pack(self.r.h, bd.ctypes.data, nb, axis, halo, bs.ctypes.data,
+                                                 n_records, C.c_void_p(send.data_ptr())))
 
-    def slab_import(self, recv, n_records, box=None):
+    def slab_import(self, recv, n_records, box, axis, nb, own):
         bx = None if box is None else np.ascontiguousarray(box, np.uint32)
         self.r._check(self.lib.orc_ppm_slab_import(self.r.h, C.c_void_p(recv.data_ptr()), n_records,
-                                                   None if bx is None else bx.ctypes.data))
+                                                   None if bx is None else bx.ctypes.data, axis, nb, own[0],
+                                                   own[1]))
 
     def alloc(self, nfloat):
         return self.torch.zeros(nfloat, dtype=self.torch.float32)

@@ -31,26 +31,27 @@ def make_shards(scene, world, P, PH, slab=False, pipelined=False, photon_map=0, 
     return shards
 
 
-def slab_exchange(shards, world, nb=multigpu.SLAB_BINS):
+def slab_exchange(shards, world, radius, nb=multigpu.SLAB_BINS):
     hists = []
     for b in shards:
         h = b.alloc_i32(multigpu.slab_hist_words(nb))
         b.slab_histogram(h, nb)
         hists.append(h)
     H, vox, box = multigpu.split_slab_hists(torch.stack(hists).cpu().numpy(), world, nb)
-    axis, bin_dest, counts = multigpu.slab_plan(H, world, vox)
+    halo = [shards[0].slab_halo(nb, a, radius) for a in range(3)]
+    axis, bin_dest, counts = multigpu.slab_plan(H, world, vox, halo)
     sends = []
     for rank, b in enumerate(shards):
         n = counts[rank]
         base = np.concatenate([[0], np.cumsum(n)[:-1]]).astype(np.uint32)
         send = b.alloc(9 * int(n.sum()) + 9)
-        b.slab_pack(bin_dest, nb, axis, base, int(n.sum()), send)
+        b.slab_pack(bin_dest, nb, axis, halo[axis], base, int(n.sum()), send)
         sends.append((send, base, n))
     for d, b in enumerate(shards):
         parts = [s[9 * int(base[d]):9 * int(base[d] + n[d])] for s, base, n in sends]
         recv = torch.cat(parts) if parts else b.alloc(0)
         nr = int(counts[:, d].sum())
-        b.slab_import(recv.contiguous(), nr, box)
+        b.slab_import(recv.contiguous(), nr, box, axis, nb, multigpu.slab_owned(bin_dest, d))
     return axis, counts
 
 
@@ -82,7 +83,7 @@ def run_iterations(shards, scene, W, H, req, iters, slab=False, pipelined=False,
                 else:
                     b.local_photons()
         if slab:
-            plans.append(slab_exchange(shards, world))
+            plans.append(slab_exchange(shards, world, radius))
         ctx = torch.cuda.stream(side) if pipelined else torch.cuda.stream(main)
         with ctx:
             if pipelined:

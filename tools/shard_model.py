@@ -146,17 +146,19 @@ def run_slab(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None, nb=mult
             hists.append(h)
         hp_all.copy_(torch.cat(hps))
         Hh, vox, box = multigpu.split_slab_hists(torch.stack(hists).cpu().numpy(), world, nb)
-        axis, bin_dest, counts = multigpu.slab_plan(Hh, world, vox)
+        halo = [shards[0].slab_halo(nb, a, radius) for a in range(3)]
+        axis, bin_dest, counts = multigpu.slab_plan(Hh, world, vox, halo)
         sends = []
         for k, b in enumerate(shards):
             n = counts[k]
             base = np.concatenate([[0], np.cumsum(n)[:-1]]).astype(np.uint32)
             send = b.alloc(9 * int(n.sum()) + 9)
-            ms[k]["hist_pack"] += timed(lambda: b.slab_pack(bin_dest, nb, axis, base, int(n.sum()), send))
+            ms[k]["hist_pack"] += timed(lambda: b.slab_pack(bin_dest, nb, axis, halo[axis], base, int(n.sum()), send))
             sends.append((send, base, n))
         for d, b in enumerate(shards):
             recv = torch.cat([s_[9 * int(bs[d]):9 * int(bs[d] + n_[d])] for s_, bs, n_ in sends]).contiguous()
-            ms[d]["import_grid"] += timed(lambda: b.slab_import(recv, int(counts[:, d].sum()), box))
+            ms[d]["import_grid"] += timed(lambda: b.slab_import(recv, int(counts[:, d].sum()), box, axis, nb,
+                                                                multigpu.slab_owned(bin_dest, d)))
             ms[d]["gather"] += timed(lambda: b.gather_external(hp_all, world, part))
             if it == iters - 1:
                 # diagnostic: the non-specular hit points whose sphere reaches this rank's photons
@@ -168,8 +170,14 @@ def run_slab(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None, nb=mult
                     A = hp_all.view(world, -1)[:, :mr * W * 4].reshape(-1, 4)
                     ns = (A[:, 3].view(torch.int32) & (1 << 27)) != 0
                     q = A[:, :3]
-                    hit = ns & ((q + radius >= lo) & (q - radius <= hi)).all(1)
-                    diag.append((d, int(ns.sum()), int(hit.sum()), int(pr.shape[0])))
+                    # owned hit points: bin of the slab axis in this rank's range (float32 as the device)
+                    alo, ahi = np.float32(scene.aabb_min[axis]), np.float32(scene.aabb_max[axis])
+                    inv = np.float32(nb) / (ahi - alo)
+                    v = q[:, axis].cpu().numpy().astype(np.float32)
+                    bins = np.clip(np.floor((v - alo) * inv), 0, nb - 1).astype(np.int64)
+                    o0, o1 = multigpu.slab_owned(bin_dest, d)
+                    own = ns.cpu().numpy() & (bins >= o0) & (bins <= o1)
+                    diag.append((d, int(ns.sum()), int(own.sum()), int(pr.shape[0])))
             ms[d]["finish"] += timed(lambda: b.finish(part[:mr * W * 3].contiguous()))
         if it >= warm:
             for k in range(world):
@@ -182,7 +190,7 @@ def run_slab(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None, nb=mult
     slowest = max(range(world), key=lambda k: sum(per_rank[k].values()))
     for b in shards:
         b.r.destroy()
-    print("  (rank, NS hit points, gathered, photons):", diag, flush=True)
+    print("  (rank, NS hit points, owned, photons received):", diag, flush=True)
     return per_rank, slowest, a2a_mb, int(axis), counts
 
 
