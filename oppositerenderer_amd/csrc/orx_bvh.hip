@@ -385,7 +385,8 @@ __global__ void k_bvh_collapse(CollapseBufs C, const CollapseItem* __restrict__ 
             for (uint32_t i = 0; i < nc && good; i++) good = quantise8(lo[k], e, B[ch[i]].lo[k], B[ch[i]].hi[k], ql[i], qh[i]);
             if (!good) continue;
             uint32_t wl = 0, wh = 0;
-            for (int i = 0; i < 4; i++) wl |= ql[i] << (8 * i), wh |= qh[i] << (8 * i);
+            /* an empty slot gets the empty box lo = 255 > hi = 0: every ray misses it */
+            for (int i = 0; i < 4; i++) wl |= ((uint32_t)i < nc ? ql[i] : 255u) << (8 * i), wh |= qh[i] << (8 * i);
             nd.qlo[k] = wl;
             nd.qhi[k] = wh;
             (k == 0 ? nd.sx : k == 1 ? nd.sy : nd.sz) = ldexpf(1.0f, e); /* 2^e, exact for e in [-126, 127] */

@@ -252,7 +252,8 @@ struct Bvh4Builder {
                     good = quantise(lo[k], e, B[ch[i]].lo[k], B[ch[i]].hi[k], ql[i], qh[i]);
                 if (!good) continue;
                 uint32_t wl = 0, wh = 0;
-                for (int i = 0; i < 4; i++) wl |= ql[i] << (8 * i), wh |= qh[i] << (8 * i);
+                /* an empty slot gets the empty box lo = 255 > hi = 0: every ray misses it */
+                for (int i = 0; i < 4; i++) wl |= ((size_t)i < ch.size() ? ql[i] : 255u) << (8 * i), wh |= qh[i] << (8 * i);
                 nd.qlo[k] = wl;
                 nd.qhi[k] = wh;
                 (k == 0 ? nd.sx : k == 1 ? nd.sy : nd.sz) = ldexpf(1.0f, e); /* 2^e, exact for e in [-126, 127] */
@@ -583,6 +584,9 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
         if (s0 != ORX_OK) return s0;
     }
     const uint32_t nq = s->n_quads, ns = s->n_spheres, nt = s->n_triangles, nm = s->n_materials;
+    /* the traversal addresses triangles (48 B) and BVH4 nodes (64 B, fewer than triangles) with
+     * 32-bit byte offsets */
+    if (nt >= (1u << 26)) return set_err(r, ORX_ERR_UNSUPPORTED, "more than 2^26 triangles");
     /* validate material indices and triangle vertex indices */
     for (uint32_t i = 0; i < nq; i++)
         if (s->quad_material[i] >= nm) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "quad material out of range");

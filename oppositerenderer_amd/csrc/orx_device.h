@@ -439,14 +439,26 @@ __device__ __forceinline__ void node_test_q(const float4 A, const float4 B, cons
             const int i = 2 * h + e;
             const float t0 = fmaxf(fmaxf(fmaxf(tnx[e], tny[e]), tnz[e]), tmin);
             const float t1 = fminf(fminf(fminf(tfx[e], tfy[e]), tfz[e]), tmax);
-            t[i] = (t0 <= t1 && c[i] != ORX_EMPTY) ? t0 : INFINITY;
+            t[i] = t0 <= t1 ? t0 : INFINITY; /* an empty slot holds an empty box (lo 255 > hi 0) */
         }
     }
 }
+/* Node and triangle loads are buffer loads: one 32-bit byte offset per lane (a shift, where a
+ * 64-bit address costs two 64-bit VALU operations), the resource in SGPRs.  orx_init_scene keeps
+ * the node and triangle arrays below 4 GiB. */
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t orx_rsrc(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0xffffffff, 0x00020000);
+}
+__device__ __forceinline__ float4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t bo) {
+    typedef uint32_t u4b __attribute__((ext_vector_type(4)));
+    const u4b v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)bo, 0, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
 __device__ __forceinline__ void node_test(const DevBvh4* nodes, uint32_t idx, const RayBox& rb, float tmin, float tmax,
                                           float t[4], uint32_t c[4]) {
-    const float4* p = reinterpret_cast<const float4*>(nodes + idx);
-    node_test_q(p[0], p[1], p[2], p[3], rb, tmin, tmax, t, c);
+    const __amdgpu_buffer_rsrc_t r = orx_rsrc(nodes);
+    const uint32_t bo = idx << 6;
+    node_test_q(ld16(r, bo), ld16(r, bo + 16), ld16(r, bo + 32), ld16(r, bo + 48), rb, tmin, tmax, t, c);
 }
 typedef float v2t __attribute__((ext_vector_type(2)));
 /* fp32-box node test: t = fma(bound, inv, -o*inv), two children per
@@ -479,14 +491,16 @@ __device__ __forceinline__ void node_test(const DevBvh4F* nodes, uint32_t idx, c
         t[i] = (t0 <= t1 && c[i] != 0xffffffffu) ? t0 : INFINITY;
     }
 }
+/* compare-exchange by entry distance; the distances by min/max (never NaN here: +inf or a
+ * max with tmin), which leaves the compare's mask to the two reference selects */
 __device__ __forceinline__ void cswap(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {
     const bool sw = tb < ta;
-    const float t = sw ? tb : ta;
     const uint32_t c = sw ? cb : ca;
-    tb = sw ? ta : tb;
     cb = sw ? ca : cb;
-    ta = t;
     ca = c;
+    const float lo = fminf(ta, tb);
+    tb = fmaxf(ta, tb);
+    ta = lo;
 }
 
 /* Traversal policies (trace_closest_t / trace_any_t): the stack (StackL: the
@@ -634,8 +648,10 @@ __device__ inline bool trace_closest_t(const DevScene& S, f3 o, f3 d, float tmin
                 ORX_TS_INC(ts_leaves, 1);
                 ORX_TS_INC(ts_tris, cnt);
                 ORX_TS_WAVE(ts_wl);
+                const __amdgpu_buffer_rsrc_t tr = orx_rsrc(S.tri_v);
                 for (uint32_t k = first; k < first + cnt; k++) {
-                    const float4 v0 = S.tri_v[3 * k], v1 = S.tri_v[3 * k + 1], v2 = S.tri_v[3 * k + 2];
+                    const uint32_t tb = k * 48u;
+                    const float4 v0 = ld16(tr, tb), v1 = ld16(tr, tb + 16), v2 = ld16(tr, tb + 32);
                     const int32_t gid = (int32_t)(base + __float_as_uint(v0.w));
                     float b, g;
                     /* accept t < best, or t == best from a lower primitive id */
@@ -669,6 +685,7 @@ __device__ __forceinline__ bool trace_closest(const DevScene& S, f3 o, f3 d, flo
                                               uint32_t* stk) {
     return trace_closest_t(S, o, d, tmin, tmax, h, StackL{stk}, NodesG{});
 }
+
 /* any hit in (tmin,tmax): every material's RayType::SHADOW any-hit is
  * gatherAnyHitOnNonEmitter (Material.cpp:18-26, DirectRadianceEstimation.cu:79-83) */
 template <class STK, class NODES>
@@ -730,10 +747,12 @@ __device__ inline bool trace_any_t(const DevScene& S, f3 o, f3 d, float tmin, fl
                 const uint32_t first = (lf & 0x7fffffffu) >> 3, cnt = (lf & 7u) + 1u;
                 ORX_TS_INC(ts_leaves, 1);
                 ORX_TS_WAVE(ts_wl);
+                const __amdgpu_buffer_rsrc_t tr = orx_rsrc(S.tri_v);
                 for (uint32_t k = first; k < first + cnt; k++) {
                     float b, g;
                     ORX_TS_INC(ts_tris, 1);
-                    if (isect_tri(ld_f3(S.tri_v[3 * k]), ld_f3(S.tri_v[3 * k + 1]), ld_f3(S.tri_v[3 * k + 2]), o, d,
+                    const uint32_t tb = k * 48u;
+                    if (isect_tri(ld_f3(ld16(tr, tb)), ld_f3(ld16(tr, tb + 16)), ld_f3(ld16(tr, tb + 32)), o, d,
                                   tmin, tmax, t, b, g)) {
                         ORX_TS_FLUSH(4);
                         return true;

@@ -210,26 +210,17 @@ __device__ __forceinline__ void photon_emit(const DevScene& S, const PixelBufs& 
     P.mask = 0;
 }
 
-/* One bounce of a photon path (Diffuse.cu:92-135, Glossy.cu:94-137, Mirror.cu:65-77,
- * Glass.cu:164-205, DiffuseEmitter.cu:56-59); false once the path has ended (its
- * deposit mask and RNG state are then stored). */
-template <bool MEDIA, class STK, class NODES>
-__device__ __forceinline__ bool photon_bounce(const DevScene& S, const PixelBufs& px, const PhotonBufs& pb,
-                                              const Consts& c, PhotonPath& P, Rng& rs, const STK& stk,
-                                              const NODES& nodes, float& lo_x, float& lo_y, float& lo_z,
-                                              float& hi_x, float& hi_y, float& hi_z, const VolMap& vm,
-                                              PhotonMedia& M, const MediaBufs& mb) {
+/* What a photon does at the end of its ray (Diffuse.cu:92-135, Glossy.cu:94-137, Mirror.cu:65-77,
+ * Glass.cu:164-205, DiffuseEmitter.cu:56-59, ParticipatingMedium.cu:110-201): deposit,
+ * Russian roulette and the next ray in P; false once the path has ended (its deposit mask and
+ * RNG state are then stored). */
+template <bool MEDIA>
+__device__ __forceinline__ bool photon_after_hit(const DevScene& S, const PixelBufs& px, const PhotonBufs& pb,
+                                                 const Consts& c, PhotonPath& P, Rng& rs, bool hit, const Hit& h,
+                                                 bool had_probe, float& lo_x, float& lo_y, float& lo_z, float& hi_x,
+                                                 float& hi_y, float& hi_z, const VolMap& vm, PhotonMedia& M,
+                                                 const MediaBufs& mb) {
     bool done = false;
-    Hit h;
-    bool had_probe = false;
-    bool hit;
-    if (MEDIA) {
-        had_probe = M.probe;
-        M.probe = false;
-        hit = trace_closest_m(S, vm, P.o, P.d, P.tmin, M.tmax, M.inmed, h, stk, nodes);
-    } else {
-        hit = trace_closest_t(S, P.o, P.d, P.tmin, RT_DEFAULT_MAX, h, stk, nodes);
-    }
     if (!hit) {
         done = true;
     } else if (MEDIA && h.prim == MED_PRIM) {
@@ -365,6 +356,27 @@ __device__ __forceinline__ bool photon_bounce(const DevScene& S, const PixelBufs
     }
     return true;
 }
+
+/* One bounce of a photon path: its ray, then photon_after_hit. */
+template <bool MEDIA, class STK, class NODES>
+__device__ __forceinline__ bool photon_bounce(const DevScene& S, const PixelBufs& px, const PhotonBufs& pb,
+                                              const Consts& c, PhotonPath& P, Rng& rs, const STK& stk,
+                                              const NODES& nodes, float& lo_x, float& lo_y, float& lo_z,
+                                              float& hi_x, float& hi_y, float& hi_z, const VolMap& vm,
+                                              PhotonMedia& M, const MediaBufs& mb) {
+    Hit h;
+    bool had_probe = false;
+    bool hit;
+    if (MEDIA) {
+        had_probe = M.probe;
+        M.probe = false;
+        hit = trace_closest_m(S, vm, P.o, P.d, P.tmin, M.tmax, M.inmed, h, stk, nodes);
+    } else {
+        hit = trace_closest_t(S, P.o, P.d, P.tmin, RT_DEFAULT_MAX, h, stk, nodes);
+    }
+    return photon_after_hit<MEDIA>(S, px, pb, c, P, rs, hit, h, had_probe, lo_x, lo_y, lo_z, hi_x, hi_y, hi_z, vm, M, mb);
+}
+
 __device__ __forceinline__ void photon_bbox_flush(const PhotonBufs& pb, float lo_x, float lo_y, float lo_z, float hi_x,
                                                   float hi_y, float hi_z, uint32_t rep, uint32_t lane) {
     /* wave AABB -> device-wide ordered-int atomics (one lane per component) */

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out/t
+timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t/gputest.log 2>&1 || { tail -30 gpurun_out/t/gputest.log; exit 1; }
+tail -2 gpurun_out/t/gputest.log
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/t/smoke.log 2>&1 && tail -1 gpurun_out/t/smoke.log
+timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/t/bench.log 2>&1 && tail -1 gpurun_out/t/bench.log | cut -c1-400

@@ -1,8 +1,7 @@
-# GPU suite, then an A/B of one switch on the default bench: tools/gpu_test_ab.sh VAR "v1 v2 ..." [pytest -k expr]
+# full GPU suite on the current liborx.so, then an A/B of in-tree libs: tools/gpu_test_ab.sh "base cur" [bench args]
 set -o pipefail
-VAR=$1; VALS=$2; K=${3:-}
+LIBS=$1; shift
 mkdir -p gpurun_out/t
-if [ -n "$K" ]; then KA=(-k "$K"); else KA=(); fi
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "${KA[@]}" > gpurun_out/t/gputest.log 2>&1 || { tail -30 gpurun_out/t/gputest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t/gputest.log 2>&1 || { tail -30 gpurun_out/t/gputest.log; exit 1; }
 tail -2 gpurun_out/t/gputest.log
-bash tools/gpu_ab.sh $VAR "$VALS"
+bash tools/gpu_lib_ab.sh "$LIBS" "$@"
