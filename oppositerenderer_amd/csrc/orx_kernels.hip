@@ -968,6 +968,31 @@ __device__ __forceinline__ void window_visits(const uint32_t* __restrict__ offse
     dC += nrows;
 }
 
+/* photonPower (IndirectRadianceEstimation.cu:59-67), w = alpha*(1 - (1 - exp(-beta d^2 / 2r^2)) /
+ * (1 - e^-beta)), evaluated as one degree-5 polynomial in u = d^2/r^2: the minimax fit of w(u) on
+ * [0, 1] (relative error 7.7e-7; 1.2e-6 with fp32 coefficients and Horner rounding).  One v_pk_mul
+ * and five v_pk_fma_f32 per pair of photons, the coefficients compile-time constants (SGPRs); the
+ * accepted photons are decided by the exact distance test, so only the weights (and the sums,
+ * summed in another order anyway) differ from the oracle's. */
+constexpr float ORX_W5_C0 = 1.8179986476898193f, ORX_W5_C1 = -2.0686328411102295f;
+constexpr float ORX_W5_C2 = 1.0091534852981567f, ORX_W5_C3 = -0.32518523931503296f;
+constexpr float ORX_W5_C4 = 0.07352562248706818f, ORX_W5_C5 = -0.009477914310991764f;
+__device__ __forceinline__ v2f weight2(v2f ir2, v2f d2) {
+    const v2f u = d2 * ir2;
+    v2f p = __builtin_elementwise_fma(v2f{ORX_W5_C5, ORX_W5_C5}, u, v2f{ORX_W5_C4, ORX_W5_C4});
+    p = __builtin_elementwise_fma(p, u, v2f{ORX_W5_C3, ORX_W5_C3});
+    p = __builtin_elementwise_fma(p, u, v2f{ORX_W5_C2, ORX_W5_C2});
+    p = __builtin_elementwise_fma(p, u, v2f{ORX_W5_C1, ORX_W5_C1});
+    return __builtin_elementwise_fma(p, u, v2f{ORX_W5_C0, ORX_W5_C0});
+}
+/* int8 facing prefilter dot product: v_dot4_i32_i8 with the inline 0 accumulator (the builtin
+ * selects v_dot4c_i32_i8, whose accumulator costs a v_mov per use) */
+__device__ __forceinline__ int32_t sdot4_0(int32_t a, int32_t b) {
+    int32_t r;
+    asm("v_dot4_i32_i8 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 constexpr uint32_t GQ = 8; /* chord ranges per lane per phase A (LDS: GQ * 8 B per lane) */
 
 /* the hit point's sphere (grown by a margin far above the rounding of the distance test) misses
@@ -1044,15 +1069,7 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
             if (gi.visits) window_visits(pb.offsets, g.gx, g.gy, x_lo, x_hi, y_lo, ny, z_lo, nrows, dC, dP);
         }
     }
-    const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
-    const float inv2r2 = 1.0f / (2 * radius2);
-    const float invDen = 1.0f / (1 - expNegativeBeta);
-    const float kx = -beta * inv2r2;
-    const float wB = alpha * invDen, wA = alpha - wB; /* w = A + B*exp(x) */
-    const v2f kx2 = v2f{kx, kx};
-    const v2f wc6 = wB * ORX_EXPU_C6, wc5 = wB * ORX_EXPU_C5, wc4 = wB * ORX_EXPU_C4;
-    const v2f wc3 = wB * ORX_EXPU_C3, wc2 = wB * ORX_EXPU_C2, wc1 = wB * ORX_EXPU_C1;
-    const v2f wc0 = v2f{wA + wB, wA + wB};
+    const v2f ir2 = v2f{1.0f / radius2, 1.0f / radius2};
     v2f accx = v2f{0.f, 0.f}, accy = accx, accz = accx;
     const v2f px2 = v2f{pos.x, pos.x}, py2 = v2f{pos.y, pos.y}, pz2 = v2f{pos.z, pos.z};
     const v2f nx2 = v2f{B.x, B.x}, ny2 = v2f{B.y, B.y}, nz2 = v2f{B.z, B.z};
@@ -1136,10 +1153,8 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
             if (!(in0 | in1 | in2 | in3)) continue;
             /* facing: dot(-dir, n) >= 0  <=>  dot(dir, n) <= 0 (negation is exact) */
             const u4v Q = __builtin_amdgcn_raw_buffer_load_b128(SR, (int)bo, (int)(SP_DIRQ * PB), 0);
-            const int32_t q0 = __builtin_amdgcn_sdot4((int32_t)Q.x, nq, 0, false);
-            const int32_t q1 = __builtin_amdgcn_sdot4((int32_t)Q.y, nq, 0, false);
-            const int32_t q2 = __builtin_amdgcn_sdot4((int32_t)Q.z, nq, 0, false);
-            const int32_t q3 = __builtin_amdgcn_sdot4((int32_t)Q.w, nq, 0, false);
+            const int32_t q0 = sdot4_0((int32_t)Q.x, nq), q1 = sdot4_0((int32_t)Q.y, nq);
+            const int32_t q2 = sdot4_0((int32_t)Q.z, nq), q3 = sdot4_0((int32_t)Q.w, nq);
             in0 = in0 && q0 <= DIRQ_BAND;
             in1 = in1 && q1 <= DIRQ_BAND;
             in2 = in2 && q2 <= DIRQ_BAND;
@@ -1157,20 +1172,8 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
             }
             if (!(in0 | in1 | in2 | in3)) continue;
             const f4u WX = ldp(SR, SP_PX * PB, bo), WY = ldp(SR, SP_PY * PB, bo), WZ = ldp(SR, SP_PZ * PB, bo);
-            /* photonPower: alpha*(1 - (1 - exp(x)) / (1 - e^-beta)), x = -beta d^2 / 2r^2,
-             * folded into one Horner chain w = (A + B) + x*B*p(x) with A = alpha*(1 - 1/den),
-             * B = alpha/den, evaluated with fused multiply-adds, two photons per v_pk_fma_f32.
-             * Rejected photons (whose x may lie outside [-beta/2, 0]) get weight 0 by
-             * select, so their polynomial value is never used */
-            const v2f x0 = d20 * kx2;
-            const v2f x1 = d21 * kx2;
-            v2f p0 = wc6, p1 = wc6;
-            p0 = __builtin_elementwise_fma(p0, x0, wc5); p1 = __builtin_elementwise_fma(p1, x1, wc5);
-            p0 = __builtin_elementwise_fma(p0, x0, wc4); p1 = __builtin_elementwise_fma(p1, x1, wc4);
-            p0 = __builtin_elementwise_fma(p0, x0, wc3); p1 = __builtin_elementwise_fma(p1, x1, wc3);
-            p0 = __builtin_elementwise_fma(p0, x0, wc2); p1 = __builtin_elementwise_fma(p1, x1, wc2);
-            p0 = __builtin_elementwise_fma(p0, x0, wc1); p1 = __builtin_elementwise_fma(p1, x1, wc1);
-            v2f w0 = __builtin_elementwise_fma(p0, x0, wc0), w1 = __builtin_elementwise_fma(p1, x1, wc0);
+            /* the weight of every photon of the batch (rejected ones get 0 by select) */
+            v2f w0 = weight2(ir2, d20), w1 = weight2(ir2, d21);
             ORX_TS_INC(ts_tris, (uint32_t)in0 + (uint32_t)in1 + (uint32_t)in2 + (uint32_t)in3);
             w0.x = in0 ? w0.x : 0.f;
             w0.y = in1 ? w0.y : 0.f;
@@ -1270,7 +1273,7 @@ struct UAcc {
     v2f accx, accy, accz;
 };
 struct UConst {
-    v2f px2, py2, pz2, nx2, ny2, nz2, kx2, wc6, wc5, wc4, wc3, wc2, wc1, wc0;
+    v2f px2, py2, pz2, nx2, ny2, nz2, ir2;
     int32_t nq;
     const float* SDX;
     const float* SDY;
@@ -1309,10 +1312,8 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
         }
         if (!wave_any(in0 | in1 | in2 | in3)) continue;
         const uint4 Q = reinterpret_cast<const uint4*>(L4)[48 + (e >> 2)];
-        const int32_t q0 = __builtin_amdgcn_sdot4((int32_t)Q.x, k.nq, 0, false);
-        const int32_t q1 = __builtin_amdgcn_sdot4((int32_t)Q.y, k.nq, 0, false);
-        const int32_t q2 = __builtin_amdgcn_sdot4((int32_t)Q.z, k.nq, 0, false);
-        const int32_t q3 = __builtin_amdgcn_sdot4((int32_t)Q.w, k.nq, 0, false);
+        const int32_t q0 = sdot4_0((int32_t)Q.x, k.nq), q1 = sdot4_0((int32_t)Q.y, k.nq);
+        const int32_t q2 = sdot4_0((int32_t)Q.z, k.nq), q3 = sdot4_0((int32_t)Q.w, k.nq);
         in0 = in0 && q0 <= DIRQ_BAND;
         in1 = in1 && q1 <= DIRQ_BAND;
         in2 = in2 && q2 <= DIRQ_BAND;
@@ -1331,15 +1332,7 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
         }
         if (!wave_any(in0 | in1 | in2 | in3)) continue;
         const float4 WX = L4[64 + (e >> 2)], WY = L4[80 + (e >> 2)], WZ = L4[96 + (e >> 2)];
-        const v2f x0 = d20 * k.kx2;
-        const v2f x1 = d21 * k.kx2;
-        v2f p0 = k.wc6, p1 = k.wc6;
-        p0 = __builtin_elementwise_fma(p0, x0, k.wc5); p1 = __builtin_elementwise_fma(p1, x1, k.wc5);
-        p0 = __builtin_elementwise_fma(p0, x0, k.wc4); p1 = __builtin_elementwise_fma(p1, x1, k.wc4);
-        p0 = __builtin_elementwise_fma(p0, x0, k.wc3); p1 = __builtin_elementwise_fma(p1, x1, k.wc3);
-        p0 = __builtin_elementwise_fma(p0, x0, k.wc2); p1 = __builtin_elementwise_fma(p1, x1, k.wc2);
-        p0 = __builtin_elementwise_fma(p0, x0, k.wc1); p1 = __builtin_elementwise_fma(p1, x1, k.wc1);
-        v2f w0 = __builtin_elementwise_fma(p0, x0, k.wc0), w1 = __builtin_elementwise_fma(p1, x1, k.wc0);
+        v2f w0 = weight2(k.ir2, d20), w1 = weight2(k.ir2, d21);
         w0.x = in0 ? w0.x : 0.f;
         w0.y = in1 ? w0.y : 0.f;
         w1.x = in2 ? w1.x : 0.f;
@@ -1408,15 +1401,6 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
             window_visits(pb.offsets, g.gx, g.gy, x_lo, x_hi, y_lo, y_hi - y_lo + 1, z_lo,
                           (z_hi - z_lo + 1) * (y_hi - y_lo + 1), dC, dP);
     }
-    const float alpha = 1.818f, beta = 1.953f, expNegativeBeta = 0.141847f;
-    const float inv2r2 = 1.0f / (2 * radius2);
-    const float invDen = 1.0f / (1 - expNegativeBeta);
-    const float kx = -beta * inv2r2;
-    const float wB = alpha * invDen, wA = alpha - wB;
-    const v2f kx2 = v2f{kx, kx};
-    const v2f wc6 = wB * ORX_EXPU_C6, wc5 = wB * ORX_EXPU_C5, wc4 = wB * ORX_EXPU_C4;
-    const v2f wc3 = wB * ORX_EXPU_C3, wc2 = wB * ORX_EXPU_C2, wc1 = wB * ORX_EXPU_C1;
-    const v2f wc0 = v2f{wA + wB, wA + wB};
     v2f accx = v2f{0.f, 0.f}, accy = accx, accz = accx;
     const v2f px2 = v2f{pos.x, pos.x}, py2 = v2f{pos.y, pos.y}, pz2 = v2f{pos.z, pos.z};
     const v2f nx2 = v2f{B.x, B.x}, ny2 = v2f{B.y, B.y}, nz2 = v2f{B.z, B.z};
@@ -1434,7 +1418,7 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
     const float m = g.cell * 1e-3f;
     constexpr uint32_t HS = NSUB > 1 ? SUBR : 1u;
     const float hc = g.cell / (float)HS;
-    const UConst UK{px2, py2, pz2, nx2, ny2, nz2, kx2, wc6, wc5, wc4, wc3, wc2, wc1, wc0, nq, SDX, SDY, SDZ};
+    const UConst UK{px2, py2, pz2, nx2, ny2, nz2, v2f{1.0f / radius2, 1.0f / radius2}, nq, SDX, SDY, SDZ};
     UAcc UA{accx, accy, accz};
     /* the union of the lanes' windows (rows) */
     const uint32_t UZ0 = wave_min_u32(act ? z_lo : 0xffffffffu), UZ1 = wave_max_u32(act ? z_hi : 0u);
