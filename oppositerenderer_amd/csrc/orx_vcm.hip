@@ -973,8 +973,6 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
                         npend++;
                     }
                 }
-                /* unused reserved rows: no test */
-                for (uint32_t k = npend; k < want; ++k) q[2 * (qbase + k)] = make_float4(0.f, 0.f, 0.f, -1.f);
             }
             /* the next vertex's direction before the shadow tests: it consumes the RNG after
              * the connections (the reference order) and needs neither their outcome nor the
@@ -987,16 +985,33 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
                     if (C.done) alive = false;
                 }
             }
-            const uint32_t total_q = __shfl(incl, 63, 64);
+            /* the wave's pending rays, compacted: entry e (of npend summed over the lanes) is row
+             * qbase[L] + e - pbase[L] of the lane L with pbase[L] <= e < pbase[L] + npend[L] (the
+             * largest lane with pbase[L] <= e), so every lane traces a ray in every round of the
+             * loop below (the reserved rows of failed connections are skipped) */
+            uint32_t pincl = npend;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(pincl, o, 64);
+                if (lane >= (uint32_t)o) pincl += y;
+            }
+            const uint32_t pbase = pincl - npend;
+            const uint32_t total_p = __shfl(pincl, 63, 64);
             __threadfence_block();
             /* all lanes trace the wave's shadow rays; the result goes into .w of the contribution row */
-            for (uint32_t e = lane; e < total_q; e += 64) {
-                const float4 r0 = q[2 * e];
-                if (r0.w < 0.f) continue;
-                const float4 r1 = q[2 * e + 1];
+            for (uint32_t e0 = 0; e0 < total_p; e0 += 64) {
+                /* the owner search runs on every lane (the shuffles read all lanes' bases) */
+                const uint32_t e = e0 + lane;
+                uint32_t L = 0;
+#pragma unroll
+                for (uint32_t st = 32; st; st >>= 1)
+                    if ((uint32_t)__shfl((int)pbase, (int)(L + st), 64) <= e) L += st;
+                const uint32_t row = (uint32_t)__shfl((int)qbase, (int)L, 64) + e - (uint32_t)__shfl((int)pbase, (int)L, 64);
+                if (e >= total_p) continue;
+                const float4 r0 = q[2 * row];
+                const float4 r1 = q[2 * row + 1];
                 const float4 hp = qhit[__float_as_uint(r1.w)];
                 const bool occ = occluded(S, mk(hp.x, hp.y, hp.z), mk(r0.x, r0.y, r0.z), r0.w, stk);
-                q[2 * e] = make_float4(r0.x, r0.y, r0.z, occ ? -2.f : -3.f);
+                q[2 * row] = make_float4(r0.x, r0.y, r0.z, occ ? -2.f : -3.f);
             }
             __threadfence_block();
             for (uint32_t k = 0; k < npend; ++k) {
