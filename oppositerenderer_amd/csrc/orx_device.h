@@ -771,6 +771,92 @@ __device__ __forceinline__ bool trace_any(const DevScene& S, f3 o, f3 d, float t
     return trace_any_t(S, o, d, tmin, tmax, StackL{stk}, NodesG{});
 }
 
+/* Several shadow rays per lane in one traversal loop: a lane whose ray has ended (occluder found,
+ * or stack empty) starts its next ray at once instead of waiting for the slowest lane of the wave
+ * to finish the current one, so a wave runs for the maximum over its lanes of their summed walks,
+ * not for the sum over the rays of the slowest walk.  Each ray's own test sequence is trace_any's
+ * (the same result, occluded or not).  RAYS supplies the lane's rays in order:
+ *   bool next(f3& o, f3& d, float& tmin, float& tmax)  — false when the lane has no more;
+ *   void result(bool occluded)                          — the outcome of the ray `next` gave last. */
+template <class RAYS>
+__device__ __forceinline__ void trace_any_chain(const DevScene& S, RAYS& R, uint32_t* stkp) {
+    const StackL stk{stkp};
+    f3 o = mk1(0.f), d = mk1(0.f);
+    float tmin = 0.f, tmax = 0.f;
+    RayBox rb = ray_box(o, mk1(1.f));
+    int sp = 0;
+    uint32_t ref = ORX_DONE, lf = 0;
+    /* the lane's next ray that needs a BVH walk (quad and sphere hits, and scenes without
+     * triangles, are decided here) */
+    auto fetch = [&]() -> bool {
+        while (R.next(o, d, tmin, tmax)) {
+            float t;
+            bool hit = false;
+            for (uint32_t i = 0; i < S.nq && !hit; i++) hit = isect_quad(S.quads[i], o, d, tmin, tmax, t);
+            for (uint32_t i = 0; i < S.ns && !hit; i++) {
+                f3 n;
+                hit = isect_sphere(S.spheres[i], o, d, tmin, tmax, t, n);
+            }
+            if (hit || !S.nt) {
+                R.result(hit);
+                continue;
+            }
+            rb = ray_box(o, d);
+            sp = 0;
+            ref = 0;
+            lf = 0;
+            return true;
+        }
+        return false;
+    };
+    bool have = fetch();
+    const __amdgpu_buffer_rsrc_t tr = orx_rsrc(S.tri_v);
+    while (__ballot(have)) {
+        if (!have) continue;
+        /* one round of trace_any_t's speculative while-while */
+        while (!(ref & ORX_LEAF) && ref != ORX_DONE) {
+            float ct[4];
+            uint32_t cc[4];
+            node_test(S.bvh4, ref, rb, tmin, tmax, ct, cc);
+            const int h0 = ct[0] != INFINITY, h1 = ct[1] != INFINITY, h2 = ct[2] != INFINITY, h3 = ct[3] != INFINITY;
+            stk.put(sp, cc[0]);
+            sp += h0;
+            stk.put(sp, cc[1]);
+            sp += h1;
+            stk.put(sp, cc[2]);
+            sp += h2;
+            stk.put(sp, cc[3]);
+            sp += h3;
+            const uint32_t next = h3 ? cc[3] : h2 ? cc[2] : h1 ? cc[1] : h0 ? cc[0] : ORX_DONE;
+            sp -= next != ORX_DONE;
+            ref = next != ORX_DONE ? next : (sp ? stk.pop(sp) : ORX_DONE);
+            if ((ref & ORX_LEAF) && !(lf & ORX_LEAF)) {
+                lf = ref;
+                ref = sp ? stk.pop(sp) : ORX_DONE;
+            }
+            if (!__ballot(!(lf & ORX_LEAF))) break;
+        }
+        bool occl = false;
+        while ((lf & ORX_LEAF) && !occl) {
+            const uint32_t first = (lf & 0x7fffffffu) >> 3, cnt = (lf & 7u) + 1u;
+            for (uint32_t k = first; k < first + cnt && !occl; k++) {
+                float t, b, g;
+                const uint32_t tb = k * 48u;
+                occl = isect_tri(ld_f3(ld16(tr, tb)), ld_f3(ld16(tr, tb + 16)), ld_f3(ld16(tr, tb + 32)), o, d, tmin,
+                                 tmax, t, b, g);
+            }
+            if (!occl) {
+                lf = ref;
+                if (ref & ORX_LEAF) ref = sp ? stk.pop(sp) : ORX_DONE;
+            }
+        }
+        if (occl || ref == ORX_DONE) {
+            R.result(occl);
+            have = fetch();
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t prim_material(const DevScene& S, const Hit& h) {
     if ((uint32_t)h.prim < S.nq) return S.qmat[h.prim];
     if ((uint32_t)h.prim < S.nq + S.ns) return S.smat[h.prim - S.nq];
@@ -1260,8 +1346,9 @@ __device__ inline void trace_radiance_vol(const DevScene& S, const VolMap& vm, u
 }
 
 /* getLightContribution (helpers/light.h:29-87) */
-__device__ inline f3 light_contribution(const DevScene& S, const DevLight& light, f3 pos, f3 normal, Rng& rs,
-                                        uint32_t* stk) {
+/* The sample half of light_contribution: the point on the light, the unshadowed contribution
+ * power * lightFactor and the shadow ray; false (contribution 0, no ray) when lightFactor <= 0 */
+__device__ inline bool light_sample(const DevLight& light, f3 pos, f3 normal, Rng& rs, f3& lc, f3& dir, float& tmax) {
     float lightFactor = 1;
     f3 pointOnLight;
     if (light.type == LIGHT_AREA) {
@@ -1272,7 +1359,7 @@ __device__ inline f3 light_contribution(const DevScene& S, const DevLight& light
         pointOnLight = light.position;
         lightFactor *= 1.f / 4.f;
     } else {
-        return mk1(0);
+        return false;
     }
     f3 towardsLight = pointOnLight - pos;
     float lightDistance = length(towardsLight);
@@ -1280,13 +1367,19 @@ __device__ inline f3 light_contribution(const DevScene& S, const DevLight& light
     float n_dot_l = maxf(0, dot(normal, towardsLight));
     lightFactor *= n_dot_l / (ORX_PI_F * lightDistance * lightDistance);
     if (light.type == LIGHT_AREA) lightFactor *= maxf(0, dot(-towardsLight, light.normal));
-    if (lightFactor > 0.0f) {
-        float tmax = (float)((double)lightDistance - 0.0001);
-        float att = trace_any(S, pos, towardsLight, 0.0001f, tmax, stk) ? 0.0f : 1.0f;
-        lightFactor *= att;
-        return light.power * lightFactor;
-    }
-    return mk1(0);
+    if (!(lightFactor > 0.0f)) return false;
+    tmax = (float)((double)lightDistance - 0.0001);
+    dir = towardsLight;
+    lc = light.power * lightFactor; /* = power * (lightFactor * att) for att = 1; occluded: 0 */
+    return true;
+}
+/* helpers/light.h:29-87 (shadow ray from pos + 0.0001 towards the light sample) */
+__device__ inline f3 light_contribution(const DevScene& S, const DevLight& light, f3 pos, f3 normal, Rng& rs,
+                                        uint32_t* stk) {
+    f3 lc, dir;
+    float tmax;
+    if (!light_sample(light, pos, normal, rs, lc, dir, tmax)) return mk1(0);
+    return trace_any(S, pos, dir, 0.0001f, tmax, stk) ? mk1(0.f) : lc;
 }
 
 }  // namespace orx

@@ -784,6 +784,43 @@ __device__ inline bool connect_light(const DevScene& S, const Subpath& C, const 
     return true;
 }
 
+/* The camera pass's deferred shadow rays for trace_any_chain: entry e of the wave's compacted
+ * list is row qqb[L] + e - qpb[L] of the lane L with qpb[L] <= e < qpb[L + 1] (binary search
+ * over the lanes' pending-count prefix); a lane takes entries lane, lane + 64, ...  The test is
+ * occluded()'s (segments shorter than 3 eps are unoccluded without a walk). */
+struct CamShadowRays {
+    float4* q;
+    const float4* qhit;
+    const uint32_t* pb;
+    const uint32_t* qb;
+    uint32_t e, total, row;
+    __device__ __forceinline__ bool next(f3& o, f3& d, float& tmin, float& tmax) {
+        while (e < total) {
+            uint32_t L = 0;
+#pragma unroll
+            for (uint32_t st = 32; st; st >>= 1)
+                if (pb[L + st] <= e) L += st;
+            row = qb[L] + e - pb[L];
+            e += 64;
+            const float4 r0 = q[2 * row];
+            if (r0.w < 3.f * VCM_EPS_RAY) {
+                reinterpret_cast<float*>(q + 2 * row)[3] = -3.f;
+                continue;
+            }
+            const float4 hp = qhit[__float_as_uint(q[2 * row + 1].w)];
+            o = mk(hp.x, hp.y, hp.z);
+            d = mk(r0.x, r0.y, r0.z);
+            tmin = VCM_EPS_RAY;
+            tmax = r0.w - 2.f * VCM_EPS_RAY;
+            return true;
+        }
+        return false;
+    }
+    __device__ __forceinline__ void result(bool occluded) {
+        reinterpret_cast<float*>(q + 2 * row)[3] = occluded ? -2.f : -3.f;
+    }
+};
+
 /* cameraPass (VCMCameraPass.cu:48-80), initCameraPayload (:100-135), cameraHit (vcm.h:527-628)
  *
  * Persistent waves with per-lane refill: a wave takes 64-pixel work items (one 8x8 tile
@@ -853,6 +890,7 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
      * utilisation.  Every subpath still adds its unoccluded contributions in
      * the reference order (light sample, then light vertices 0..n-1), so the
      * colour is unchanged bit for bit. */
+    __shared__ uint32_t qpb[64], qqb[64]; /* the lanes' pending-ray prefix and queue bases */
     float4* q = vb.shq + (size_t)blockIdx.x * VCM_SHQ_PER_WAVE;   /* [64 * 10][2] entries */
     float4* qhit = q + 2 * 64 * (VCM_MAX_VERTS + 1);              /* [64] connection points */
     CamPixel px;
@@ -996,22 +1034,15 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
             }
             const uint32_t pbase = pincl - npend;
             const uint32_t total_p = __shfl(pincl, 63, 64);
+            qpb[lane] = pbase;
+            qqb[lane] = qbase;
             __threadfence_block();
-            /* all lanes trace the wave's shadow rays; the result goes into .w of the contribution row */
-            for (uint32_t e0 = 0; e0 < total_p; e0 += 64) {
-                /* the owner search runs on every lane (the shuffles read all lanes' bases) */
-                const uint32_t e = e0 + lane;
-                uint32_t L = 0;
-#pragma unroll
-                for (uint32_t st = 32; st; st >>= 1)
-                    if ((uint32_t)__shfl((int)pbase, (int)(L + st), 64) <= e) L += st;
-                const uint32_t row = (uint32_t)__shfl((int)qbase, (int)L, 64) + e - (uint32_t)__shfl((int)pbase, (int)L, 64);
-                if (e >= total_p) continue;
-                const float4 r0 = q[2 * row];
-                const float4 r1 = q[2 * row + 1];
-                const float4 hp = qhit[__float_as_uint(r1.w)];
-                const bool occ = occluded(S, mk(hp.x, hp.y, hp.z), mk(r0.x, r0.y, r0.z), r0.w, stk);
-                q[2 * row] = make_float4(r0.x, r0.y, r0.z, occ ? -2.f : -3.f);
+            __builtin_amdgcn_wave_barrier();
+            /* all lanes trace the wave's shadow rays (lane l: entries l, l + 64, ..., chained in
+             * one traversal loop); the result goes into .w of the contribution row */
+            {
+                CamShadowRays R{q, qhit, qpb, qqb, lane, total_p, 0u};
+                trace_any_chain(S, R, stk);
             }
             __threadfence_block();
             for (uint32_t k = 0; k < npend; ++k) {
