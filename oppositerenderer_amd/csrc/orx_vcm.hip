@@ -830,7 +830,8 @@ struct CamShadowRays {
  * form measured a node-loop SIMT efficiency of 0.21).  Each subpath's arithmetic is
  * unchanged; only which lane runs it, and when, differs. */
 #ifndef ORX_VCM_CAMERA_WAVES
-#define ORX_VCM_CAMERA_WAVES 4 /* waves per SIMD the camera kernel is register-capped for (A/B: make vcm3) */
+#define ORX_VCM_CAMERA_WAVES 3 /* waves per SIMD the camera kernel is register-capped for: at 4 (128 VGPRs) it
+                                 * spilled ~120 VGPRs to scratch, 7.00 ms against 6.37 at 3 (A/B: make vcm4) */
 #endif
 struct CamPixel {
     uint32_t p;

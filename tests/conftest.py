@@ -5,6 +5,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+# torch's HIP runtime is loaded before liborx.so's first HIP call whatever tests a run selects:
+# loaded only after liborx had initialised HIP, torch's lazy device init reported "No HIP GPUs are
+# available" (a -k selection whose first torch user came after liborx tests)
+import torch  # noqa: E402,F401
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through liborx.so on HIP)")
