@@ -1607,11 +1607,15 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
     const uint32_t ntx = (gi.W + 15) / 16, nty = (rows + 15) / 16, ntiles = ntx * nty;
     const dim3 grid(8 * ((ntiles + 7) / 8));
     /* The sharded gather (segments = ranks, cell-order layout, no visit counters) meets 1/N of
-     * the photons: at N >= 8 the wave union's per-row work outweighs the photons it shares, and
-     * the per-lane kernel is faster (hall 1080p, tools/shard_model.py, per-rank gather union /
-     * per-lane: N=2 1.29 / 1.56 ms, N=4 0.73 / 0.80, N=8 0.47 / 0.43).  Measured on one device
-     * (serial hall gather / 4K conference frame): per-lane 2.5 ms / 120 ms, union 1.91 / 53.3. */
-    if (gi.segments >= 8 && !gi.cull) { /* a slab shard meets the single-device density: union */
+     * the photons.  Where a rank's photons are sparse in the grid the wave union's per-row work
+     * outweighs the photons it shares and the per-lane kernel is faster: hall 1080p, 2048^2
+     * launch (tools/shard_model.py, per-rank gather union / per-lane: N=2 1.29 / 1.56 ms, N=4
+     * 0.73 / 0.80, N=8 0.47 / 0.43, i.e. 4.2 / 2.1 slots per grid cell at N=4 / 8); at the 4K
+     * conference's 16M-photon launch the union is far ahead at N=8 too (8.4 slots per cell:
+     * 6.41 / 9.34 ms).  So the per-lane kernel takes row shards of 8+ segments below 3 slots per
+     * cell.  Measured on one device (serial hall gather / 4K conference frame): per-lane 2.5 ms /
+     * 120 ms, union 1.91 / 53.3. */
+    if (gi.segments >= 8 && !gi.cull && pb.S < 3u * pb.gmax) {
         if (pb.nsub == 1) hipLaunchKernelGGL((k_ppm_gather<1>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
         else hipLaunchKernelGGL((k_ppm_gather<SUBR * SUBR>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
         return;
