@@ -1473,7 +1473,8 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
     vb.splat = r->d_vsplat.as<float>();
     vb.splat_in = vb.splat + (size_t)r->rank * r->max_rows * r->W * 3;
     {
-        const size_t waves = vcm_camera_waves(((r->W + 7) / 8) * ((r->rows + 7) / 8));
+        const size_t waves = std::max(vcm_camera_waves(((r->W + 7) / 8) * ((r->rows + 7) / 8)),
+                                      vcm_light_waves((uint32_t)((lpx + 63) / 64)));
         HIPCHK(r, r->d_vshq.ensure(waves * VCM_SHQ_PER_WAVE * 16 + 16));
         vb.shq = r->d_vshq.as<float4>();
         HIPCHK(r, r->d_vwork.ensure(16));

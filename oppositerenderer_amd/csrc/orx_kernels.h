@@ -276,7 +276,7 @@ struct VcmBufs {
     float4* vC;         /* [9][W*H] normal.xyz | dVC */
     float4* vD;         /* [9][W*H] localDirFix.xyz | dVM */
     float4* vE;         /* [9][lcount] texel colour of Texture vertices (NULL without Texture materials) */
-    float4* shq;        /* [camera-pass waves][VCM_SHQ_PER_WAVE] deferred shadow-ray queues */
+    float4* shq;        /* [max(camera-, light-pass waves)][VCM_SHQ_PER_WAVE] deferred shadow-ray queues */
     float* splat;       /* [world][max_rows][W][3] connectCameraT1 accumulation of this iteration (owner-block layout) */
     const float* splat_in; /* [rows][W][3] summed splats of the own rows (camera pass) */
     float* cam;         /* [W*H*3] camera subpath colour of this iteration */
@@ -296,5 +296,6 @@ struct VcmConsts {
 void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c, bool estimate);
 void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c);
 uint32_t vcm_camera_waves(uint32_t tiles); /* persistent camera-pass waves for `tiles` 8x8 tiles */
+uint32_t vcm_light_waves(uint32_t items);  /* persistent light-pass waves for `items` 64-subpath items */
 
 }  // namespace orx

@@ -450,11 +450,13 @@ __device__ inline void sample_scattering(Subpath& p, f3 hit, const VBsdf& bs, co
     p.origin = hit;
 }
 
-/* connectCameraT1 (vcm.h:52-150) */
-__device__ inline void connect_camera(const DevScene& S, const Subpath& L, const VBsdf& bs, f3 hit,
-                                      const VcmConsts& c, float* splat, uint32_t* stk) {
+/* connectCameraT1 (vcm.h:52-150) without its shadow ray: true when the connection contributes,
+ * with the ray (hit, dirToCamera, distance) and the splat (float offset in the owner-block
+ * splat buffer, contribution) in the queue entry qa/qb/qc (LightShadowRays traces it) */
+__device__ inline bool connect_camera_prep(const Subpath& L, const VBsdf& bs, f3 hit, const VcmConsts& c, float4& qa,
+                                           float4& qb, float4& qc) {
     f3 dirToCamera = c.eye - hit;
-    if (dot(c.lookdir, -dirToCamera) <= 0.f) return;
+    if (dot(c.lookdir, -dirToCamera) <= 0.f) return false;
     const float distance = length(dirToCamera);
     dirToCamera = dirToCamera / distance;
     const float cosAtCamera = dot(c.lookdirN, -dirToCamera);
@@ -464,7 +466,7 @@ __device__ inline void connect_camera(const DevScene& S, const Subpath& L, const
     const f3 c2p = ippw - ipc;
     const float pu = dot(c2p, c.unitU);
     const float pv = dot(c2p, c.unitV);
-    if (!(2.f * fabsf(pu) < c.ipsx && 2.f * fabsf(pv) < c.ipsy)) return;
+    if (!(2.f * fabsf(pu) < c.ipsx && 2.f * fabsf(pv) < c.ipsy)) return false;
     const float pcx = (pu + 0.5f * c.ipsx) / c.ipsx;
     const float pcy = (pv + 0.5f * c.ipsy) / c.ipsy;
     uint32_t ix = orx_f2u_sat(pcx * (float)c.W), iy = orx_f2u_sat(pcy * (float)c.H);
@@ -472,7 +474,7 @@ __device__ inline void connect_camera(const DevScene& S, const Subpath& L, const
     iy = iy > c.H - 1 ? c.H - 1 : iy;
     float cosToCamera = 0.f, dpdf, rpdf;
     const f3 f = bs.vcm_f(dirToCamera, cosToCamera, dpdf, rpdf);
-    if (iszero(f)) return;
+    if (iszero(f)) return false;
     rpdf *= bs.cont;
     const float i2s = (ipd * ipd) / cosAtCamera;
     const float pixelArea = c.psfx * c.ipsx * c.psfx * c.ipsy;
@@ -483,14 +485,48 @@ __device__ inline void connect_camera(const DevScene& S, const Subpath& L, const
     const float misWeight = 1.f / (wLight + 1.f);
     const float conv = 1.f / cameraPdfA;
     const f3 contrib = ((L.throughput * misWeight) * f) / ((float)c.count * conv);
-    if (!occluded(S, hit, dirToCamera, distance, stk)) {
-        /* owner-block layout [world][max_rows][W]: row iy belongs to rank iy % world */
-        float* o = splat + 3 * (((size_t)(iy % c.world) * c.max_rows + iy / c.world) * c.W + ix);
-        unsafeAtomicAdd(o + 0, contrib.x);
-        unsafeAtomicAdd(o + 1, contrib.y);
-        unsafeAtomicAdd(o + 2, contrib.z);
-    }
+    /* owner-block layout [world][max_rows][W]: row iy belongs to rank iy % world */
+    const uint32_t o = 3u * (uint32_t)(((size_t)(iy % c.world) * c.max_rows + iy / c.world) * c.W + ix);
+    qa = make_float4(hit.x, hit.y, hit.z, distance);
+    qb = make_float4(dirToCamera.x, dirToCamera.y, dirToCamera.z, __uint_as_float(o));
+    qc = make_float4(contrib.x, contrib.y, contrib.z, 0.f);
+    return true;
 }
+/* The light pass's queued camera connections for trace_any_chain (entries e = lane, lane + 64,
+ * ... of q[3e .. 3e + 2]): occluded()'s test, and the unoccluded ones splat (atomic adds, as the
+ * inline form: their order was never fixed) */
+struct LightShadowRays {
+    const float4* q;
+    float* splat;
+    uint32_t e, total, cur;
+    __device__ __forceinline__ void add(uint32_t k) const {
+        const float4 b = q[3 * k + 1], cc = q[3 * k + 2];
+        float* o = splat + __float_as_uint(b.w);
+        unsafeAtomicAdd(o + 0, cc.x);
+        unsafeAtomicAdd(o + 1, cc.y);
+        unsafeAtomicAdd(o + 2, cc.z);
+    }
+    __device__ __forceinline__ bool next(f3& o, f3& d, float& tmin, float& tmax) {
+        while (e < total) {
+            cur = e;
+            e += 64;
+            const float4 a = q[3 * cur], b = q[3 * cur + 1];
+            if (a.w < 3.f * VCM_EPS_RAY) { /* occluded() without a walk: not occluded */
+                add(cur);
+                continue;
+            }
+            o = mk(a.x, a.y, a.z);
+            d = mk(b.x, b.y, b.z);
+            tmin = VCM_EPS_RAY;
+            tmax = a.w - 2.f * VCM_EPS_RAY;
+            return true;
+        }
+        return false;
+    }
+    __device__ __forceinline__ void result(bool occluded) {
+        if (!occluded) add(cur);
+    }
+};
 
 /* lightPass (VCMLightPass.cu:52-93), initLightPayload (:120-176), lightHit (vcm.h:210-309)
  *
@@ -596,6 +632,8 @@ __global__ __launch_bounds__(64, ORX_VCM_LIGHT_WAVES) void k_vcm_light(DevScene 
     bool alive = false;
     uint32_t next = 0, end = 0; /* the wave's current work item range (uniform) */
     bool exhausted = false;
+    float4* lq = vb.shq + (size_t)blockIdx.x * VCM_SHQ_PER_WAVE; /* [128][3] queued camera connections */
+    uint32_t lqn = 0;                                            /* queued (uniform) */
     for (;;) {
         for (;;) { /* refill: lanes without a subpath start the next ones of the wave's item */
             const uint64_t need = __ballot(!alive);
@@ -622,55 +660,82 @@ __global__ __launch_bounds__(64, ORX_VCM_LIGHT_WAVES) void k_vcm_light(DevScene 
             next += n < avail ? n : avail;
         }
         if (!__ballot(alive)) break; /* only once the work is exhausted */
-        if (!alive) continue;
         /* one bounce */
-        bool end_path = false;
-        Hit h;
-        if (!trace_closest(S, L.origin, L.direction, VCM_RAY_LEN_MIN, RT_DEFAULT_MAX, h, stk)) {
-            end_path = true;
-        } else {
-            const uint32_t mi = prim_material(S, h);
-            const DevMaterial& m = S.mats[mi];
-            const f3 hit = L.origin + L.direction * h.t;
-            VBsdf bs;
-            f3 N;
-            const f3 kd = TEX && m.type == MAT_TEXTURE ? tex_color(S, m, h) : m.Kd;
-            if (m.type == MAT_EMITTER || !material_bsdf(m, kd, geometric_normal(S, h), L.direction, true, bs, N)) {
+        bool conn = false; /* this bounce's camera connection (connectCameraT1) is queued */
+        float4 qa, qb, qc;
+        if (alive) {
+            bool end_path = false;
+            Hit h;
+            if (!trace_closest(S, L.origin, L.direction, VCM_RAY_LEN_MIN, RT_DEFAULT_MAX, h, stk)) {
                 end_path = true;
             } else {
-                L.depth++;
-                const float cosIn = dot(N, -L.direction);
-                if (cosIn < VCM_EPS_COSINE) {
+                const uint32_t mi = prim_material(S, h);
+                const DevMaterial& m = S.mats[mi];
+                const f3 hit = L.origin + L.direction * h.t;
+                VBsdf bs;
+                f3 N;
+                const f3 kd = TEX && m.type == MAT_TEXTURE ? tex_color(S, m, h) : m.Kd;
+                if (m.type == MAT_EMITTER || !material_bsdf(m, kd, geometric_normal(S, h), L.direction, true, bs, N)) {
                     end_path = true;
                 } else {
-                    mis_on_hit(L, cosIn, h.t);
-                    const bool spec = bs.is_specular();
-                    if (!spec) {
-                        const uint32_t k = ls.nverts++;
-                        if (!ESTIMATE && k < VCM_MAX_VERTS) {
-                            const size_t o = (size_t)k * c.lcount + ls.p;
-                            vb.vA[o] = make_float4(hit.x, hit.y, hit.z, __uint_as_float(mi));
-                            vb.vB[o] = make_float4(L.throughput.x, L.throughput.y, L.throughput.z, L.dVCM);
-                            vb.vC[o] = make_float4(N.x, N.y, N.z, L.dVC);
-                            vb.vD[o] = make_float4(bs.fix.x, bs.fix.y, bs.fix.z, L.dVM);
-                            if (TEX && m.type == MAT_TEXTURE) vb.vE[o] = make_float4(kd.x, kd.y, kd.z, 0.f);
-                        }
-                        if (!ESTIMATE) connect_camera(S, L, bs, hit, c, vb.splat, stk);
-                    }
-                    if (c.maxPathLen < L.depth + 2) {
+                    L.depth++;
+                    const float cosIn = dot(N, -L.direction);
+                    if (cosIn < VCM_EPS_COSINE) {
                         end_path = true;
                     } else {
-                        sample_scattering(L, hit, bs, c, rs);
-                        if (L.done) end_path = true;
+                        mis_on_hit(L, cosIn, h.t);
+                        const bool spec = bs.is_specular();
+                        if (!spec) {
+                            const uint32_t k = ls.nverts++;
+                            if (!ESTIMATE && k < VCM_MAX_VERTS) {
+                                const size_t o = (size_t)k * c.lcount + ls.p;
+                                vb.vA[o] = make_float4(hit.x, hit.y, hit.z, __uint_as_float(mi));
+                                vb.vB[o] = make_float4(L.throughput.x, L.throughput.y, L.throughput.z, L.dVCM);
+                                vb.vC[o] = make_float4(N.x, N.y, N.z, L.dVC);
+                                vb.vD[o] = make_float4(bs.fix.x, bs.fix.y, bs.fix.z, L.dVM);
+                                if (TEX && m.type == MAT_TEXTURE) vb.vE[o] = make_float4(kd.x, kd.y, kd.z, 0.f);
+                            }
+                            if (!ESTIMATE) conn = connect_camera_prep(L, bs, hit, c, qa, qb, qc);
+                        }
+                        if (c.maxPathLen < L.depth + 2) {
+                            end_path = true;
+                        } else {
+                            sample_scattering(L, hit, bs, c, rs);
+                            if (L.done) end_path = true;
+                        }
                     }
                 }
             }
+            if (end_path) {
+                vb.vcount[ls.p] = ls.nverts;
+                rng_store(vb.rng, ls.slot, rs);
+                alive = false;
+            }
         }
-        if (end_path) {
-            vb.vcount[ls.p] = ls.nverts;
-            rng_store(vb.rng, ls.slot, rs);
-            alive = false;
+        /* the connections' shadow rays wait in the wave's queue until 64 are pending, then all
+         * lanes trace them, chained (traced in place, inside the divergent bounce, a wave ran
+         * them at the lanes that happened to connect) */
+        if (!ESTIMATE) {
+            const uint64_t m = __ballot(conn);
+            if (conn) {
+                const uint32_t k = lqn + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                lq[3 * k] = qa;
+                lq[3 * k + 1] = qb;
+                lq[3 * k + 2] = qc;
+            }
+            lqn += (uint32_t)__popcll(m);
+            if (lqn >= 64) {
+                __threadfence_block();
+                LightShadowRays R{lq, vb.splat, lane, lqn, 0u};
+                trace_any_chain(S, R, stk);
+                lqn = 0;
+            }
         }
+    }
+    if (!ESTIMATE && lqn) {
+        __threadfence_block();
+        LightShadowRays R{lq, vb.splat, lane, lqn, 0u};
+        trace_any_chain(S, R, stk);
     }
 }
 
@@ -1057,7 +1122,7 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
 }
 
 /* persistent light-pass waves: as many as can be resident at once (4 per SIMD) */
-static uint32_t vcm_light_waves(uint32_t items) {
+uint32_t vcm_light_waves(uint32_t items) {
     static uint32_t resident = 0;
     if (!resident) {
         int dev = 0, cus = 256;

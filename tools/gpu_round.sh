@@ -1,6 +1,5 @@
 set -o pipefail
-mkdir -p gpurun_out/t gpurun_out/sm
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t/gputest.log 2>&1 || { tail -30 gpurun_out/t/gputest.log; exit 1; }
-tail -2 gpurun_out/t/gputest.log
-timeout -k 10 400 python -u tools/shard_model.py --config 4 1 2 4 8 > gpurun_out/sm/conf4k_rows.txt 2>&1 && grep N= gpurun_out/sm/conf4k_rows.txt | cut -c1-160
-timeout -k 10 300 python -u tools/shard_model.py 1 2 4 8 > gpurun_out/sm/hall_rows.txt 2>&1 && grep N= gpurun_out/sm/hall_rows.txt | cut -c1-160
+mkdir -p gpurun_out/t
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_sharded.py tests/test_gpu_features.py -m gpu -x -q --timeout 200 --timeout-method thread -k "vcm or VCM" > gpurun_out/t/gt.log 2>&1 || { tail -30 gpurun_out/t/gt.log; exit 1; }
+tail -2 gpurun_out/t/gt.log
+bash tools/gpu_lib_ab.sh "base cur base cur" --method vcm --steps 16 --warmup 2
