@@ -1,5 +1,3 @@
 set -o pipefail
-mkdir -p gpurun_out/t
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_sharded.py tests/test_gpu_features.py -m gpu -x -q --timeout 200 --timeout-method thread -k "vcm or VCM" > gpurun_out/t/gt.log 2>&1 || { tail -30 gpurun_out/t/gt.log; exit 1; }
-tail -2 gpurun_out/t/gt.log
-bash tools/gpu_lib_ab.sh "base cur base cur" --method vcm --steps 16 --warmup 2
+timeout -k 10 900 bash tools/profile_round.sh r03f_hall SyntheticHall:1920x1080:ppm:P2048 > gpurun_out/prof_hall.log 2>&1 || { tail -20 gpurun_out/prof_hall.log; exit 1; }
+tail -3 gpurun_out/prof_hall.log | cut -c1-300
