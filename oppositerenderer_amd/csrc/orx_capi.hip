@@ -425,7 +425,7 @@ struct orx_renderer {
     bool vcm_kd = false;      /* d_vkd sized for the current vcm_npx */
     VcmBufs vcm_vb{};
     VcmConsts vcm_c{};
-    DevBuf d_vcount, d_vverts, d_vsplat, d_vcam, d_vkd, d_vshq, d_vwork, d_tstats;
+    DevBuf d_vcount, d_vverts, d_vsplat, d_vcam, d_vkd, d_vshq, d_vwork, d_vconst, d_tstats;
     std::vector<DevLight> host_lights;
     /* participating medium (cfg.enable_media with a medium box): the box, this frame's per-pixel
      * volumetricRadiance and per-photon last events, the volumetric table of the last photon pass */
@@ -1479,6 +1479,8 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
         vb.shq = r->d_vshq.as<float4>();
         HIPCHK(r, r->d_vwork.ensure(16));
         vb.work = r->d_vwork.as<uint32_t>();
+        HIPCHK(r, r->d_vconst.ensure(sizeof(VcmConsts)));
+        vb.consts = r->d_vconst.as<VcmConsts>();
     }
     vb.cam = r->d_vcam.as<float>();
     vb.output = r->d_out.as<float>();

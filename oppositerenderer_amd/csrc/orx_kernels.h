@@ -282,6 +282,7 @@ struct VcmBufs {
     float* cam;         /* [W*H*3] camera subpath colour of this iteration */
     float* output;      /* [W*H*3] running sum */
     uint32_t* work;     /* [2] camera-pass, light-pass work-item counters (zeroed by the launches) */
+    struct VcmConsts* consts; /* device copy of the pass constants (written by the launches) */
 };
 struct VcmConsts {
     f3 eye, lookdir, u, v;          /* Camera (Camera.cpp:333-345) */

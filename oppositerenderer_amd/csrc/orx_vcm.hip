@@ -619,7 +619,8 @@ __device__ __forceinline__ void light_start(const DevScene& S, const VcmBufs& vb
 #define ORX_VCM_LIGHT_WAVES 3 /* waves per SIMD the light kernel is register-capped for (4: 3.63 ms, 3: 3.33) */
 #endif
 template <bool ESTIMATE, bool TEX>
-__global__ __launch_bounds__(64, ORX_VCM_LIGHT_WAVES) void k_vcm_light(DevScene S, VcmBufs vb, VcmConsts c) {
+__global__ __launch_bounds__(64, ORX_VCM_LIGHT_WAVES) void k_vcm_light(DevScene S, VcmBufs vb, const VcmConsts* __restrict__ cp) {
+    const VcmConsts& c = *cp;
     ORX_STACK_DECL;
     uint32_t* stk = ORX_STACK_PTR;
     const uint32_t lane = threadIdx.x & 63;
@@ -944,7 +945,9 @@ __device__ __forceinline__ void camera_finish(const VcmBufs& vb, const CamPixel&
 }
 
 template <bool TEX>
-__global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScene S, VcmBufs vb, VcmConsts c) {
+__global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScene S, VcmBufs vb, const VcmConsts* __restrict__ cp) {
+    const VcmConsts& c = *cp; /* read by scalar loads where used: as a by-value argument it kept ~40 more
+                               * SGPRs live and the kernel spilled VGPRs */
     ORX_STACK_DECL;
     uint32_t* stk = ORX_STACK_PTR;
     const uint32_t tilesX = (c.W + 7) / 8;
@@ -1144,25 +1147,29 @@ uint32_t vcm_camera_waves(uint32_t tiles) {
     return tiles < resident ? tiles : resident;
 }
 
+__global__ void k_vcm_consts(VcmConsts c, VcmConsts* dst) { *dst = c; }
+
 void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c, bool estimate) {
+    hipLaunchKernelGGL(k_vcm_consts, dim3(1), dim3(1), 0, s, c, vb.consts);
     const uint32_t blocks = vcm_light_waves((c.lcount + 63) / 64);
     if (blocks == 0) return;
     hipMemsetAsync(vb.work + 1, 0, 4, s);
     const size_t lds = ORX_STACK_BYTES(S);
     if (vb.vE) {
-        if (estimate) hipLaunchKernelGGL((k_vcm_light<true, true>), dim3(blocks), dim3(64), lds, s, S, vb, c);
-        else hipLaunchKernelGGL((k_vcm_light<false, true>), dim3(blocks), dim3(64), lds, s, S, vb, c);
+        if (estimate) hipLaunchKernelGGL((k_vcm_light<true, true>), dim3(blocks), dim3(64), lds, s, S, vb, vb.consts);
+        else hipLaunchKernelGGL((k_vcm_light<false, true>), dim3(blocks), dim3(64), lds, s, S, vb, vb.consts);
     } else {
-        if (estimate) hipLaunchKernelGGL((k_vcm_light<true, false>), dim3(blocks), dim3(64), lds, s, S, vb, c);
-        else hipLaunchKernelGGL((k_vcm_light<false, false>), dim3(blocks), dim3(64), lds, s, S, vb, c);
+        if (estimate) hipLaunchKernelGGL((k_vcm_light<true, false>), dim3(blocks), dim3(64), lds, s, S, vb, vb.consts);
+        else hipLaunchKernelGGL((k_vcm_light<false, false>), dim3(blocks), dim3(64), lds, s, S, vb, vb.consts);
     }
 }
 void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
+    hipLaunchKernelGGL(k_vcm_consts, dim3(1), dim3(1), 0, s, c, vb.consts);
     const uint32_t blocks = vcm_camera_waves(((c.W + 7) / 8) * ((c.rows + 7) / 8));
     if (blocks == 0) return;
     hipMemsetAsync(vb.work, 0, 4, s);
-    if (vb.vE) hipLaunchKernelGGL(k_vcm_camera<true>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
-    else hipLaunchKernelGGL(k_vcm_camera<false>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, c);
+    if (vb.vE) hipLaunchKernelGGL(k_vcm_camera<true>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, vb.consts);
+    else hipLaunchKernelGGL(k_vcm_camera<false>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, vb.consts);
 }
 
 }  // namespace orx
