@@ -615,7 +615,6 @@ __device__ inline bool trace_closest_t(const DevScene& S, f3 o, f3 d, float tmin
                 cswap(ct[1], cc[1], ct[2], cc[2]);
                 /* (dropping the last two exchanges, a near-first order only for the first
                  * child, measured 4.03 -> 4.29 ms on the hall photon pass: order matters) */
-#ifndef ORX_TRAV_BRANCHED_PUSH
                 {
                     /* branch-free pushes: the three entries are written unconditionally at
                      * their final positions (misses sort last), then the pointer moves by the
@@ -627,16 +626,6 @@ __device__ inline bool trace_closest_t(const DevScene& S, f3 o, f3 d, float tmin
                     sp += n3 + n2 + n1;
                     ref = ct[0] != INFINITY ? cc[0] : (sp ? stk.pop(sp) : ORX_DONE);
                 }
-#else
-                if (ct[0] != INFINITY) {
-                    if (ct[3] != INFINITY) stk.push(sp, cc[3]);
-                    if (ct[2] != INFINITY) stk.push(sp, cc[2]);
-                    if (ct[1] != INFINITY) stk.push(sp, cc[1]);
-                    ref = cc[0];
-                } else {
-                    ref = sp ? stk.pop(sp) : ORX_DONE;
-                }
-#endif
                 if ((ref & ORX_LEAF) && !(lf & ORX_LEAF)) {
                     lf = ref;
                     ref = sp ? stk.pop(sp) : ORX_DONE;
@@ -711,7 +700,6 @@ __device__ inline bool trace_any_t(const DevScene& S, f3 o, f3 d, float tmin, fl
                 nodes.test(S, ref, rb, tmin, tmax, ct, cc);
                 ORX_TS_INC(ts_nodes, 1);
                 ORX_TS_WAVE(ts_wn);
-#ifndef ORX_TRAV_BRANCHED_PUSH
                 /* branch-free: every hit child is written to the stack (the order does not
                  * matter for any hit), the last one is taken back from registers */
                 const int h0 = ct[0] != INFINITY, h1 = ct[1] != INFINITY, h2 = ct[2] != INFINITY,
@@ -726,16 +714,6 @@ __device__ inline bool trace_any_t(const DevScene& S, f3 o, f3 d, float tmin, fl
                 sp += h3;
                 const uint32_t next = h3 ? cc[3] : h2 ? cc[2] : h1 ? cc[1] : h0 ? cc[0] : ORX_DONE;
                 sp -= next != ORX_DONE;
-#else
-                uint32_t next = ORX_DONE;
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    if (ct[i] != INFINITY) {
-                        if (next != ORX_DONE) stk.push(sp, next);
-                        next = cc[i];
-                    }
-                }
-#endif
                 ref = next != ORX_DONE ? next : (sp ? stk.pop(sp) : ORX_DONE);
                 if ((ref & ORX_LEAF) && !(lf & ORX_LEAF)) {
                     lf = ref;
