@@ -1235,14 +1235,26 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
  * Per batch of four photons: positions -> d^2 test and the lane's range test;
  * a batch no lane accepts ends there (one ballot); then the int8 direction
  * words -> facing, exact directions only inside the band; then powers. */
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+/* Wave-uniform min / max over the 64 lanes (callers run with EXEC all ones): DPP moves inside
+ * each row of 16 lanes (quad_perm [1,0,3,2], [2,3,0,1], row_ror 4, row_ror 8: VALU operands, no
+ * LDS round trip), then the four row results by v_readlane and scalar min/max.  A __shfl_xor
+ * butterfly is six dependent ds_bpermute_b32 round trips; the union gather reduces twice per
+ * sub-row. */
+template <bool MIN>
+__device__ __forceinline__ uint32_t wave_minmax_u32(uint32_t v) {
+    auto op = [](uint32_t a, uint32_t b) { return MIN ? min(a, b) : max(a, b); };
+    v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false));
+    v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false));
+    v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, false));
+    v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false));
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
+    const uint32_t r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+    return op(op(r0, r1), op(r2, r3));
 }
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) { return wave_minmax_u32<true>(v); }
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) { return wave_minmax_u32<false>(v); }
 /* uniform 16-B read of a photon plane through the scalar unit */
 __device__ __forceinline__ f4u sload4(const float* __restrict__ plane, uint32_t k) {
     return *reinterpret_cast<const f4u*>(plane + k);

@@ -171,10 +171,10 @@ def test_configs4_conference4k_ppm_single_and_8_shards():
        per-cell photon multisets, direct, visit counters bit-exact; indirect rel-L2 <= 1e-5).
     2. The same frame through eight row-interleaved shards in the 8-GPU bench's strong-scaling
        partition (each shard: 1/8 of the pixel rows, photon launch rows and RNG rows; cell-order
-       photon layout and the per-lane gather that world >= 8 selects), exchanging hit points,
-       photons (slab mode, the bench's default) and partial indirect through torch ops
-       (tests/shard_emul.py), against the oracle's output: rel-L2 <= 1e-5, with spatial photon
-       slabs and with the row partition."""
+       photon layout and the gather that world >= 8 selects), exchanging hit points, photons
+       (slab mode) and partial indirect through torch ops (tests/shard_emul.py), against the
+       oracle's output: rel-L2 <= 1e-5, with spatial photon slabs and with the row partition
+       (the bench's default, `bench.py --partition rows`)."""
     import torch
 
     from oppositerenderer_amd import multigpu
@@ -199,7 +199,7 @@ def test_configs4_conference4k_ppm_single_and_8_shards():
 
     world = 8
     req = det.to_abi()
-    for slab in (True, False):  # the bench's default spatial slabs, and the row partition
+    for slab in (True, False):  # spatial slabs, and the row partition (the bench default)
         shards = shard_emul.make_shards(scene, world, P, P, slab=slab)
         got, plans = shard_emul.run_iterations(shards, scene, W, H, req, 1, slab=slab)
         assert np.isfinite(got).all()
