@@ -1222,16 +1222,17 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
  * The per-lane gather above is bound by the vector-memory address path: every
  * dwordx4 photon load costs the TA ~16-20 cycles whatever the lanes share, for
  * four photons of one lane.  Here a wave walks, sub-row by sub-row, the union
- * of its 64 lanes' chords and reads each photon ONCE through the scalar unit
- * (s_load into SGPRs, operands of every lane's VALU instructions): no per-lane
- * photon traffic at all, and the cost per photon is the lanes' arithmetic.
+ * of its 64 lanes' chords and reads each photon ONCE: 64 photons per coalesced
+ * load into the wave's LDS image, then every lane reads the same batch of four
+ * (ds_read_b128 broadcast), so the cost per photon is the lanes' arithmetic
+ * (union_chunk_lds; only the exact directions inside the facing band are
+ * scalar loads).
  * Each lane accepts exactly the photons of its own chord range (the per-lane
  * kernel's candidate set, [subofs[a0], subofs[a1 + 1]) inside its reference
  * window) that pass its distance and facing tests, so the accepted set per
  * pixel is the per-lane kernel's (= the reference's); the union only adds
  * photons a lane rejects.  Lanes are 8x8 pixel tiles (hitpoints of neighbouring
- * pixels are near each other in the scene), or, with `order`, consecutive
- * hitpoints of a list sorted by position (tighter unions).
+ * pixels are near each other in the scene).
  * Per batch of four photons: positions -> d^2 test and the lane's range test;
  * a batch no lane accepts ends there (one ballot); then the int8 direction
  * words -> facing, exact directions only inside the band; then powers. */

@@ -1,11 +1,9 @@
+# final-tree check: GPU suite, smoke, hall PPM profile round (bench line + rocprof + PMC)
 set -o pipefail
 mkdir -p gpurun_out/t
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -k "gather or ppm or PPM or shard" --timeout 250 --timeout-method thread > gpurun_out/t/gtest.log 2>&1 || { tail -30 gpurun_out/t/gtest.log; exit 1; }
-tail -2 gpurun_out/t/gtest.log
-bash tools/gpu_lib_ab.sh "base cur base cur" --config 2 || exit 1
-bash tools/gpu_lib_ab.sh "base cur" --config 4 --steps 8 --warmup 2 || exit 1
-for n in base cur; do
-  L=$PWD/oppositerenderer_amd/liborx_$n.so; [ $n = cur ] && L=$PWD/oppositerenderer_amd/liborx.so
-  ORX_LIB=$L timeout -k 10 300 python -u tools/shard_model.py --config 4 1 8 > gpurun_out/t/sm_$n.log 2>&1 || { tail -5 gpurun_out/t/sm_$n.log; exit 1; }
-  echo $n; grep "per-rank" gpurun_out/t/sm_$n.log | cut -c1-120
-done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t/gputest.log 2>&1 || { tail -30 gpurun_out/t/gputest.log; exit 1; }
+tail -1 gpurun_out/t/gputest.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/t/smoke.log 2>&1 || { tail -20 gpurun_out/t/smoke.log; exit 1; }
+tail -2 gpurun_out/t/smoke.log
+timeout -k 10 900 bash tools/profile_round.sh r03g_hall_ppm SyntheticHall:1920x1080:ppm:P2048 > gpurun_out/prof_hall.log 2>&1 || { tail -20 gpurun_out/prof_hall.log; exit 1; }
+tail -1 gpurun_out/r03g_hall_ppm/bench.json | cut -c1-300
