@@ -744,19 +744,25 @@ __global__ __launch_bounds__(64, ORX_VCM_LIGHT_WAVES) void k_vcm_light(DevScene 
 template <bool TEX>
 __device__ inline bool connect_vertex(const DevScene& S, const Subpath& C, const VBsdf& cb, f3 hit, const VcmBufs& vb,
                                       size_t o, const VcmConsts& c, f3& sdir, float& sdist, f3& add) {
-    const float4 A = vb.vA[o];
+    /* the vertex's planes and its material in flight together: loaded where first used, each
+     * waited for a full memory latency after the BSDF work of the previous step (the empty asm
+     * keeps the compiler from sinking them below the early return) */
+    const float4 A = vb.vA[o], Cn = vb.vC[o], D = vb.vD[o];
     f3 direction = mk(A.x, A.y, A.z) - hit;
+    const DevMaterial& m = S.mats[__float_as_uint(A.w)];
+    const uint32_t mtype = m.type;
+    const f3 mKd = m.Kd, mKs = m.Ks;
+    const float mexp = m.exponent;
     const float dist2 = dot(direction, direction);
     const float distance = sqrtf(dist2);
     direction = direction / distance;
     float camCos = 0.f, cDir, cRev;
     const f3 camF = cb.vcm_f(direction, camCos, cDir, cRev);
+    asm volatile("" ::"v"(Cn.x), "v"(Cn.y), "v"(Cn.z), "v"(Cn.w), "v"(D.x), "v"(D.y), "v"(D.z), "v"(mtype),
+                 "v"(mKd.x), "v"(mKd.y), "v"(mKd.z));
     if (iszero(camF)) return false;
     cDir *= cb.cont;
     cRev *= cb.cont;
-    const float4 Cn = vb.vC[o];
-    const float4 D = vb.vD[o];
-    const DevMaterial& m = S.mats[__float_as_uint(A.w)];
     VBsdf lb;
     const f3 N = mk(Cn.x, Cn.y, Cn.z);
     lb.dg = frame_from_normal(N);
@@ -765,13 +771,13 @@ __device__ inline bool connect_vertex(const DevScene& S, const Subpath& C, const
     lb.fix = mk(D.x, D.y, D.z);
     lb.n = 0;
     lb.cont = 0.f;
-    f3 kd = m.Kd;
-    if (TEX && m.type == MAT_TEXTURE) { /* texel colour kept beside the 64-B record */
+    f3 kd = mKd;
+    if (TEX && mtype == MAT_TEXTURE) { /* texel colour kept beside the 64-B record */
         const float4 E = vb.vE[o];
         kd = mk(E.x, E.y, E.z);
     }
     lb.add(mk_bx(T_LAMBERT, kd));
-    if (m.type == MAT_GLOSSY) lb.add(mk_bx(T_PHONG, m.Ks, m.exponent));
+    if (mtype == MAT_GLOSSY) lb.add(mk_bx(T_PHONG, mKs, mexp));
     float lightCos = 0.f, lDir, lRev;
     const f3 lightF = lb.vcm_f(-direction, lightCos, lDir, lRev);
     if (iszero(lightF)) return false;
