@@ -1,11 +1,7 @@
-# final-tree check: GPU suite, smoke, VCM profile round, default bench line
+# per-rank strong-scaling model on the final tree (tools/shard_model.py): configs[4] and the hall
 set -o pipefail
 mkdir -p gpurun_out/t
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t/gputest.log 2>&1 || { tail -30 gpurun_out/t/gputest.log; exit 1; }
-tail -1 gpurun_out/t/gputest.log
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/t/smoke.log 2>&1 || { tail -20 gpurun_out/t/smoke.log; exit 1; }
-tail -1 gpurun_out/t/smoke.log
-timeout -k 10 600 bash tools/profile_round.sh r03g_vcm SyntheticHall:1920x1080:vcm --method vcm > gpurun_out/prof_vcm.log 2>&1 || { tail -20 gpurun_out/prof_vcm.log; exit 1; }
-tail -1 gpurun_out/r03g_vcm/bench.json | cut -c1-200
-timeout -k 10 400 python -u bench.py > gpurun_out/t/bench_default.json 2> gpurun_out/t/bench_default.err || { tail -20 gpurun_out/t/bench_default.err; exit 1; }
-tail -1 gpurun_out/t/bench_default.json | cut -c1-200
+timeout -k 10 500 python -u tools/shard_model.py --config 4 > gpurun_out/t/sm_conf4k.txt 2>&1 || { tail -5 gpurun_out/t/sm_conf4k.txt; exit 1; }
+grep -v amdgpu.ids gpurun_out/t/sm_conf4k.txt | cut -c1-160
+timeout -k 10 300 python -u tools/shard_model.py --config 2 > gpurun_out/t/sm_hall.txt 2>&1 || { tail -5 gpurun_out/t/sm_hall.txt; exit 1; }
+grep -v amdgpu.ids gpurun_out/t/sm_hall.txt | cut -c1-160
