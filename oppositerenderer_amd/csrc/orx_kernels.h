@@ -64,7 +64,10 @@ constexpr uint32_t BBOX_REPLICAS = 64;
 /* grid-ordered photon planes (PhotonBufs::sorted): position, the int8 direction
  * prefilter word of the gather's facing test, exact direction, power */
 enum : uint32_t { SP_X = 0, SP_Y, SP_Z, SP_DIRQ, SP_DX, SP_DY, SP_DZ, SP_PX, SP_PY, SP_PZ, SP_PLANES };
-constexpr uint32_t SUBX = 4; /* sub-cells per grid cell along x (bucket-sort grid, gather chord trimming) */
+#ifndef ORX_SUBX
+#define ORX_SUBX 4
+#endif
+constexpr uint32_t SUBX = ORX_SUBX; /* sub-cells per grid cell along x (bucket-sort grid, gather chord trimming) */
 constexpr uint32_t SUBR = 2; /* sub-rows per grid cell along y and along z (bucket-sort grid, nsub = SUBR^2) */
 
 struct PhotonBufs {

@@ -1,7 +1,6 @@
-# per-rank strong-scaling model on the final tree (tools/shard_model.py): configs[4] and the hall
 set -o pipefail
 mkdir -p gpurun_out/t
-timeout -k 10 500 python -u tools/shard_model.py --config 4 > gpurun_out/t/sm_conf4k.txt 2>&1 || { tail -5 gpurun_out/t/sm_conf4k.txt; exit 1; }
-grep -v amdgpu.ids gpurun_out/t/sm_conf4k.txt | cut -c1-160
-timeout -k 10 300 python -u tools/shard_model.py --config 2 > gpurun_out/t/sm_hall.txt 2>&1 || { tail -5 gpurun_out/t/sm_hall.txt; exit 1; }
-grep -v amdgpu.ids gpurun_out/t/sm_hall.txt | cut -c1-160
+ORX_LIB=$PWD/oppositerenderer_amd/liborx_subx8.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -k "ppm or PPM or gather or grid" --timeout 300 --timeout-method thread > gpurun_out/t/stest.log 2>&1 || { tail -30 gpurun_out/t/stest.log; exit 1; }
+tail -1 gpurun_out/t/stest.log
+bash tools/gpu_lib_ab.sh "base subx8 base subx8" --config 4 --steps 8 --warmup 2 || exit 1
+bash tools/gpu_lib_ab.sh "base subx8 base subx8" --config 2 || exit 1
