@@ -926,8 +926,8 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     }
     HIPCHK(r, r->d_slots.ensure(S_cap * 64));
     HIPCHK(r, r->d_vmask.ensure(S_cap / D + 1));
-    /* 64 photons of tail padding per plane: the union gather loads whole 64-photon chunks (and
-     * prefetches the next one) up to index U1 + 63 of the last plane */
+    /* 64 photons of tail padding per plane: the union gather loads whole 64-photon chunks, up to
+     * index U1 + 63 of the last plane */
     const size_t splane = ((S_cap + 64) + 3) & ~(size_t)3;
     if ((size_t)SP_PLANES * splane * 4 > 0xffffff00ull) /* the gather addresses the planes with 32-bit buffer offsets */
         return set_err(r, ORX_ERR_UNSUPPORTED, "photon slots per device exceed the 4 GiB sorted-photon window");

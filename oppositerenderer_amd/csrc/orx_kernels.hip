@@ -1364,8 +1364,12 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
  * the chunk registers measured 2.81 ms against 1.91 on the serial hall gather, 16x4 and 4x16
  * wave tiles slower than 8x8.)  Block = 16x16 pixels, four 8x8 wave tiles; blocks are dealt
  * XCD-major (block b runs on XCD b % 8 and takes the tiles [k per, (k+1) per) of XCD k). */
+/* 6 waves per SIMD (at most 80 VGPRs): the next chunk's loads are no longer issued ahead of the
+ * current chunk's batches (that prefetch held 7 VGPRs and kept the kernel at 5 waves); the
+ * extra wave hides more of the load latency than the prefetch did: 4K conference serial gather
+ * 26.2 -> 24.9 ms, configs[4] 8-rank gather 6.39 -> 6.15 ms, hall unchanged */
 template <uint32_t NSUB>
-__global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
+__global__ __launch_bounds__(256, 6) void k_ppm_gather_union(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
                                                           uint32_t ntiles) {
     __shared__ float ulds[4][7 * 64];
     const uint32_t tid = threadIdx.x, w = tid >> 6, l = tid & 63;
@@ -1501,10 +1505,9 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
                 const float r2 = a0 <= a1 ? radius2 : -1.f;
                 float* L = ulds[w];
                 uint32_t cc = U0;
-                UChunk cur = uload_chunk(SX, SY, SZ, SQ, SPX, SPY, SPZ, cc + l);
                 while (cc < U1) {
                     const uint32_t cn = cc + 64;
-                    const UChunk nxt = uload_chunk(SX, SY, SZ, SQ, SPX, SPY, SPZ, (cn < U1 ? cn : cc) + l);
+                    const UChunk cur = uload_chunk(SX, SY, SZ, SQ, SPX, SPY, SPZ, cc + l);
                     const uint32_t ce = U1 - cc < 64 ? U1 - cc : 64;
                     L[l] = cc + l < U1 ? cur.X : INFINITY;
                     L[64 + l] = cur.Y;
@@ -1517,7 +1520,6 @@ __global__ __launch_bounds__(256) void k_ppm_gather_union(GatherIn gi, PhotonBuf
                     if (range) union_chunk_lds<true>(L, cc, ce, lo, len, r2, UK, UA);
                     else union_chunk_lds<false>(L, cc, ce, lo, len, r2, UK, UA);
                     __builtin_amdgcn_wave_barrier();
-                    cur = nxt;
                     cc = cn;
                 }
             }
