@@ -977,8 +977,9 @@ __device__ __forceinline__ void window_visits(const uint32_t* __restrict__ offse
 constexpr float ORX_W5_C0 = 1.8179986476898193f, ORX_W5_C1 = -2.0686328411102295f;
 constexpr float ORX_W5_C2 = 1.0091534852981567f, ORX_W5_C3 = -0.32518523931503296f;
 constexpr float ORX_W5_C4 = 0.07352562248706818f, ORX_W5_C5 = -0.009477914310991764f;
-__device__ __forceinline__ v2f weight2(v2f ir2, v2f d2) {
-    const v2f u = d2 * ir2;
+__device__ __forceinline__ v2f weight2u(v2f u);
+__device__ __forceinline__ v2f weight2(v2f ir2, v2f d2) { return weight2u(d2 * ir2); }
+__device__ __forceinline__ v2f weight2u(v2f u) {
     v2f p = __builtin_elementwise_fma(v2f{ORX_W5_C5, ORX_W5_C5}, u, v2f{ORX_W5_C4, ORX_W5_C4});
     p = __builtin_elementwise_fma(p, u, v2f{ORX_W5_C3, ORX_W5_C3});
     p = __builtin_elementwise_fma(p, u, v2f{ORX_W5_C2, ORX_W5_C2});
@@ -1285,8 +1286,32 @@ __device__ __forceinline__ UChunk uload_chunk(const float* __restrict__ SX, cons
 struct UAcc {
     v2f accx, accy, accz;
 };
+/* packed broadcasts through op_sel: `pair.lo - x`, `pair.hi - x`, `a * pair.lo`, `a * pair.hi`
+ * on both halves of x / a.  The union kernel keeps its hit point, normal and 1/r^2 two to a
+ * register pair (four pairs instead of seven broadcast pairs: the kernel's VGPR budget sets its
+ * waves per SIMD); the arithmetic is the same IEEE operation as the broadcast form. */
+__device__ __forceinline__ v2f pk_sub_blo(v2f pair, v2f x) {
+    v2f r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(pair), "v"(x));
+    return r;
+}
+__device__ __forceinline__ v2f pk_sub_bhi(v2f pair, v2f x) {
+    v2f r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(pair), "v"(x));
+    return r;
+}
+__device__ __forceinline__ v2f pk_mul_blo(v2f a, v2f pair) {
+    v2f r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(pair));
+    return r;
+}
+__device__ __forceinline__ v2f pk_mul_bhi(v2f a, v2f pair) {
+    v2f r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(pair));
+    return r;
+}
 struct UConst {
-    v2f px2, py2, pz2, nx2, ny2, nz2, ir2;
+    v2f pxy, pzn, nyz, irr; /* (p.x, p.y), (p.z, n.x), (n.y, n.z), (1/r^2, -) */
     int32_t nq;
     const float* SDX;
     const float* SDY;
@@ -1310,9 +1335,9 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
     for (uint32_t e = 0; e < ce; e += 4) {
         const uint32_t kb = c + e;
         const float4 X = L4[e >> 2], Y = L4[16 + (e >> 2)], Z = L4[32 + (e >> 2)];
-        const v2f dx0 = k.px2 - lo2(X), dx1 = k.px2 - hi2(X);
-        const v2f dy0 = k.py2 - lo2(Y), dy1 = k.py2 - hi2(Y);
-        const v2f dz0 = k.pz2 - lo2(Z), dz1 = k.pz2 - hi2(Z);
+        const v2f dx0 = pk_sub_blo(k.pxy, lo2(X)), dx1 = pk_sub_blo(k.pxy, hi2(X));
+        const v2f dy0 = pk_sub_bhi(k.pxy, lo2(Y)), dy1 = pk_sub_bhi(k.pxy, hi2(Y));
+        const v2f dz0 = pk_sub_blo(k.pzn, lo2(Z)), dz1 = pk_sub_blo(k.pzn, hi2(Z));
         const v2f d20 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
         const v2f d21 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
         bool in0 = d20.x <= r2, in1 = d20.y <= r2, in2 = d21.x <= r2, in3 = d21.y <= r2;
@@ -1336,8 +1361,8 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
         if (wave_any(u0 | u1 | u2 | u3)) { /* inside the band: the exact test (rare) */
             const uint32_t ku = (uint32_t)__builtin_amdgcn_readfirstlane((int)kb);
             const f4u DX = sload4(k.SDX, ku), DY = sload4(k.SDY, ku), DZ = sload4(k.SDZ, ku);
-            const v2f nd0 = (lo2(DX) * k.nx2 + lo2(DY) * k.ny2) + lo2(DZ) * k.nz2;
-            const v2f nd1 = (hi2(DX) * k.nx2 + hi2(DY) * k.ny2) + hi2(DZ) * k.nz2;
+            const v2f nd0 = (pk_mul_bhi(lo2(DX), k.pzn) + pk_mul_blo(lo2(DY), k.nyz)) + pk_mul_bhi(lo2(DZ), k.nyz);
+            const v2f nd1 = (pk_mul_bhi(hi2(DX), k.pzn) + pk_mul_blo(hi2(DY), k.nyz)) + pk_mul_bhi(hi2(DZ), k.nyz);
             in0 = in0 && (!u0 || nd0.x <= 0.f);
             in1 = in1 && (!u1 || nd0.y <= 0.f);
             in2 = in2 && (!u2 || nd1.x <= 0.f);
@@ -1345,7 +1370,7 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
         }
         if (!wave_any(in0 | in1 | in2 | in3)) continue;
         const float4 WX = L4[64 + (e >> 2)], WY = L4[80 + (e >> 2)], WZ = L4[96 + (e >> 2)];
-        v2f w0 = weight2(k.ir2, d20), w1 = weight2(k.ir2, d21);
+        v2f w0 = weight2u(pk_mul_blo(d20, k.irr)), w1 = weight2u(pk_mul_blo(d21, k.irr));
         w0.x = in0 ? w0.x : 0.f;
         w0.y = in1 ? w0.y : 0.f;
         w1.x = in2 ? w1.x : 0.f;
@@ -1364,12 +1389,14 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
  * the chunk registers measured 2.81 ms against 1.91 on the serial hall gather, 16x4 and 4x16
  * wave tiles slower than 8x8.)  Block = 16x16 pixels, four 8x8 wave tiles; blocks are dealt
  * XCD-major (block b runs on XCD b % 8 and takes the tiles [k per, (k+1) per) of XCD k). */
-/* 6 waves per SIMD (at most 80 VGPRs): the next chunk's loads are no longer issued ahead of the
- * current chunk's batches (that prefetch held 7 VGPRs and kept the kernel at 5 waves); the
- * extra wave hides more of the load latency than the prefetch did: 4K conference serial gather
- * 26.2 -> 24.9 ms, configs[4] 8-rank gather 6.39 -> 6.15 ms, hall unchanged */
+/* 7 waves per SIMD (at most 72 VGPRs): the next chunk's loads are not issued ahead of the
+ * current chunk's batches (that prefetch held 7 VGPRs and kept the kernel at 5 waves), and the
+ * hit point, normal and 1/r^2 sit two to a register pair, broadcast by op_sel (pk_sub_blo ...);
+ * the extra waves hide more of the load latency than the prefetch did: 4K conference serial
+ * gather 26.2 -> 24.7 ms at 6 waves, 24.2 at 7; configs[4] 8-rank gather 6.39 -> 6.01 ms; hall
+ * unchanged.  The cell-order instance spills 8 VGPRs outside the batch loop. */
 template <uint32_t NSUB>
-__global__ __launch_bounds__(256, 6) void k_ppm_gather_union(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
+__global__ __launch_bounds__(256, 7) void k_ppm_gather_union(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
                                                           uint32_t ntiles) {
     __shared__ float ulds[4][7 * 64];
     const uint32_t tid = threadIdx.x, w = tid >> 6, l = tid & 63;
@@ -1419,8 +1446,6 @@ __global__ __launch_bounds__(256, 6) void k_ppm_gather_union(GatherIn gi, Photon
                           (z_hi - z_lo + 1) * (y_hi - y_lo + 1), dC, dP);
     }
     v2f accx = v2f{0.f, 0.f}, accy = accx, accz = accx;
-    const v2f px2 = v2f{pos.x, pos.x}, py2 = v2f{pos.y, pos.y}, pz2 = v2f{pos.z, pos.z};
-    const v2f nx2 = v2f{B.x, B.x}, ny2 = v2f{B.y, B.y}, nz2 = v2f{B.z, B.z};
     const int32_t nq = (int32_t)dir_q8(B.x, B.y, B.z);
     const float* __restrict__ SX = pb.sorted + (size_t)SP_X * pb.splane;
     const float* __restrict__ SY = pb.sorted + (size_t)SP_Y * pb.splane;
@@ -1435,7 +1460,7 @@ __global__ __launch_bounds__(256, 6) void k_ppm_gather_union(GatherIn gi, Photon
     const float m = g.cell * 1e-3f;
     constexpr uint32_t HS = NSUB > 1 ? SUBR : 1u;
     const float hc = g.cell / (float)HS;
-    const UConst UK{px2, py2, pz2, nx2, ny2, nz2, v2f{1.0f / radius2, 1.0f / radius2}, nq, SDX, SDY, SDZ};
+    const UConst UK{v2f{pos.x, pos.y}, v2f{pos.z, B.x}, v2f{B.y, B.z}, v2f{1.0f / radius2, 0.f}, nq, SDX, SDY, SDZ};
     UAcc UA{accx, accy, accz};
     /* the union of the lanes' windows (rows) */
     const uint32_t UZ0 = wave_min_u32(act ? z_lo : 0xffffffffu), UZ1 = wave_max_u32(act ? z_hi : 0u);
