@@ -979,6 +979,30 @@ constexpr float ORX_W5_C2 = 1.0091534852981567f, ORX_W5_C3 = -0.3251852393150329
 constexpr float ORX_W5_C4 = 0.07352562248706818f, ORX_W5_C5 = -0.009477914310991764f;
 __device__ __forceinline__ v2f weight2u(v2f u);
 __device__ __forceinline__ v2f weight2(v2f ir2, v2f d2) { return weight2u(d2 * ir2); }
+/* packed broadcasts through op_sel: `pair.lo - x`, `pair.hi - x`, `a * pair.lo`, `a * pair.hi`
+ * on both halves of x / a.  The union kernel keeps its hit point, normal and 1/r^2 two to a
+ * register pair (four pairs instead of seven broadcast pairs: the kernel's VGPR budget sets its
+ * waves per SIMD); the arithmetic is the same IEEE operation as the broadcast form. */
+__device__ __forceinline__ v2f pk_sub_blo(v2f pair, v2f x) {
+    v2f r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(pair), "v"(x));
+    return r;
+}
+__device__ __forceinline__ v2f pk_sub_bhi(v2f pair, v2f x) {
+    v2f r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(pair), "v"(x));
+    return r;
+}
+__device__ __forceinline__ v2f pk_mul_blo(v2f a, v2f pair) {
+    v2f r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(pair));
+    return r;
+}
+__device__ __forceinline__ v2f pk_mul_bhi(v2f a, v2f pair) {
+    v2f r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(pair));
+    return r;
+}
 __device__ __forceinline__ v2f weight2u(v2f u) {
     v2f p = __builtin_elementwise_fma(v2f{ORX_W5_C5, ORX_W5_C5}, u, v2f{ORX_W5_C4, ORX_W5_C4});
     p = __builtin_elementwise_fma(p, u, v2f{ORX_W5_C3, ORX_W5_C3});
@@ -1018,7 +1042,7 @@ __device__ __forceinline__ bool gather_skips(const GatherIn& gi, const GridParam
 /* NSUB: sub-rows per cell row (SUBR^2, or 1 for the cell-order layout) */
 template <uint32_t NSUB>
 #ifndef ORX_GATHER_LANE_WAVES
-#define ORX_GATHER_LANE_WAVES 6 /* waves per SIMD the per-lane gather is register-capped for (no spills) */
+#define ORX_GATHER_LANE_WAVES 7 /* waves per SIMD the per-lane gather is register-capped for (72 VGPRs, no spills) */
 #endif
 __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
                                                     uint32_t ntiles) {
@@ -1070,10 +1094,9 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
             if (gi.visits) window_visits(pb.offsets, g.gx, g.gy, x_lo, x_hi, y_lo, ny, z_lo, nrows, dC, dP);
         }
     }
-    const v2f ir2 = v2f{1.0f / radius2, 1.0f / radius2};
+    const v2f irr = v2f{1.0f / radius2, 0.f}; /* pairs broadcast through op_sel (pk_sub_blo ...) */
     v2f accx = v2f{0.f, 0.f}, accy = accx, accz = accx;
-    const v2f px2 = v2f{pos.x, pos.x}, py2 = v2f{pos.y, pos.y}, pz2 = v2f{pos.z, pos.z};
-    const v2f nx2 = v2f{B.x, B.x}, ny2 = v2f{B.y, B.y}, nz2 = v2f{B.z, B.z};
+    const v2f pxy = v2f{pos.x, pos.y}, pzn = v2f{pos.z, B.x}, nyz = v2f{B.y, B.z};
     const int32_t nq = (int32_t)dir_q8(B.x, B.y, B.z);
     /* SP_PLANES * splane * 4 < 4 GiB: checked on the host (resize) */
     const __amdgpu_buffer_rsrc_t SR = __builtin_amdgcn_make_buffer_rsrc((void*)pb.sorted, 0, 0xffffffff, 0x00020000);
@@ -1141,9 +1164,9 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
             ORX_TS_WAVE(ts_wn);
             const uint32_t bo = kb << 2;
             const f4u X = ldp(SR, SP_X * PB, bo), Y = ldp(SR, SP_Y * PB, bo), Z = ldp(SR, SP_Z * PB, bo);
-            const v2f dx0 = px2 - lo2(X), dx1 = px2 - hi2(X);
-            const v2f dy0 = py2 - lo2(Y), dy1 = py2 - hi2(Y);
-            const v2f dz0 = pz2 - lo2(Z), dz1 = pz2 - hi2(Z);
+            const v2f dx0 = pk_sub_blo(pxy, lo2(X)), dx1 = pk_sub_blo(pxy, hi2(X));
+            const v2f dy0 = pk_sub_bhi(pxy, lo2(Y)), dy1 = pk_sub_bhi(pxy, hi2(Y));
+            const v2f dz0 = pk_sub_blo(pzn, lo2(Z)), dz1 = pk_sub_blo(pzn, hi2(Z));
             const v2f d20 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
             const v2f d21 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
             bool in0 = d20.x <= radius2;
@@ -1164,8 +1187,8 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
             const bool u2 = in2 && q2 >= -DIRQ_BAND, u3 = in3 && q3 >= -DIRQ_BAND;
             if (u0 | u1 | u2 | u3) { /* inside the band: the exact test */
                 const f4u DX = ldp(SR, SP_DX * PB, bo), DY = ldp(SR, SP_DY * PB, bo), DZ = ldp(SR, SP_DZ * PB, bo);
-                const v2f nd0 = (lo2(DX) * nx2 + lo2(DY) * ny2) + lo2(DZ) * nz2;
-                const v2f nd1 = (hi2(DX) * nx2 + hi2(DY) * ny2) + hi2(DZ) * nz2;
+                const v2f nd0 = (pk_mul_bhi(lo2(DX), pzn) + pk_mul_blo(lo2(DY), nyz)) + pk_mul_bhi(lo2(DZ), nyz);
+                const v2f nd1 = (pk_mul_bhi(hi2(DX), pzn) + pk_mul_blo(hi2(DY), nyz)) + pk_mul_bhi(hi2(DZ), nyz);
                 in0 = in0 && (!u0 || nd0.x <= 0.f);
                 in1 = in1 && (!u1 || nd0.y <= 0.f);
                 in2 = in2 && (!u2 || nd1.x <= 0.f);
@@ -1174,7 +1197,7 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
             if (!(in0 | in1 | in2 | in3)) continue;
             const f4u WX = ldp(SR, SP_PX * PB, bo), WY = ldp(SR, SP_PY * PB, bo), WZ = ldp(SR, SP_PZ * PB, bo);
             /* the weight of every photon of the batch (rejected ones get 0 by select) */
-            v2f w0 = weight2(ir2, d20), w1 = weight2(ir2, d21);
+            v2f w0 = weight2u(pk_mul_blo(d20, irr)), w1 = weight2u(pk_mul_blo(d21, irr));
             ORX_TS_INC(ts_tris, (uint32_t)in0 + (uint32_t)in1 + (uint32_t)in2 + (uint32_t)in3);
             w0.x = in0 ? w0.x : 0.f;
             w0.y = in1 ? w0.y : 0.f;
@@ -1286,30 +1309,6 @@ __device__ __forceinline__ UChunk uload_chunk(const float* __restrict__ SX, cons
 struct UAcc {
     v2f accx, accy, accz;
 };
-/* packed broadcasts through op_sel: `pair.lo - x`, `pair.hi - x`, `a * pair.lo`, `a * pair.hi`
- * on both halves of x / a.  The union kernel keeps its hit point, normal and 1/r^2 two to a
- * register pair (four pairs instead of seven broadcast pairs: the kernel's VGPR budget sets its
- * waves per SIMD); the arithmetic is the same IEEE operation as the broadcast form. */
-__device__ __forceinline__ v2f pk_sub_blo(v2f pair, v2f x) {
-    v2f r;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(pair), "v"(x));
-    return r;
-}
-__device__ __forceinline__ v2f pk_sub_bhi(v2f pair, v2f x) {
-    v2f r;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(pair), "v"(x));
-    return r;
-}
-__device__ __forceinline__ v2f pk_mul_blo(v2f a, v2f pair) {
-    v2f r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(pair));
-    return r;
-}
-__device__ __forceinline__ v2f pk_mul_bhi(v2f a, v2f pair) {
-    v2f r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(pair));
-    return r;
-}
 struct UConst {
     v2f pxy, pzn, nyz, irr; /* (p.x, p.y), (p.z, n.x), (n.y, n.z), (1/r^2, -) */
     int32_t nq;

@@ -1,5 +1,9 @@
-# final-tree hall PPM profile round (bench line + rocprof + PMC)
 set -o pipefail
 mkdir -p gpurun_out/t
-timeout -k 10 900 bash tools/profile_round.sh r03j_hall_ppm SyntheticHall:1920x1080:ppm:P2048 > gpurun_out/prof_hall.log 2>&1 || { tail -20 gpurun_out/prof_hall.log; exit 1; }
-tail -1 gpurun_out/r03j_hall_ppm/bench.json | cut -c1-200
+ORX_LIB=$PWD/oppositerenderer_amd/liborx_lane7.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -k "shard or gather or ppm or PPM" --timeout 300 --timeout-method thread > gpurun_out/t/ltest.log 2>&1 || { tail -30 gpurun_out/t/ltest.log; exit 1; }
+tail -1 gpurun_out/t/ltest.log
+for n in base lane7 base lane7; do
+  ORX_LIB=$PWD/oppositerenderer_amd/liborx_$n.so timeout -k 10 300 python -u tools/shard_model.py --config 2 1 8 > gpurun_out/t/smh_$n.log 2>&1 || { tail -5 gpurun_out/t/smh_$n.log; exit 1; }
+  echo $n; grep "per-rank" gpurun_out/t/smh_$n.log | cut -c1-110
+done
+bash tools/gpu_lib_ab.sh "base lane7" --config 2 || exit 1
