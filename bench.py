@@ -264,10 +264,14 @@ def launch_ranks(n, argv):
     import socket
     import subprocess
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    port = os.environ.get("MASTER_PORT")  # a caller-chosen port avoids the probe below
+    if not port:
+        # probe a free port (another process could take it before rank 0 binds it: set
+        # MASTER_PORT to pin one where that matters)
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
     procs = []
     for rank in range(n):
         env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),

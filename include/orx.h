@@ -181,7 +181,11 @@ typedef struct {
                                          (orx_scene.media) scatters photons and eye rays gather its volumetric
                                          photons (ParticipatingMedium.cu, VolumetricPhotonSphere*.cu); the PPM
                                          direct pass takes no shadow samples (DirectRadianceEstimation.cu:54).
-                                         PPM on one device only (other methods / world > 1: ORX_ERR_UNSUPPORTED) */
+                                         All of this applies only when the scene has a medium box: with
+                                         enable_media set and orx_scene.n_media == 0 the renderer runs exactly
+                                         as with enable_media = 0 (the direct pass keeps its 4 shadow samples,
+                                         unlike a reference build with the macro on).  PPM on one device only
+                                         (other methods / world > 1: ORX_ERR_UNSUPPORTED) */
     uint32_t volumetric_photons;      /* NUM_VOLUMETRIC_PHOTONS = 200000 (config.h:35): volumetric photon table */
     uint32_t reserved[3];
 } orx_config;

@@ -14,7 +14,8 @@
 #include <cmath>
 #include <stdexcept>
 
-const unsigned int OptixRenderer::EMITTED_PHOTONS_PER_ITERATION = 1024u * 1024u;
+unsigned int OptixRenderer::EMITTED_PHOTONS_PER_ITERATION = 1024u * 1024u;
+unsigned int OptixRenderer::s_liveRenderers = 0;
 
 static void check(orx_renderer* r, orx_status s) {
     if (s != ORX_OK) throw std::runtime_error(r ? orx_last_error(r) : "orx: invalid renderer");
@@ -54,15 +55,29 @@ float IScene::getSceneInitialPPMRadiusEstimate() const {
 
 OptixRenderer::OptixRenderer() : m_orx(nullptr), m_initialized(false) { orx_default_config(&m_cfg); }
 
-OptixRenderer::~OptixRenderer() { orx_destroy(m_orx); }
+OptixRenderer::~OptixRenderer() {
+    orx_destroy(m_orx);
+    if (m_initialized) s_liveRenderers--;
+}
 
 void OptixRenderer::setConfig(const orx_config& cfg) {
     if (m_initialized) throw std::runtime_error("OptixRenderer::setConfig after initialize");
+    const unsigned long long launch = (unsigned long long)cfg.photon_launch_width * cfg.photon_launch_height;
+    if (launch == 0 || launch > 0xFFFFFFFFull)
+        throw std::invalid_argument("OptixRenderer::setConfig: photon launch must hold 1 .. 2^32-1 photons");
+    if (s_liveRenderers > 0 && launch != EMITTED_PHOTONS_PER_ITERATION)
+        throw std::invalid_argument("OptixRenderer::setConfig: EMITTED_PHOTONS_PER_ITERATION is process-wide and an "
+                                    "initialized renderer uses a different photon launch");
     m_cfg = cfg;
+    EMITTED_PHOTONS_PER_ITERATION = (unsigned int)launch;
 }
 
 void OptixRenderer::initialize(const ComputeDevice& device) {
     if (m_initialized) throw std::runtime_error("ERROR: Multiple OptixRenderer::initialize!");
+    const unsigned int launch = m_cfg.photon_launch_width * m_cfg.photon_launch_height;
+    if (s_liveRenderers > 0 && launch != EMITTED_PHOTONS_PER_ITERATION)
+        throw std::invalid_argument("OptixRenderer::initialize: another initialized renderer uses a different "
+                                    "photon launch (EMITTED_PHOTONS_PER_ITERATION is process-wide)");
     orx_renderer* r = nullptr;
     if (orx_create(device.getDeviceId(), &m_cfg, &r) != ORX_OK) {
         orx_destroy(r);
@@ -70,6 +85,8 @@ void OptixRenderer::initialize(const ComputeDevice& device) {
     }
     m_orx = r;
     m_initialized = true;
+    s_liveRenderers++;
+    EMITTED_PHOTONS_PER_ITERATION = orx_emitted_photons_per_iteration(r); /* this renderer's launch */
 }
 
 void OptixRenderer::initScene(IScene& scene) {

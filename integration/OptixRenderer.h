@@ -90,14 +90,20 @@ public:
     unsigned int getWidth() const;
     unsigned int getHeight() const;
     unsigned int getScreenBufferSizeBytes() const;
-    /* PHOTON_LAUNCH_WIDTH * PHOTON_LAUNCH_HEIGHT (OptixRenderer.h:43) */
-    static const unsigned int EMITTED_PHOTONS_PER_ITERATION;
+    /* PHOTON_LAUNCH_WIDTH * PHOTON_LAUNCH_HEIGHT (OptixRenderer.h:43).  The reference compiles
+     * the launch size in, so this is process-wide: it follows the photon launch of the last
+     * setConfig (1024 x 1024 by default) and callers read it as before
+     * (DistributedApplication.cpp:133-134).  Not const, since setConfig sets it. */
+    static unsigned int EMITTED_PHOTONS_PER_ITERATION;
 
     /* not in the reference: the config.h constants the engine otherwise compiles in
-     * (photon launch size, seed, ...), before initialize() */
+     * (photon launch size, seed, ...), before initialize().  Throws std::invalid_argument when
+     * the photon launch differs from the one of a renderer that is already initialized in this
+     * process (EMITTED_PHOTONS_PER_ITERATION can hold only one value, as in the reference) */
     void setConfig(const orx_config& cfg);
 
 private:
+    static unsigned int s_liveRenderers; /* initialized, not yet destroyed */
     orx_renderer* m_orx;
     orx_config m_cfg;
     bool m_initialized;

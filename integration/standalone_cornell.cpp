@@ -118,6 +118,17 @@ int main(int argc, char** argv) {
             std::printf("%.9g %.9g %.9g\n", c.hfov, c.vfov, Cornell().getSceneInitialPPMRadiusEstimate());
             return 0;
         }
+        if (!std::strcmp(argv[i], "--print-emitted") && i + 1 < argc) {
+            /* the process-wide constant before and after setConfig (no device needed) */
+            const unsigned before = OptixRenderer::EMITTED_PHOTONS_PER_ITERATION;
+            OptixRenderer r;
+            orx_config cfg;
+            orx_default_config(&cfg);
+            cfg.photon_launch_width = cfg.photon_launch_height = (unsigned)std::atoi(argv[i + 1]);
+            r.setConfig(cfg);
+            std::printf("%u %u\n", before, OptixRenderer::EMITTED_PHOTONS_PER_ITERATION);
+            return 0;
+        }
         if (i + 1 >= argc) break;
         if (!std::strcmp(argv[i], "--method")) method = argv[++i];
         else if (!std::strcmp(argv[i], "--width")) W = (unsigned)std::atoi(argv[++i]);
@@ -162,8 +173,8 @@ int main(int argc, char** argv) {
         }
         double sum = 0;
         for (float v : img) sum += v;
-        std::printf("ok %s %ux%u photons %u iterations %u mean %.9g\n", method, W, H, P * P, iters,
-                    sum / (double)img.size());
+        std::printf("ok %s %ux%u photons %u iterations %u mean %.9g\n", method, W, H,
+                    OptixRenderer::EMITTED_PHOTONS_PER_ITERATION, iters, sum / (double)img.size());
     } catch (const std::exception& e) {
         std::fprintf(stderr, "error: %s\n", e.what());
         return 1;

@@ -1682,6 +1682,10 @@ __device__ __forceinline__ bool slot_valid(const PhotonBufs& pb, uint32_t s) {
  * voxel counters are 16-bit halves of one word (photons low, hit points high), so a block takes
  * a contiguous chunk of at most 65535 slots and 65535 pixels. */
 constexpr uint32_t SLAB_MAX_BINS = 1024;
+/* 24 KB of axis bins + 128 KB of voxel counts: one block per CU on gfx950's 160 KB LDS
+ * (the Makefile's ARCH is gfx950 only; a smaller-LDS target fails here, not at launch) */
+static_assert((6 * SLAB_MAX_BINS + SLAB_VOX * SLAB_VOX * SLAB_VOX) * 4 <= 160 * 1024,
+              "k_slab_hist's LDS histograms exceed gfx950's 160 KB per workgroup");
 __global__ __launch_bounds__(256) void k_slab_hist(PhotonBufs pb, PixelBufs px, SlabBins sb, SlabBins vb,
                                                    uint32_t cs, uint32_t cp, uint32_t* hist) {
     __shared__ uint32_t lh[6 * SLAB_MAX_BINS];

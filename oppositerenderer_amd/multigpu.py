@@ -533,7 +533,7 @@ def bench_main(args, metric, cpu_baseline=None):
     if vcm or pt:
         sharded = (ShardedVCM if vcm else ShardedPT)(backend, dist, world, rank, W, H)
     else:
-        slab = getattr(args, "partition", "slab") == "slab" and world > 1
+        slab = getattr(args, "partition", "rows") == "slab" and world > 1
         sharded = ShardedPPM(backend, dist, world, rank, W, H, pipeline=os.environ.get("ORX_PIPELINE", "1") != "0",
                              slab=slab)
     it = 0

@@ -14,3 +14,11 @@ import torch  # noqa: E402,F401
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through liborx.so on HIP)")
     config.addinivalue_line("markers", "slow: longer CPU-oracle runs")
+    config.addinivalue_line("markers", "fresh_process: spawns a child that must start before this process "
+                                       "makes its first HIP call (run first)")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    # tests that start a fresh GPU child process go first, before any test of this process has
+    # initialised HIP (tests/test_gpu_steady_state.py::test_rccl_world1_sharded_paths_match_oracle)
+    items.sort(key=lambda it: 0 if it.get_closest_marker("fresh_process") else 1)

@@ -76,6 +76,11 @@ def run_iterations(shards, scene, W, H, req, iters, slab=False, pipelined=False,
                 b.local_passes(it, it, radius, req)
             b.export_hitpoints(t)
         hp_all.copy_(torch.cat(hp_loc))
+        # the all-gather's completion: the side stream waits for this and nothing else, as
+        # ShardedPPM's work.wait() does, so the gather relies on the library's own events for the
+        # grid, the slab import and the direct pass (orx_capi.hip ev_grid_done / ev_direct_done)
+        hp_ready = torch.cuda.Event()
+        hp_ready.record(main)
         if pipelined:
             for b in shards:
                 if slab:
@@ -87,7 +92,7 @@ def run_iterations(shards, scene, W, H, req, iters, slab=False, pipelined=False,
         ctx = torch.cuda.stream(side) if pipelined else torch.cuda.stream(main)
         with ctx:
             if pipelined:
-                side.wait_stream(main)
+                side.wait_event(hp_ready)
             for b, part in zip(shards, parts):
                 b.gather_external(hp_all, world, part)
             total.copy_(torch.stack(parts).sum(0))

@@ -183,10 +183,12 @@ def test_sharded_device_pipelined_matches_single(world, W, H, P):
             b.local_eye(it, it, radius, req)
             b.export_hitpoints(t)
         hp_all.copy_(torch.cat(hp_loc))  # the all-gather, on the compute stream
+        hp_ready = torch.cuda.Event()  # its completion is all the side stream waits for (work.wait())
+        hp_ready.record(main)
         for b in shards:
             b.local_photons()
         with torch.cuda.stream(side):
-            side.wait_stream(main)
+            side.wait_event(hp_ready)
             for b, part in zip(shards, parts):
                 b.gather_external(hp_all, world, part)
             total.copy_(torch.stack(parts).sum(0))  # the reduce-scatter, on the side stream
@@ -333,10 +335,12 @@ def test_sharded_world4_world8_match_oracle(world, W, H, P, PH, photon_map, pipe
                 b.local_eye(it, it, radius, req)
                 b.export_hitpoints(t)
             hp_all.copy_(torch.cat(hp_loc))
+            hp_ready = torch.cuda.Event()  # the all-gather's completion only, as work.wait()
+            hp_ready.record(main)
             for b in shards:
                 b.local_photons()
             with torch.cuda.stream(side):
-                side.wait_stream(main)
+                side.wait_event(hp_ready)
                 for b, part in zip(shards, parts):
                     b.gather_external(hp_all, world, part)
                 total.copy_(torch.stack(parts).sum(0))

@@ -33,6 +33,16 @@ def test_camera_and_radius_match_python(W, H):
     assert r0 == np.float32(sc.initial_ppm_radius())
 
 
+@pytest.mark.parametrize("P", [64, 1024, 2048])
+def test_emitted_photons_constant_follows_config(P):
+    """OptixRenderer::EMITTED_PHOTONS_PER_ITERATION (OptixRenderer.h:43), which the client reads to
+    count photons (DistributedApplication.cpp:133-134), is 1024^2 by default and follows the photon
+    launch setConfig installs."""
+    out = subprocess.run([binary(), "--print-emitted", str(P)], capture_output=True, text=True, check=True)
+    before, after = (int(v) for v in out.stdout.split())
+    assert before == 1024 * 1024 and after == P * P
+
+
 def test_links_only_declared_symbols():
     nm = subprocess.run(["nm", "-D", "--undefined-only", binary()], capture_output=True, text=True, check=True)
     used = sorted({l.split()[-1] for l in nm.stdout.splitlines() if l.split()[-1].startswith("orx_")})
@@ -58,6 +68,7 @@ def test_shim_matches_golden(case, method, P, tmp_path):
                         "--iterations", "2", "--seed", "1645301512", "--out", str(out)],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
+    assert f"photons {P * P} " in r.stdout, r.stdout  # EMITTED_PHOTONS_PER_ITERATION follows the config
     got = np.fromfile(out, np.float32)
     ref = np.load(os.path.join(GOLDEN, case + ".npz"))["OUTPUT"]
     assert got.shape == ref.shape and got.mean() > 0
