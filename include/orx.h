@@ -312,7 +312,12 @@ orx_status orx_set_stream(orx_renderer* r, void* hip_stream, int use_external);
 /* rows owned by this rank for the current resolution, and ceil(H/world) */
 uint32_t orx_local_rows(const orx_renderer* r);
 uint32_t orx_max_local_rows(const orx_renderer* r);
-size_t orx_hitpoint_export_bytes(const orx_renderer* r); /* max_local_rows * W * 40 */
+/* max_local_rows * W * 28: plane A (position | flags bits, float4) then plane N (the normal of a
+ * non-specular hit, the radiance of another, float3), max_local_rows * W pixels each.  The
+ * attenuation stays with the owner: orx_ppm_gather_external returns the unattenuated estimate
+ * (sum of weighted photon powers / (pi r^2 emitted)) and orx_ppm_finish multiplies the summed own
+ * rows by their hit points' attenuation (IndirectRadianceEstimation.cu:220; fp32 order differs) */
+size_t orx_hitpoint_export_bytes(const orx_renderer* r);
 orx_status orx_ppm_local_passes(orx_renderer* r, uint64_t iteration_number, uint64_t local_iteration_number,
                                 float ppm_radius, const orx_request* details);
 /* the two halves of orx_ppm_local_passes, so that the hitpoint all-gather can
@@ -325,7 +330,8 @@ orx_status orx_export_hitpoints(orx_renderer* r, void* dst_device, size_t dst_by
  * segments * max_local_rows * W * 3 floats */
 orx_status orx_ppm_gather_external(orx_renderer* r, const void* hitpoints_device, uint32_t segments,
                                    void* indirect_device, size_t indirect_bytes);
-/* indirect_device: max_local_rows * W * 3 floats for the own rows */
+/* indirect_device: max_local_rows * W * 3 floats for the own rows: the summed unattenuated
+ * estimates (times each own hit point's attenuation here) */
 orx_status orx_ppm_finish(orx_renderer* r, const void* indirect_device, size_t indirect_bytes);
 /* Pipelined sharded PPM (uniform grid or kd-tree: the hash is single-device, and pipelines on
  * its own without this call; call before the first iteration, like orx_set_shard):

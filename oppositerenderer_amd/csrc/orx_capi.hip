@@ -1064,6 +1064,19 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
         HIPCHK(r, hipMemsetAsync(r->d_kdcount.p, 0, 64, r->stream));
     }
     pb.gmax = r->cfg.photon_grid_max_size;
+    /* ORX_SHARD_CELLS=2: a row shard of world N sizes its cells for gmax / N cells (N times the
+     * single-device volume, the single-device photons per cell; the accepted set does not depend on
+     * the cell size).  Measured slower (tools/shard_model.py, N = 8: configs[4] per-rank gather
+     * 5.96 -> 8.43 ms in cell order, 5.82 -> 6.24 ms on sub-rows; hall 0.42 ms either way): a
+     * window of radius r ~ one single-device cell then walks 2^3 cells of twice the edge, about 2.4x
+     * the volume of the 3^3 it walks otherwise, so the default keeps single-device cells */
+    {
+        static const int scaled = [] {
+            const char* e = getenv("ORX_SHARD_CELLS");
+            return e && atoi(e) == 2 ? 1 : 0;
+        }();
+        pb.gcells = (r->world >= 2 && !r->slab && scaled) ? std::max(1u, pb.gmax / r->world) : pb.gmax;
+    }
     pb.slots = r->d_slots.as<float4>();
     pb.vmask = r->d_vmask.as<uint8_t>();
     pb.sorted = r->d_sorted.as<float>();
@@ -1331,6 +1344,21 @@ static orx_status begin_iteration(orx_renderer* r, uint64_t local_iteration_numb
     return ORX_OK;
 }
 
+/* The gather's tile order (GatherIn.order) for an image of `px` pixels: super-tiles of 8 x 8 tiles
+ * (128 x 128 pixels) from 4M pixels up, image bands per XCD below.  At configs[4] the super-tiles
+ * halve the union gather's fetches from beyond L2 (2 x FETCH_SIZE 22.3 -> 11.8 GB per launch;
+ * 16 x 16: 10.4 GB) and the frame gains 2.8 % (serial gather 24.1 -> 23.1 ms); on the 1080p hall
+ * the serial gather gains too (1.37 -> 1.21 ms) but the pipelined frame, where the gather overlaps
+ * the next iteration's passes, does not (977 / 971 Mpaths/s, two runs each;
+ * tools/gpu_r04_order.sh, tools/gpu_ab_order.sh).  ORX_GATHER_ORDER=S forces S (0: bands). */
+static uint32_t gather_order(size_t px) {
+    static const int o = [] {
+        const char* e = getenv("ORX_GATHER_ORDER");
+        return e ? std::max(0, std::min(64, atoi(e))) : -1;
+    }();
+    return o >= 0 ? (uint32_t)o : (px >= (4u << 20) ? 8u : 0u);
+}
+
 static GatherIn local_gather_in(orx_renderer* r) {
     GatherIn gi;
     gi.base = (const uint8_t*)r->d_hp.p;
@@ -1342,6 +1370,7 @@ static GatherIn local_gather_in(orx_renderer* r) {
     gi.dbg = r->cfg.debug_counters ? r->d_dbg.as<uint32_t>() : nullptr;
     gi.cull = 0;
     gi.visits = 1;
+    gi.order = gather_order((size_t)r->W * r->H);
     return gi;
 }
 
@@ -1875,10 +1904,11 @@ orx_status orx_ppm_slab_import(orx_renderer* r, const void* recv, uint64_t n, co
 
 orx_status orx_export_hitpoints(orx_renderer* r, void* dst, size_t bytes) {
     if (!r || !dst) return ORX_ERR_INVALID_ARGUMENT;
-    size_t need = (size_t)r->max_rows * r->W * 40;
+    const size_t npx = (size_t)r->max_rows * r->W, need = npx * 28;
     if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "destination too small");
     HIPCHK(r, hipSetDevice(r->device));
-    HIPCHK(r, hipMemcpyAsync(dst, r->d_hp.p, need, hipMemcpyDeviceToDevice, cur_stream(r)));
+    launch_export_hp(cur_stream(r), r->px, (uint32_t)npx, (float*)dst);
+    HIPCHK(r, hipGetLastError());
     return ORX_OK;
 }
 
@@ -1891,7 +1921,8 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hp, uint32_t seg
     HIPCHK(r, hipSetDevice(r->device));
     GatherIn gi;
     gi.base = (const uint8_t*)hp;
-    gi.seg_bytes = (size_t)r->max_rows * r->W * 40;
+    gi.seg_bytes = (size_t)r->max_rows * r->W * 28;
+    gi.raw = 1;
     gi.segments = segments;
     gi.seg_rows = r->max_rows;
     gi.W = r->W;
@@ -1903,6 +1934,7 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hp, uint32_t seg
     gi.own_hi = r->own_hi;
     if (r->slab) gi.own_sb = slab_bins(r, r->own_nb);
     gi.visits = 0; /* rank-local counts are not the reference's; no per-pixel debug buffers here */
+    gi.order = gather_order((size_t)r->W * r->H);
     hipStream_t st = cur_stream(r);
     if (r->last_pipelined) { /* on the side stream, after the grid build */
         st = gather_stream(r);
@@ -1933,7 +1965,7 @@ orx_status orx_ppm_finish(orx_renderer* r, const void* indirect, size_t bytes) {
     HIPCHK(r, hipSetDevice(r->device));
     if (r->last_pipelined) { /* output only (direct ran beside the grid build), on the side stream */
         hipStream_t g = gather_stream(r);
-        HIPCHK(r, hipMemcpyAsync(r->d_ind.p, indirect, need, hipMemcpyDeviceToDevice, g));
+        launch_indirect_atten(g, r->px, (uint32_t)(need / 12), (const float*)indirect);
         HIPCHK(r, hipStreamWaitEvent(g, r->ev_direct_done, 0));
         ev_begin_on(r, P_DIRECT, g);
         launch_ppm_direct_output(g, r->scene, r->px, r->last_consts, 2);
@@ -1944,7 +1976,7 @@ orx_status orx_ppm_finish(orx_renderer* r, const void* indirect, size_t bytes) {
         return ORX_OK;
     }
     hipStream_t st = cur_stream(r);
-    HIPCHK(r, hipMemcpyAsync(r->d_ind.p, indirect, need, hipMemcpyDeviceToDevice, st));
+    launch_indirect_atten(st, r->px, (uint32_t)(need / 12), (const float*)indirect);
     ev_begin(r, P_DIRECT);
     launch_ppm_direct_output(st, r->scene, r->px, r->last_consts);
     ev_end(r, P_DIRECT);
@@ -2024,7 +2056,7 @@ orx_status orx_set_stream(orx_renderer* r, void* stream, int use_external) {
 uint32_t orx_local_rows(const orx_renderer* r) { return r ? r->rows : 0; }
 uint32_t orx_max_local_rows(const orx_renderer* r) { return r ? (r->H + r->world - 1) / r->world : 0; }
 size_t orx_hitpoint_export_bytes(const orx_renderer* r) {
-    return r ? (size_t)((r->H + r->world - 1) / r->world) * r->W * 40 : 0;
+    return r ? (size_t)((r->H + r->world - 1) / r->world) * r->W * 28 : 0;
 }
 
 static orx_status check_grid_error(orx_renderer* r) {

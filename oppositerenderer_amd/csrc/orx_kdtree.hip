@@ -687,15 +687,7 @@ __global__ __launch_bounds__(64) void k_ppm_gather_kd_wave(GatherIn gi, PhotonBu
     const size_t i = (size_t)j * gi.W + x;
     float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
     float2 Cc = make_float2(0.f, 0.f);
-    if (inimg) {
-        const uint32_t seg = j / gi.seg_rows, lj = j - seg * gi.seg_rows;
-        const size_t plane = (size_t)gi.seg_rows * gi.W;
-        const uint8_t* b = gi.base + seg * gi.seg_bytes;
-        const size_t li = (size_t)lj * gi.W + x;
-        A = ((const float4*)b)[li];
-        B = ((const float4*)(b + plane * 16))[li];
-        Cc = ((const float2*)(b + plane * 32))[li];
-    }
+    if (inimg) hp_load(gi, j, x, A, B, Cc);
     const uint32_t flags = __float_as_uint(A.w);
     const bool gathers = inimg && (flags & PRD_HIT_NON_SPECULAR);
     f3 acc = mk1(0.0f);

@@ -75,7 +75,10 @@ struct PhotonBufs {
     uint32_t prows;     /* local photon rows */
     uint32_t D;         /* max deposits per emitted photon */
     uint32_t S;         /* local slots = prows*PW*D */
-    uint32_t gmax;      /* PHOTON_GRID_MAX_SIZE */
+    uint32_t gmax;      /* PHOTON_GRID_MAX_SIZE: capacity of the cell arrays */
+    uint32_t gcells;    /* cell count the cell size is chosen for (getSmallestPossibleCellSize): gmax, or
+                         * gmax / N for a row shard of world N, whose 1/N of the photons would otherwise
+                         * sit in single-device cells (cell edge x N^(1/3), the same photons per cell) */
     float4* slots;      /* [S][4] 64-B deposit records: pos.xyz|power.x, dir.xyz|power.y, power.z, unused
                          * (one record per cache-line half: the grid permute reads it in one go) */
     uint8_t* vmask;     /* [S/D] bit k: deposit k stored with fmaxf(power) > 0 */
@@ -228,6 +231,11 @@ struct GatherIn {
      * dealt to the XCDs in contiguous bands; NULL: every tile */
     const uint32_t* tile_list = nullptr;
     const uint32_t* tile_count = nullptr;
+    uint32_t order = 0; /* tile order: 0 image bands per XCD, S > 0 super-tiles of S x S tiles (gather_tile) */
+    uint32_t raw = 0;   /* 1: the sharded gather's exported hit points (orx_export_hitpoints): planes A pos|flags
+                         * float4 and N normal float3, 28 B per pixel, no attenuation; the estimate is left
+                         * unattenuated and the owner applies its hit point's attenuation (orx_ppm_finish).
+                         * 0: the renderer's own planes (40 B per pixel: A, B normal|atten.x, C atten.yz) */
     uint32_t visits;    /* 1: count the reference's per-pixel visits (IndirectRadianceEstimation.cu:113/124)
                          * into dbg and the stats; 0 for the sharded gather, which has no per-pixel
                          * debug buffers and whose rank-local counts are not the reference's
@@ -243,10 +251,35 @@ __device__ __forceinline__ uint32_t gather_row(const GatherIn& gi, uint32_t y) {
     const uint32_t s = y % gi.segments, lj = y / gi.segments;
     return s * gi.seg_rows + lj;
 }
+/* The gather's hit point j (row of the segment-major layout), pixel x: position|flags (A),
+ * normal|attenuation.x (B) and attenuation.yz (C).  gi.raw: the 28-B export layout, attenuation 1
+ * (the owner applies it, orx_ppm_finish) */
+__device__ __forceinline__ void hp_load(const GatherIn& gi, uint32_t j, uint32_t x, float4& A, float4& B, float2& Cc) {
+    const uint32_t seg = j / gi.seg_rows, lj = j - seg * gi.seg_rows;
+    const size_t plane = (size_t)gi.seg_rows * gi.W;
+    const uint8_t* b = gi.base + seg * gi.seg_bytes;
+    const size_t li = (size_t)lj * gi.W + x;
+    A = ((const float4*)b)[li];
+    if (gi.raw) {
+        const float* n = (const float*)(b + plane * 16) + 3 * li;
+        B = make_float4(n[0], n[1], n[2], 1.0f);
+        Cc = make_float2(1.0f, 1.0f);
+    } else {
+        B = ((const float4*)(b + plane * 16))[li];
+        Cc = ((const float2*)(b + plane * 32))[li];
+    }
+}
+__device__ __forceinline__ float4 hp_load_a(const GatherIn& gi, uint32_t j, uint32_t x) {
+    const uint32_t seg = j / gi.seg_rows, lj = j - seg * gi.seg_rows;
+    return ((const float4*)(gi.base + seg * gi.seg_bytes))[(size_t)lj * gi.W + x];
+}
+
 /* 8x8-pixel wave tiles; the wave-union kernel, or the per-lane kernel for gathers of >= 8 segments */
 void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c);
 /* slab mode: flags[tile] / the ascending list of the tiles with a hit point that gathers here
  * (the others' indirect is zeroed here); ntiles of the gather's 16x16 tiling */
+void launch_export_hp(hipStream_t s, const PixelBufs& px, uint32_t n, float* dst);
+void launch_indirect_atten(hipStream_t s, const PixelBufs& px, uint32_t n, const float* in);
 void launch_gather_tiles(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, uint8_t* flags,
                          uint32_t* list, uint32_t* count);
 constexpr uint32_t SLAB_VOX = 32; /* coarse voxels per axis of the slab histogram (include/orx.h) */

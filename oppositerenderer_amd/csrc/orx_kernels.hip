@@ -476,7 +476,7 @@ __global__ void k_grid_setup(PhotonBufs pb, GridBox gb) {
     f3 ext = hi - lo;
     /* getSmallestPossibleCellSize (SpatialHash.cu:62-71) */
     float sceneVolume = ext.x * ext.y * ext.z;
-    float minVolumePerCell = sceneVolume / (float)pb.gmax;
+    float minVolumePerCell = sceneVolume / (float)pb.gcells;
     float radiusC = orx_powf(minVolumePerCell, 1.0f / 3.0f);
     f3 ncf = ext / radiusC;
     uint32_t nx = orx_f2u_sat(orx_floorf(ncf.x)), ny = orx_f2u_sat(orx_floorf(ncf.y)),
@@ -869,32 +869,32 @@ void launch_grid_bucket_place(hipStream_t s, const PhotonBufs& pb) {
 /* ------------------------------------------------------------------ */
 /* indirect radiance estimate: uniform-grid gather                     */
 /* ------------------------------------------------------------------ */
-struct HpRef {
-    const float4* A;
-    const float4* B;
-    const float2* C;
-    size_t li;
-};
-__device__ __forceinline__ HpRef hp_ref(const GatherIn& gi, uint32_t j, uint32_t x) {
-    uint32_t seg = j / gi.seg_rows, lj = j - seg * gi.seg_rows;
-    const size_t plane = (size_t)gi.seg_rows * gi.W;
-    const uint8_t* b = gi.base + seg * gi.seg_bytes;
-    HpRef r;
-    r.A = (const float4*)b;
-    r.B = (const float4*)(b + plane * 16);
-    r.C = (const float2*)(b + plane * 32);
-    r.li = (size_t)lj * gi.W + x;
-    return r;
-}
-
 /* XCD-aware tile order: block b runs on XCD b % 8; XCD k takes tiles [k per, (k+1) per) of the
  * image's tiles, or of the slab mode's list of tiles that gather here (a band of the image
  * would otherwise leave most XCDs idle when the rank's hit points cluster in the image).
- * false: no tile for this block. */
-__device__ __forceinline__ bool gather_tile(const GatherIn& gi, uint32_t ntiles, uint32_t& tile) {
+ * gi.order = S > 0: the image's tiles taken in super-tiles of S x S tiles (super-tiles row-major,
+ * tiles row-major inside), XCD k a contiguous run of that order, so the blocks an XCD runs at
+ * once cover a patch S tiles tall instead of a strip one tile tall (fewer photon-plane lines
+ * fetched into its L2 per tile).  false: no tile for this block. */
+__host__ __device__ __forceinline__ uint32_t gather_order_count(uint32_t order, uint32_t ntx, uint32_t nty) {
+    if (!order) return ntx * nty;
+    return ((ntx + order - 1) / order) * ((nty + order - 1) / order) * order * order;
+}
+__device__ __forceinline__ bool gather_tile(const GatherIn& gi, uint32_t ntx, uint32_t ntiles, uint32_t& tile) {
     if (!gi.tile_list) {
-        const uint32_t per = (ntiles + 7) / 8;
-        tile = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+        if (!gi.order) {
+            const uint32_t per = (ntiles + 7) / 8;
+            tile = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+            return true;
+        }
+        const uint32_t S = gi.order, nty = ntiles / ntx, nsx = (ntx + S - 1) / S;
+        const uint32_t total = gather_order_count(S, ntx, nty), per = (total + 7) / 8;
+        const uint32_t o = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+        if (o >= total) return false;
+        const uint32_t st = o / (S * S), w = o - st * (S * S);
+        const uint32_t tx = (st % nsx) * S + w % S, ty = (st / nsx) * S + w / S;
+        if (tx >= ntx || ty >= nty) return false;
+        tile = ty * ntx + tx;
         return true;
     }
     const uint32_t n = *gi.tile_count, per = (n + 7) / 8;
@@ -1049,7 +1049,7 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
     __shared__ uint2 rq[GQ][256];
     const uint32_t tid = threadIdx.x;
     uint32_t tile;
-    if (!gather_tile(gi, ntiles, tile)) return; /* block-uniform */
+    if (!gather_tile(gi, ntx, ntiles, tile)) return; /* block-uniform */
     const uint32_t w = tid >> 6, l = tid & 63;
     const uint32_t x = (tile % ntx) * 16 + (w & 1) * 8 + (l & 7);
     const uint32_t y = (tile / ntx) * 16 + (w >> 1) * 8 + (l >> 3);
@@ -1063,10 +1063,7 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
     size_t i = 0;
     if (live) {
         i = (size_t)j * gi.W + x;
-        const HpRef hr = hp_ref(gi, j, x);
-        A = hr.A[hr.li];
-        B = hr.B[hr.li];
-        Cc = hr.C[hr.li];
+        hp_load(gi, j, x, A, B, Cc);
     }
     const uint32_t flags = __float_as_uint(A.w);
     const f3 pos = mk(A.x, A.y, A.z);
@@ -1400,7 +1397,7 @@ __global__ __launch_bounds__(256, 7) void k_ppm_gather_union(GatherIn gi, Photon
     __shared__ float ulds[4][7 * 64];
     const uint32_t tid = threadIdx.x, w = tid >> 6, l = tid & 63;
     uint32_t tile;
-    if (!gather_tile(gi, ntiles, tile)) return; /* block-uniform */
+    if (!gather_tile(gi, ntx, ntiles, tile)) return; /* block-uniform */
     const uint32_t x = (tile % ntx) * 16 + (w & 1) * 8 + (l & 7);
     const uint32_t y = (tile / ntx) * 16 + (w >> 1) * 8 + (l >> 3);
     const uint32_t j = gather_row(gi, y);
@@ -1413,10 +1410,7 @@ __global__ __launch_bounds__(256, 7) void k_ppm_gather_union(GatherIn gi, Photon
     size_t i = 0;
     if (live) {
         i = (size_t)j * gi.W + x;
-        const HpRef hr = hp_ref(gi, j, x);
-        A = hr.A[hr.li];
-        B = hr.B[hr.li];
-        Cc = hr.C[hr.li];
+        hp_load(gi, j, x, A, B, Cc);
     }
     const uint32_t flags = __float_as_uint(A.w);
     const f3 pos = mk(A.x, A.y, A.z);
@@ -1591,8 +1585,7 @@ __global__ __launch_bounds__(256) void k_gather_tiles(GatherIn gi, PhotonBufs pb
     const GridParams g = *pb.grid;
     bool act = false;
     if (live) {
-        const HpRef hr = hp_ref(gi, j, x);
-        const float4 A = hr.A[hr.li];
+        const float4 A = hp_load_a(gi, j, x);
         act = (__float_as_uint(A.w) & PRD_HIT_NON_SPECULAR) && g.G &&
               !gather_skips(gi, g, mk(A.x, A.y, A.z), c.ppm_radius);
     }
@@ -1633,6 +1626,36 @@ __global__ __launch_bounds__(1024) void k_tile_compact(const uint8_t* flags, uin
     }
     if (tid == 0) *count = base;
 }
+/* orx_export_hitpoints: the own rows' gather inputs in the 28-B exchange layout (plane A
+ * pos|flags float4, plane N normal float3; GatherIn.raw) — the attenuation stays with the owner */
+__global__ __launch_bounds__(256) void k_export_hp(PixelBufs px, uint32_t n, float* __restrict__ dst) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 B = px.hpB[i];
+    reinterpret_cast<float4*>(dst)[i] = px.hpA[i];
+    float* N = dst + 4 * (size_t)n + 3 * (size_t)i;
+    N[0] = B.x;
+    N[1] = B.y;
+    N[2] = B.z;
+}
+/* orx_ppm_finish of a shard: own-row indirect = the summed unattenuated estimate times the hit
+ * point's attenuation (IndirectRadianceEstimation.cu:220 multiplies before the normalisation;
+ * the same value up to fp32 order) */
+__global__ __launch_bounds__(256) void k_indirect_atten(PixelBufs px, uint32_t n, const float* __restrict__ in) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 B = px.hpB[i];
+    const float2 Cc = px.hpC[i];
+    px.indirect[3 * (size_t)i + 0] = in[3 * (size_t)i + 0] * B.w;
+    px.indirect[3 * (size_t)i + 1] = in[3 * (size_t)i + 1] * Cc.x;
+    px.indirect[3 * (size_t)i + 2] = in[3 * (size_t)i + 2] * Cc.y;
+}
+void launch_export_hp(hipStream_t s, const PixelBufs& px, uint32_t n, float* dst) {
+    hipLaunchKernelGGL(k_export_hp, dim3((n + 255) / 256), dim3(256), 0, s, px, n, dst);
+}
+void launch_indirect_atten(hipStream_t s, const PixelBufs& px, uint32_t n, const float* in) {
+    hipLaunchKernelGGL(k_indirect_atten, dim3((n + 255) / 256), dim3(256), 0, s, px, n, in);
+}
 void launch_gather_tiles(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c, uint8_t* flags,
                          uint32_t* list, uint32_t* count) {
     const uint32_t rows = gi.segments * gi.seg_rows;
@@ -1644,7 +1667,8 @@ void launch_gather_tiles(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb
 void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, const Consts& c) {
     const uint32_t rows = gi.segments * gi.seg_rows;
     const uint32_t ntx = (gi.W + 15) / 16, nty = (rows + 15) / 16, ntiles = ntx * nty;
-    const dim3 grid(8 * ((ntiles + 7) / 8));
+    const uint32_t norder = gi.tile_list ? ntiles : gather_order_count(gi.order, ntx, nty);
+    const dim3 grid(8 * ((norder + 7) / 8));
     /* The sharded gather (segments = ranks, cell-order layout, no visit counters) meets 1/N of
      * the photons.  Where a rank's photons are sparse in the grid the wave union's per-row work
      * outweighs the photons it shares and the per-lane kernel is faster: hall 1080p, 2048^2
@@ -1654,7 +1678,12 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
      * 6.41 / 9.34 ms).  So the per-lane kernel takes row shards of 8+ segments below 3 slots per
      * cell.  Measured on one device (serial hall gather / 4K conference frame): per-lane 2.5 ms /
      * 120 ms, union 1.91 / 53.3. */
-    if (gi.segments >= 8 && !gi.cull && pb.S < 3u * pb.gmax) {
+    static const int kern = [] { /* ORX_GATHER_KERNEL: 0 auto, 1 union, 2 per-lane (A/B) */
+        const char* e = getenv("ORX_GATHER_KERNEL");
+        return e ? atoi(e) : 0;
+    }();
+    const bool lane = kern == 2 || (kern == 0 && gi.segments >= 8 && !gi.cull && pb.S < 3u * pb.gcells);
+    if (lane) {
         if (pb.nsub == 1) hipLaunchKernelGGL((k_ppm_gather<1>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
         else hipLaunchKernelGGL((k_ppm_gather<SUBR * SUBR>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
         return;
@@ -1922,10 +1951,7 @@ __global__ __launch_bounds__(64) void k_ppm_gather_hash(GatherIn gi, PhotonBufs 
     float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
     float2 Cc = make_float2(0.f, 0.f);
     if (inimg) {
-        const HpRef hr = hp_ref(gi, j, x);
-        A = hr.A[hr.li];
-        B = hr.B[hr.li];
-        Cc = hr.C[hr.li];
+        hp_load(gi, j, x, A, B, Cc);
     }
     const uint32_t flags = __float_as_uint(A.w);
     f3 acc = mk1(0.0f);

@@ -1117,7 +1117,13 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
              * one traversal loop); the result goes into .w of the contribution row */
             {
                 CamShadowRays R{q, qhit, qpb, qqb, lane, total_p, 0u};
+#ifndef ORX_VCM_NO_SHADOW
                 trace_any_chain(S, R, stk);
+#else /* timing A/B only (make variant NAME=noshadow DEFS=-DORX_VCM_NO_SHADOW): every connection unoccluded */
+                f3 o_, d_;
+                float a_, b_;
+                while (R.next(o_, d_, a_, b_)) R.result(false);
+#endif
             }
             __threadfence_block();
             for (uint32_t k = 0; k < npend; ++k) {

@@ -7,10 +7,10 @@ thread (x,y) aliases RNG slot (x,y), OptixRenderer_SpatialHash.cu:310-334),
 so RNG state never crosses GPUs.  Per PPM iteration:
 
   1. local passes   eye rays for own pixel rows, own photon batch, photon grid over own photons
-  2. all-gather     compact hitpoints (40 B/pixel) of every rank           (RCCL all_gather)
+  2. all-gather     compact hitpoints (28 B/pixel) of every rank           (RCCL all_gather)
   3. gather         ALL pixels against the own photon grid -> partial indirect radiance
   4. reduce-scatter partial indirect, summed, to the row owners            (RCCL reduce_scatter)
-  5. finish         direct light + running-sum output on own rows
+  5. finish         own hit points' attenuation, direct light + running-sum output on own rows
 
 The gather is linear in the photon set and normalises by the global emitted
 count, so the result equals one GPU running the union photon launch, up to
@@ -32,6 +32,9 @@ import os
 import time
 
 import numpy as np
+
+
+HP_EXPORT_FLOATS = 7  # orx_export_hitpoints: 28 B per pixel (position|flags float4, normal float3)
 
 
 def local_rows(H, rank, world):
@@ -162,8 +165,9 @@ class ShardedPPM:
             self.recv = backend.alloc(9 * s_global + 9)
             self.last_plan = None
         nsets = 2 if self.pipe else 1
-        self.sets = [(backend.alloc(self.max_rows * W * 10),             # own hitpoints, 40 B/px as float32
-                      backend.alloc(world * self.max_rows * W * 10),     # all hitpoints
+        hpf = HP_EXPORT_FLOATS
+        self.sets = [(backend.alloc(self.max_rows * W * hpf),            # own hitpoints, 28 B/px as float32
+                      backend.alloc(world * self.max_rows * W * hpf),    # all hitpoints
                       backend.alloc(world * self.max_rows * W * 3),      # partial indirect, all pixels
                       backend.alloc(self.max_rows * W * 3))              # summed indirect, own rows
                      for _ in range(nsets)]

@@ -1679,9 +1679,11 @@ static void ppm_gather_hash(orc_renderer* r, float ppmRadiusSquared, float emitt
     r->sum_cells_visited = sumC;
 }
 
-/* hitpoint source for the gather: the own rows, or `segments` export buffers
- * (plane layout A: pos+flags float4, B: normal|radiance + atten.x float4,
- * C: atten.yz float2; seg_rows*W pixels per plane) */
+/* hitpoint source for the gather: the own rows, or `segments` export buffers of the sharded
+ * gather (include/orx.h orx_export_hitpoints: plane A pos + flags float4, plane N the normal
+ * float3; seg_rows*W pixels per plane, 28 B per pixel).  The export carries no attenuation: the
+ * sharded gather returns the unattenuated estimate and the owner applies its hit point's
+ * attenuation in orc_ppm_finish. */
 typedef struct {
     const hitpoint_t* own;
     const float* ext;
@@ -1691,17 +1693,16 @@ static hitpoint_t hp_fetch(const orc_renderer* r, const hp_src* src, size_t px) 
     if (src->own) return src->own[px];
     const size_t plane = (size_t)src->seg_rows * r->W;
     size_t seg = px / plane, li = px - seg * plane;
-    const float* b = src->ext + seg * plane * 10;
+    const float* b = src->ext + seg * plane * 7;
     const float* A = b + 4 * li;
-    const float* B = b + 4 * plane + 4 * li;
-    const float* Cc = b + 8 * plane + 2 * li;
+    const float* N = b + 4 * plane + 3 * li;
     hitpoint_t h;
     memset(&h, 0, sizeof h);
     h.position = mk(A[0], A[1], A[2]);
     memcpy(&h.flags, &A[3], 4);
-    if (h.flags & PRD_HIT_NON_SPECULAR) h.normal = mk(B[0], B[1], B[2]);
-    else h.radiance = mk(B[0], B[1], B[2]);
-    h.attenuation = mk(B[3], Cc[0], Cc[1]);
+    if (h.flags & PRD_HIT_NON_SPECULAR) h.normal = mk(N[0], N[1], N[2]);
+    else h.radiance = mk(N[0], N[1], N[2]);
+    h.attenuation = mk1(1.0f);
     return h;
 }
 
@@ -2188,7 +2189,7 @@ orx_status orc_set_shard(orc_renderer* r, uint32_t rank, uint32_t world) {
 }
 uint32_t orc_max_local_rows(const orc_renderer* r) { return (r->H + r->world - 1) / r->world; }
 uint32_t orc_local_rows(const orc_renderer* r) { return r->rows; }
-size_t orc_hitpoint_export_bytes(const orc_renderer* r) { return (size_t)orc_max_local_rows(r) * r->W * 40; }
+size_t orc_hitpoint_export_bytes(const orc_renderer* r) { return (size_t)orc_max_local_rows(r) * r->W * 28; }
 
 orx_status orc_ppm_local_passes(orc_renderer* r, uint64_t iter, uint64_t local, float ppmRadius, const orx_request* det) {
     (void)iter;
@@ -2320,19 +2321,17 @@ orx_status orc_ppm_slab_import(orc_renderer* r, const float* recv, uint64_t n, c
 
 orx_status orc_export_hitpoints(orc_renderer* r, void* dst, size_t bytes) {
     const size_t plane = (size_t)r->max_rows * r->W;
-    if (!dst || bytes < plane * 40) return ORX_ERR_INVALID_ARGUMENT;
+    if (!dst || bytes < plane * 28) return ORX_ERR_INVALID_ARGUMENT;
     float* b = (float*)dst;
-    memset(b, 0, plane * 40);
+    memset(b, 0, plane * 28);
     for (size_t i = 0; i < (size_t)r->rows * r->W; i++) {
         const hitpoint_t* h = &r->hp[i];
         float* A = b + 4 * i;
-        float* B = b + 4 * plane + 4 * i;
-        float* Cc = b + 8 * plane + 2 * i;
+        float* N = b + 4 * plane + 3 * i;
         A[0] = h->position.x; A[1] = h->position.y; A[2] = h->position.z;
         memcpy(&A[3], &h->flags, 4);
         v3 nr = (h->flags & PRD_HIT_NON_SPECULAR) ? h->normal : h->radiance;
-        B[0] = nr.x; B[1] = nr.y; B[2] = nr.z; B[3] = h->attenuation.x;
-        Cc[0] = h->attenuation.y; Cc[1] = h->attenuation.z;
+        N[0] = nr.x; N[1] = nr.y; N[2] = nr.z;
     }
     return ORX_OK;
 }
@@ -2348,7 +2347,11 @@ orx_status orc_ppm_gather_external(orc_renderer* r, const void* hp, uint32_t seg
 }
 orx_status orc_ppm_finish(orc_renderer* r, const void* indirect, size_t bytes) {
     if (!indirect || bytes < (size_t)r->max_rows * r->W * 12) return ORX_ERR_INVALID_ARGUMENT;
-    memcpy(r->indirect, indirect, (size_t)r->rows * r->W * 12);
+    /* the summed unattenuated estimates of the own rows times each hit point's attenuation
+     * (the single-device gather multiplies inside, IndirectRadianceEstimation.cu:220: the same
+     * value up to fp32 order) */
+    const v3* in = (const v3*)indirect;
+    for (size_t i = 0; i < (size_t)r->rows * r->W; i++) r->indirect[i] = mul(in[i], r->hp[i].attenuation);
     ppm_direct(r);
     ppm_output(r, r->last_local);
     return ORX_OK;

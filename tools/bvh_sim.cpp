@@ -43,6 +43,7 @@ std::vector<Tri> tris;
 std::vector<uint32_t> prims;
 std::vector<N2> b2;
 int LEAF_MAX = 8;
+int QBITS = 0;
 float LEAF_SAH = 0.6f;
 
 static float area(const float* lo, const float* hi) {
@@ -217,7 +218,25 @@ int collapse(int n2, int W, bool octant) {
     }
     for (size_t i = 0; i < ch.size(); i++) {
         int s = slot_of[i];
-        for (int k = 0; k < 3; k++) wn[idx].lo[s][k] = b2[ch[i]].lo[k], wn[idx].hi[s][k] = b2[ch[i]].hi[k];
+        for (int k = 0; k < 3; k++) {
+            float lo = b2[ch[i]].lo[k], hi = b2[ch[i]].hi[k];
+            /* the builder's conservative 1e-6 expansion, then outward quantisation on QBITS bits
+             * against the node box (QBITS 0: exact) */
+            const float m = std::max(std::fabs(lo), std::fabs(hi)), e = m * 1e-6f + 1e-20f;
+            lo -= e;
+            hi += e;
+            if (QBITS) {
+                float nlo = INFINITY, nhi = -INFINITY;
+                for (size_t j = 0; j < ch.size(); j++) nlo = std::min(nlo, b2[ch[j]].lo[k] - e), nhi = std::max(nhi, b2[ch[j]].hi[k] + e);
+                const float steps = (float)((1 << QBITS) - 1);
+                int ee;
+                std::frexp((nhi - nlo) / steps, &ee);
+                const float sc = std::ldexp(1.0f, ee);  /* power-of-two step >= extent/steps */
+                lo = nlo + std::floor((lo - nlo) / sc) * sc;
+                hi = nlo + std::ceil((hi - nlo) / sc) * sc;
+            }
+            wn[idx].lo[s][k] = lo, wn[idx].hi[s][k] = hi;
+        }
         int c = ch[i];
         int ref = b2[c].l < 0 ? ~c : collapse(c, W, octant);
         wn[idx].child[s] = ref;
@@ -347,7 +366,7 @@ int main(int argc, char** argv) {
         std::fread(L, 4, 9, f) != 9)
         return 1;
     int nrays = argc > 2 ? std::atoi(argv[2]) : 200000;
-    if (argc > 3) LEAF_MAX = std::atoi(argv[3]);
+    if (argc > 3) QBITS = std::atoi(argv[3]);
     tris.resize(nt);
     for (uint32_t t = 0; t < nt; t++) {
         for (int k = 0; k < 3; k++) tris[t].lo[k] = INFINITY, tris[t].hi[k] = -INFINITY;

@@ -23,6 +23,18 @@ from oppositerenderer_amd import _abi, multigpu, synthetic  # noqa: E402
 from oppositerenderer_amd.renderer import OptixRenderer, RenderRequestDetails, next_ppm_radius  # noqa: E402
 
 SEED = 1645301512
+XGMI_LINK_GBS = 153.0  # one xGMI link per direction (MI355X: 7 links per GPU)
+
+
+def collectives_ms(ag_mb, rs_mb, world):
+    """The exchange per iteration and rank over xGMI, two bounds: every rank receives (N-1)/N of
+    the all-gather and of the reduce-scatter.  'one link': a single ring (each step one link,
+    153 GB/s); 'all links': the N-1 peer links of a fully connected node used at once."""
+    if world == 1:
+        return 0.0, 0.0
+    recv_mb = (ag_mb + rs_mb) * (world - 1) / world
+    one = recv_mb * 1e6 / (XGMI_LINK_GBS * 1e9) * 1e3
+    return one, one / (world - 1)
 
 
 def run(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None):
@@ -44,18 +56,17 @@ def run(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None):
     full.initialize(0)
     full.initScene(scene)
     fb = multigpu.DeviceShard(full, torch, dev)
-    fhp = fb.alloc(H * W * 10)
+    fhp = fb.alloc(H * W * multigpu.HP_EXPORT_FLOATS)
     mr = (H + world - 1) // world
-    hp = b.alloc(mr * W * 10)
+    hp = b.alloc(mr * W * multigpu.HP_EXPORT_FLOATS)
 
     def segments(t):
-        """[H][W] planes A (4), B (4), C (2) -> N segments of mr rows, rows y = s + lj*N"""
+        """[H][W] planes A (4), N (3) -> N segments of mr rows, rows y = s + lj*N"""
         A = t[:H * W * 4].view(H, W, 4)
-        B = t[H * W * 4:H * W * 8].view(H, W, 4)
-        Cc = t[H * W * 8:].view(H, W, 2)
+        Nn = t[H * W * 4:].view(H, W, 3)
         out = []
         for s_ in range(world):
-            for P_, k in ((A, 4), (B, 4), (Cc, 2)):
+            for P_, k in ((A, 4), (Nn, 3)):
                 blk = torch.zeros(mr, W, k, device=dev)
                 rows = P_[s_::world]
                 blk[:rows.shape[0]] = rows
@@ -94,7 +105,7 @@ def run(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None):
     st = r.stats()
     ni = max(1, st.timed_iterations)
     passes = {name: round(st.pass_ms[i] / ni, 3) for i, name in enumerate(_abi.PASS_NAMES) if st.pass_ms[i] > 0}
-    allgather_mb = world * mr * W * 40 / 1e6
+    allgather_mb = world * mr * W * 4 * multigpu.HP_EXPORT_FLOATS / 1e6
     rs_mb = world * mr * W * 12 / 1e6
     r.destroy()
     full.destroy()
@@ -119,8 +130,8 @@ def run_slab(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None, nb=mult
         b.enable_slab()
         shards.append(b)
     mr = (H + world - 1) // world
-    hps = [b.alloc(mr * W * 10) for b in shards]
-    hp_all = shards[0].alloc(world * mr * W * 10)
+    hps = [b.alloc(mr * W * multigpu.HP_EXPORT_FLOATS) for b in shards]
+    hp_all = shards[0].alloc(world * mr * W * multigpu.HP_EXPORT_FLOATS)
     part = shards[0].alloc(world * mr * W * 3)
     names = ("local", "hist_pack", "import_grid", "gather", "finish")
     tot = [dict.fromkeys(names, 0.0) for _ in range(world)]
@@ -217,7 +228,17 @@ if __name__ == "__main__":
                   f"rank sums {[round(sum(p.values()), 3) for p in per_rank]} | axis {axis}, photons per rank "
                   f"{counts.sum(0).tolist()}, all-to-all {a2a:.0f} MB", flush=True)
         sys.exit(0)
+    base = None
     for n in worlds:
         ms, passes, ag, rs = run(n, **kw)
-        print(f"N={n}: per-rank serial {sum(ms.values()):.3f} ms {ms} | all-gather {ag:.0f} MB, "
-              f"reduce-scatter {rs:.0f} MB | passes {passes}", flush=True)
+        comp = sum(ms.values())
+        one, alll = collectives_ms(ag, rs, n)
+        base = comp if n == 1 else base
+        # projected frame: the all-gather overlaps the photon pass and the reduce-scatter the next
+        # iteration's local passes in the pipelined schedule ('hidden': max(compute, exchange));
+        # 'exposed': compute + exchange (nothing overlapped)
+        proj = (f" | exchange {one:.3f} ms on one link, {alll:.3f} ms over {n - 1} links; projected frame "
+                f"{max(comp, alll):.3f}-{comp + one:.3f} ms" + (f" ({base / (comp + one):.1f}-{base / max(comp, alll):.1f}x"
+                                                                f" of N=1)" if base else "")) if n > 1 else ""
+        print(f"N={n}: per-rank serial {comp:.3f} ms {ms} | all-gather {ag:.0f} MB, "
+              f"reduce-scatter {rs:.0f} MB{proj} | passes {passes}", flush=True)
