@@ -267,7 +267,8 @@ typedef struct {
     uint64_t photons_visited_total; /* summed since orx_reset_timing */
     uint64_t cells_visited_total;
     uint64_t valid_photons_total;
-    uint64_t gather_staged_total;   /* reserved: 0 */
+    uint32_t vcm_shadow_rays;     /* VCM: connection shadow rays the last camera pass deferred (launch_vcm_camera) */
+    uint32_t vcm_shadow_overflow; /* VCM: 1 if they exceeded the entry list and the pass reran in place */
     uint32_t timed_iterations;   /* iterations since orx_reset_timing */
     uint32_t bvh_stack_entries;  /* LDS traversal stack depth bound of the scene's BVH4 */
     float pass_ms[16];           /* device time per orx_pass summed since orx_reset_timing */

@@ -122,7 +122,7 @@ class OrxStats(C.Structure):
                 ("valid_photons", C.c_uint32), ("num_cells", C.c_uint32),
                 ("photons_visited", C.c_uint64), ("cells_visited", C.c_uint64),
                 ("photons_visited_total", C.c_uint64), ("cells_visited_total", C.c_uint64),
-                ("valid_photons_total", C.c_uint64), ("gather_staged_total", C.c_uint64),
+                ("valid_photons_total", C.c_uint64), ("vcm_shadow_rays", C.c_uint32), ("vcm_shadow_overflow", C.c_uint32),
                 ("timed_iterations", C.c_uint32), ("bvh_stack_entries", C.c_uint32), ("pass_ms", C.c_float * 16)]
 
 

@@ -426,6 +426,7 @@ struct orx_renderer {
     VcmBufs vcm_vb{};
     VcmConsts vcm_c{};
     DevBuf d_vcount, d_vverts, d_vsplat, d_vcam, d_vkd, d_vshq, d_vwork, d_vconst, d_tstats;
+    DevBuf d_vdq, d_vdpx, d_vrngsave; /* VCM camera pass: deferred shadow-ray entries, per-pixel list heads, RNG copy */
     std::vector<DevLight> host_lights;
     /* participating medium (cfg.enable_media with a medium box): the box, this frame's per-pixel
      * volumetricRadiance and per-photon last events, the volumetric table of the last photon pass */
@@ -1506,13 +1507,43 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
                                       vcm_light_waves((uint32_t)((lpx + 63) / 64)));
         HIPCHK(r, r->d_vshq.ensure(waves * VCM_SHQ_PER_WAVE * 16 + 16));
         vb.shq = r->d_vshq.as<float4>();
-        HIPCHK(r, r->d_vwork.ensure(16));
+        HIPCHK(r, r->d_vwork.ensure(32));
         vb.work = r->d_vwork.as<uint32_t>();
         HIPCHK(r, r->d_vconst.ensure(sizeof(VcmConsts)));
         vb.consts = r->d_vconst.as<VcmConsts>();
     }
     vb.cam = r->d_vcam.as<float>();
     vb.output = r->d_out.as<float>();
+    {
+        /* ORX_VCM_DEFER=N: the camera pass defers its connection shadow rays to k_vcm_shadow through an
+         * entry list of N per own pixel (launch_vcm_camera; small N exercises the overflow rerun,
+         * tests/test_gpu_parity.py).  Off by default: on the hall it measured slower than tracing them
+         * in place (camera pass 6.46 against 6.21 ms: camera kernel 3.23 + shadow kernel 2.81 + colour
+         * sums 0.34 ms for 6.5 rays per pixel; the shadow kernel, LDS-stack bound at 4 waves per SIMD,
+         * traces them no faster than the camera kernel's compacted chain at 3) */
+        static const uint32_t per_px = [] {
+            const char* e = getenv("ORX_VCM_DEFER");
+            return e ? (uint32_t)std::max(0, atoi(e)) : 0u;
+        }();
+        if (per_px) {
+            const size_t cap = lpx * per_px;
+            const size_t nslot = (size_t)r->rows * r->RW;
+            HIPCHK(r, r->d_vdq.ensure(cap * 49 + 64));
+            HIPCHK(r, r->d_vdpx.ensure(lpx * 20 + 64));
+            HIPCHK(r, r->d_vrngsave.ensure(nslot * 24 + 16));
+            vb.dq0 = r->d_vdq.as<float4>();
+            vb.dq1 = vb.dq0 + cap;
+            vb.dq2 = vb.dq1 + cap;
+            vb.docc = (uint8_t*)(vb.dq2 + cap);
+            vb.demis = r->d_vdpx.as<float4>();
+            vb.dhead = (uint32_t*)(vb.demis + lpx);
+            vb.dctl = vb.work + 4; /* d_vwork: [0..1] work counters, [4..7] the deferred-entry control words */
+            vb.dcap = (uint32_t)std::min<size_t>(cap, 0xfffffff0u);
+            vb.rng_save = r->d_vrngsave.as<uint32_t>();
+        } else {
+            vb.dq0 = nullptr;
+        }
+    }
     VcmConsts& c = r->vcm_c;
     float ulen = 0.f, vlen = 0.f;
     DevCamera cam = camera_setup(det->camera, &ulen, &vlen);
@@ -2310,15 +2341,19 @@ orx_status orx_get_stats(orx_renderer* r, orx_stats* out) {
         out->photons_visited_total = g.photons_visited_total;
         out->cells_visited_total = g.cells_visited_total;
         out->valid_photons_total = g.valid_total;
-        out->gather_staged_total = g.union_photons_total;
         if (r->pipe_bufs && r->d_grid2.p) { /* the other buffer set's share of the totals */
             GridParams g2;
             HIPCHK(r, hipMemcpy(&g2, r->d_grid2.p, sizeof g2, hipMemcpyDeviceToHost));
             out->photons_visited_total += g2.photons_visited_total;
             out->cells_visited_total += g2.cells_visited_total;
             out->valid_photons_total += g2.valid_total;
-            out->gather_staged_total += g2.union_photons_total;
         }
+    }
+    if (r->vcm_vb.dq0 && r->vcm_npx) { /* the last VCM camera pass's deferred connection shadow rays */
+        uint32_t ctl[2] = {0, 0};
+        HIPCHK(r, hipMemcpy(ctl, r->vcm_vb.dctl, 8, hipMemcpyDeviceToHost));
+        out->vcm_shadow_rays = ctl[0];
+        out->vcm_shadow_overflow = ctl[1];
     }
     for (int p = 0; p < P_COUNT; p++) {
         double tot = 0.0;

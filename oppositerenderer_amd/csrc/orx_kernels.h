@@ -27,7 +27,7 @@ struct GridParams {
     uint64_t photons_visited_total; /* since orx_reset_timing */
     uint64_t cells_visited_total;
     uint64_t valid_total;
-    uint64_t union_photons_total; /* reserved (stats ABI: gather_staged_total, always 0) */
+    uint64_t union_photons_total; /* reserved (always 0) */
     uint64_t st_lane_batches, st_wave_batches, st_lane_rows, st_wave_rows; /* ORX_TRAV_STATS builds: gather SIMT */
     uint64_t st_accepted;   /* ORX_TRAV_STATS builds: gather photons within r and facing the normal */
     float clo[3], chi[3];   /* the AABB of the photons in the grid (slab mode's gather cull; empty: +inf/-inf) */
@@ -302,6 +302,7 @@ void launch_pt(hipStream_t s, const DevScene& S, const DevCamera& cam, const Pix
 constexpr uint32_t VCM_MAX_VERTS = 9; /* VCM_MAX_PATH_LENGTH - 1 (OptixRenderer.cpp:343-344) */
 /* camera pass shadow-ray queue per wave, in float4: [64 lanes x (1 + 9) tests][2] + [64] points */
 constexpr uint32_t VCM_SHQ_PER_WAVE = 2 * 64 * (VCM_MAX_VERTS + 1) + 64;
+constexpr uint32_t VCM_END = 0xffffffffu;     /* end of a pixel's deferred-entry list */
 /* light subpath p = x + y*W pairs with pixel p; RNG slot y*RW + x serves both */
 struct VcmBufs {
     uint32_t RW;
@@ -318,6 +319,17 @@ struct VcmBufs {
     float* cam;         /* [W*H*3] camera subpath colour of this iteration */
     float* output;      /* [W*H*3] running sum */
     uint32_t* work;     /* [2] camera-pass, light-pass work-item counters (zeroed by the launches) */
+    /* the camera pass's connection shadow rays, deferred to k_vcm_shadow (launch_vcm_camera): one entry
+     * per connection in creation order, each pixel's entries linked in the order the reference adds them */
+    float4* dq0;        /* [dcap] connection point xyz | distance */
+    float4* dq1;        /* [dcap] direction xyz | next entry of the pixel (uint bits, VCM_END) */
+    float4* dq2;        /* [dcap] unoccluded contribution xyz | unused */
+    uint8_t* docc;      /* [dcap] 1: occluded (k_vcm_shadow) */
+    uint32_t* dhead;    /* [lcount] the pixel's first entry, or VCM_END */
+    float4* demis;      /* [lcount] the emitter contribution ending the subpath xyz | 1 if there is one */
+    uint32_t* dctl;     /* [4] entries written, overflow flag (more entries than dcap: the pass reruns in place) */
+    uint32_t dcap;
+    uint32_t* rng_save; /* [6][rows*RW] the RNG planes before the camera pass (restored for the in-place rerun) */
     struct VcmConsts* consts; /* device copy of the pass constants (written by the launches) */
 };
 struct VcmConsts {

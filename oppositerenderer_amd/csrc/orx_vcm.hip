@@ -24,6 +24,8 @@
  * The same quirks as the CPU restatement (oracle/orx_oracle_vcm.c.inc) are
  * reproduced; everything but the splat sums is bit-identical to it.
  */
+#include <algorithm>
+
 #include "orx_kernels.h"
 
 namespace orx {
@@ -950,8 +952,15 @@ __device__ __forceinline__ void camera_finish(const VcmBufs& vb, const CamPixel&
     rng_store(vb.rng, px.slot, rs);
 }
 
-template <bool TEX>
-__global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScene S, VcmBufs vb, const VcmConsts* __restrict__ cp) {
+/* MODE 0: connection shadow rays traced in place (below); 1: deferred to k_vcm_shadow, the colour
+ * summed by k_vcm_accum; 2: in place, only if the deferred pass ran out of entries (vb.dctl[1]) */
+#ifndef ORX_VCM_CAMERA_DEFER_WAVES
+#define ORX_VCM_CAMERA_DEFER_WAVES 3 /* the deferred form (no traversal of the shadow rays inside) */
+#endif
+template <bool TEX, int MODE>
+__global__ __launch_bounds__(64, MODE == 1 ? ORX_VCM_CAMERA_DEFER_WAVES : ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScene S, VcmBufs vb, const VcmConsts* __restrict__ cp) {
+    constexpr bool DEFER = MODE == 1;
+    if (MODE == 2 && !vb.dctl[1]) return;
     const VcmConsts& c = *cp; /* read by scalar loads where used: as a by-value argument it kept ~40 more
                                * SGPRs live and the kernel spilled VGPRs */
     ORX_STACK_DECL;
@@ -975,6 +984,8 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
     Rng rs = {};
     Subpath C = {};
     bool alive = false;
+    uint32_t tail = VCM_END;  /* DEFER: the pixel's last entry so far */
+    bool emis = false;        /* DEFER: the subpath ended on an emitter (its contribution is in C.color) */
     uint32_t next = 0, end = 0; /* the wave's current work item range (uniform) */
     bool exhausted = false;
     for (;;) {
@@ -1002,6 +1013,8 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
                 if (x < c.W && j < c.rows) {
                     camera_start(vb, c, x, j, px, rs, C);
                     alive = true;
+                    tail = VCM_END;
+                    emis = false;
                 }
             }
             const uint32_t n = (uint32_t)__popcll(need);
@@ -1028,6 +1041,7 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
                         const float lightPickProb = 1.f / (float)S.nl;
                         float directPdfA = m.inverseArea;
                         float emissionPdfW = maxf(0.f, dot(N, -C.direction)) * ORX_1_PI_F * m.inverseArea;
+                        emis = true;
                         if (C.depth == 1) {
                             C.color = C.color + C.throughput * m.Lemit;
                         } else {
@@ -1109,6 +1123,40 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
             }
             const uint32_t pbase = pincl - npend;
             const uint32_t total_p = __shfl(pincl, 63, 64);
+            if (DEFER) {
+                /* the wave's connections go to the global entry list, each lane's in its reference order
+                 * (light sample, then light vertices 0..n-1), linked behind the pixel's earlier ones */
+                uint32_t base = 0;
+                if (lane == 0 && total_p) base = atomicAdd(&vb.dctl[0], total_p);
+                base = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)base, 0, 64));
+                if (total_p && (base > vb.dcap || total_p > vb.dcap - base)) {
+                    /* out of entries: the pass is rerun in place (MODE 2) after restoring the RNG; stop */
+                    if (lane == 0) atomicOr(&vb.dctl[1], 1u);
+                    return;
+                }
+                const uint32_t first = base + pbase;
+                const float4 hp4 = qhit[lane];
+                for (uint32_t k = 0; k < npend; ++k) {
+                    const float4 r0 = q[2 * (qbase + k)];
+                    const float4 r1 = q[2 * (qbase + k) + 1];
+                    const uint32_t e = first + k;
+                    vb.dq0[e] = make_float4(hp4.x, hp4.y, hp4.z, r0.w);
+                    vb.dq1[e] = make_float4(r0.x, r0.y, r0.z, __uint_as_float(k + 1 < npend ? e + 1 : VCM_END));
+                    vb.dq2[e] = make_float4(r1.x, r1.y, r1.z, 0.f);
+                }
+                if (npend) {
+                    if (tail == VCM_END) vb.dhead[px.p] = first;
+                    else reinterpret_cast<uint32_t*>(vb.dq1 + tail)[3] = first;
+                    tail = first + npend - 1;
+                }
+                if (was_alive && !alive) {
+                    /* camera_finish without the colour: RNG, the emitter term, the list end */
+                    rng_store(vb.rng, px.slot, rs);
+                    vb.demis[px.p] = make_float4(C.color.x, C.color.y, C.color.z, emis ? 1.f : 0.f);
+                    if (tail == VCM_END) vb.dhead[px.p] = VCM_END;
+                }
+                continue;
+            }
             qpb[lane] = pbase;
             qqb[lane] = qbase;
             __threadfence_block();
@@ -1134,6 +1182,79 @@ __global__ __launch_bounds__(64, ORX_VCM_CAMERA_WAVES) void k_vcm_camera(DevScen
         }
         if (was_alive && !alive) camera_finish(vb, px, rs, C);
     }
+}
+
+/* The camera pass's deferred connection shadow rays (k_vcm_camera<TEX, 1>), traced by a lean
+ * any-hit kernel at the occupancy its registers allow: in the camera kernel they ran at its 3 waves
+ * per SIMD and took 2.96 of its 6.21 ms on the hall (timing A/B against a build that skips them).
+ * Entry e of the list goes to lane e mod (grid lanes); a lane chains its entries in one traversal
+ * loop (trace_any_chain).  The test is occluded()'s (vcm.h:43-58): a segment shorter than 3 eps is
+ * unoccluded without a walk. */
+struct DeferredShadowRays {
+    const float4* dq0;
+    const float4* dq1;
+    uint8_t* occ;
+    uint32_t e, n, stride, cur;
+    __device__ __forceinline__ bool next(f3& o, f3& d, float& tmin, float& tmax) {
+        while (e < n) {
+            cur = e;
+            e += stride;
+            const float4 a = dq0[cur];
+            if (a.w < 3.f * VCM_EPS_RAY) {
+                occ[cur] = 0;
+                continue;
+            }
+            const float4 b = dq1[cur];
+            o = mk(a.x, a.y, a.z);
+            d = mk(b.x, b.y, b.z);
+            tmin = VCM_EPS_RAY;
+            tmax = a.w - 2.f * VCM_EPS_RAY;
+            return true;
+        }
+        return false;
+    }
+    __device__ __forceinline__ void result(bool occluded) { occ[cur] = occluded ? 1 : 0; }
+};
+#ifndef ORX_VCM_SHADOW_WAVES
+#define ORX_VCM_SHADOW_WAVES 8
+#endif
+__global__ __launch_bounds__(64, ORX_VCM_SHADOW_WAVES) void k_vcm_shadow(DevScene S, VcmBufs vb) {
+    if (vb.dctl[1]) return; /* out of entries: the camera pass reruns in place */
+    ORX_STACK_DECL;
+    const uint32_t n = min(vb.dctl[0], vb.dcap);
+    DeferredShadowRays R{vb.dq0, vb.dq1, vb.docc, blockIdx.x * 64u + threadIdx.x, n, gridDim.x * 64u, 0u};
+    trace_any_chain(S, R, ORX_STACK_PTR);
+}
+/* the colour of every own pixel's camera subpath from its deferred entries, in the order the
+ * in-place pass adds them (C.color = C.color + contribution for each unoccluded connection, then the
+ * emitter term), then camera_finish's writes */
+__global__ __launch_bounds__(256) void k_vcm_accum(VcmBufs vb, uint32_t lcount) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= lcount || vb.dctl[1]) return;
+    f3 color = mk1(0.f);
+    for (uint32_t e = vb.dhead[p]; e != VCM_END; e = __float_as_uint(vb.dq1[e].w))
+        if (!vb.docc[e]) {
+            const float4 a = vb.dq2[e];
+            color = color + mk(a.x, a.y, a.z);
+        }
+    const float4 em = vb.demis[p];
+    if (em.w != 0.f) color = color + mk(em.x, em.y, em.z);
+    const size_t o3 = 3 * (size_t)p;
+    vb.cam[o3 + 0] = color.x;
+    vb.cam[o3 + 1] = color.y;
+    vb.cam[o3 + 2] = color.z;
+    const float ox = vb.output[o3 + 0] + vb.splat_in[o3 + 0];
+    const float oy = vb.output[o3 + 1] + vb.splat_in[o3 + 1];
+    const float oz = vb.output[o3 + 2] + vb.splat_in[o3 + 2];
+    vb.output[o3 + 0] = ox + color.x;
+    vb.output[o3 + 1] = oy + color.y;
+    vb.output[o3 + 2] = oz + color.z;
+}
+/* before the in-place rerun: the RNG planes as they were before the deferred pass */
+__global__ __launch_bounds__(256) void k_vcm_rng_restore(VcmBufs vb, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !vb.dctl[1]) return;
+    for (int k = 0; k < 6; k++) vb.rng.p[k][i] = vb.rng_save[(size_t)k * n + i];
 }
 
 /* persistent light-pass waves: as many as can be resident at once (4 per SIMD) */
@@ -1175,13 +1296,42 @@ void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const
         else hipLaunchKernelGGL((k_vcm_light<false, false>), dim3(blocks), dim3(64), lds, s, S, vb, vb.consts);
     }
 }
+template <int MODE>
+static void launch_camera_kernel(hipStream_t s, const DevScene& S, const VcmBufs& vb, uint32_t blocks) {
+    hipMemsetAsync(vb.work, 0, 4, s);
+    if (vb.vE) hipLaunchKernelGGL((k_vcm_camera<true, MODE>), dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, vb.consts);
+    else hipLaunchKernelGGL((k_vcm_camera<false, MODE>), dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, vb.consts);
+}
+/* The camera pass: the subpaths with their connections (k_vcm_camera<., 1>), the connections' shadow
+ * rays (k_vcm_shadow), the colours (k_vcm_accum).  Should the entry list overflow (more than
+ * vb.dcap connections in all, ORX_VCM_DEFER per own pixel), the pass is redone with the shadow rays traced in
+ * place from the saved RNG planes (k_vcm_rng_restore, k_vcm_camera<., 2>); both exit at once
+ * otherwise.  vb.dq0 == NULL: in place only. */
 void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
     hipLaunchKernelGGL(k_vcm_consts, dim3(1), dim3(1), 0, s, c, vb.consts);
     const uint32_t blocks = vcm_camera_waves(((c.W + 7) / 8) * ((c.rows + 7) / 8));
     if (blocks == 0) return;
-    hipMemsetAsync(vb.work, 0, 4, s);
-    if (vb.vE) hipLaunchKernelGGL(k_vcm_camera<true>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, vb.consts);
-    else hipLaunchKernelGGL(k_vcm_camera<false>, dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, vb.consts);
+    if (!vb.dq0) {
+        launch_camera_kernel<0>(s, S, vb, blocks);
+        return;
+    }
+    const uint32_t nslot = c.rows * vb.RW;
+    for (int k = 0; k < 6; k++)
+        hipMemcpyAsync(vb.rng_save + (size_t)k * nslot, vb.rng.p[k], (size_t)nslot * 4, hipMemcpyDeviceToDevice, s);
+    hipMemsetAsync(vb.dctl, 0, 16, s);
+    launch_camera_kernel<1>(s, S, vb, blocks);
+    static const uint32_t cus = [] {
+        int dev = 0, n = 256;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return (uint32_t)n;
+    }();
+    /* as many one-wave blocks as are resident at once: the register cap, or the LDS stacks (160 KB per CU) */
+    const uint32_t per_cu = std::min<uint32_t>(4u * ORX_VCM_SHADOW_WAVES, (uint32_t)((160u << 10) / ORX_STACK_BYTES(S)));
+    hipLaunchKernelGGL(k_vcm_shadow, dim3(cus * std::max(1u, per_cu)), dim3(64), ORX_STACK_BYTES(S), s, S, vb);
+    hipLaunchKernelGGL(k_vcm_accum, dim3((c.lcount + 255) / 256), dim3(256), 0, s, vb, c.lcount);
+    hipLaunchKernelGGL(k_vcm_rng_restore, dim3((nslot + 255) / 256), dim3(256), 0, s, vb, nslot);
+    launch_camera_kernel<2>(s, S, vb, blocks);
 }
 
 }  // namespace orx

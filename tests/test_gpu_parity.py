@@ -480,6 +480,58 @@ print(json.dumps({"errs": errs, "pipelined": gpu.pipelined()}))
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("defer", ["24", "0", "1"])
+def test_vcm_camera_shadow_modes(defer):
+    """The VCM camera pass's connection shadow rays (vcm.h:315-400, connectLightSourceS1 :406-488):
+    traced in place inside the camera kernel (the default, ORX_VCM_DEFER=0), deferred to k_vcm_shadow
+    with the colours summed by k_vcm_accum in the reference's order (ORX_VCM_DEFER=24: 24 entries per
+    pixel, ~6.5 rays per pixel on the hall), and
+    deferred into a list too small for them (1 per pixel: the pass overflows, restores the RNG planes
+    and reruns in place).  Camera colours, RNG and vertex counts bit-exact against the oracle, two
+    iterations back to back, and the overflow flag as expected."""
+    import subprocess, sys, os, json
+    code = r'''
+import json, sys, numpy as np
+sys.path.insert(0, "tests")
+import oracle_lib
+from oppositerenderer_amd import _abi, scenes
+from oppositerenderer_amd.renderer import OptixRenderer, RenderRequestDetails, next_ppm_radius
+scene = scenes.scene_by_name("CornellSmall")
+W, H = 96, 72
+cfg = _abi.default_config(seed=1645301512, photon_launch_width=64, photon_launch_height=64)
+gpu = OptixRenderer(cfg); gpu.initialize(0); gpu.initScene(scene)
+ora = oracle_lib.OracleRenderer(_abi.default_config(seed=1645301512, photon_launch_width=64, photon_launch_height=64))
+ora.init_scene(scene)
+cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+det = RenderRequestDetails(cam, scene.name, _abi.VCM_BIDIRECTIONAL_PATH_TRACING, W, H)
+r = scene.initial_ppm_radius()
+for it in range(2):
+    gpu.renderNextIteration(it, it, r, True, det)
+    ora.render_next_iteration(it, it, r, det.to_abi())
+    r = next_ppm_radius(r, it)
+bad = {}
+for buf, name in ((_abi.BUF_RNG, "rng"), (_abi.BUF_VCM_CAMERA, "camera"), (_abi.BUF_VCM_VERTEX_COUNT, "counts")):
+    g, o = gpu.read_buffer(buf, np.uint32), ora.read_buffer(buf, np.uint32)
+    bad[name] = int(np.count_nonzero(g != o))
+g, o = gpu.getOutputBuffer().astype(np.float64), ora.output().astype(np.float64)
+st = gpu.stats()
+print(json.dumps({"bad": bad, "err": float(np.sqrt(((g - o) ** 2).sum() / (o ** 2).sum())), "mean": float(g.mean()),
+                  "rays": int(st.vcm_shadow_rays), "overflow": int(st.vcm_shadow_overflow)}))
+'''
+    env = dict(os.environ, ORX_VCM_DEFER=defer)
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert all(v == 0 for v in res["bad"].values()), res
+    assert res["err"] < 1e-5 and res["mean"] > 0, res
+    if defer == "24":
+        assert res["rays"] > 0 and res["overflow"] == 0, res
+    elif defer == "1":
+        assert res["overflow"] == 1, res  # the rerun path ran
+
+
+@pytest.mark.gpu
 def test_method_switches_without_reads():
     """PPM (pipelined), PT and VCM iterations issued back to back with no read in between: the
     deferred PPM gather/output is ordered before the next method's passes, the RNG chain runs
