@@ -355,6 +355,43 @@ static bool trace(int root, V3 o, V3 d, float& best, uint32_t& bt, int mode, Sta
     return hit;
 }
 
+/* any hit in (1e-4, tmax): children in slot order, all hits pushed */
+static bool trace_any(int root, V3 o, V3 d, float tmax, Stats& st) {
+    V3 inv = {1.f / d.x, 1.f / d.y, 1.f / d.z};
+    std::vector<int> stk;
+    stk.reserve(64);
+    int cur = root;
+    st.rays++;
+    for (;;) {
+        if (cur >= 0) {
+            const WNode& n = wn[cur];
+            st.nodes++;
+            for (int s = 0; s < n.n; s++) {
+                if (n.child[s] == INT32_MIN) continue;
+                st.boxes++;
+                float t0 = 1e-4f, t1 = tmax;
+                for (int k = 0; k < 3; k++) {
+                    float a = (n.lo[s][k] - comp(o, k)) * comp(inv, k), b = (n.hi[s][k] - comp(o, k)) * comp(inv, k);
+                    t0 = std::max(t0, std::min(a, b));
+                    t1 = std::min(t1, std::max(a, b));
+                }
+                if (t0 <= t1) stk.push_back(n.child[s]), st.pushes++;
+            }
+        } else {
+            const N2& l = b2[~cur];
+            st.leaves++;
+            for (uint32_t k = l.first; k < l.first + l.count; k++) {
+                st.tris++;
+                float t;
+                if (isect_tri(prims[k], o, d, tmax, t)) return true;
+            }
+        }
+        if (stk.empty()) return false;
+        cur = stk.back();
+        stk.pop_back();
+    }
+}
+
 int main(int argc, char** argv) {
     FILE* f = std::fopen(argc > 1 ? argv[1] : "scratch/hall.bin", "rb");
     uint32_t nv, nt;
@@ -386,7 +423,7 @@ int main(int argc, char** argv) {
         int W;
         bool oct;
         int mode;
-    } vars[] = {{"w4-sort", 4, false, 0}, {"w8-sort", 8, false, 0}, {"w8-oct", 8, true, 1}, {"w8-oct-sorted", 8, true, 0}, {"w4-treelet", 4, false, 2}, {"w8-treelet", 8, false, 2}, {"w4-none", 4, false, 3}};
+    } vars[] = {{"w4-sort", 4, false, 0}, {"w8-sort", 8, false, 0}, {"w8-oct", 8, true, 1}, {"w8-oct-sorted", 8, true, 0}, {"w4-treelet", 4, false, 2}, {"w8-treelet", 8, false, 2}, {"w4-none", 4, false, 3}, {"w8-none", 8, false, 3}};
     V3 Lp = {L[0], L[1], L[2]}, L1 = {L[3], L[4], L[5]}, L2 = {L[6], L[7], L[8]};
     V3 Ln = norm(cross(L1, L2));
     for (auto& v : vars) {
@@ -417,6 +454,32 @@ int main(int argc, char** argv) {
         std::printf("%-14s nodes %zu  per ray: nodes %.2f boxes %.1f pushes %.2f leaves %.2f tris %.2f  (rays %.0f)\n",
                     v.name, wn.size(), st.nodes / st.rays, st.boxes / st.rays, st.pushes / st.rays, st.leaves / st.rays,
                     st.tris / st.rays, st.rays);
+        if (v.mode == 0 || v.mode == 3) {
+            /* shadow segments between two photon-path hit points (VCM connections) */
+            Stats sa;
+            std::mt19937 rng2(11);
+            std::vector<V3> pts;
+            for (int r = 0; r < nrays && (int)pts.size() < 60000; r++) {
+                V3 o = Lp + L1 * U(rng2) + L2 * U(rng2);
+                float u1 = U(rng2), u2 = U(rng2), rr = std::sqrt(u1), ph = 6.2831853f * u2;
+                V3 a = std::fabs(Ln.x) > 0.5f ? V3{0, 1, 0} : V3{1, 0, 0};
+                V3 t1 = norm(cross(a, Ln)), t2 = cross(Ln, t1);
+                V3 d = norm(t1 * (rr * std::cos(ph)) + t2 * (rr * std::sin(ph)) + Ln * std::sqrt(std::max(0.f, 1 - u1)));
+                float best = 1e27f;
+                uint32_t bt = 0;
+                Stats dummy;
+                if (trace(root, o, d, best, bt, 0, dummy)) pts.push_back(o + d * (best * 0.999f));
+            }
+            int occl = 0;
+            for (size_t i = 0; i + 1 < pts.size(); i += 2) {
+                V3 d = pts[i + 1] - pts[i];
+                float len = std::sqrt(dot(d, d));
+                d = d * (1.f / len);
+                occl += trace_any(root, pts[i], d, len * 0.999f, sa);
+            }
+            std::printf("   any-hit segments: nodes %.2f boxes %.1f leaves %.2f tris %.2f (segments %.0f, occluded %d)\n",
+                        sa.nodes / sa.rays, sa.boxes / sa.rays, sa.leaves / sa.rays, sa.tris / sa.rays, sa.rays, occl);
+        }
     }
     return 0;
 }
