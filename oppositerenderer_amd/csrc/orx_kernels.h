@@ -68,7 +68,10 @@ enum : uint32_t { SP_X = 0, SP_Y, SP_Z, SP_DIRQ, SP_DX, SP_DY, SP_DZ, SP_PX, SP_
 #define ORX_SUBX 4
 #endif
 constexpr uint32_t SUBX = ORX_SUBX; /* sub-cells per grid cell along x (bucket-sort grid, gather chord trimming) */
-constexpr uint32_t SUBR = 2; /* sub-rows per grid cell along y and along z (bucket-sort grid, nsub = SUBR^2) */
+#ifndef ORX_SUBR
+#define ORX_SUBR 2
+#endif
+constexpr uint32_t SUBR = ORX_SUBR; /* sub-rows per grid cell along y and along z (bucket-sort grid, nsub = SUBR^2) */
 
 struct PhotonBufs {
     uint32_t PW, PH;    /* photon launch (full) */
