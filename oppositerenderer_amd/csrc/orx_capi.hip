@@ -426,7 +426,7 @@ struct orx_renderer {
     VcmBufs vcm_vb{};
     VcmConsts vcm_c{};
     DevBuf d_vcount, d_vverts, d_vsplat, d_vcam, d_vkd, d_vshq, d_vwork, d_vconst, d_tstats;
-    DevBuf d_vdq, d_vdpx, d_vrngsave; /* VCM camera pass: deferred shadow-ray entries, per-pixel list heads, RNG copy */
+    DevBuf d_vdq, d_vdpx, d_vrngsave, d_vshstk; /* VCM camera pass: deferred shadow-ray entries, per-pixel list heads, RNG copy, deep stack */
     std::vector<DevLight> host_lights;
     /* participating medium (cfg.enable_media with a medium box): the box, this frame's per-pixel
      * volumetricRadiance and per-photon last events, the volumetric table of the last photon pass */
@@ -1515,15 +1515,15 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
     vb.cam = r->d_vcam.as<float>();
     vb.output = r->d_out.as<float>();
     {
-        /* ORX_VCM_DEFER=N: the camera pass defers its connection shadow rays to k_vcm_shadow through an
-         * entry list of N per own pixel (launch_vcm_camera; small N exercises the overflow rerun,
-         * tests/test_gpu_parity.py).  Off by default: on the hall it measured slower than tracing them
-         * in place (camera pass 6.46 against 6.21 ms: camera kernel 3.23 + shadow kernel 2.81 + colour
-         * sums 0.34 ms for 6.5 rays per pixel; the shadow kernel, LDS-stack bound at 4 waves per SIMD,
-         * traces them no faster than the camera kernel's compacted chain at 3) */
+        /* The camera pass defers its connection shadow rays to k_vcm_shadow through an entry list of
+         * ORX_VCM_DEFER = N per own pixel (default 16; the hall averages 6.5; a list that overflows makes
+         * the pass rerun in place, small N exercises that, tests/test_gpu_parity.py); 0 traces them in
+         * place inside the camera kernel.  Hall camera pass 6.21 -> 5.74 ms (473 -> 500 Mpaths/s): the
+         * shadow kernel (61 VGPRs) runs at 8 waves per SIMD with a 16-entry LDS stack continued in
+         * global memory, against the camera kernel's 3 (profiles/r04g_vcm_shadow_short_stack.txt) */
         static const uint32_t per_px = [] {
             const char* e = getenv("ORX_VCM_DEFER");
-            return e ? (uint32_t)std::max(0, atoi(e)) : 0u;
+            return e ? (uint32_t)std::max(0, atoi(e)) : 16u;
         }();
         if (per_px) {
             const size_t cap = lpx * per_px;
@@ -1540,6 +1540,15 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
             vb.dctl = vb.work + 4; /* d_vwork: [0..1] work counters, [4..7] the deferred-entry control words */
             vb.dcap = (uint32_t)std::min<size_t>(cap, 0xfffffff0u);
             vb.rng_save = r->d_vrngsave.as<uint32_t>();
+            /* the shadow kernel's deep stack entries: (stack bound + 2 - 16) per lane of the largest grid */
+            int dev = 0, cus = 256;
+            hipGetDevice(&dev);
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            const size_t lanes = (size_t)cus * 32 * 64;
+            const size_t deep = r->scene.stack_entries + 2 > 16 ? r->scene.stack_entries + 2 - 16 : 1;
+            HIPCHK(r, r->d_vshstk.ensure(deep * lanes * 4 + 64));
+            vb.shstk = r->d_vshstk.as<uint32_t>();
+            vb.shstk_lanes = (uint32_t)lanes;
         } else {
             vb.dq0 = nullptr;
         }

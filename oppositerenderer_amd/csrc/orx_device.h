@@ -515,6 +515,27 @@ struct StackL {
     /* write entry k without moving the stack pointer (k may run two past the bound) */
     __device__ __forceinline__ void put(int k, uint32_t v) const { s[k * 64] = v; }
 };
+/* A short LDS stack continued in global memory: entries k < NL in the lane's LDS column, deeper
+ * ones at g[(k - NL) * gstride] (a per-lane column of a global array).  For kernels whose
+ * occupancy the full-depth LDS stack limits (k_vcm_shadow: 61 VGPRs, 4 waves per SIMD with
+ * 35 LDS entries, 8 with 16); each operation branches on the depth, uniformly while no lane of the
+ * wave is deeper than NL. */
+template <int NL>
+struct StackH {
+    uint32_t* s;
+    uint32_t* g;
+    uint32_t gstride;
+    __device__ __forceinline__ void push(int& sp, uint32_t v) const { put(sp++, v); }
+    __device__ __forceinline__ uint32_t pop(int& sp) const {
+        --sp;
+        if (sp < NL) return s[sp * 64];
+        return g[(size_t)(sp - NL) * gstride];
+    }
+    __device__ __forceinline__ void put(int k, uint32_t v) const {
+        if (k < NL) s[k * 64] = v;
+        else g[(size_t)(k - NL) * gstride] = v;
+    }
+};
 struct NodesG {
     __device__ __forceinline__ void test(const DevScene& S, uint32_t idx, const RayBox& rb, float tmin, float tmax,
                                          float t[4], uint32_t c[4]) const {
@@ -756,9 +777,8 @@ __device__ __forceinline__ bool trace_any(const DevScene& S, f3 o, f3 d, float t
  * (the same result, occluded or not).  RAYS supplies the lane's rays in order:
  *   bool next(f3& o, f3& d, float& tmin, float& tmax)  — false when the lane has no more;
  *   void result(bool occluded)                          — the outcome of the ray `next` gave last. */
-template <class RAYS>
-__device__ __forceinline__ void trace_any_chain(const DevScene& S, RAYS& R, uint32_t* stkp) {
-    const StackL stk{stkp};
+template <class RAYS, class STK>
+__device__ __forceinline__ void trace_any_chain_t(const DevScene& S, RAYS& R, const STK& stk) {
     f3 o = mk1(0.f), d = mk1(0.f);
     float tmin = 0.f, tmax = 0.f;
     RayBox rb = ray_box(o, mk1(1.f));
@@ -833,6 +853,10 @@ __device__ __forceinline__ void trace_any_chain(const DevScene& S, RAYS& R, uint
             have = fetch();
         }
     }
+}
+template <class RAYS>
+__device__ __forceinline__ void trace_any_chain(const DevScene& S, RAYS& R, uint32_t* stkp) {
+    trace_any_chain_t(S, R, StackL{stkp});
 }
 
 __device__ __forceinline__ uint32_t prim_material(const DevScene& S, const Hit& h) {

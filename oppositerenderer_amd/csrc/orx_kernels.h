@@ -333,6 +333,8 @@ struct VcmBufs {
     uint32_t* dctl;     /* [4] entries written, overflow flag (more entries than dcap: the pass reruns in place) */
     uint32_t dcap;
     uint32_t* rng_save; /* [6][rows*RW] the RNG planes before the camera pass (restored for the in-place rerun) */
+    uint32_t* shstk;    /* k_vcm_shadow's traversal-stack entries below its LDS part: [depth][shstk_lanes] */
+    uint32_t shstk_lanes;
     struct VcmConsts* consts; /* device copy of the pass constants (written by the launches) */
 };
 struct VcmConsts {

@@ -1218,12 +1218,15 @@ struct DeferredShadowRays {
 #ifndef ORX_VCM_SHADOW_WAVES
 #define ORX_VCM_SHADOW_WAVES 8
 #endif
+constexpr int VCM_SHADOW_LDS_STACK = 16; /* LDS entries per lane; deeper ones in vb.shstk */
 __global__ __launch_bounds__(64, ORX_VCM_SHADOW_WAVES) void k_vcm_shadow(DevScene S, VcmBufs vb) {
     if (vb.dctl[1]) return; /* out of entries: the camera pass reruns in place */
     ORX_STACK_DECL;
     const uint32_t n = min(vb.dctl[0], vb.dcap);
-    DeferredShadowRays R{vb.dq0, vb.dq1, vb.docc, blockIdx.x * 64u + threadIdx.x, n, gridDim.x * 64u, 0u};
-    trace_any_chain(S, R, ORX_STACK_PTR);
+    const uint32_t gid = blockIdx.x * 64u + threadIdx.x;
+    DeferredShadowRays R{vb.dq0, vb.dq1, vb.docc, gid, n, gridDim.x * 64u, 0u};
+    const StackH<VCM_SHADOW_LDS_STACK> stk{ORX_STACK_PTR, vb.shstk + gid, gridDim.x * 64u};
+    trace_any_chain_t(S, R, stk);
 }
 /* the colour of every own pixel's camera subpath from its deferred entries, in the order the
  * in-place pass adds them (C.color = C.color + contribution for each unoccluded connection, then the
@@ -1326,9 +1329,12 @@ void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, cons
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
         return (uint32_t)n;
     }();
-    /* as many one-wave blocks as are resident at once: the register cap, or the LDS stacks (160 KB per CU) */
-    const uint32_t per_cu = std::min<uint32_t>(4u * ORX_VCM_SHADOW_WAVES, (uint32_t)((160u << 10) / ORX_STACK_BYTES(S)));
-    hipLaunchKernelGGL(k_vcm_shadow, dim3(cus * std::max(1u, per_cu)), dim3(64), ORX_STACK_BYTES(S), s, S, vb);
+    /* as many one-wave blocks as are resident at once: the register cap, or the short LDS stacks (160 KB
+     * per CU); vb.shstk holds the deeper entries of that many lanes */
+    const size_t lds = (size_t)(VCM_SHADOW_LDS_STACK + 2) * 64 * 4;
+    const uint32_t per_cu = std::min<uint32_t>(4u * ORX_VCM_SHADOW_WAVES, (uint32_t)((160u << 10) / lds));
+    const uint32_t sblocks = std::min(cus * std::max(1u, per_cu), vb.shstk_lanes / 64u);
+    hipLaunchKernelGGL(k_vcm_shadow, dim3(sblocks), dim3(64), lds, s, S, vb);
     hipLaunchKernelGGL(k_vcm_accum, dim3((c.lcount + 255) / 256), dim3(256), 0, s, vb, c.lcount);
     hipLaunchKernelGGL(k_vcm_rng_restore, dim3((nslot + 255) / 256), dim3(256), 0, s, vb, nslot);
     launch_camera_kernel<2>(s, S, vb, blocks);

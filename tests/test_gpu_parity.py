@@ -480,12 +480,12 @@ print(json.dumps({"errs": errs, "pipelined": gpu.pipelined()}))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("defer", ["24", "0", "1"])
+@pytest.mark.parametrize("defer", ["16", "0", "1"])
 def test_vcm_camera_shadow_modes(defer):
     """The VCM camera pass's connection shadow rays (vcm.h:315-400, connectLightSourceS1 :406-488):
-    traced in place inside the camera kernel (the default, ORX_VCM_DEFER=0), deferred to k_vcm_shadow
-    with the colours summed by k_vcm_accum in the reference's order (ORX_VCM_DEFER=24: 24 entries per
-    pixel, ~6.5 rays per pixel on the hall), and
+    deferred to k_vcm_shadow with the colours summed by k_vcm_accum in the reference's order (the
+    default, ORX_VCM_DEFER=16 entries per pixel; ~6.5 rays per pixel on the hall), traced in place
+    inside the camera kernel (ORX_VCM_DEFER=0), and
     deferred into a list too small for them (1 per pixel: the pass overflows, restores the RNG planes
     and reruns in place).  Camera colours, RNG and vertex counts bit-exact against the oracle, two
     iterations back to back, and the overflow flag as expected."""
@@ -525,7 +525,7 @@ print(json.dumps({"bad": bad, "err": float(np.sqrt(((g - o) ** 2).sum() / (o ** 
     res = json.loads(out.stdout.strip().splitlines()[-1])
     assert all(v == 0 for v in res["bad"].values()), res
     assert res["err"] < 1e-5 and res["mean"] > 0, res
-    if defer == "24":
+    if defer == "16":
         assert res["rays"] > 0 and res["overflow"] == 0, res
     elif defer == "1":
         assert res["overflow"] == 1, res  # the rerun path ran
