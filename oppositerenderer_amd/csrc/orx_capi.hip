@@ -399,6 +399,7 @@ struct orx_renderer {
     DevBuf d_offsets, d_bbox, d_grid;
     DevBuf d_pos4, d_bstable, d_bspartials, d_bspairs, d_subofs;  /* bucket-sort grid build */
     DevBuf d_hcount, d_hwin;  /* stochastic hash table */
+    DevBuf d_ptrav;           /* photon pass: the deep traversal-stack entries */
     DevBuf d_hp2, d_dir2, d_sorted2, d_subofs2, d_offsets2, d_grid2; /* second buffer set (pipelining) */
     DevBuf d_kdtree2; /* kd-tree photon map: the second tree */
     DevBuf d_slots2, d_hcount2, d_hwin2; /* stochastic hash: second deposit records and table */
@@ -449,6 +450,7 @@ static orx_status set_err(orx_renderer* r, orx_status s, const std::string& m) {
     } while (0)
 
 static orx_status sync_all(orx_renderer* r);
+static orx_status photon_stack_ensure(orx_renderer* r);
 
 extern "C" {
 
@@ -886,9 +888,20 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     S.bs_r = sqrtf(e.x * e.x + e.y * e.y + e.z * e.x);
     r->vcm_estimated = false;
     r->scene_ready = true;
-    return ORX_OK;
+    return photon_stack_ensure(r);
 }
 
+/* the photon pass's deep traversal-stack entries: (stack bound + 2 - its LDS entries) per photon of
+ * the device (1.4 GB for 4096^2 photons on the conference room; touched only by paths whose stack
+ * outgrows LDS); sized again whenever a scene or a resize comes in */
+static orx_status photon_stack_ensure(orx_renderer* r) {
+    const size_t lanes = ((size_t)r->pb.prows * r->pb.PW + 63) / 64 * 64;
+    const size_t deep = r->scene.stack_entries + 2 > 16 ? r->scene.stack_entries + 2 - 16 : 1;
+    HIPCHK(r, r->d_ptrav.ensure(256 + deep * lanes * 4));
+    r->pb.tstk = r->d_ptrav.as<uint32_t>();
+    r->pb.tlanes = (uint32_t)lanes;
+    return ORX_OK;
+}
 static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     const uint32_t PW = r->cfg.photon_launch_width, PH = r->cfg.photon_launch_height;
     const bool hash = r->cfg.photon_map == 1;
@@ -1006,6 +1019,10 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
         pb.hnum = (uint32_t)hnum;
         pb.hcount = r->d_hcount.as<uint32_t>();
         pb.hwin = r->d_hwin.as<uint32_t>();
+    }
+    {
+        const orx_status st = photon_stack_ensure(r);
+        if (st != ORX_OK) return st;
     }
     if (r->cfg.photon_map == 2) {
         /* m_photonKdTreeSize = pow2roundup(NUM_PHOTONS + 1) - 1 (OptixRenderer.cpp:65-74, :207) */

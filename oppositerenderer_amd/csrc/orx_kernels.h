@@ -106,6 +106,9 @@ struct PhotonBufs {
     uint32_t hnum;      /* photonsSize = NUM_PHOTONS = PW * PH * max deposits (OptixRenderer.cpp:50) */
     uint32_t* hcount;   /* [hnum] photonsHashTableCount */
     uint32_t* hwin;     /* [hnum] slot + 1 of the photon the cell keeps (0: empty) */
+    /* the photon pass's traversal-stack entries below the LDS part, [depth][tlanes] (a column per photon) */
+    uint32_t* tstk;
+    uint32_t tlanes;
 };
 
 /* kd-tree photon map (orx_config.photon_map = 2, orx_kdtree.hip): the implicit

@@ -137,13 +137,9 @@ void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, cons
 /* ------------------------------------------------------------------ */
 /* PPM photon pass (+ AABB of the valid deposits)                      */
 /* ------------------------------------------------------------------ */
-/* Photon pass as persistent threads (PhotonGenerator.cu:83-128 + the photon
- * closest-hit programs).  Each lane carries one photon path; a lane whose
- * path ends takes the next photon index from a device counter (one atomic
- * per wave for all the lanes that need work), so the lanes of a wave stay
- * busy however unequal the path lengths are.  Photon p = j*PW + x always
- * uses RNG slot (j, x) and deposit slots [p*D, p*D + D), so the result does
- * not depend on which lane traced it. */
+/* Photon pass (PhotonGenerator.cu:83-128 + the photon closest-hit programs).  Each lane carries
+ * one photon path.  Photon p = j*PW + x always uses RNG slot (j, x) and deposit slots
+ * [p*D, p*D + D), so the result does not depend on which lane traced it. */
 struct PhotonPath {
     f3 o, d, power;
     float weight, tmin;
@@ -393,15 +389,26 @@ __device__ __forceinline__ void photon_bbox_flush(const PhotonBufs& pb, float lo
     }
 }
 
-/* one photon per lane: block b traces photons [64b, 64b + 64) (per-lane refill from a device
- * counter, a wavefront pass with per-bounce queues and a direction-binned photon order were
- * measured slower on the hall: DESIGN.md section 4) */
+/* One photon per lane: block b traces photons [64b, 64b + 64).  The kernel is register-capped at
+ * ORX_PHOTON_WAVES waves per SIMD (6: 80 VGPRs and 13 spilled; uncapped it took 121 and ran at 4;
+ * hall frame 6.43 ms at 4 waves, 6.33 at 5, 6.19 at 6, 7 no better) and its traversal stack is PHOTON_LDS_STACK entries per lane in LDS continued in global memory
+ * (StackH, one column per photon): the whole stack in LDS (35 entries on the hall, 9.5 KB per wave)
+ * would hold a CU to 16 waves.  (Persistent waves on a work counter spilled at 5 waves and ran
+ * slower; per-lane refill from a device counter, a wavefront pass with
+ * per-bounce queues and a direction-binned photon order were measured slower on the hall: DESIGN.md
+ * section 4.) */
+#ifndef ORX_PHOTON_WAVES
+#define ORX_PHOTON_WAVES 6
+#endif
+constexpr int PHOTON_LDS_STACK = 16;
 template <bool MEDIA>
-__global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, PhotonBufs pb, Consts c, MediaBufs mb) {
+__global__ __launch_bounds__(64, ORX_PHOTON_WAVES) void k_ppm_photon(DevScene S, PixelBufs px, PhotonBufs pb, Consts c,
+                                                                     MediaBufs mb) {
     ORX_STACK_DECL;
-    const StackL stk{ORX_STACK_PTR};
     const uint32_t lane = threadIdx.x;
     const uint32_t total = pb.prows * pb.PW;
+    const uint32_t p = blockIdx.x * 64u + lane;
+    const StackH<PHOTON_LDS_STACK> stk{ORX_STACK_PTR, pb.tstk + p, gridDim.x * 64u};
     float lo_x = INFINITY, lo_y = INFINITY, lo_z = INFINITY;
     float hi_x = -INFINITY, hi_y = -INFINITY, hi_z = -INFINITY;
     PhotonPath P;
@@ -411,7 +418,6 @@ __global__ __launch_bounds__(64) void k_ppm_photon(DevScene S, PixelBufs px, Pho
     M.pdepth = M.nev = 0;
     M.spos = M.ev_pos = M.ev_pow = mk1(0.f);
     Rng rs;
-    const uint32_t p = blockIdx.x * 64u + lane;
     bool alive = p < total;
     if (alive) photon_emit(S, px, pb, p, P, rs);
     while (__ballot(alive)) {
@@ -426,12 +432,16 @@ void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, co
                        const MediaBufs* mb) {
     const uint32_t total = pb.prows * pb.PW;
     if (total == 0) return;
+    const uint32_t blocks = (total + 63) / 64;
+    if ((size_t)blocks * 64 > pb.tlanes) { /* the host sizes tstk for every photon (photon_stack_ensure) */
+        fprintf(stderr, "orx: photon pass of %u photons exceeds its stack buffer (%u lanes)\n", total, pb.tlanes);
+        abort();
+    }
+    const size_t lds = (size_t)PHOTON_LDS_STACK * 64 * 4;
     if (mb)
-        hipLaunchKernelGGL((k_ppm_photon<true>), dim3((total + 63) / 64), dim3(64), ORX_STACK_BYTES(S), s, S, px, pb, c,
-                           *mb);
+        hipLaunchKernelGGL((k_ppm_photon<true>), dim3(blocks), dim3(64), lds, s, S, px, pb, c, *mb);
     else
-        hipLaunchKernelGGL((k_ppm_photon<false>), dim3((total + 63) / 64), dim3(64), ORX_STACK_BYTES(S), s, S, px, pb,
-                           c, MediaBufs{});
+        hipLaunchKernelGGL((k_ppm_photon<false>), dim3(blocks), dim3(64), lds, s, S, px, pb, c, MediaBufs{});
 }
 
 /* ------------------------------------------------------------------ */
