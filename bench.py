@@ -19,9 +19,11 @@ Single GPU:  python bench.py [--config C] [--steps K --warmup W]
 Multi GPU:   python bench.py --gpus N   (bench.py starts N rank processes itself, one per GPU,
              RCCL over xGMI), or under a launcher that sets WORLD_SIZE/RANK/LOCAL_RANK
              (torchrun --nproc-per-node N bench.py --gpus N).
-             Default --scaling strong: the workload is fixed (its photon launch rows and
-             pixel rows are dealt round-robin to the ranks); --scaling weak gives every
-             rank a full photon launch.  See DESIGN.md "Multi-GPU".
+             Default --partition batch (the reference's distributed mode): every
+             rank renders its own whole iterations of the workload and the accumulated
+             radiance is reduced over RCCL (weak scaling).  --partition rows: one frame split
+             by rows over the ranks (strong scaling; --scaling weak gives every rank a full
+             photon launch).  See DESIGN.md "Multi-GPU".
 """
 import argparse
 import json
@@ -67,11 +69,17 @@ def parse(argv=None):
     p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                    help="multi-GPU PPM: strong = fixed global photon launch split by rows over the ranks "
                         "(the default); weak = a full photon launch per rank")
-    p.add_argument("--partition", choices=["slab", "rows"], default="rows",
-                   help="multi-GPU PPM gather: rows = every rank gathers all hit points against its own photons "
-                        "(the default: per-rank hall frame at N=8 1.43 ms against 2.92 ms for slab, "
-                        "tools/shard_model.py); slab = each rank gathers the hit points that reach the photons "
-                        "of its spatial slab (all-to-all of the photons; on par with rows at 4K)")
+    p.add_argument("--partition", choices=["batch", "rows", "slab"], default="batch",
+                   help="multi-GPU: batch = photon-batch (iteration) partition, the reference's distributed mode "
+                        "and the default: every rank renders its own whole iterations (global iteration numbers "
+                        "dealt round-robin, its own RNG streams) and the accumulated radiance is summed by an RCCL "
+                        "reduce every --reduce-every iterations (weak scaling); rows = one frame split by "
+                        "row-interleaved RNG/pixel/photon ownership, every rank gathers all hit points against "
+                        "its own photons (strong scaling, equal to one device up to fp32 order; per-rank hall "
+                        "frame at N=8 1.43 ms, tools/shard_model.py); slab = rows with the gather partitioned "
+                        "by spatial photon slabs (all-to-all of the photons; PPM only)")
+    p.add_argument("--reduce-every", type=int, default=8,
+                   help="photon-batch partition: local iterations between two reduces of the radiance buffers")
     p.add_argument("--force-sharded", action="store_true",
                    help="run the torch.distributed/RCCL sharded path even with one rank (tests the N>1 code)")
     p.add_argument("--no-serial-pass-times", action="store_true",
@@ -398,7 +406,9 @@ def main():
             "no assets or checkpoints")
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mpaths/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "strong",
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        # one GPU: the per-GPU work of the default multi-GPU partition (batch: whole iterations per GPU)
+        "scaling": "weak" if args.partition == "batch" else "strong",
         "vs_baseline": None, "dtype": "f32", "data": data,
         "config": {"workload": f"{scene.name} {W}x{H} {_METHOD_NAME[method]}"
                                + (f", {P * P} photons/iter" if method == 2 else ""),

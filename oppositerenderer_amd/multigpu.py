@@ -144,6 +144,72 @@ def assemble_rows(blocks, W, H, world):
     return img
 
 
+def batch_seed(seed, rank):
+    """Rank g's RNG seed in the photon-batch partition.  Rank 0 keeps the configured seed, so a
+    one-rank job renders exactly the single-device sequence; the others get their own XORWOW
+    streams, as the reference's render servers each seed from their own clock
+    (OptixRenderer_SpatialHash.cu:319-334).  0 (seed from the clock) stays 0 on every rank."""
+    if seed == 0 or rank == 0:
+        return seed
+    return ((seed + 0x9E3779B9 * rank) & 0xFFFFFFFF) or 1
+
+
+def batch_iteration(i, rank, world):
+    """Global iteration number of rank's i-th local iteration: the reference's client deals
+    consecutive iteration numbers round-robin to its render servers (DistributedApplication.cpp:96-122)."""
+    return i * world + rank
+
+
+def radius_sequence(r0, n, alpha=2.0 / 3.0):
+    """PPM radii of global iterations 0..n-1 (the client's host-computed sequence, StandaloneRenderManager.cpp:105-107)."""
+    from .renderer import next_ppm_radius
+
+    out = [float(r0)]
+    for k in range(n - 1):
+        out.append(next_ppm_radius(out[-1], k, alpha))
+    return out
+
+
+class BatchSharded:
+    """Photon-batch partition, the reference's own multi-GPU mode: its client deals consecutive
+    iteration numbers with the host-computed radius sequence to the render servers
+    (DistributedApplication.cpp:96-122) and merges their running-sum buffers
+    (RenderResultPacketReceiver.cpp:63-190).  Rank g renders global iterations g, g + N, g + 2N, ...
+    of the whole frame with a full photon launch and its own RNG streams (batch_seed) on the
+    single-device path (pipelined PPM, VCM, PT), so an iteration needs no exchange at all; the
+    accumulated radiance buffers are summed by one reduce to rank 0 (RCCL over xGMI) every
+    `reduce_every` local iterations and on image().  The merged buffer is the sum of the ranks'
+    running sums: divide by the total iteration count to display, as for one device.
+
+    Backends expose render_next / output_local_tensor(rows)."""
+
+    def __init__(self, backend, dist, world, rank, W, H, reduce_every=8):
+        self.b, self.dist, self.world, self.rank, self.W, self.H = backend, dist, world, rank, W, H
+        self.reduce_every = int(reduce_every)
+        self.n = 0
+        self.merged = None
+
+    def iteration(self, it, local_it, radius, request):
+        """`it` is the global iteration number (batch_iteration), `local_it` the rank's own count."""
+        self.b.render_next(it, local_it, radius, request)
+        self.n += 1
+        if self.reduce_every > 0 and self.n % self.reduce_every == 0:
+            self.reduce()
+
+    def reduce(self):
+        """Sum of every rank's running-sum radiance buffer, on rank 0 (collective)."""
+        t = self.b.output_local_tensor(self.H)
+        self.dist.reduce(t, dst=0)
+        self.merged = t
+
+    def image(self):
+        """The merged running sum on rank 0 (None elsewhere; collective)."""
+        self.reduce()
+        if self.rank != 0:
+            return None
+        return self.merged.detach().cpu().numpy().reshape(self.H, self.W, 3).copy()
+
+
 class ShardedPPM:
     """Runs the 5-step sharded iteration for any backend exposing
     local_passes / export_hitpoints / gather_external / finish / alloc."""
@@ -458,6 +524,49 @@ class DeviceShard:
         return t
 
 
+class DeviceBatch:
+    """liborx.so backend of the photon-batch partition: a whole-frame renderer on its own streams
+    (the single-device pipelined path); the radiance buffer is copied out on the renderer's stream
+    and handed to torch's stream for the collective."""
+
+    def __init__(self, renderer, torch, device):
+        self.r, self.torch, self.device = renderer, torch, device
+        self.ext = None
+
+    def render_next(self, it, local_it, radius, request):
+        self.r._check(self.r._lib.orx_render_next_iteration(self.r._h, it, local_it, radius, 1, C.byref(request)))
+
+    def alloc(self, nfloat):
+        return self.torch.zeros(nfloat, dtype=self.torch.float32, device=self.device)
+
+    def output_local_tensor(self, rows):
+        torch = self.torch
+        if self.ext is None:
+            self.ext = torch.cuda.ExternalStream(self.r.stream_handle(), device=self.device)
+        cur = torch.cuda.current_stream(self.device)
+        t = torch.empty(rows * self.r.getWidth() * 3, dtype=torch.float32, device=self.device)
+        self.ext.wait_stream(cur)  # t's block may have been read by the last collective on cur
+        self.r.getOutputBufferDevice(t.data_ptr(), t.numel() * 4)  # after the pipelined output pass
+        cur.wait_stream(self.ext)
+        return t
+
+
+def device_batch_factory(cfg, rank, world, local_rank, scene):
+    """The photon-batch backend on HIP device `local_rank`: rank's seed (batch_seed), whole frame,
+    full photon launch (raises without a GPU or without liborx.so; no CPU fallback)."""
+    import torch
+
+    from .renderer import OptixRenderer
+
+    torch.cuda.set_device(local_rank)
+    c = type(cfg).from_buffer_copy(cfg)
+    c.seed = batch_seed(cfg.seed, rank)
+    r = OptixRenderer(c)
+    r.initialize(local_rank)
+    r.initScene(scene)
+    return DeviceBatch(r, torch, torch.device("cuda", local_rank))
+
+
 def device_shard_factory(cfg, rank, world, local_rank, scene):
     """The product backend of the multi-GPU bench: liborx.so on HIP device `local_rank`
     (raises without a GPU or without liborx.so; there is no CPU fallback)."""
@@ -473,16 +582,20 @@ def device_shard_factory(cfg, rank, world, local_rank, scene):
     return DeviceShard(r, torch, torch.device("cuda", local_rank), (rank, world))
 
 
-def _resolve_factory():
-    """ORX_SHARD_BACKEND=module:function swaps the shard backend; only the CPU launcher test
-    (tests/test_bench_launch.py) sets it, to run the orchestration under gloo on the oracle."""
-    spec = os.environ.get("ORX_SHARD_BACKEND")
+def _resolve_factory(batch=False):
+    """ORX_SHARD_BACKEND=module:function swaps the shard backend (ORX_BATCH_BACKEND for the
+    photon-batch partition); only the CPU launcher test (tests/test_bench_launch.py) sets them, to
+    run the orchestration under gloo on the oracle."""
+    spec = os.environ.get("ORX_BATCH_BACKEND" if batch else "ORX_SHARD_BACKEND")
     if not spec:
-        return device_shard_factory, "hip"
+        return (device_batch_factory if batch else device_shard_factory), "hip"
     import importlib
 
     mod, fn = spec.split(":")
     return getattr(importlib.import_module(mod), fn), spec
+
+
+_METHOD = {0: "PT", 1: "VCM", 2: "PPM"}  # orx_method (include/orx.h)
 
 
 def bench_main(args, metric, cpu_baseline=None):
@@ -495,7 +608,7 @@ def bench_main(args, metric, cpu_baseline=None):
     import torch.distributed as dist
 
     from . import _abi, scenes
-    from .renderer import RenderRequestDetails, next_ppm_radius
+    from .renderer import RenderRequestDetails
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -504,8 +617,10 @@ def bench_main(args, metric, cpu_baseline=None):
         raise SystemExit("the sharded bench runs ppm, vcm or pt")
     vcm = method == "vcm"
     pt = method == "pt"
+    partition = getattr(args, "partition", "batch")
+    batch = partition == "batch"
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    factory, backend_name = _resolve_factory()
+    factory, backend_name = _resolve_factory(batch)
     on_gpu = backend_name == "hip"
     # RCCL prints its version banner on fd 1: keep stdout for the one JSON line
     json_out = os.fdopen(os.dup(1), "w")
@@ -522,8 +637,8 @@ def bench_main(args, metric, cpu_baseline=None):
 
     W, H, P = args.width, args.height, args.photon_launch
     scene = scenes.scene_by_name(args.scene)
-    weak = getattr(args, "scaling", "strong") == "weak"
-    PH = P * world if weak else P  # global photon launch height
+    weak = getattr(args, "scaling", "strong") == "weak" and not batch
+    PH = P * world if weak else P  # global photon launch height (batch: every rank's own launch)
     cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=PH,
                               gather_variant=args.gather_variant)
     backend = factory(cfg, rank, world, local_rank, scene)
@@ -533,18 +648,26 @@ def bench_main(args, metric, cpu_baseline=None):
              else _abi.PROGRESSIVE_PHOTON_MAPPING)
     det = RenderRequestDetails(cam, scene.name, mcode, W, H)
     req = det.to_abi()
-    radius = scene.initial_ppm_radius()
-    if vcm or pt:
+    n_total = max(1, args.warmup) + args.steps
+    radii = radius_sequence(scene.initial_ppm_radius(), n_total * (world if batch else 1))
+    if batch:
+        sharded = BatchSharded(backend, dist, world, rank, W, H, reduce_every=getattr(args, "reduce_every", 8))
+    elif vcm or pt:
         sharded = (ShardedVCM if vcm else ShardedPT)(backend, dist, world, rank, W, H)
     else:
-        slab = getattr(args, "partition", "rows") == "slab" and world > 1
+        slab = partition == "slab" and world > 1
         sharded = ShardedPPM(backend, dist, world, rank, W, H, pipeline=os.environ.get("ORX_PIPELINE", "1") != "0",
                              slab=slab)
-    it = 0
+
+    def step(i):
+        """local iteration i: the rank's global iteration number (batch: dealt round-robin) and its radius"""
+        it = batch_iteration(i, rank, world) if batch else i
+        sharded.iteration(it, i, radii[it], req)
+
+    i = 0
     for _ in range(max(1, args.warmup)):
-        sharded.iteration(it, it, radius, req)
-        radius = next_ppm_radius(radius, it)
-        it += 1
+        step(i)
+        i += 1
     sync()
     dist.barrier()
     if hasattr(r, "reset_timing"):
@@ -553,9 +676,10 @@ def bench_main(args, metric, cpu_baseline=None):
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        sharded.iteration(it, it, radius, req)
-        radius = next_ppm_radius(radius, it)
-        it += 1
+        step(i)
+        i += 1
+    if batch and sharded.reduce_every > 0 and sharded.n % sharded.reduce_every:
+        sharded.reduce()  # the timed job ends with its radiance merged on rank 0
     sync()
     dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -569,16 +693,23 @@ def bench_main(args, metric, cpu_baseline=None):
         # PPM: the global launch P x PH (PH = P strong, P * world weak); VCM: the W*H light +
         # W*H camera subpaths are split over the ranks (strong scaling)
         paths = 2 * W * H if vcm else W * H if pt else W * H + P * PH
+        if batch:  # every rank renders whole iterations: W*H eye (+ W*H light) paths and P x P photons each
+            paths *= world
         n_it = max(1, st.timed_iterations)
         per_pass = {name: st.pass_ms[i] / n_it for i, name in enumerate(_abi.PASS_NAMES)}
         per_pass = {k: v for k, v in per_pass.items() if v > 0}
         # pipelined PPM: gather and output overlap the next iteration (side stream)
-        overlapped = ["ppm_gather", "ppm_direct_output"] if getattr(sharded, "pipe", False) else []
+        overlapped = (["ppm_gather", "ppm_direct_output"]
+                      if getattr(sharded, "pipe", False) or (batch and getattr(r, "pipelined", lambda: False)()) else [])
         critical = {k: v for k, v in per_pass.items() if k not in overlapped} or per_pass
         dominant = max(critical, key=critical.get) if critical else None
         valid_avg = st.valid_photons_total / n_it
-        rows0 = local_rows(H, 0, world)
-        if pt:
+        rows0 = H if batch else local_rows(H, 0, world)
+        if batch:  # rank 0's passes are the single-device passes
+            pb = roofline.pass_bytes(mcode, W, H, P * P, valid_avg, st.num_cells,
+                                     **({"light_vertices": int(np.minimum(r.read_buffer(
+                                         _abi.BUF_VCM_VERTEX_COUNT, np.uint32), 9).sum())} if vcm else {}))
+        elif pt:
             pb = roofline.pass_bytes(mcode, W, rows0, 0)
         elif vcm:  # rank 0 traces its own rows' subpaths; light vertices counted in the stats
             lv = int(np.minimum(r.read_buffer(_abi.BUF_VCM_VERTEX_COUNT, np.uint32), 9).sum())
@@ -593,10 +724,22 @@ def bench_main(args, metric, cpu_baseline=None):
             "metric": metric, "value": round(paths * args.steps / t_max / 1e6, 3), "unit": "Mpaths/s",
             "n_gpus": world_size, "world_size": world_size, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t_max * 1e3 / args.steps, 4), "higher_is_better": True,
-            "scaling": "weak" if (weak and not (vcm or pt)) else "strong",
+            "scaling": "weak" if (batch or (weak and not (vcm or pt))) else "strong",
             "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic: seeded procedural scene ({scene.name}), XORWOW streams seeded 1645301512",
-            "config": ({"workload": f"{scene.name} {W}x{H} PT, 1 spp/iter (strong scaling)",
+            "config": ({"workload": (f"{scene.name} {W}x{H} {_METHOD[mcode]}"
+                                     + (f", {P * P:,} photons/iter" if not (vcm or pt) else "")
+                                     + f" per GPU, photon-batch partition: each of {world} GPUs renders its own "
+                                       "iterations (weak scaling)"),
+                        "baseline_config": getattr(args, "config", None),
+                        "scene": scene.name, "width": W, "height": H, "method": _METHOD[mcode],
+                        "photons_per_iteration": 0 if (vcm or pt) else P * P,
+                        "paths_per_iteration": paths,
+                        "parallelism": f"photon-batch (iteration) partition x{world}: global iterations dealt "
+                                       f"round-robin, per-rank RNG streams, RCCL reduce of the accumulated radiance "
+                                       f"every {sharded.reduce_every} iterations and at the end"}
+                       if batch else
+                       {"workload": f"{scene.name} {W}x{H} PT, 1 spp/iter (strong scaling)",
                         "scene": scene.name, "width": W, "height": H, "method": "PT",
                         "paths_per_iteration": paths,
                         "parallelism": f"row-interleaved RNG/pixel ownership x{world}, no per-iteration exchange"}

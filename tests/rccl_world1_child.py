@@ -13,7 +13,12 @@ and compares each variant's image with the CPU oracle's single renderer:
   ppm_slab_serial
   vcm                 reduce_scatter_tensor of the light-tracing splats (ShardedVCM)
   pt                  no per-iteration exchange (ShardedPT), bit-exact
-Every variant ends with ShardedPPM.image()'s all_gather.  Prints one JSON line.
+  {ppm,vcm,pt}_batch  the photon-batch partition (bench.py's default multi-GPU mode, BatchSharded over
+                      multigpu.device_batch_factory): the single-device path, reduce of the radiance
+  ppm_batch2_emulated two photon-batch ranks' renderers on the one GPU (seeds batch_seed(SEED, 0/1),
+                      global iterations dealt round-robin), their radiance summed, against the oracle's
+                      two renderers
+Every rows/slab variant ends with ShardedPPM.image()'s all_gather.  Prints one JSON line.
 
 The rendezvous is a FileStore (argv[1]): no TCP port to race for."""
 import json
@@ -42,16 +47,22 @@ def rel_l2(a, b):
     return float(np.sqrt(((a - b) ** 2).sum()) / max(np.sqrt((b * b).sum()), 1e-30))
 
 
-def oracle_image(scene, method, req):
-    ora = oracle_lib.OracleRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P))
-    ora.init_scene(scene)
-    radius = scene.initial_ppm_radius()
-    for it in range(ITERS):
-        ora.render_next_iteration(it, it, radius, req)
-        radius = next_ppm_radius(radius, it)
-    out = ora.output().copy()
-    ora.close()
-    return out
+def oracle_image(scene, method, req, world=1):
+    """world > 1: the photon-batch partition's sum of `world` renderers (multigpu.batch_seed, global
+    iterations g, g + world, ...)"""
+    radii = multigpu.radius_sequence(scene.initial_ppm_radius(), ITERS * world)
+    out = None
+    for g in range(world):
+        cfg = _abi.default_config(seed=multigpu.batch_seed(SEED, g), photon_launch_width=P, photon_launch_height=P)
+        ora = oracle_lib.OracleRenderer(cfg)
+        ora.init_scene(scene)
+        for i in range(ITERS):
+            it = multigpu.batch_iteration(i, g, world)
+            ora.render_next_iteration(it, i, radii[it], req)
+        o = ora.output().astype(np.float64)
+        out = o if out is None else out + o
+        ora.close()
+    return out.astype(np.float32) if world == 1 else out
 
 
 def main():
@@ -96,6 +107,47 @@ def main():
         backend.r.destroy()
         torch.cuda.synchronize()
         print(name, entry, file=sys.stderr, flush=True)
+    for name, method in (("ppm_batch", "ppm"), ("vcm_batch", "vcm"), ("pt_batch", "pt")):
+        mcode = {"ppm": _abi.PROGRESSIVE_PHOTON_MAPPING, "vcm": _abi.VCM_BIDIRECTIONAL_PATH_TRACING,
+                 "pt": _abi.PATH_TRACING}[method]
+        req = RenderRequestDetails(cam, scene.name, mcode, W, H).to_abi()
+        cfg = _abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P)
+        backend = multigpu.device_batch_factory(cfg, 0, 1, 0, scene)
+        sh = multigpu.BatchSharded(backend, dist, 1, 0, W, H, reduce_every=2)
+        radii = multigpu.radius_sequence(scene.initial_ppm_radius(), ITERS)
+        for i in range(ITERS):
+            sh.iteration(multigpu.batch_iteration(i, 0, 1), i, radii[i], req)
+        pipelined = bool(backend.r.pipelined())
+        img = sh.image()
+        ref = refs[method]
+        entry = {"rel_l2": rel_l2(img, ref), "mean": float(img.mean()), "pipelined": pipelined,
+                 "expect_pipelined": method == "ppm",
+                 "bit_exact": bool(np.array_equal(img.view(np.uint32), ref.view(np.uint32)))}
+        res["variants"][name] = entry
+        backend.r.destroy()
+        torch.cuda.synchronize()
+        print(name, entry, file=sys.stderr, flush=True)
+    # two photon-batch ranks emulated on the one GPU (the collective is the sum below)
+    mcode = _abi.PROGRESSIVE_PHOTON_MAPPING
+    req = RenderRequestDetails(cam, scene.name, mcode, W, H).to_abi()
+    cfg = _abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P)
+    radii = multigpu.radius_sequence(scene.initial_ppm_radius(), ITERS * 2)
+    acc = None
+    for g in range(2):
+        backend = multigpu.device_batch_factory(cfg, g, 2, 0, scene)
+        for i in range(ITERS):
+            it = multigpu.batch_iteration(i, g, 2)
+            backend.render_next(it, i, radii[it], req)
+        t = backend.output_local_tensor(H)
+        torch.cuda.synchronize()
+        o = t.cpu().numpy().astype(np.float64).reshape(H, W, 3)
+        acc = o if acc is None else acc + o
+        backend.r.destroy()
+    ref2 = oracle_image(scene, mcode, req, world=2)
+    entry = {"rel_l2": rel_l2(acc, ref2), "mean": float(acc.mean()),
+             "rank_images_differ": bool(rel_l2(acc, 2 * refs["ppm"]) > 1e-3)}
+    res["variants"]["ppm_batch2_emulated"] = entry
+    print("ppm_batch2_emulated", entry, file=sys.stderr, flush=True)
     dist.barrier()
     dist.destroy_process_group()
     print(json.dumps(res), flush=True)

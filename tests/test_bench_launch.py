@@ -10,24 +10,41 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_bench_gpus2_self_launch_prints_one_json_line():
+def _launch(extra):
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     env["ORX_SHARD_BACKEND"] = "shard_backends:oracle_shard"
+    env["ORX_BATCH_BACKEND"] = "shard_backends:oracle_batch"
     env["PYTHONPATH"] = os.pathsep.join([os.path.join(ROOT, "tests"), ROOT, env.get("PYTHONPATH", "")])
     env["OMP_NUM_THREADS"] = "2"
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
-           "--scene", "Cornell", "--width", "48", "--height", "40", "--photon-launch", "32", "--no-cpu-baseline"]
+           "--scene", "Cornell", "--width", "48", "--height", "40", "--photon-launch", "32",
+           "--no-cpu-baseline"] + extra
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, p.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["world_size"] == 2
+    assert "launcher test" in out["backend"]
+    return out
+
+
+def test_bench_gpus2_self_launch_prints_one_json_line():
+    """the default multi-GPU partition: photon batches (every rank its own whole iterations)"""
+    out = _launch([])
+    assert out["value"] > 0 and out["steps"] == 2 and out["scaling"] == "weak"
+    assert out["config"]["photons_per_iteration"] == 32 * 32
+    assert out["config"]["paths_per_iteration"] == 2 * (48 * 40 + 32 * 32)
+    assert "photon-batch" in out["config"]["parallelism"]
+
+
+def test_bench_gpus2_rows_partition():
+    out = _launch(["--partition", "rows"])
     assert out["value"] > 0 and out["steps"] == 2 and out["scaling"] == "strong"
     assert out["config"]["photons_per_iteration"] == 32 * 32
-    assert "launcher test" in out["backend"]
+    assert out["config"]["paths_per_iteration"] == 48 * 40 + 32 * 32
 
 
 def test_bench_rank_failure_ends_the_launch():

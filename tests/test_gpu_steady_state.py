@@ -119,3 +119,6 @@ def test_rccl_world1_sharded_paths_match_oracle(tmp_path):
         assert r["mean"] > 0, (name, r)
         if r.get("expect_pipelined"):
             assert r["pipelined"], (name, r)
+    assert {"ppm_batch", "vcm_batch", "pt_batch", "ppm_batch2_emulated"} <= set(res["variants"]), res
+    assert res["variants"]["pt_batch"]["bit_exact"], res["variants"]["pt_batch"]
+    assert res["variants"]["ppm_batch2_emulated"]["rank_images_differ"], res["variants"]["ppm_batch2_emulated"]

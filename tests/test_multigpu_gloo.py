@@ -221,3 +221,69 @@ def test_assemble_rows_roundtrip():
         b[:len(rows)] = rows
         blocks.append(b)
     assert np.array_equal(multigpu.assemble_rows(blocks, W, H, world), img)
+
+
+def batch_worker(rank, world, port, out_path, W, H, P, iters, method, reduce_every):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import shard_backends
+
+    scene = scenes.cornell()
+    cfg = _abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P)
+    b = shard_backends.oracle_batch(cfg, rank, world, rank, scene)
+    sh = multigpu.BatchSharded(b, dist, world, rank, W, H, reduce_every=reduce_every)
+    req = request(scene, W, H, method)
+    radii = multigpu.radius_sequence(scene.initial_ppm_radius(), iters * world)
+    for i in range(iters):
+        it = multigpu.batch_iteration(i, rank, world)
+        sh.iteration(it, i, radii[it], req)
+    img = sh.image()
+    if rank == 0:
+        np.save(out_path, img)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,method,reduce_every", [(2, _abi.PROGRESSIVE_PHOTON_MAPPING, 1),
+                                                       (3, _abi.PROGRESSIVE_PHOTON_MAPPING, 2),
+                                                       (2, _abi.VCM_BIDIRECTIONAL_PATH_TRACING, 0),
+                                                       (2, _abi.PATH_TRACING, 1)])
+def test_batch_partition_is_the_sum_of_independent_renderers(world, method, reduce_every):
+    """Photon-batch partition (the bench's default multi-GPU mode, the reference's client/server
+    iteration dealing): the reduced radiance equals the sum of `world` independent renderers, rank
+    g seeded batch_seed(SEED, g) rendering global iterations g, g + N, ... with the global radius
+    sequence; rank 0 alone is the single-device run's seed."""
+    W, H, P, iters = 40, 32, 24, 3
+    out = os.path.join(tempfile.mkdtemp(), "img.npy")
+    mp.spawn(batch_worker, args=(world, free_port(), out, W, H, P, iters, method, reduce_every), nprocs=world,
+             join=True)
+    got = np.load(out)
+    scene = scenes.cornell()
+    radii = multigpu.radius_sequence(scene.initial_ppm_radius(), iters * world)
+    ref = np.zeros((H, W, 3), np.float64)
+    for g in range(world):
+        cfg = _abi.default_config(seed=multigpu.batch_seed(SEED, g), photon_launch_width=P, photon_launch_height=P)
+        r = oracle_lib.OracleRenderer(cfg)
+        r.init_scene(scene)
+        req = request(scene, W, H, method)
+        for i in range(iters):
+            it = multigpu.batch_iteration(i, g, world)
+            r.render_next_iteration(it, i, radii[it], req)
+        ref += r.output().astype(np.float64)
+    err = np.sqrt(((got.astype(np.float64) - ref) ** 2).sum() / (ref ** 2).sum())
+    assert err < 1e-6, err
+    assert got.mean() > 0
+
+
+def test_batch_seeds_and_iterations():
+    assert multigpu.batch_seed(SEED, 0) == SEED
+    seeds = {multigpu.batch_seed(SEED, g) for g in range(64)}
+    assert len(seeds) == 64 and 0 not in seeds
+    assert multigpu.batch_seed(0, 5) == 0  # clock-seeded renderers stay clock-seeded
+    assert sorted(multigpu.batch_iteration(i, g, 4) for i in range(3) for g in range(4)) == list(range(12))
+    r = multigpu.radius_sequence(1.0, 5)
+    x = 1.0
+    for k in range(4):
+        x = next_ppm_radius(x, k)
+        assert r[k + 1] == x
