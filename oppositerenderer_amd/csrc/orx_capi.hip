@@ -2145,7 +2145,10 @@ orx_status orx_get_output_device(orx_renderer* r, void* dst, size_t bytes) {
     if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "destination too small");
     if (!r->d_out.p) return set_err(r, ORX_ERR_STATE, "no frame rendered yet");
     HIPCHK(r, hipSetDevice(r->device));
-    flush_pipeline(r);
+    /* after the last pipelined output pass; the pipeline itself stays unbroken (the copy only
+     * reads the running sum, which the next output pass, on the gather stream after the grid
+     * build that follows this copy on the main stream, writes) */
+    if (r->pend) HIPCHK(r, hipStreamWaitEvent(cur_stream(r), r->ev_gdone[r->pp], 0));
     HIPCHK(r, hipMemcpyAsync(dst, r->d_out.p, need, hipMemcpyDeviceToDevice, cur_stream(r)));
     return ORX_OK;
 }

@@ -625,8 +625,19 @@ def bench_main(args, metric, cpu_baseline=None):
     # RCCL prints its version banner on fd 1: keep stdout for the one JSON line
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+    W, H, P = args.width, args.height, args.photon_launch
+    scene = scenes.scene_by_name(args.scene)
+    weak = getattr(args, "scaling", "strong") == "weak" and not batch
+    PH = P * world if weak else P  # global photon launch height (batch: every rank's own launch)
+    cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=PH,
+                              gather_variant=args.gather_variant)
+    # the renderer (and its streams) before the process group: RCCL's streams then take the
+    # hardware queues after the renderer's three
     if on_gpu:
         torch.cuda.set_device(local_rank)
+    backend = factory(cfg, rank, world, local_rank, scene)
+    r = backend.r
+    if on_gpu:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         dist.init_process_group("gloo")
@@ -635,14 +646,6 @@ def bench_main(args, metric, cpu_baseline=None):
         if on_gpu:
             torch.cuda.synchronize()
 
-    W, H, P = args.width, args.height, args.photon_launch
-    scene = scenes.scene_by_name(args.scene)
-    weak = getattr(args, "scaling", "strong") == "weak" and not batch
-    PH = P * world if weak else P  # global photon launch height (batch: every rank's own launch)
-    cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=PH,
-                              gather_variant=args.gather_variant)
-    backend = factory(cfg, rank, world, local_rank, scene)
-    r = backend.r
     cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
     mcode = (_abi.VCM_BIDIRECTIONAL_PATH_TRACING if vcm else _abi.PATH_TRACING if pt
              else _abi.PROGRESSIVE_PHOTON_MAPPING)
