@@ -1,6 +1,12 @@
 """Multi-GPU progressive photon mapping: one process per GPU, torch.distributed
 (backend "nccl" = RCCL over xGMI on MI355X; "gloo" for the CPU tests).
 
+Two partitions.  The photon-batch partition (BatchSharded, bench.py's default) is the
+reference's own distributed mode: every rank renders whole iterations (global iteration
+numbers dealt round-robin, the global radius sequence, its own RNG streams) and the
+accumulated radiance buffers are summed by one reduce every few iterations.  The row
+partition (ShardedPPM / ShardedVCM / ShardedPT) splits one frame over the ranks:
+
 Sharding (option A) — rank g of N owns every RNG-slot row
 y with y % N == g, i.e. its pixel rows AND its photon-launch rows (photon
 thread (x,y) aliases RNG slot (x,y), OptixRenderer_SpatialHash.cu:310-334),
