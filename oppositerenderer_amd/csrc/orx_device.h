@@ -494,20 +494,21 @@ __device__ __forceinline__ void node_test(const DevBvh4F* nodes, uint32_t idx, c
 /* compare-exchange by entry distance; the distances by min/max (never NaN here: +inf or a
  * max with tmin), which leaves the compare's mask to the two reference selects */
 __device__ __forceinline__ void cswap(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {
-    const bool sw = tb < ta;
+    /* the distances are >= tmin >= 0 or +inf, so their bit patterns order like the values: unsigned
+     * compare and min/max (fminf/fmaxf had cost two NaN-quieting v_max_f32 per exchange) */
+    const uint32_t ua = __float_as_uint(ta), ub = __float_as_uint(tb);
+    const bool sw = ub < ua;
     const uint32_t c = sw ? cb : ca;
     cb = sw ? ca : cb;
     ca = c;
-    const float lo = fminf(ta, tb);
-    tb = fmaxf(ta, tb);
-    ta = lo;
+    ta = __uint_as_float(ua < ub ? ua : ub);
+    tb = __uint_as_float(ua < ub ? ub : ua);
 }
 
 /* Traversal policies (trace_closest_t / trace_any_t): the stack (StackL: the
- * lane's column of the dynamic-LDS array [stack_entries][64]) and the node
- * source (NodesG: S.bvh4).  Measured and dropped: a short LDS stack continued
- * in global memory (5-8 waves per SIMD) and the top 85 / 341 nodes in LDS
- * (DESIGN.md §4); neither made the photon pass faster. */
+ * lane's column of the dynamic-LDS array [stack_entries][64]; StackH below) and the
+ * node source (NodesG: S.bvh4).  Measured and dropped: the top 85 / 341 nodes in LDS
+ * (DESIGN.md §4). */
 struct StackL {
     uint32_t* s;
     __device__ __forceinline__ void push(int& sp, uint32_t v) const { s[(sp++) * 64] = v; }
@@ -516,24 +517,31 @@ struct StackL {
     __device__ __forceinline__ void put(int k, uint32_t v) const { s[k * 64] = v; }
 };
 /* A short LDS stack continued in global memory: entries k < NL in the lane's LDS column, deeper
- * ones at g[(k - NL) * gstride] (a per-lane column of a global array).  For kernels whose
- * occupancy the full-depth LDS stack limits (k_vcm_shadow: 61 VGPRs, 4 waves per SIMD with
- * 35 LDS entries, 8 with 16); each operation branches on the depth, uniformly while no lane of the
- * wave is deeper than NL. */
+ * ones in a global array [depth][gstride] at column `lane`, through buffer loads/stores (a 32-bit
+ * offset; kept apart from the LDS accesses, which the compiler would otherwise merge with them into
+ * flat loads).  The LDS column holds NL + 1 entries: a push always writes LDS, at min(k, NL) (entry
+ * NL is a dump slot), and only a push or pop past NL takes the branch to global memory, so a wave
+ * whose lanes all stay shallow runs one skipped branch per operation.  For kernels whose occupancy
+ * the full-depth LDS stack limits (k_vcm_shadow: 61 VGPRs, 4 waves per SIMD with 35 LDS entries,
+ * 8 with 16; k_ppm_photon). */
 template <int NL>
 struct StackH {
     uint32_t* s;
-    uint32_t* g;
-    uint32_t gstride;
+    __amdgpu_buffer_rsrc_t g;
+    uint32_t lane, gstride;
+    static constexpr size_t lds_bytes() { return (size_t)(NL + 1) * 64 * 4; }
+    __device__ __forceinline__ StackH(uint32_t* s_, uint32_t* g_, uint32_t lane_, uint32_t gstride_)
+        : s(s_), g(__builtin_amdgcn_make_buffer_rsrc(g_, 0, 0xffffffff, 0x00020000)), lane(lane_), gstride(gstride_) {}
     __device__ __forceinline__ void push(int& sp, uint32_t v) const { put(sp++, v); }
     __device__ __forceinline__ uint32_t pop(int& sp) const {
         --sp;
-        if (sp < NL) return s[sp * 64];
-        return g[(size_t)(sp - NL) * gstride];
+        uint32_t v = s[(sp < NL ? sp : NL) * 64];
+        if (sp >= NL) v = __builtin_amdgcn_raw_buffer_load_b32(g, (int)(((uint32_t)(sp - NL) * gstride + lane) * 4u), 0, 0);
+        return v;
     }
     __device__ __forceinline__ void put(int k, uint32_t v) const {
-        if (k < NL) s[k * 64] = v;
-        else g[(size_t)(k - NL) * gstride] = v;
+        s[(k < NL ? k : NL) * 64] = v;
+        if (k >= NL) __builtin_amdgcn_raw_buffer_store_b32(v, g, (int)(((uint32_t)(k - NL) * gstride + lane) * 4u), 0, 0);
     }
 };
 struct NodesG {

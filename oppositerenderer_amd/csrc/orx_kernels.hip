@@ -408,7 +408,7 @@ __global__ __launch_bounds__(64, ORX_PHOTON_WAVES) void k_ppm_photon(DevScene S,
     const uint32_t lane = threadIdx.x;
     const uint32_t total = pb.prows * pb.PW;
     const uint32_t p = blockIdx.x * 64u + lane;
-    const StackH<PHOTON_LDS_STACK> stk{ORX_STACK_PTR, pb.tstk + p, gridDim.x * 64u};
+    const StackH<PHOTON_LDS_STACK> stk{ORX_STACK_PTR, pb.tstk, p, gridDim.x * 64u};
     float lo_x = INFINITY, lo_y = INFINITY, lo_z = INFINITY;
     float hi_x = -INFINITY, hi_y = -INFINITY, hi_z = -INFINITY;
     PhotonPath P;
@@ -437,7 +437,7 @@ void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, co
         fprintf(stderr, "orx: photon pass of %u photons exceeds its stack buffer (%u lanes)\n", total, pb.tlanes);
         abort();
     }
-    const size_t lds = (size_t)PHOTON_LDS_STACK * 64 * 4;
+    const size_t lds = StackH<PHOTON_LDS_STACK>::lds_bytes();
     if (mb)
         hipLaunchKernelGGL((k_ppm_photon<true>), dim3(blocks), dim3(64), lds, s, S, px, pb, c, *mb);
     else
@@ -855,6 +855,8 @@ void launch_grid_bucket_scan(hipStream_t s, const PhotonBufs& pb) {
     hipLaunchKernelGGL(k_bs_scan_apply, dim3(nscan), dim3(256), 0, s, pb);
 }
 void launch_grid_bucket_place(hipStream_t s, const PhotonBufs& pb) {
+    /* (staging a half chunk's pairs in LDS bucket by bucket, so that the writes of a wave go out in
+     * runs, measured slower on the pipelined hall frame: 1034-1035 -> 1026-1028 Mpaths/s) */
     hipLaunchKernelGGL(k_bs_place, dim3(pb.bs_nchunk), dim3(BS_THREADS), 0, s, pb);
     const uint32_t cb = 1u << pb.bshift;
     const uint32_t nbmax = (pb.gmax * pb.nsub + cb - 1) / cb;

@@ -1225,7 +1225,7 @@ __global__ __launch_bounds__(64, ORX_VCM_SHADOW_WAVES) void k_vcm_shadow(DevScen
     const uint32_t n = min(vb.dctl[0], vb.dcap);
     const uint32_t gid = blockIdx.x * 64u + threadIdx.x;
     DeferredShadowRays R{vb.dq0, vb.dq1, vb.docc, gid, n, gridDim.x * 64u, 0u};
-    const StackH<VCM_SHADOW_LDS_STACK> stk{ORX_STACK_PTR, vb.shstk + gid, gridDim.x * 64u};
+    const StackH<VCM_SHADOW_LDS_STACK> stk{ORX_STACK_PTR, vb.shstk, gid, gridDim.x * 64u};
     trace_any_chain_t(S, R, stk);
 }
 /* the colour of every own pixel's camera subpath from its deferred entries, in the order the
