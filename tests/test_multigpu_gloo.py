@@ -247,6 +247,7 @@ def batch_worker(rank, world, port, out_path, W, H, P, iters, method, reduce_eve
 
 @pytest.mark.parametrize("world,method,reduce_every", [(2, _abi.PROGRESSIVE_PHOTON_MAPPING, 1),
                                                        (3, _abi.PROGRESSIVE_PHOTON_MAPPING, 2),
+                                                       (4, _abi.PROGRESSIVE_PHOTON_MAPPING, 8),
                                                        (2, _abi.VCM_BIDIRECTIONAL_PATH_TRACING, 0),
                                                        (2, _abi.PATH_TRACING, 1)])
 def test_batch_partition_is_the_sum_of_independent_renderers(world, method, reduce_every):
