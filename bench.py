@@ -21,9 +21,10 @@ Multi GPU:   python bench.py --gpus N   (bench.py starts N rank processes itself
              (torchrun --nproc-per-node N bench.py --gpus N).
              Default --partition batch (the reference's distributed mode): every
              rank renders its own whole iterations of the workload and the accumulated
-             radiance is reduced over RCCL (weak scaling).  --partition rows: one frame split
-             by rows over the ranks (strong scaling; --scaling weak gives every rank a full
-             photon launch).  See DESIGN.md "Multi-GPU".
+             radiance is reduced over RCCL (weak scaling).  --partition rows (the default for
+             --config 4, BASELINE's "pixel-tile shard over 8xMI355X"): one frame split by rows
+             over the ranks (strong scaling; --scaling weak gives every rank a full photon
+             launch).  See DESIGN.md "Multi-GPU".
 """
 import argparse
 import json
@@ -69,15 +70,16 @@ def parse(argv=None):
     p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                    help="multi-GPU PPM: strong = fixed global photon launch split by rows over the ranks "
                         "(the default); weak = a full photon launch per rank")
-    p.add_argument("--partition", choices=["batch", "rows", "slab"], default="batch",
+    p.add_argument("--partition", choices=["batch", "rows", "slab"], default=None,
                    help="multi-GPU: batch = photon-batch (iteration) partition, the reference's distributed mode "
-                        "and the default: every rank renders its own whole iterations (global iteration numbers "
-                        "dealt round-robin, its own RNG streams) and the accumulated radiance is summed by an RCCL "
-                        "reduce every --reduce-every iterations (weak scaling); rows = one frame split by "
-                        "row-interleaved RNG/pixel/photon ownership, every rank gathers all hit points against "
-                        "its own photons (strong scaling, equal to one device up to fp32 order; per-rank hall "
-                        "frame at N=8 1.43 ms, tools/shard_model.py); slab = rows with the gather partitioned "
-                        "by spatial photon slabs (all-to-all of the photons; PPM only)")
+                        "and the default except for --config 4: every rank renders its own whole iterations "
+                        "(global iteration numbers dealt round-robin, its own RNG streams) and the accumulated "
+                        "radiance is summed by an RCCL reduce every --reduce-every iterations (weak scaling); "
+                        "rows = one frame split by row-interleaved RNG/pixel/photon ownership, every rank "
+                        "gathers all hit points against its own photons (strong scaling, equal to one device up "
+                        "to fp32 order) -- the default for --config 4, whose BASELINE entry is a pixel-tile "
+                        "shard over 8 GPUs; slab = rows with the gather partitioned by spatial photon slabs "
+                        "(all-to-all of the photons; PPM only)")
     p.add_argument("--reduce-every", type=int, default=8,
                    help="photon-batch partition: local iterations between two reduces of the radiance buffers")
     p.add_argument("--force-sharded", action="store_true",
@@ -86,10 +88,16 @@ def parse(argv=None):
                    help="skip the few serial (unpipelined) iterations after the timed region that give each "
                         "pass's stand-alone time")
     a = p.parse_args(argv)
+    requested = a.config
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
     a.config = matching_config(a)
+    if a.partition is None:
+        # BASELINE.json configs[4] is "pixel-tile shard over 8xMI355X + RCCL radiance reduce": one frame
+        # split over the GPUs (strong scaling); the other configs keep the reference's own distributed
+        # mode, whole iterations per GPU (weak)
+        a.partition = "rows" if requested == 4 and a.method == "ppm" else "batch"
     return a
 
 

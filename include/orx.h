@@ -210,6 +210,10 @@ const char* orx_last_error(const orx_renderer* r);
 void orx_destroy(orx_renderer* r);
 
 /* ---- inspection (parity tests, profiling; not part of the reference API) ---- */
+/* test hook: pretend the photon pass's deep-stack buffer covers only `lanes` lanes (bookkeeping only;
+ * the next resize or initScene sizes it again), so that the next PPM photon pass must return
+ * ORX_ERR_STATE instead of launching past the buffer (OptixRenderer.cpp:816-820 throws) */
+orx_status orx_debug_limit_photon_stack(orx_renderer* r, uint32_t lanes);
 typedef enum {
     ORX_BUF_RNG = 0,        /* uint32 [slots][6]: xorwow v0..v4, d */
     ORX_BUF_HITPOINTS = 1,  /* float  [W*H][13]: pos3 normal3 atten3 radiance3 flags(bits) */
@@ -313,8 +317,9 @@ orx_status orx_set_stream(orx_renderer* r, void* hip_stream, int use_external);
 /* rows owned by this rank for the current resolution, and ceil(H/world) */
 uint32_t orx_local_rows(const orx_renderer* r);
 uint32_t orx_max_local_rows(const orx_renderer* r);
-/* max_local_rows * W * 28: plane A (position | flags bits, float4) then plane N (the normal of a
- * non-specular hit, the radiance of another, float3), max_local_rows * W pixels each.  The
+/* P * 28 with P = max_local_rows * W rounded up to a multiple of 4: plane A (position | flags bits,
+ * float4) then plane N (the normal of a non-specular hit, the radiance of another, float3), P
+ * pixels each (the padding keeps every segment of an all-gathered buffer 16-B aligned).  The
  * attenuation stays with the owner: orx_ppm_gather_external returns the unattenuated estimate
  * (sum of weighted photon powers / (pi r^2 emitted)) and orx_ppm_finish multiplies the summed own
  * rows by their hit points' attenuation (IndirectRadianceEstimation.cu:220; fp32 order differs) */

@@ -896,10 +896,11 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
  * outgrows LDS); sized again whenever a scene or a resize comes in */
 static orx_status photon_stack_ensure(orx_renderer* r) {
     const size_t lanes = ((size_t)r->pb.prows * r->pb.PW + 63) / 64 * 64;
-    const size_t deep = r->scene.stack_entries + 2 > 16 ? r->scene.stack_entries + 2 - 16 : 1;
-    HIPCHK(r, r->d_ptrav.ensure(256 + deep * lanes * 4));
+    const uint32_t deep = photon_stack_deep(r->scene.stack_entries);
+    HIPCHK(r, r->d_ptrav.ensure(256 + (size_t)deep * lanes * 4));
     r->pb.tstk = r->d_ptrav.as<uint32_t>();
     r->pb.tlanes = (uint32_t)lanes;
+    r->pb.tdeep = deep;
     return ORX_OK;
 }
 static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
@@ -1368,7 +1369,7 @@ static orx_status begin_iteration(orx_renderer* r, uint64_t local_iteration_numb
  * 16 x 16: 10.4 GB) and the frame gains 2.8 % (serial gather 24.1 -> 23.1 ms); on the 1080p hall
  * the serial gather gains too (1.37 -> 1.21 ms) but the pipelined frame, where the gather overlaps
  * the next iteration's passes, does not (977 / 971 Mpaths/s, two runs each;
- * tools/gpu_r04_order.sh, tools/gpu_ab_order.sh).  ORX_GATHER_ORDER=S forces S (0: bands). */
+ * profiles/r04b_gather_order_ab.txt).  ORX_GATHER_ORDER=S forces S (0: bands). */
 static uint32_t gather_order(size_t px) {
     static const int o = [] {
         const char* e = getenv("ORX_GATHER_ORDER");
@@ -1423,17 +1424,17 @@ static HashParams hash_params(const orx_renderer* r, float ppm_radius) {
 static void ppm_grid_build(orx_renderer* r, const PhotonBufs& pb, const GridBox& gb = GridBox{});
 /* photon pass (+ the overlapped direct pass), then the photon map (build_map: false in slab
  * mode, whose grid is built over the imported photons by orx_ppm_slab_import) */
-static void ppm_photons_grid(orx_renderer* r, const Consts& c, bool build_map = true) {
+static orx_status ppm_photons_grid(orx_renderer* r, const Consts& c, bool build_map = true) {
     hipStream_t st = cur_stream(r);
     ev_begin(r, P_PHOTON);
     r->eye_chain = false;
-    if (r->media) {
-        const MediaBufs mb = media_bufs(r);
-        launch_ppm_photon(st, r->scene, r->px, r->pb, c, &mb);
-        vol_build(r, st, c.ppm_radius);
-    } else {
-        launch_ppm_photon(st, r->scene, r->px, r->pb, c);
+    MediaBufs mb{};
+    if (r->media) mb = media_bufs(r);
+    if (!launch_ppm_photon(st, r->scene, r->px, r->pb, c, r->media ? &mb : nullptr)) {
+        ev_end(r, P_PHOTON);
+        return set_err(r, ORX_ERR_STATE, "photon pass larger than its traversal-stack buffer (photon_stack_ensure)");
     }
+    if (r->media) vol_build(r, st, c.ppm_radius);
     ev_end(r, P_PHOTON);
     if (r->overlap_direct) {
         /* the direct pass needs the hitpoints and the RNG states the photon pass
@@ -1447,20 +1448,21 @@ static void ppm_photons_grid(orx_renderer* r, const Consts& c, bool build_map = 
         ev_end_on(r, P_DIRECT, r->aux);
         hipEventRecord(r->ev_direct_done, r->aux);
     }
-    if (!build_map) return;
+    if (!build_map) return ORX_OK;
     if (r->pb.hash) {
         ev_begin(r, P_SETUP_HASH);
         launch_hash_build(st, r->pb, hash_params(r, c.ppm_radius));
         ev_end(r, P_SETUP_HASH);
-        return;
+        return ORX_OK;
     }
     if (r->cfg.photon_map == 2) { /* createPhotonKdTreeOnCPU, on the device */
         ev_begin(r, P_SETUP_HASH);
         launch_kd_build(st, r->pb, r->kd);
         ev_end(r, P_SETUP_HASH);
-        return;
+        return ORX_OK;
     }
     ppm_grid_build(r, r->pb);
+    return ORX_OK;
 }
 /* grid build: the atomic-free bucket sort (an atomic-rank counting sort measured slower:
  * one device-scope atomic per photon into a 4 MB histogram) */
@@ -1477,9 +1479,9 @@ static void ppm_grid_build(orx_renderer* r, const PhotonBufs& pb, const GridBox&
     launch_grid_bucket_place(st, pb);
     ev_end(r, P_SCATTER);
 }
-static void ppm_local_passes(orx_renderer* r, const DevCamera& cam, const Consts& c) {
+static orx_status ppm_local_passes(orx_renderer* r, const DevCamera& cam, const Consts& c) {
     ppm_eye(r, cam, c);
-    ppm_photons_grid(r, c);
+    return ppm_photons_grid(r, c);
 }
 
 /* VCM_BIDIRECTIONAL_PATH_TRACING branch of renderNextIteration (OptixRenderer.cpp:675-795) */
@@ -1562,10 +1564,11 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
             hipGetDevice(&dev);
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             const size_t lanes = (size_t)cus * 32 * 64;
-            const size_t deep = r->scene.stack_entries + 2 > 16 ? r->scene.stack_entries + 2 - 16 : 1;
-            HIPCHK(r, r->d_vshstk.ensure(deep * lanes * 4 + 64));
+            const uint32_t deep = vcm_shadow_stack_deep(r->scene.stack_entries);
+            HIPCHK(r, r->d_vshstk.ensure((size_t)deep * lanes * 4 + 64));
             vb.shstk = r->d_vshstk.as<uint32_t>();
             vb.shstk_lanes = (uint32_t)lanes;
+            vb.shdeep = deep;
         } else {
             vb.dq0 = nullptr;
         }
@@ -1665,8 +1668,9 @@ static orx_status ppm_pipelined_iteration(orx_renderer* r, const orx_request* de
     HIPCHK(r, hipEventRecord(r->ev_eye_done, r->aux));
     HIPCHK(r, hipStreamWaitEvent(st, r->ev_eye_done, 0));
     r->overlap_direct = true;
-    ppm_photons_grid(r, c); /* photon, direct (aux), grid */
+    const orx_status sp = ppm_photons_grid(r, c); /* photon, direct (aux), grid */
     r->overlap_direct = false;
+    if (sp != ORX_OK) return sp;
     HIPCHK(r, hipEventRecord(r->ev_grid_done, st));
     hipStream_t g = r->gstream;
     HIPCHK(r, hipStreamWaitEvent(g, r->ev_grid_done, 0));
@@ -1743,7 +1747,11 @@ static orx_status render_next_iteration(orx_renderer* r, uint64_t local_iteratio
         /* the direct pass on the aux stream beside the grid build and the gather; the output
          * accumulation after both */
         r->overlap_direct = true;
-        ppm_local_passes(r, cam, c);
+        const orx_status sp = ppm_local_passes(r, cam, c);
+        if (sp != ORX_OK) {
+            r->overlap_direct = false;
+            return sp;
+        }
         ev_begin(r, P_GATHER);
         if (r->pb.hash) launch_ppm_gather_hash(st, local_gather_in(r), r->pb, hash_params(r, c.ppm_radius), c);
         else if (r->cfg.photon_map == 2) launch_ppm_gather_kd(st, local_gather_in(r), r->pb, r->kd, c);
@@ -1774,7 +1782,8 @@ orx_status orx_ppm_local_passes(orx_renderer* r, uint64_t iteration_number, uint
     if (s0 != ORX_OK) return s0;
     DevCamera cam = camera_setup(det->camera);
     Consts c = make_consts(r, ppm_radius, local_iteration_number);
-    ppm_local_passes(r, cam, c);
+    const orx_status sp = ppm_local_passes(r, cam, c);
+    if (sp != ORX_OK) return sp;
     HIPCHK(r, hipGetLastError());
     r->last_method = (uint64_t)det->method;
     r->last_consts = c;
@@ -1816,8 +1825,9 @@ orx_status orx_ppm_local_photons(orx_renderer* r) {
     if (!r->rng_ready) return set_err(r, ORX_ERR_STATE, "orx_ppm_local_eye first");
     HIPCHK(r, hipSetDevice(r->device));
     r->overlap_direct = r->last_pipelined; /* direct pass on the aux stream right after the photons */
-    ppm_photons_grid(r, r->last_consts);
+    const orx_status sp = ppm_photons_grid(r, r->last_consts);
     r->overlap_direct = false;
+    if (sp != ORX_OK) return sp;
     if (r->last_pipelined) HIPCHK(r, hipEventRecord(r->ev_grid_done, cur_stream(r)));
     HIPCHK(r, hipGetLastError());
     return ORX_OK;
@@ -1849,7 +1859,8 @@ orx_status orx_ppm_local_trace(orx_renderer* r, uint64_t iteration_number, uint6
     DevCamera cam = camera_setup(det->camera);
     Consts c = make_consts(r, ppm_radius, local_iteration_number);
     ppm_eye(r, cam, c);
-    ppm_photons_grid(r, c, false);
+    const orx_status sp = ppm_photons_grid(r, c, false);
+    if (sp != ORX_OK) return sp;
     HIPCHK(r, hipGetLastError());
     r->last_method = (uint64_t)det->method;
     r->last_consts = c;
@@ -1862,8 +1873,9 @@ orx_status orx_ppm_local_photon_trace(orx_renderer* r) {
     if (!r->slab) return set_err(r, ORX_ERR_STATE, "orx_ppm_local_photon_trace is a slab-mode phase");
     HIPCHK(r, hipSetDevice(r->device));
     r->overlap_direct = r->last_pipelined; /* direct pass on the aux stream right after the photons */
-    ppm_photons_grid(r, r->last_consts, false);
+    const orx_status sp = ppm_photons_grid(r, r->last_consts, false);
     r->overlap_direct = false;
+    if (sp != ORX_OK) return sp;
     HIPCHK(r, hipGetLastError());
     return ORX_OK;
 }
@@ -1959,9 +1971,15 @@ orx_status orx_ppm_slab_import(orx_renderer* r, const void* recv, uint64_t n, co
     return ORX_OK;
 }
 
+orx_status orx_debug_limit_photon_stack(orx_renderer* r, uint32_t lanes) {
+    if (!r) return ORX_ERR_INVALID_ARGUMENT;
+    if (lanes < r->pb.tlanes) r->pb.tlanes = lanes;
+    return ORX_OK;
+}
+
 orx_status orx_export_hitpoints(orx_renderer* r, void* dst, size_t bytes) {
     if (!r || !dst) return ORX_ERR_INVALID_ARGUMENT;
-    const size_t npx = (size_t)r->max_rows * r->W, need = npx * 28;
+    const size_t npx = (size_t)r->max_rows * r->W, need = hp_export_plane(npx) * 28;
     if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "destination too small");
     HIPCHK(r, hipSetDevice(r->device));
     launch_export_hp(cur_stream(r), r->px, (uint32_t)npx, (float*)dst);
@@ -1978,7 +1996,7 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hp, uint32_t seg
     HIPCHK(r, hipSetDevice(r->device));
     GatherIn gi;
     gi.base = (const uint8_t*)hp;
-    gi.seg_bytes = (size_t)r->max_rows * r->W * 28;
+    gi.seg_bytes = hp_export_plane((size_t)r->max_rows * r->W) * 28;
     gi.raw = 1;
     gi.segments = segments;
     gi.seg_rows = r->max_rows;
@@ -2113,7 +2131,7 @@ orx_status orx_set_stream(orx_renderer* r, void* stream, int use_external) {
 uint32_t orx_local_rows(const orx_renderer* r) { return r ? r->rows : 0; }
 uint32_t orx_max_local_rows(const orx_renderer* r) { return r ? (r->H + r->world - 1) / r->world : 0; }
 size_t orx_hitpoint_export_bytes(const orx_renderer* r) {
-    return r ? (size_t)((r->H + r->world - 1) / r->world) * r->W * 28 : 0;
+    return r ? hp_export_plane((size_t)((r->H + r->world - 1) / r->world) * r->W) * 28 : 0;
 }
 
 static orx_status check_grid_error(orx_renderer* r) {

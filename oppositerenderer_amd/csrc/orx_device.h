@@ -517,9 +517,10 @@ struct StackL {
     __device__ __forceinline__ void put(int k, uint32_t v) const { s[k * 64] = v; }
 };
 /* A short LDS stack continued in global memory: entries k < NL in the lane's LDS column, deeper
- * ones in a global array [depth][gstride] at column `lane`, through buffer loads/stores (a 32-bit
- * offset; kept apart from the LDS accesses, which the compiler would otherwise merge with them into
- * flat loads).  The LDS column holds NL + 1 entries: a push always writes LDS, at min(k, NL) (entry
+ * ones in the block's own global array [depth][64] at column `lane` (g_ = the block's base, so the
+ * 32-bit buffer offsets stay below depth * 256 B whatever the launch size), through buffer
+ * loads/stores (kept apart from the LDS accesses, which the compiler would otherwise merge with
+ * them into flat loads).  The LDS column holds NL + 1 entries: a push always writes LDS, at min(k, NL) (entry
  * NL is a dump slot), and only a push or pop past NL takes the branch to global memory, so a wave
  * whose lanes all stay shallow runs one skipped branch per operation.  For kernels whose occupancy
  * the full-depth LDS stack limits (k_vcm_shadow: 61 VGPRs, 4 waves per SIMD with 35 LDS entries,
@@ -528,10 +529,15 @@ template <int NL>
 struct StackH {
     uint32_t* s;
     __amdgpu_buffer_rsrc_t g;
-    uint32_t lane, gstride;
+    uint32_t lane;
+    static constexpr uint32_t gstride = 64;
     static constexpr size_t lds_bytes() { return (size_t)(NL + 1) * 64 * 4; }
-    __device__ __forceinline__ StackH(uint32_t* s_, uint32_t* g_, uint32_t lane_, uint32_t gstride_)
-        : s(s_), g(__builtin_amdgcn_make_buffer_rsrc(g_, 0, 0xffffffff, 0x00020000)), lane(lane_), gstride(gstride_) {}
+    /* global entries per lane for a tree whose stack bound is `entries` (the pushes run two past it) */
+    __host__ __device__ static constexpr uint32_t deep(uint32_t entries) { return entries + 2 > NL ? entries + 2 - NL : 1u; }
+    /* g_: the buffer of every block's [deep][64] entries, block `blk`'s part is used */
+    __device__ __forceinline__ StackH(uint32_t* s_, uint32_t* g_, uint32_t blk, uint32_t ndeep, uint32_t lane_)
+        : s(s_), g(__builtin_amdgcn_make_buffer_rsrc(g_ + (size_t)blk * ndeep * 64u, 0, ndeep * 256u, 0x00020000)),
+          lane(lane_) {}
     __device__ __forceinline__ void push(int& sp, uint32_t v) const { put(sp++, v); }
     __device__ __forceinline__ uint32_t pop(int& sp) const {
         --sp;

@@ -106,9 +106,10 @@ struct PhotonBufs {
     uint32_t hnum;      /* photonsSize = NUM_PHOTONS = PW * PH * max deposits (OptixRenderer.cpp:50) */
     uint32_t* hcount;   /* [hnum] photonsHashTableCount */
     uint32_t* hwin;     /* [hnum] slot + 1 of the photon the cell keeps (0: empty) */
-    /* the photon pass's traversal-stack entries below the LDS part, [depth][tlanes] (a column per photon) */
+    /* the photon pass's traversal-stack entries below the LDS part: [block][tdeep][64] for tlanes
+     * lanes (StackH: a block's offsets stay small whatever the launch size) */
     uint32_t* tstk;
-    uint32_t tlanes;
+    uint32_t tlanes, tdeep;
 };
 
 /* kd-tree photon map (orx_config.photon_map = 2, orx_kdtree.hip): the implicit
@@ -197,7 +198,11 @@ void launch_rng_init(hipStream_t s, RngPlanes rng, uint32_t RW, uint32_t rows, u
                      uint32_t seed);
 void launch_ppm_eye(hipStream_t s, const DevScene& S, const DevCamera& cam, const PixelBufs& px, const Consts& c,
                     const MediaBufs* mb = nullptr);
-void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c,
+/* global (deep) traversal-stack entries per lane of k_ppm_photon / k_vcm_shadow for a tree whose
+ * stack bound is `entries` (StackH::deep of their LDS depths) */
+uint32_t photon_stack_deep(uint32_t entries);
+uint32_t vcm_shadow_stack_deep(uint32_t entries);
+bool launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c,
                        const MediaBufs* mb = nullptr);
 void launch_grid_setup(hipStream_t s, const PhotonBufs& pb, const GridBox& gb = GridBox{});
 /* atomic-free grid build: keys + bucket histogram / scan of the table /
@@ -260,9 +265,12 @@ __device__ __forceinline__ uint32_t gather_row(const GatherIn& gi, uint32_t y) {
 /* The gather's hit point j (row of the segment-major layout), pixel x: position|flags (A),
  * normal|attenuation.x (B) and attenuation.yz (C).  gi.raw: the 28-B export layout, attenuation 1
  * (the owner applies it, orx_ppm_finish) */
+/* pixels per plane of the 28-B export layout: padded to a multiple of 4, so every segment's
+ * planes stay 16-B aligned (plane A is read as float4) */
+__host__ __device__ __forceinline__ size_t hp_export_plane(size_t npx) { return (npx + 3) & ~(size_t)3; }
 __device__ __forceinline__ void hp_load(const GatherIn& gi, uint32_t j, uint32_t x, float4& A, float4& B, float2& Cc) {
     const uint32_t seg = j / gi.seg_rows, lj = j - seg * gi.seg_rows;
-    const size_t plane = (size_t)gi.seg_rows * gi.W;
+    const size_t plane = gi.raw ? hp_export_plane((size_t)gi.seg_rows * gi.W) : (size_t)gi.seg_rows * gi.W;
     const uint8_t* b = gi.base + seg * gi.seg_bytes;
     const size_t li = (size_t)lj * gi.W + x;
     A = ((const float4*)b)[li];
@@ -336,8 +344,8 @@ struct VcmBufs {
     uint32_t* dctl;     /* [4] entries written, overflow flag (more entries than dcap: the pass reruns in place) */
     uint32_t dcap;
     uint32_t* rng_save; /* [6][rows*RW] the RNG planes before the camera pass (restored for the in-place rerun) */
-    uint32_t* shstk;    /* k_vcm_shadow's traversal-stack entries below its LDS part: [depth][shstk_lanes] */
-    uint32_t shstk_lanes;
+    uint32_t* shstk;    /* k_vcm_shadow's traversal-stack entries below its LDS part: [block][shdeep][64] */
+    uint32_t shstk_lanes, shdeep;
     struct VcmConsts* consts; /* device copy of the pass constants (written by the launches) */
 };
 struct VcmConsts {

@@ -408,7 +408,7 @@ __global__ __launch_bounds__(64, ORX_PHOTON_WAVES) void k_ppm_photon(DevScene S,
     const uint32_t lane = threadIdx.x;
     const uint32_t total = pb.prows * pb.PW;
     const uint32_t p = blockIdx.x * 64u + lane;
-    const StackH<PHOTON_LDS_STACK> stk{ORX_STACK_PTR, pb.tstk, p, gridDim.x * 64u};
+    const StackH<PHOTON_LDS_STACK> stk{ORX_STACK_PTR, pb.tstk, blockIdx.x, pb.tdeep, lane};
     float lo_x = INFINITY, lo_y = INFINITY, lo_z = INFINITY;
     float hi_x = -INFINITY, hi_y = -INFINITY, hi_z = -INFINITY;
     PhotonPath P;
@@ -428,20 +428,21 @@ __global__ __launch_bounds__(64, ORX_PHOTON_WAVES) void k_ppm_photon(DevScene S,
     photon_bbox_flush(pb, lo_x, lo_y, lo_z, hi_x, hi_y, hi_z, blockIdx.x & (BBOX_REPLICAS - 1), lane);
 }
 
-void launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c,
+uint32_t photon_stack_deep(uint32_t entries) { return StackH<PHOTON_LDS_STACK>::deep(entries); }
+/* false (nothing launched): the deep-stack buffer does not cover the launch (the caller reports
+ * ORX_ERR_STATE; photon_stack_ensure sizes it at every scene and resize) */
+bool launch_ppm_photon(hipStream_t s, const DevScene& S, const PixelBufs& px, const PhotonBufs& pb, const Consts& c,
                        const MediaBufs* mb) {
     const uint32_t total = pb.prows * pb.PW;
-    if (total == 0) return;
+    if (total == 0) return true;
     const uint32_t blocks = (total + 63) / 64;
-    if ((size_t)blocks * 64 > pb.tlanes) { /* the host sizes tstk for every photon (photon_stack_ensure) */
-        fprintf(stderr, "orx: photon pass of %u photons exceeds its stack buffer (%u lanes)\n", total, pb.tlanes);
-        abort();
-    }
+    if ((size_t)blocks * 64 > pb.tlanes || pb.tdeep < StackH<PHOTON_LDS_STACK>::deep(S.stack_entries)) return false;
     const size_t lds = StackH<PHOTON_LDS_STACK>::lds_bytes();
     if (mb)
         hipLaunchKernelGGL((k_ppm_photon<true>), dim3(blocks), dim3(64), lds, s, S, px, pb, c, *mb);
     else
         hipLaunchKernelGGL((k_ppm_photon<false>), dim3(blocks), dim3(64), lds, s, S, px, pb, c, MediaBufs{});
+    return true;
 }
 
 /* ------------------------------------------------------------------ */
@@ -1647,7 +1648,7 @@ __global__ __launch_bounds__(256) void k_export_hp(PixelBufs px, uint32_t n, flo
     if (i >= n) return;
     const float4 B = px.hpB[i];
     reinterpret_cast<float4*>(dst)[i] = px.hpA[i];
-    float* N = dst + 4 * (size_t)n + 3 * (size_t)i;
+    float* N = dst + 4 * hp_export_plane(n) + 3 * (size_t)i;
     N[0] = B.x;
     N[1] = B.y;
     N[2] = B.z;

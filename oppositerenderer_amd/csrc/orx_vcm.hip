@@ -1219,13 +1219,14 @@ struct DeferredShadowRays {
 #define ORX_VCM_SHADOW_WAVES 8
 #endif
 constexpr int VCM_SHADOW_LDS_STACK = 16; /* LDS entries per lane; deeper ones in vb.shstk */
+uint32_t vcm_shadow_stack_deep(uint32_t entries) { return StackH<VCM_SHADOW_LDS_STACK>::deep(entries); }
 __global__ __launch_bounds__(64, ORX_VCM_SHADOW_WAVES) void k_vcm_shadow(DevScene S, VcmBufs vb) {
     if (vb.dctl[1]) return; /* out of entries: the camera pass reruns in place */
     ORX_STACK_DECL;
     const uint32_t n = min(vb.dctl[0], vb.dcap);
     const uint32_t gid = blockIdx.x * 64u + threadIdx.x;
     DeferredShadowRays R{vb.dq0, vb.dq1, vb.docc, gid, n, gridDim.x * 64u, 0u};
-    const StackH<VCM_SHADOW_LDS_STACK> stk{ORX_STACK_PTR, vb.shstk, gid, gridDim.x * 64u};
+    const StackH<VCM_SHADOW_LDS_STACK> stk{ORX_STACK_PTR, vb.shstk, blockIdx.x, vb.shdeep, threadIdx.x};
     trace_any_chain_t(S, R, stk);
 }
 /* the colour of every own pixel's camera subpath from its deferred entries, in the order the

@@ -43,6 +43,12 @@ import numpy as np
 HP_EXPORT_FLOATS = 7  # orx_export_hitpoints: 28 B per pixel (position|flags float4, normal float3)
 
 
+def hp_export_floats(max_rows, W):
+    """float32 words of one rank's orx_export_hitpoints buffer (orx_hitpoint_export_bytes / 4): two
+    planes of max_rows * W pixels rounded up to a multiple of 4 (16-B aligned segments)"""
+    return HP_EXPORT_FLOATS * ((max_rows * W + 3) // 4 * 4)
+
+
 def local_rows(H, rank, world):
     return (H - rank + world - 1) // world if H > rank else 0
 
@@ -150,13 +156,19 @@ def assemble_rows(blocks, W, H, world):
     return img
 
 
-def batch_seed(seed, rank):
+def batch_seed(seed, rank, clock_ns=None):
     """Rank g's RNG seed in the photon-batch partition.  Rank 0 keeps the configured seed, so a
     one-rank job renders exactly the single-device sequence; the others get their own XORWOW
     streams, as the reference's render servers each seed from their own clock
-    (OptixRenderer_SpatialHash.cu:319-334).  0 (seed from the clock) stays 0 on every rank."""
-    if seed == 0 or rank == 0:
+    (OptixRenderer_SpatialHash.cu:319-334).  Seed 0 (the renderer seeds from clock()/time(NULL)):
+    rank 0 keeps 0; every other rank gets a seed from this process's nanosecond clock with the rank
+    mixed in, since ranks started in the same second would otherwise share time(NULL) and draw
+    correlated streams."""
+    if rank == 0:
         return seed
+    if seed == 0:
+        t = time.time_ns() if clock_ns is None else int(clock_ns)
+        seed = (t ^ (t >> 32)) & 0xFFFFFFFF
     return ((seed + 0x9E3779B9 * rank) & 0xFFFFFFFF) or 1
 
 
@@ -237,9 +249,9 @@ class ShardedPPM:
             self.recv = backend.alloc(9 * s_global + 9)
             self.last_plan = None
         nsets = 2 if self.pipe else 1
-        hpf = HP_EXPORT_FLOATS
-        self.sets = [(backend.alloc(self.max_rows * W * hpf),            # own hitpoints, 28 B/px as float32
-                      backend.alloc(world * self.max_rows * W * hpf),    # all hitpoints
+        hpf = hp_export_floats(self.max_rows, W)
+        self.sets = [(backend.alloc(hpf),                                # own hitpoints, 28 B/px as float32
+                      backend.alloc(world * hpf),                        # all hitpoints
                       backend.alloc(world * self.max_rows * W * 3),      # partial indirect, all pixels
                       backend.alloc(self.max_rows * W * 3))              # summed indirect, own rows
                      for _ in range(nsets)]

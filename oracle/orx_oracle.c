@@ -1681,7 +1681,7 @@ static void ppm_gather_hash(orc_renderer* r, float ppmRadiusSquared, float emitt
 
 /* hitpoint source for the gather: the own rows, or `segments` export buffers of the sharded
  * gather (include/orx.h orx_export_hitpoints: plane A pos + flags float4, plane N the normal
- * float3; seg_rows*W pixels per plane, 28 B per pixel).  The export carries no attenuation: the
+ * float3; seg_rows*W pixels per plane padded to a multiple of 4, 28 B per pixel).  The export carries no attenuation: the
  * sharded gather returns the unattenuated estimate and the owner applies its hit point's
  * attenuation in orc_ppm_finish. */
 typedef struct {
@@ -1691,11 +1691,11 @@ typedef struct {
 } hp_src;
 static hitpoint_t hp_fetch(const orc_renderer* r, const hp_src* src, size_t px) {
     if (src->own) return src->own[px];
-    const size_t plane = (size_t)src->seg_rows * r->W;
+    const size_t plane = (size_t)src->seg_rows * r->W, p4 = (plane + 3) & ~(size_t)3;
     size_t seg = px / plane, li = px - seg * plane;
-    const float* b = src->ext + seg * plane * 7;
+    const float* b = src->ext + seg * p4 * 7;
     const float* A = b + 4 * li;
-    const float* N = b + 4 * plane + 3 * li;
+    const float* N = b + 4 * p4 + 3 * li;
     hitpoint_t h;
     memset(&h, 0, sizeof h);
     h.position = mk(A[0], A[1], A[2]);
@@ -2189,7 +2189,9 @@ orx_status orc_set_shard(orc_renderer* r, uint32_t rank, uint32_t world) {
 }
 uint32_t orc_max_local_rows(const orc_renderer* r) { return (r->H + r->world - 1) / r->world; }
 uint32_t orc_local_rows(const orc_renderer* r) { return r->rows; }
-size_t orc_hitpoint_export_bytes(const orc_renderer* r) { return (size_t)orc_max_local_rows(r) * r->W * 28; }
+size_t orc_hitpoint_export_bytes(const orc_renderer* r) {
+    return (((size_t)orc_max_local_rows(r) * r->W + 3) & ~(size_t)3) * 28;
+}
 
 orx_status orc_ppm_local_passes(orc_renderer* r, uint64_t iter, uint64_t local, float ppmRadius, const orx_request* det) {
     (void)iter;
@@ -2320,7 +2322,7 @@ orx_status orc_ppm_slab_import(orc_renderer* r, const float* recv, uint64_t n, c
 }
 
 orx_status orc_export_hitpoints(orc_renderer* r, void* dst, size_t bytes) {
-    const size_t plane = (size_t)r->max_rows * r->W;
+    const size_t plane = (((size_t)r->max_rows * r->W) + 3) & ~(size_t)3; /* padded: 16-B aligned planes */
     if (!dst || bytes < plane * 28) return ORX_ERR_INVALID_ARGUMENT;
     float* b = (float*)dst;
     memset(b, 0, plane * 28);

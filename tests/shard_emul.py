@@ -60,7 +60,7 @@ def run_iterations(shards, scene, W, H, req, iters, slab=False, pipelined=False,
     mr = (H + world - 1) // world
     blk = mr * W * 3
     nsets = 2 if pipelined else 1
-    sets = [([b.alloc(mr * W * multigpu.HP_EXPORT_FLOATS) for b in shards], shards[0].alloc(world * mr * W * multigpu.HP_EXPORT_FLOATS),
+    sets = [([b.alloc(multigpu.hp_export_floats(mr, W)) for b in shards], shards[0].alloc(world * multigpu.hp_export_floats(mr, W)),
              [b.alloc(world * blk) for b in shards], shards[0].alloc(world * blk)) for _ in range(nsets)]
     main = torch.cuda.current_stream()
     radius = scene.initial_ppm_radius()

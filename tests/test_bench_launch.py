@@ -47,6 +47,20 @@ def test_bench_gpus2_rows_partition():
     assert out["config"]["paths_per_iteration"] == 48 * 40 + 32 * 32
 
 
+def test_bench_config4_defaults_to_the_rows_partition():
+    """--config 4 (BASELINE configs[4]: a pixel-tile shard over 8 GPUs) runs the strong-scaling row
+    partition by default; the sizes are overridden so that the oracle backend finishes quickly."""
+    out = _launch(["--config", "4"])
+    assert out["scaling"] == "strong"
+    assert "row-interleaved" in out["config"]["parallelism"]
+    assert out["config"]["paths_per_iteration"] == 48 * 40 + 32 * 32
+    import bench
+    assert bench.parse(["--config", "4"]).partition == "rows"
+    assert bench.parse(["--config", "4", "--partition", "batch"]).partition == "batch"
+    assert bench.parse([]).partition == "batch"
+    assert bench.parse(["--config", "3"]).partition == "batch"
+
+
 def test_bench_rank_failure_ends_the_launch():
     """A rank that fails (here: an unknown scene) ends the launch with its exit code instead of
     leaving the other rank waiting in a collective."""

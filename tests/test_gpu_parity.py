@@ -164,6 +164,33 @@ def test_error_paths():
     r.destroy()
 
 
+def test_photon_stack_error_is_a_status():
+    """A photon pass whose deep-stack buffer does not cover the launch returns ORX_ERR_STATE through
+    the ABI (the reference throws, OptixRenderer.cpp:816-820) instead of aborting the host process;
+    the renderer recovers at the next resize."""
+    import ctypes as C
+
+    from oppositerenderer_amd.renderer import OrxError
+    scene = scenes.cornell()
+    W, H, P = 32, 24, 32
+    r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P))
+    r.initialize(0)
+    r.initScene(scene)
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    det = RenderRequestDetails(cam, scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W, H)
+    radius = scene.initial_ppm_radius()
+    r.renderNextIteration(0, 0, radius, False, det)
+    f = r._lib.orx_debug_limit_photon_stack
+    f.argtypes, f.restype = [C.c_void_p, C.c_uint32], C.c_int
+    assert f(r._h, 64) == 0
+    with pytest.raises(OrxError, match="traversal-stack"):
+        r.renderNextIteration(1, 1, radius, False, det)
+    det2 = RenderRequestDetails(cam, scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W + 8, H)
+    r.renderNextIteration(0, 0, radius, True, det2)  # a resize sizes the buffer again
+    assert r.getOutputBuffer().sum() > 0
+    r.destroy()
+
+
 @pytest.mark.parametrize("method", [_abi.PROGRESSIVE_PHOTON_MAPPING, _abi.PATH_TRACING])
 def test_mesh_bvh_parity(method):
     """Synthetic Sponza-class hall (261k triangles, smooth normals): the device
@@ -583,3 +610,29 @@ def test_pipelining_starts_after_other_methods():
     assert rel_l2(g, o) < 1e-5 and g.mean() > 0
     gpu.destroy()
     ora.close()
+
+
+@pytest.mark.fresh_process
+@pytest.mark.parametrize("order", [8, 3])
+def test_gather_tile_order(order, tmp_path):
+    """The super-tile gather order (orx_capi.hip gather_order; on by default from 4M pixels) on an
+    image whose 13 x 10 tiles are multiples of neither 8 nor 3: the local gather and the three-shard
+    external gather against the oracle in a fresh process with ORX_GATHER_ORDER set
+    (tests/gather_order_child.py).  No lit pixel may be left dark (a skipped tile)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ORX_GATHER_ORDER=str(order))
+    out = subprocess.run([sys.executable, "-u", os.path.join(root, "tests", "gather_order_child.py")], env=env,
+                         capture_output=True, text=True, timeout=150, cwd=root)
+    assert out.returncode == 0, (out.stdout[-2000:], out.stderr[-3000:])
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["order"] == str(order)
+    assert res["lit_pixels"] > 1000, res
+    assert res["dark_pixels"] == 0, res
+    assert res["local_indirect_rel_l2"] < 1e-5, res
+    assert res["local_output_rel_l2"] < 1e-4, res
+    assert res["rows3_output_rel_l2"] < 1e-5, res

@@ -35,7 +35,7 @@ def test_sharded_device_path_matches_single(world, W, H, P, photon_map):
             b.local_passes(it, it, radius, req)
         hps = []
         for b in shards:
-            t = b.alloc(mr * W * multigpu.HP_EXPORT_FLOATS)
+            t = b.alloc(multigpu.hp_export_floats(mr, W))
             b.export_hitpoints(t)
             hps.append(t)
         hp_all = torch.cat(hps)
@@ -173,7 +173,7 @@ def test_sharded_device_pipelined_matches_single(world, W, H, P):
         shards.append(b)
     main = torch.cuda.current_stream(dev)
     mr = (H + world - 1) // world
-    sets = [([b.alloc(mr * W * multigpu.HP_EXPORT_FLOATS) for b in shards], shards[0].alloc(world * mr * W * multigpu.HP_EXPORT_FLOATS),
+    sets = [([b.alloc(multigpu.hp_export_floats(mr, W)) for b in shards], shards[0].alloc(world * multigpu.hp_export_floats(mr, W)),
              [b.alloc(world * mr * W * 3) for b in shards], shards[0].alloc(world * mr * W * 3)) for _ in range(2)]
     radius = scene.initial_ppm_radius()
     iters = 5
@@ -251,7 +251,7 @@ def test_full_size_conference_sharded_equals_single():
         b.local_passes(0, 0, radius, req)
     hps = []
     for b in shards:
-        t = b.alloc(mr * W * multigpu.HP_EXPORT_FLOATS)
+        t = b.alloc(multigpu.hp_export_floats(mr, W))
         b.export_hitpoints(t)
         hps.append(t)
     hp_all = torch.cat(hps)
@@ -324,7 +324,7 @@ def test_sharded_world4_world8_match_oracle(world, W, H, P, PH, photon_map, pipe
     mr = (H + world - 1) // world
     blk = mr * W * 3
     nsets = 2 if pipelined else 1
-    sets = [([b.alloc(mr * W * multigpu.HP_EXPORT_FLOATS) for b in shards], shards[0].alloc(world * mr * W * multigpu.HP_EXPORT_FLOATS),
+    sets = [([b.alloc(multigpu.hp_export_floats(mr, W)) for b in shards], shards[0].alloc(world * multigpu.hp_export_floats(mr, W)),
              [b.alloc(world * blk) for b in shards], shards[0].alloc(world * blk)) for _ in range(nsets)]
     radius = scene.initial_ppm_radius()
     iters = 3

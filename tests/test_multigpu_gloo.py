@@ -69,12 +69,15 @@ def worker(rank, world, port, out_path, W, H, P, iters, method=_abi.PROGRESSIVE_
 
 @pytest.mark.parametrize("world,W,H,photon_map,scaling", [(2, 48, 40, 0, "weak"), (3, 40, 37, 0, "weak"),
                                                             (2, 48, 40, 2, "weak"), (2, 48, 40, 0, "strong"),
-                                                            (3, 40, 37, 0, "strong"), (2, 48, 40, 2, "strong")])
+                                                            (3, 40, 37, 0, "strong"), (2, 48, 40, 2, "strong"),
+                                                            (3, 41, 37, 0, "strong")])
 def test_sharded_ppm_matches_single(world, W, H, photon_map, scaling):
     """photon_map 2: each rank builds a kd-tree over its own photons and gathers every rank's
     hit points against it (the gather is linear in the photon set, like the grid's).
     strong: a fixed 48 x 41 global photon launch (the bench's default multi-GPU mode) whose
-    rows are dealt to the ranks (41 rows: uneven shares); weak: a full 32 x 32 batch per rank."""
+    rows are dealt to the ranks (41 rows: uneven shares); weak: a full 32 x 32 batch per rank.
+    41 x 37 over 3 ranks: 13 x 41 = 533 pixels per segment, an odd count (the export planes are
+    padded to a multiple of 4 pixels, so every segment stays 16-B aligned)."""
     P, iters = (32, 2) if scaling == "weak" else (48, 2)
     PH = P * world if scaling == "weak" else 41
     out = os.path.join(tempfile.mkdtemp(), "img.npy")
@@ -281,7 +284,11 @@ def test_batch_seeds_and_iterations():
     assert multigpu.batch_seed(SEED, 0) == SEED
     seeds = {multigpu.batch_seed(SEED, g) for g in range(64)}
     assert len(seeds) == 64 and 0 not in seeds
-    assert multigpu.batch_seed(0, 5) == 0  # clock-seeded renderers stay clock-seeded
+    # seed 0 (the reference's clock seed): rank 0 keeps it; the other ranks get a clock-derived seed
+    # with the rank mixed in, so ranks started in the same second still draw different streams
+    assert multigpu.batch_seed(0, 0) == 0
+    clock = {multigpu.batch_seed(0, g) for g in range(1, 64)}
+    assert len(clock) == 63 and 0 not in clock
     assert sorted(multigpu.batch_iteration(i, g, 4) for i in range(3) for g in range(4)) == list(range(12))
     r = multigpu.radius_sequence(1.0, 5)
     x = 1.0

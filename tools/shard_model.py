@@ -56,21 +56,24 @@ def run(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None):
     full.initialize(0)
     full.initScene(scene)
     fb = multigpu.DeviceShard(full, torch, dev)
-    fhp = fb.alloc(H * W * multigpu.HP_EXPORT_FLOATS)
+    fhp = fb.alloc(multigpu.hp_export_floats(H, W))
     mr = (H + world - 1) // world
-    hp = b.alloc(mr * W * multigpu.HP_EXPORT_FLOATS)
+    hp = b.alloc(multigpu.hp_export_floats(mr, W))
 
     def segments(t):
-        """[H][W] planes A (4), N (3) -> N segments of mr rows, rows y = s + lj*N"""
+        """[H][W] planes A (4), N (3) -> N segments of mr rows, rows y = s + lj*N (planes padded to
+        a multiple of 4 pixels, multigpu.hp_export_floats)"""
+        P1 = multigpu.hp_export_floats(H, W) // 7
         A = t[:H * W * 4].view(H, W, 4)
-        Nn = t[H * W * 4:].view(H, W, 3)
+        Nn = t[P1 * 4:P1 * 4 + H * W * 3].view(H, W, 3)
+        Pm = multigpu.hp_export_floats(mr, W) // 7
         out = []
         for s_ in range(world):
             for P_, k in ((A, 4), (Nn, 3)):
-                blk = torch.zeros(mr, W, k, device=dev)
+                blk = torch.zeros(Pm * k, device=dev)
                 rows = P_[s_::world]
-                blk[:rows.shape[0]] = rows
-                out.append(blk.reshape(-1))
+                blk[:rows.shape[0] * W * k] = rows.reshape(-1)
+                out.append(blk)
         return torch.cat(out)
 
     part = b.alloc(world * mr * W * 3)
@@ -105,7 +108,7 @@ def run(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None):
     st = r.stats()
     ni = max(1, st.timed_iterations)
     passes = {name: round(st.pass_ms[i] / ni, 3) for i, name in enumerate(_abi.PASS_NAMES) if st.pass_ms[i] > 0}
-    allgather_mb = world * mr * W * 4 * multigpu.HP_EXPORT_FLOATS / 1e6
+    allgather_mb = world * 4 * multigpu.hp_export_floats(mr, W) / 1e6
     rs_mb = world * mr * W * 12 / 1e6
     r.destroy()
     full.destroy()
@@ -130,8 +133,8 @@ def run_slab(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None, nb=mult
         b.enable_slab()
         shards.append(b)
     mr = (H + world - 1) // world
-    hps = [b.alloc(mr * W * multigpu.HP_EXPORT_FLOATS) for b in shards]
-    hp_all = shards[0].alloc(world * mr * W * multigpu.HP_EXPORT_FLOATS)
+    hps = [b.alloc(multigpu.hp_export_floats(mr, W)) for b in shards]
+    hp_all = shards[0].alloc(world * multigpu.hp_export_floats(mr, W))
     part = shards[0].alloc(world * mr * W * 3)
     names = ("local", "hist_pack", "import_grid", "gather", "finish")
     tot = [dict.fromkeys(names, 0.0) for _ in range(world)]

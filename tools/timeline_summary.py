@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Concurrency summary of a rocprofv3 --kernel-trace database of the pipelined bench (tools/gpu_r04_timeline.sh):
+"""Concurrency summary of a rocprofv3 --kernel-trace database of the pipelined bench (tools/gpu.sh timeline):
 the last N photon-pass iterations, how much of that wall time 0/1/2/3 kernels run, and each kernel's wall time
 per iteration.  Usage: timeline_summary.py run_results.db [iterations]"""
 import collections
