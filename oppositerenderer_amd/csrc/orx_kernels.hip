@@ -1514,6 +1514,7 @@ __global__ __launch_bounds__(256, 7) void k_ppm_gather_union(GatherIn gi, Photon
                 }
                 const uint32_t A0 = wave_min_u32(a0), A1 = wave_max_u32(a1);
                 if (A0 > A1) continue;
+                if (l == 0) ORX_TS_INC(ts_wl, 1); /* trav stats: sub-rows a wave walks */
                 const uint32_t* so = pb.subofs + ((size_t)rowc * NSUB + sr) * g.gx * SUBX;
                 const uint32_t U0 = so[A0], U1 = so[A1 + 1]; /* uniform: scalar loads */
                 if (U0 >= U1) continue;
@@ -1565,6 +1566,7 @@ __global__ __launch_bounds__(256, 7) void k_ppm_gather_union(GatherIn gi, Photon
     atomicAdd((unsigned long long*)&pb.grid->st_lane_batches, (unsigned long long)ts_nodes);
     atomicAdd((unsigned long long*)&pb.grid->st_wave_batches, (unsigned long long)ts_wn);
     atomicAdd((unsigned long long*)&pb.grid->st_lane_rows, (unsigned long long)ts_leaves);
+    atomicAdd((unsigned long long*)&pb.grid->st_wave_rows, (unsigned long long)ts_wl);
     atomicAdd((unsigned long long*)&pb.grid->st_accepted, (unsigned long long)ts_tris);
 #endif
     if (live) {

@@ -13,6 +13,7 @@ configs[2] hall 1080p with a 2048^2 photon launch (default), configs[4] conferen
 with 4096^2."""
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -208,7 +209,146 @@ def run_slab(world, W=1920, H=1080, P=2048, iters=6, warm=2, scene=None, nb=mult
     return per_rank, slowest, a2a_mb, int(axis), counts
 
 
+def full_hitpoints(scene, W, H, world, n_iters, dev, req):
+    """The full image's exported hit points of iterations 0 .. n_iters-1 (an unsharded renderer's eye
+    pass, its radius sequence), each rearranged into the N ranks' row-interleaved segments: what the
+    all-gather delivers to every rank.  Computed before any timing."""
+    full = OptixRenderer(_abi.default_config(seed=SEED + 1, photon_launch_width=16, photon_launch_height=16))
+    full.initialize(0)
+    full.initScene(scene)
+    fb = multigpu.DeviceShard(full, torch, dev)
+    fhp = fb.alloc(multigpu.hp_export_floats(H, W))
+    mr = (H + world - 1) // world
+    P1, Pm = multigpu.hp_export_floats(H, W) // 7, multigpu.hp_export_floats(mr, W) // 7
+    out = []
+    radius = scene.initial_ppm_radius()
+    for it in range(n_iters):
+        fb.local_passes(it, it, radius, req)
+        fb.export_hitpoints(fhp)
+        A = fhp[:H * W * 4].view(H, W, 4)
+        Nn = fhp[P1 * 4:P1 * 4 + H * W * 3].view(H, W, 3)
+        seg = []
+        for s_ in range(world):
+            for P_, k in ((A, 4), (Nn, 3)):
+                blk = torch.zeros(Pm * k, device=dev)
+                rows = P_[s_::world]
+                blk[:rows.shape[0] * W * k] = rows.reshape(-1)
+                seg.append(blk)
+        out.append(torch.cat(seg))
+        radius = next_ppm_radius(radius, it)
+    torch.cuda.synchronize()
+    full.destroy()
+    return out
+
+
+def run_pipelined(world, W=1920, H=1080, P=2048, warm=4, steps=32, scene=None):
+    """Rank 0 of N in the pipelined row-partition schedule ShardedPPM(pipeline=True) runs
+    (multigpu.py): per iteration the local eye pass and hit-point export on the compute stream, an
+    event standing for the all-gather's completion (work.wait()), the local photon pass + grid
+    build (+ the own rows' direct pass on the renderer's aux stream), and on the side stream the
+    gather of ALL W*H hit points (the full image's, precomputed per iteration) against the local
+    photons, the own block's copy (the reduce-scatter's place) and the finish -- so the gather of
+    iteration i runs beside iteration i+1's local passes, as on the real ranks.  The iteration
+    window is the bench's (warmup `warm`, `steps` timed iterations, the global radius sequence), and
+    the wall time between two synchronisations gives the per-rank frame without the collectives."""
+    dev = torch.device("cuda", 0)
+    scene = scene or synthetic.synthetic_hall()
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    req = RenderRequestDetails(cam, scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W, H).to_abi()
+    n = warm + steps
+    hps = full_hitpoints(scene, W, H, world, n, dev, req)
+    radii = multigpu.radius_sequence(scene.initial_ppm_radius(), n)
+    r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P))
+    r.initialize(0)
+    r.set_shard(0, world)
+    r.initScene(scene)
+    b = multigpu.DeviceShard(r, torch, dev)
+    side = torch.cuda.Stream(dev)
+    b.enable_pipeline(side)
+    main = torch.cuda.current_stream(dev)
+    mr = (H + world - 1) // world
+    sets = [(b.alloc(multigpu.hp_export_floats(mr, W)), b.alloc(world * mr * W * 3), b.alloc(mr * W * 3))
+            for _ in range(2)]
+
+    def step(it):
+        hp_loc, part, own = sets[it % 2]
+        b.local_eye(it, it, radii[it], req)
+        b.export_hitpoints(hp_loc)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        b.local_photons()
+        with torch.cuda.stream(side):
+            side.wait_event(ready)
+            b.gather_external(hps[it], world, part)
+            own.copy_(part[:mr * W * 3])
+            b.finish(own)
+
+    for it in range(warm):
+        step(it)
+    torch.cuda.synchronize()
+    r.reset_timing()
+    t0 = time.perf_counter()
+    for it in range(warm, n):
+        step(it)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    st = r.stats()
+    ni = max(1, st.timed_iterations)
+    passes = {name: round(st.pass_ms[i] / ni, 3) for i, name in enumerate(_abi.PASS_NAMES) if st.pass_ms[i] > 0}
+    allgather_mb = world * 4 * multigpu.hp_export_floats(mr, W) / 1e6
+    rs_mb = world * mr * W * 12 / 1e6
+    r.destroy()
+    del hps
+    torch.cuda.empty_cache()
+    return ms, passes, allgather_mb, rs_mb
+
+
+def run_single_pipelined(W=1920, H=1080, P=2048, warm=4, steps=32, scene=None):
+    """The single-device frame the bench ships (bench.py's schedule: renderNextIteration pipelined,
+    same iteration window): the reference point of the strong-scaling speed-up."""
+    scene = scene or synthetic.synthetic_hall()
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    det = RenderRequestDetails(cam, scene.name, _abi.PROGRESSIVE_PHOTON_MAPPING, W, H)
+    r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P))
+    r.initialize(0)
+    r.initScene(scene)
+    radii = multigpu.radius_sequence(scene.initial_ppm_radius(), warm + steps)
+    for it in range(warm):
+        r.renderNextIteration(it, it, radii[it], False, det)
+    r.stats()
+    t0 = time.perf_counter()
+    for it in range(warm, warm + steps):
+        r.renderNextIteration(it, it, radii[it], False, det)
+    r.stats()
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    r.destroy()
+    return ms
+
+
 if __name__ == "__main__":
+    if "--pipelined" in sys.argv:
+        # pipelined per-rank schedule against the single-device pipelined frame (bench iteration window)
+        args = [a for a in sys.argv[1:] if a != "--pipelined"]
+        conf = 2
+        if args[:1] == ["--config"]:
+            conf, args = int(args[1]), args[2:]
+        worlds = [int(v) for v in args] or [1, 2, 4, 8]
+        kw = (dict(W=3840, H=2160, P=4096, warm=2, steps=8, scene=synthetic.synthetic_conference()) if conf == 4
+              else dict(warm=4, steps=32))
+        print(f"configs[{conf}] pipelined, iterations {kw['warm']}..{kw['warm'] + kw['steps'] - 1} (the bench's window)",
+              flush=True)
+        single = run_single_pipelined(**kw)
+        print(f"single device, bench schedule: {single:.3f} ms/frame", flush=True)
+        for n in worlds:
+            ms, passes, ag, rs = run_pipelined(n, **kw)
+            one, alll = collectives_ms(ag, rs, n)
+            lo, hi = max(ms, alll), ms + one
+            print(f"N={n}: per-rank pipelined frame {ms:.3f} ms (collectives not run) | all-gather {ag:.0f} MB, "
+                  f"reduce-scatter {rs:.0f} MB; exchange {one:.3f} ms on one link, {alll:.3f} ms over {max(1, n - 1)} "
+                  f"links | projected frame {lo:.3f}-{hi:.3f} ms = {single / hi:.2f}-{single / lo:.2f}x the single-device "
+                  f"frame | passes {passes}", flush=True)
+        sys.exit(0)
+
     args = sys.argv[1:]
     conf = 2
     slab = "--slab" in args

@@ -13,6 +13,11 @@ sys.path.insert(0, ROOT)
 from oppositerenderer_amd import _abi, renderer, scenes  # noqa: E402
 
 lib = renderer.load_library(os.path.join(ROOT, "oppositerenderer_amd", "liborx_stats.so"))
+SHARD = 0
+if "--shard" in sys.argv:  # the row partition's gather of rank 0 of N (all W*H hit points, its own photons)
+    k = sys.argv.index("--shard")
+    SHARD = int(sys.argv[k + 1])
+    del sys.argv[k:k + 2]
 lib.orx_trav_stats_read.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
 scene_name = sys.argv[1] if len(sys.argv) > 1 else "SyntheticHall"
 method = {"ppm": 2, "vcm": 1, "pt": 0}[sys.argv[2] if len(sys.argv) > 2 else "ppm"]
@@ -20,6 +25,38 @@ W, H, P = (1920, 1080, 2048) if scene_name.startswith("Synthetic") else (1024, 1
 if len(sys.argv) > 3:  # WxHxP
     W, H, P = (int(v) for v in sys.argv[3].split("x"))
 sc = scenes.scene_by_name(scene_name)
+if SHARD:
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import shard_model
+    from oppositerenderer_amd import multigpu
+    dev = torch.device("cuda", 0)
+    req = renderer.RenderRequestDetails(sc.default_camera.set_aspect_ratio(W / H), sc.name, 2, W, H).to_abi()
+    its = 6
+    hps = shard_model.full_hitpoints(sc, W, H, SHARD, its, dev, req)
+    r = renderer.OptixRenderer(_abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P))
+    r.initialize(0)
+    r.set_shard(0, SHARD)
+    r.initScene(sc)
+    b = multigpu.DeviceShard(r, torch, dev)
+    mr = (H + SHARD - 1) // SHARD
+    part = b.alloc(SHARD * mr * W * 3)
+    buf = (C.c_ulonglong * 21)()
+    radii = multigpu.radius_sequence(sc.initial_ppm_radius(), its)
+    waves = SHARD * mr * W / 64
+    for it in range(its):
+        b.local_passes(it, it, radii[it], req)
+        assert lib.orx_trav_stats_read(r._h, buf, 1) == 0  # drop the local passes' counts
+        b.gather_external(hps[it], SHARD, part)
+        torch.cuda.synchronize()
+        assert lib.orx_trav_stats_read(r._h, buf, 1) == 0
+        v = list(buf)
+        lc, up, nr, wr = v[12], v[13], v[14], v[15]
+        print(f"it{it} shard 0/{SHARD} gather: lane candidates/px {lc / (W * H):8.2f}  union photons/wave {up / waves:8.1f}"
+              f"  union factor {64 * up / max(1, lc):5.2f}  lane sub-rows/px {nr / (W * H):6.2f}"
+              f"  wave sub-rows/wave {wr / waves:6.2f}  union photons per wave sub-row {up / max(1, wr):6.1f}", flush=True)
+    sys.exit(0)
 r = renderer.OptixRenderer(_abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P))
 r.initialize(0)
 r.initScene(sc)
