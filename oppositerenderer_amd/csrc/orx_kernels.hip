@@ -1395,6 +1395,7 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
     }
 }
 
+
 /* Photons are broadcast through the wave's LDS image (union_chunk_lds), with the chord test
  * dropped on sub-rows where no lane's chord is cut by its window.  (A v_readlane broadcast from
  * the chunk registers measured 2.81 ms against 1.91 on the serial hall gather, 16x4 and 4x16
@@ -1518,6 +1519,7 @@ __global__ __launch_bounds__(256, 7) void k_ppm_gather_union(GatherIn gi, Photon
                 const uint32_t* so = pb.subofs + ((size_t)rowc * NSUB + sr) * g.gx * SUBX;
                 const uint32_t U0 = so[A0], U1 = so[A1 + 1]; /* uniform: scalar loads */
                 if (U0 >= U1) continue;
+                if (l == 0) ORX_TS_INC(ts_tris, 1); /* trav stats (union kernel): sub-rows with photons */
                 /* this lane's candidates [lo, lo + len): needed only on sub-rows where some lane's
                  * chord is cut (two scattered loads) */
 #ifdef ORX_TRAV_STATS

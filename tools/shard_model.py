@@ -342,11 +342,23 @@ if __name__ == "__main__":
         for n in worlds:
             ms, passes, ag, rs = run_pipelined(n, **kw)
             one, alll = collectives_ms(ag, rs, n)
+            # overlap-aware: the all-gather of iteration i runs beside its photon pass + grid build, the
+            # reduce-scatter (side stream, after the gather) beside the next iteration's eye + photon
+            # passes; only what outlasts those windows is exposed.  One link (a single ring), the slowest case.
+            ag1 = ag * (n - 1) / n * 1e6 / (XGMI_LINK_GBS * 1e9) * 1e3 if n > 1 else 0.0
+            rs1 = rs * (n - 1) / n * 1e6 / (XGMI_LINK_GBS * 1e9) * 1e3 if n > 1 else 0.0
+            grid = sum(passes.get(k, 0.0) for k in ("grid_hash", "grid_scan", "grid_scatter"))
+            win_ag = passes.get("ppm_photon", 0.0) + grid
+            win_rs = passes.get("ppm_eye", 0.0) + passes.get("ppm_photon", 0.0)
+            exposed = max(0.0, ag1 - win_ag) + max(0.0, rs1 - win_rs)
+            ov = ms + exposed
             lo, hi = max(ms, alll), ms + one
             print(f"N={n}: per-rank pipelined frame {ms:.3f} ms (collectives not run) | all-gather {ag:.0f} MB, "
-                  f"reduce-scatter {rs:.0f} MB; exchange {one:.3f} ms on one link, {alll:.3f} ms over {max(1, n - 1)} "
-                  f"links | projected frame {lo:.3f}-{hi:.3f} ms = {single / hi:.2f}-{single / lo:.2f}x the single-device "
-                  f"frame | passes {passes}", flush=True)
+                  f"reduce-scatter {rs:.0f} MB; one link: all-gather {ag1:.3f} ms beside photon+grid {win_ag:.3f} ms, "
+                  f"reduce-scatter {rs1:.3f} ms beside eye+photon {win_rs:.3f} ms -> exposed {exposed:.3f} ms; "
+                  f"projected frame {ov:.3f} ms overlapped on one link = {single / ov:.2f}x the single-device frame "
+                  f"(bounds: {lo:.3f} ms all {max(1, n - 1)} links hidden, {hi:.3f} ms one link nothing overlapped = "
+                  f"{single / hi:.2f}-{single / lo:.2f}x) | passes {passes}", flush=True)
         sys.exit(0)
 
     args = sys.argv[1:]

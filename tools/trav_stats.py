@@ -7,12 +7,13 @@ import os
 import sys
 
 import numpy as np
+import torch  # noqa: F401  (torch's HIP runtime before liborx's first HIP call, as tests/conftest.py)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from oppositerenderer_amd import _abi, renderer, scenes  # noqa: E402
 
-lib = renderer.load_library(os.path.join(ROOT, "oppositerenderer_amd", "liborx_stats.so"))
+lib = renderer.load_library(os.environ.get("ORX_STATS_LIB") or os.path.join(ROOT, "oppositerenderer_amd", "liborx_stats.so"))
 SHARD = 0
 if "--shard" in sys.argv:  # the row partition's gather of rank 0 of N (all W*H hit points, its own photons)
     k = sys.argv.index("--shard")
@@ -26,8 +27,6 @@ if len(sys.argv) > 3:  # WxHxP
     W, H, P = (int(v) for v in sys.argv[3].split("x"))
 sc = scenes.scene_by_name(scene_name)
 if SHARD:
-    import torch
-
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import shard_model
     from oppositerenderer_amd import multigpu
@@ -55,7 +54,8 @@ if SHARD:
         lc, up, nr, wr = v[12], v[13], v[14], v[15]
         print(f"it{it} shard 0/{SHARD} gather: lane candidates/px {lc / (W * H):8.2f}  union photons/wave {up / waves:8.1f}"
               f"  union factor {64 * up / max(1, lc):5.2f}  lane sub-rows/px {nr / (W * H):6.2f}"
-              f"  wave sub-rows/wave {wr / waves:6.2f}  union photons per wave sub-row {up / max(1, wr):6.1f}", flush=True)
+              f"  wave sub-rows/wave {wr / waves:6.2f} (with photons {v[16] / waves:6.2f})"
+              f"  union photons per non-empty wave sub-row {up / max(1, v[16]):6.1f}", flush=True)
     sys.exit(0)
 r = renderer.OptixRenderer(_abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P))
 r.initialize(0)
@@ -78,7 +78,8 @@ for it in range(3):
           + " ".join(f"{v[17 + q] / max(1, v[1]):5.3f}" for q in range(4)))
     if method == 2:  # the union gather (single device)
         lc, up, nr = v[12], v[13], v[14]
+        waves = W * H / 64
         print(f"it{it} union    lane candidates/px {lc / (W * H):8.1f}  union photons/px {64 * up / (W * H):8.1f}"
-              f"  union factor {64 * up / max(1, lc):5.2f}  accepted/px {v[16] / (W * H):7.1f}"
-              f"  lane sub-rows/px {nr / (W * H):6.1f}")
+              f"  union factor {64 * up / max(1, lc):5.2f}  lane sub-rows/px {nr / (W * H):6.1f}"
+              f"  wave sub-rows/wave {v[15] / waves:6.2f} (with photons {v[16] / waves:6.2f})")
 print("bvh stack entries", r.stats().bvh_stack_entries)
