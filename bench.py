@@ -319,10 +319,16 @@ def launch_ranks(n, argv):
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))  # inherited by the ranks (see below)
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus > 1 or world > 1 or args.force_sharded:
+        # before the first HIP call: the pipelined row partition runs five streams at once (torch's compute
+        # stream, the renderer's aux stream, the gather side stream, RCCL's); with HIP's default of 4
+        # hardware queues the side stream could share the compute stream's queue and the two serialise
+        # (configs[4] N=8 per-rank frame 8.05 against 6.56 ms with 8 queues, tools/shard_model.py --pipelined)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
         from oppositerenderer_amd import multigpu
         return multigpu.bench_main(args, METRIC, cpu_baseline=None if args.no_cpu_baseline else cpu_baseline)
 

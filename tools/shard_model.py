@@ -15,6 +15,12 @@ import os
 import sys
 import time
 
+# the pipelined schedule runs five streams at once (compute, the renderer's aux stream, the gather side
+# stream, and in the bench RCCL's): with HIP's default of 4 hardware queues the gather shared the compute
+# stream's queue and the per-rank frame serialised (configs[4] N=8: 8.05 against 6.56 ms with 8 queues)
+os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))  # before torch loads HIP
+
+
 import numpy as np
 import torch
 
@@ -258,7 +264,8 @@ def run_pipelined(world, W=1920, H=1080, P=2048, warm=4, steps=32, scene=None):
     n = warm + steps
     hps = full_hitpoints(scene, W, H, world, n, dev, req)
     radii = multigpu.radius_sequence(scene.initial_ppm_radius(), n)
-    r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P))
+    gv = int(os.environ.get("MODEL_GATHER_VARIANT", "0"))  # 1: cell order, 2: sub-rows (0: the renderer's choice)
+    r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=P, photon_launch_height=P, gather_variant=gv))
     r.initialize(0)
     r.set_shard(0, world)
     r.initScene(scene)

@@ -19,6 +19,11 @@ if "--shard" in sys.argv:  # the row partition's gather of rank 0 of N (all W*H 
     k = sys.argv.index("--shard")
     SHARD = int(sys.argv[k + 1])
     del sys.argv[k:k + 2]
+GV = 0
+if "--variant" in sys.argv:  # orx_config.gather_variant: 1 cell order, 2 sub-rows (0: the renderer's choice)
+    k = sys.argv.index("--variant")
+    GV = int(sys.argv[k + 1])
+    del sys.argv[k:k + 2]
 lib.orx_trav_stats_read.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
 scene_name = sys.argv[1] if len(sys.argv) > 1 else "SyntheticHall"
 method = {"ppm": 2, "vcm": 1, "pt": 0}[sys.argv[2] if len(sys.argv) > 2 else "ppm"]
@@ -34,7 +39,8 @@ if SHARD:
     req = renderer.RenderRequestDetails(sc.default_camera.set_aspect_ratio(W / H), sc.name, 2, W, H).to_abi()
     its = 6
     hps = shard_model.full_hitpoints(sc, W, H, SHARD, its, dev, req)
-    r = renderer.OptixRenderer(_abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P))
+    r = renderer.OptixRenderer(_abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P,
+                                                   gather_variant=GV))
     r.initialize(0)
     r.set_shard(0, SHARD)
     r.initScene(sc)
