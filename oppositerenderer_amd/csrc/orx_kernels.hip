@@ -1407,8 +1407,11 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
  * the extra waves hide more of the load latency than the prefetch did: 4K conference serial
  * gather 26.2 -> 24.7 ms at 6 waves, 24.2 at 7; configs[4] 8-rank gather 6.39 -> 6.01 ms; hall
  * unchanged.  The cell-order instance spills 8 VGPRs outside the batch loop. */
+#ifndef ORX_UNION_WAVES
+#define ORX_UNION_WAVES 7 /* waves per SIMD the union gather is register-capped for (at 8 it spills 37-49 VGPRs) */
+#endif
 template <uint32_t NSUB>
-__global__ __launch_bounds__(256, 7) void k_ppm_gather_union(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
+__global__ __launch_bounds__(256, ORX_UNION_WAVES) void k_ppm_gather_union(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
                                                           uint32_t ntiles) {
     __shared__ float ulds[4][7 * 64];
     const uint32_t tid = threadIdx.x, w = tid >> 6, l = tid & 63;
