@@ -1025,12 +1025,25 @@ __device__ __forceinline__ v2f weight2u(v2f u) {
     p = __builtin_elementwise_fma(p, u, v2f{ORX_W5_C1, ORX_W5_C1});
     return __builtin_elementwise_fma(p, u, v2f{ORX_W5_C0, ORX_W5_C0});
 }
-/* int8 facing prefilter dot product: v_dot4_i32_i8 with the inline 0 accumulator (the builtin
- * selects v_dot4c_i32_i8, whose accumulator costs a v_mov per use) */
-__device__ __forceinline__ int32_t sdot4_0(int32_t a, int32_t b) {
-    int32_t r;
-    asm("v_dot4_i32_i8 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
-    return r;
+/* int8 facing prefilter dot products of four photons' direction words with the hit point's nq.
+ * gfx950 runs v_dot* like its matrix-core instructions: another VALU instruction may read a dot's
+ * result only three wait states after it.  The compiler pads the instructions it emits but not
+ * those inside inline assembly, so the four dots and the wait states are one asm block (outputs
+ * early-clobbered: no dot overwrites a word a later one reads), with the inline 0 accumulator (the
+ * builtin selects v_dot4c_i32_i8, whose accumulator costs a v_mov per dot: hall 1026 -> 1020
+ * Mpaths/s).  A single-dot asm statement was correct only while the scheduler happened to put
+ * three instructions between each dot and its compare; the two-hit-point gather variant's schedule
+ * read a result one instruction later and dropped photons (profiles/r05h_gather_two_hitpoints_ab.txt).
+ * tests/test_asm_hazards.py checks every inline dot of the compiled kernels. */
+__device__ __forceinline__ void sdot4x4(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int32_t nq, int32_t& q0,
+                                        int32_t& q1, int32_t& q2, int32_t& q3) {
+    asm("v_dot4_i32_i8 %0, %4, %8, 0\n\t"
+        "v_dot4_i32_i8 %1, %5, %8, 0\n\t"
+        "v_dot4_i32_i8 %2, %6, %8, 0\n\t"
+        "v_dot4_i32_i8 %3, %7, %8, 0\n\t"
+        "s_nop 2"
+        : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3)
+        : "v"(w0), "v"(w1), "v"(w2), "v"(w3), "v"(nq));
 }
 
 constexpr uint32_t GQ = 8; /* chord ranges per lane per phase A (LDS: GQ * 8 B per lane) */
@@ -1189,8 +1202,8 @@ __global__ __launch_bounds__(256, ORX_GATHER_LANE_WAVES) void k_ppm_gather(Gathe
             if (!(in0 | in1 | in2 | in3)) continue;
             /* facing: dot(-dir, n) >= 0  <=>  dot(dir, n) <= 0 (negation is exact) */
             const u4v Q = __builtin_amdgcn_raw_buffer_load_b128(SR, (int)bo, (int)(SP_DIRQ * PB), 0);
-            const int32_t q0 = sdot4_0((int32_t)Q.x, nq), q1 = sdot4_0((int32_t)Q.y, nq);
-            const int32_t q2 = sdot4_0((int32_t)Q.z, nq), q3 = sdot4_0((int32_t)Q.w, nq);
+            int32_t q0, q1, q2, q3;
+            sdot4x4(Q.x, Q.y, Q.z, Q.w, nq, q0, q1, q2, q3);
             in0 = in0 && q0 <= DIRQ_BAND;
             in1 = in1 && q1 <= DIRQ_BAND;
             in2 = in2 && q2 <= DIRQ_BAND;
@@ -1361,8 +1374,8 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
         }
         if (!wave_any(in0 | in1 | in2 | in3)) continue;
         const uint4 Q = reinterpret_cast<const uint4*>(L4)[48 + (e >> 2)];
-        const int32_t q0 = sdot4_0((int32_t)Q.x, k.nq), q1 = sdot4_0((int32_t)Q.y, k.nq);
-        const int32_t q2 = sdot4_0((int32_t)Q.z, k.nq), q3 = sdot4_0((int32_t)Q.w, k.nq);
+        int32_t q0, q1, q2, q3;
+        sdot4x4(Q.x, Q.y, Q.z, Q.w, k.nq, q0, q1, q2, q3);
         in0 = in0 && q0 <= DIRQ_BAND;
         in1 = in1 && q1 <= DIRQ_BAND;
         in2 = in2 && q2 <= DIRQ_BAND;
