@@ -371,11 +371,14 @@ def main():
     # pipelined PPM: the gather and output run on a side stream beside the next iteration's
     # passes, so every pass time is wall time under interference; a few serial iterations after
     # the timed region give each pass's stand-alone time
-    pipelined = method == _abi.PROGRESSIVE_PHOTON_MAPPING and r.pipelined()
+    pipelined = r.pipelined()
     # pipelined (single device): gather + output of iteration i beside iteration i+1's passes, the
     # direct pass beside the grid build, and the eye pass of i+1 on the direct pass's stream beside
     # the grid build of i, so the chain per frame is photon pass + grid build
-    overlapped = ["ppm_eye", "ppm_gather", "ppm_direct_output"] if pipelined else []
+    # VCM: the deferred shadow rays and colours of iteration i beside the light pass and camera
+    # subpaths of i+1
+    overlapped = ([] if not pipelined else ["ppm_eye", "ppm_gather", "ppm_direct_output"]
+                  if method == _abi.PROGRESSIVE_PHOTON_MAPPING else ["vcm_shadow"])
     serial = None
     if pipelined and not args.no_serial_pass_times:
         r.set_iteration_pipelining(0)
@@ -394,7 +397,8 @@ def main():
     light_vertices = 0
     if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING:
         light_vertices = int(np.minimum(r.read_buffer(_abi.BUF_VCM_VERTEX_COUNT, np.uint32), 9).sum())
-    pbytes = roofline.pass_bytes(method, W, H, P * P, valid_avg, st.num_cells, light_vertices, photon_map=pmap)
+    pbytes = roofline.pass_bytes(method, W, H, P * P, valid_avg, st.num_cells, light_vertices, photon_map=pmap,
+                                 vcm_entries=st.vcm_shadow_rays if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING else 0)
     key = (f"{scene.name}:{W}x{H}:{args.method}" + (f":P{P}" if method == 2 else "")
            + (f":{args.photon_map}" if pmap else ""))
     dominant, roof = roofline_block(per_pass, pbytes, key, pmap, serial, overlapped)

@@ -256,8 +256,9 @@ typedef enum {
     ORX_PASS_PPM_DIRECT = 6,   /* PPM_DIRECT_RADIANCE_ESTIMATION_PASS + PPM_OUTPUT_PASS */
     ORX_PASS_PT = 7,           /* PT_RAYTRACE_PASS */
     ORX_PASS_VCM_LIGHT = 8,    /* VCM_LIGHT_PASS */
-    ORX_PASS_VCM_CAMERA = 9,   /* VCM_CAMERA_PASS */
-    ORX_PASS_COUNT = 10
+    ORX_PASS_VCM_CAMERA = 9,   /* VCM_CAMERA_PASS: the camera subpaths and their connections */
+    ORX_PASS_VCM_SHADOW = 10,  /* VCM_CAMERA_PASS, second half: the connections' deferred shadow rays and colours */
+    ORX_PASS_COUNT = 11
 } orx_pass;
 
 typedef struct {
@@ -280,12 +281,13 @@ typedef struct {
 orx_status orx_get_stats(orx_renderer* r, orx_stats* out);
 /* starts a new timed region for orx_get_stats' *_total and pass_ms fields */
 orx_status orx_reset_timing(orx_renderer* r);
-/* 1 if the last PPM iteration ran pipelined: its gather and output pass (ORX_PASS_PPM_GATHER and the
+/* 1 if the last iteration ran pipelined: PPM, its gather and output pass (ORX_PASS_PPM_GATHER and the
  * output half of ORX_PASS_PPM_DIRECT) on a second stream beside the next iteration's eye, photon and
- * grid passes, so their pass_ms are overlapped wall time; 0 otherwise */
+ * grid passes; VCM, its deferred shadow rays and colours (ORX_PASS_VCM_SHADOW) beside the next
+ * iteration's light pass and camera subpaths; so those pass_ms are overlapped wall time; 0 otherwise */
 int orx_ppm_pipelined(const orx_renderer* r);
-/* Single-device PPM iteration pipelining: 1 on, 0 off (serial passes), -1 the ORX_PIPELINE
- * environment default (on).  Takes effect at the next iteration (an outstanding pipelined
+/* Single-device PPM iteration pipelining and VCM shadow-ray overlap: 1 on, 0 off (serial passes), -1
+ * the ORX_PIPELINE environment default (on).  Takes effect at the next iteration (an outstanding pipelined
  * iteration is finished first); images are identical either way. */
 orx_status orx_set_iteration_pipelining(orx_renderer* r, int mode);
 

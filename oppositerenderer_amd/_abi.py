@@ -127,7 +127,7 @@ class OrxStats(C.Structure):
 
 
 PASS_NAMES = ["ppm_eye", "ppm_photon", "grid_hash", "grid_scan", "grid_scatter", "ppm_gather", "ppm_direct_output",
-              "pt", "vcm_light", "vcm_camera"]
+              "pt", "vcm_light", "vcm_camera", "vcm_shadow"]
 
 
 def default_config(**overrides):

@@ -344,7 +344,8 @@ DevCamera camera_setup(const orx_camera& c, float* ulen_out = nullptr, float* vl
     return k;
 }
 
-enum PassId { P_EYE = 0, P_PHOTON, P_SETUP_HASH, P_SCAN, P_SCATTER, P_GATHER, P_DIRECT, P_PT, P_VCM_LIGHT, P_VCM_CAMERA, P_COUNT };
+enum PassId { P_EYE = 0, P_PHOTON, P_SETUP_HASH, P_SCAN, P_SCATTER, P_GATHER, P_DIRECT, P_PT, P_VCM_LIGHT, P_VCM_CAMERA,
+              P_VCM_SHADOW, P_COUNT };
 constexpr int EV_POOL = 1024; /* timed launches kept per pass between resets */
 
 }  // namespace
@@ -428,6 +429,16 @@ struct orx_renderer {
     VcmConsts vcm_c{};
     DevBuf d_vcount, d_vverts, d_vsplat, d_vcam, d_vkd, d_vshq, d_vwork, d_vconst, d_tstats;
     DevBuf d_vdq, d_vdpx, d_vrngsave, d_vshstk; /* VCM camera pass: deferred shadow-ray entries, per-pixel list heads, RNG copy, deep stack */
+    /* VCM overlap (single device, deferred shadow rays): the camera pass's resolve (shadow rays,
+     * colours) of iteration i runs on aux beside the light pass and walk of i+1; the light images and
+     * the entry lists with their control words alternate (d_vsplat2, d_vdq2, d_vdpx2, vcm_dpar),
+     * ev_vcam ends the walk, ev_vacc the resolve, vcm_pend: one in flight */
+    DevBuf d_vsplat2, d_vdq2, d_vdpx2;
+    uint32_t vcm_dpar = 0;
+    bool last_vcm_overlap = false;
+    size_t vcm_dqcap = 0; /* entries per list (ORX_VCM_DEFER per own pixel) */
+    hipEvent_t ev_vcam = nullptr, ev_vacc = nullptr;
+    bool vcm_pend = false;
     std::vector<DevLight> host_lights;
     /* participating medium (cfg.enable_media with a medium box): the box, this frame's per-pixel
      * volumetricRadiance and per-photon last events, the volumetric table of the last photon pass */
@@ -534,6 +545,8 @@ orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out)
         hipEventCreateWithFlags(&r->ev_photon_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_direct_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_eye_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&r->ev_vcam, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&r->ev_vacc, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_main, hipEventDisableTiming) != hipSuccess) {
         delete r;
         return ORX_ERR_DEVICE;
@@ -556,6 +569,8 @@ void orx_destroy(orx_renderer* r) {
     if (r->ev_photon_done) hipEventDestroy(r->ev_photon_done);
     if (r->ev_direct_done) hipEventDestroy(r->ev_direct_done);
     if (r->ev_eye_done) hipEventDestroy(r->ev_eye_done);
+    if (r->ev_vcam) hipEventDestroy(r->ev_vcam);
+    if (r->ev_vacc) hipEventDestroy(r->ev_vacc);
     if (r->ev_main) hipEventDestroy(r->ev_main);
     if (r->aux) hipStreamDestroy(r->aux);
     if (r->stream) hipStreamDestroy(r->stream);
@@ -1132,7 +1147,7 @@ static const char* const PASS_NAME[P_COUNT] = {
     "Creating photon map (grid_scatter)",         "OptixEntryPoint::INDIRECT_RADIANCE_ESTIMATION (ppm_gather)",
     "OptixEntryPoint::PPM_DIRECT_RADIANCE_ESTIMATION_PASS (ppm_direct_output)",
     "OptixEntryPoint::PT_RAYTRACE_PASS (pt)",     "OptixEntryPoint::VCM_LIGHT_PASS (vcm_light)",
-    "OptixEntryPoint::VCM_CAMERA_PASS (vcm_camera)"};
+    "OptixEntryPoint::VCM_CAMERA_PASS (vcm_camera)", "OptixEntryPoint::VCM_CAMERA_PASS (vcm_shadow)"};
 static inline void ev_begin(orx_renderer* r, int p) {
     roctxRangePushA(PASS_NAME[p]);
     if (!r->timing || r->ev_n[p] >= EV_POOL) return;
@@ -1174,8 +1189,17 @@ static inline hipStream_t cur_stream(orx_renderer* r) { return r->use_ext ? r->e
 /* the stream the deferred gather + output run on */
 static inline hipStream_t gather_stream(orx_renderer* r) { return r->shard_pipe ? r->side : r->gstream; }
 
+/* order everything later on the renderer's stream (and the gather stream) after a VCM camera
+ * pass's resolve half still running on aux */
+static void flush_vcm(orx_renderer* r) {
+    if (!r->vcm_pend) return;
+    hipStreamWaitEvent(cur_stream(r), r->ev_vacc, 0);
+    if (r->gstream) hipStreamWaitEvent(r->gstream, r->ev_vacc, 0);
+    r->vcm_pend = false;
+}
 /* order everything later on the renderer's stream after a deferred gather + output */
 static void flush_pipeline(orx_renderer* r) {
+    flush_vcm(r);
     r->eye_chain = false;
     if (!r->pend) return;
     hipStreamWaitEvent(cur_stream(r), r->ev_gdone[r->pp], 0);
@@ -1339,7 +1363,7 @@ static orx_status vol_build(orx_renderer* r, hipStream_t st, float R) {
 
 /* resize / RNG init / output clear common to every method (OptixRenderer.cpp:531-557) */
 static orx_status begin_iteration(orx_renderer* r, uint64_t local_iteration_number, const orx_request* det,
-                                  bool pipelined = false) {
+                                  bool pipelined = false, bool vcm_overlap = false) {
     if (!r->scene_ready) return set_err(r, ORX_ERR_STATE, "Traced before OptixRenderer was initialized.");
     if (det->width == 0 || det->height == 0) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "zero-sized request");
     HIPCHK(r, hipSetDevice(r->device));
@@ -1355,7 +1379,17 @@ static orx_status begin_iteration(orx_renderer* r, uint64_t local_iteration_numb
         if (st != ORX_OK) return st;
         if (r->use_ext) HIPCHK(r, hipStreamSynchronize(r->stream)); /* resize work ran on the own stream */
     }
-    if (!pipelined) flush_pipeline(r);
+    /* an overlapped VCM iteration leaves the last resolve running: its light pass may start beside it */
+    if (!(vcm_overlap && local_iteration_number != 0)) flush_vcm(r);
+    if (!pipelined) {
+        if (vcm_overlap) {
+            r->eye_chain = false;
+            if (r->pend) HIPCHK(r, hipStreamWaitEvent(cur_stream(r), r->ev_gdone[r->pp], 0));
+            r->pend = false;
+        } else {
+            flush_pipeline(r);
+        }
+    }
     r->timed_iterations++;
     /* the output accumulates on the gather stream when pipelined (after the previous output) */
     if (local_iteration_number == 0)
@@ -1526,7 +1560,7 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
                                       vcm_light_waves((uint32_t)((lpx + 63) / 64)));
         HIPCHK(r, r->d_vshq.ensure(waves * VCM_SHQ_PER_WAVE * 16 + 16));
         vb.shq = r->d_vshq.as<float4>();
-        HIPCHK(r, r->d_vwork.ensure(32));
+        HIPCHK(r, r->d_vwork.ensure(64)); /* [0..1] work counters, [4..7] / [8..11] entry-list control words */
         vb.work = r->d_vwork.as<uint32_t>();
         HIPCHK(r, r->d_vconst.ensure(sizeof(VcmConsts)));
         vb.consts = r->d_vconst.as<VcmConsts>();
@@ -1550,6 +1584,7 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
             HIPCHK(r, r->d_vdq.ensure(cap * 49 + 64));
             HIPCHK(r, r->d_vdpx.ensure(lpx * 20 + 64));
             HIPCHK(r, r->d_vrngsave.ensure(nslot * 24 + 16));
+            r->vcm_dqcap = cap;
             vb.dq0 = r->d_vdq.as<float4>();
             vb.dq1 = vb.dq0 + cap;
             vb.dq2 = vb.dq1 + cap;
@@ -1618,10 +1653,35 @@ static orx_status vcm_light(orx_renderer* r) {
     return ORX_OK;
 }
 
-static orx_status vcm_camera(orx_renderer* r) {
+static orx_status vcm_camera(orx_renderer* r, bool overlap = false) {
+    if (!overlap) {
+        hipStream_t st = cur_stream(r);
+        ev_begin(r, P_VCM_CAMERA);
+        launch_vcm_camera_walk(st, r->scene, r->vcm_vb, r->vcm_c);
+        launch_vcm_camera_rerun(st, r->scene, r->vcm_vb, r->vcm_c);
+        ev_end(r, P_VCM_CAMERA);
+        ev_begin(r, P_VCM_SHADOW);
+        launch_vcm_camera_resolve(st, r->scene, r->vcm_vb, r->vcm_c);
+        ev_end(r, P_VCM_SHADOW);
+        return ORX_OK;
+    }
+    /* the walk on the renderer's stream (its entry list is the one the last resolve does not read);
+     * the rerun after an overflow accumulates into the output, so it follows the last resolve; the
+     * resolve on aux, beside the next iteration's light pass and walk (the pass interval ends with
+     * the resolve) */
+    hipStream_t st = cur_stream(r);
     ev_begin(r, P_VCM_CAMERA);
-    launch_vcm_camera(cur_stream(r), r->scene, r->vcm_vb, r->vcm_c);
+    launch_vcm_camera_walk(st, r->scene, r->vcm_vb, r->vcm_c);
     ev_end(r, P_VCM_CAMERA);
+    HIPCHK(r, hipEventRecord(r->ev_vcam, st));
+    if (r->vcm_pend) HIPCHK(r, hipStreamWaitEvent(st, r->ev_vacc, 0));
+    launch_vcm_camera_rerun(st, r->scene, r->vcm_vb, r->vcm_c);
+    HIPCHK(r, hipStreamWaitEvent(r->aux, r->ev_vcam, 0));
+    ev_begin_on(r, P_VCM_SHADOW, r->aux);
+    launch_vcm_camera_resolve(r->aux, r->scene, r->vcm_vb, r->vcm_c);
+    ev_end_on(r, P_VCM_SHADOW, r->aux);
+    HIPCHK(r, hipEventRecord(r->ev_vacc, r->aux));
+    r->vcm_pend = true;
     return ORX_OK;
 }
 
@@ -1632,11 +1692,33 @@ static orx_status vcm_check_lights(orx_renderer* r) {
     return ORX_OK;
 }
 
-static orx_status vcm_iteration(orx_renderer* r, const orx_request* det, float ppm_radius) {
+static orx_status vcm_iteration(orx_renderer* r, const orx_request* det, float ppm_radius, bool overlap = false) {
     orx_status s = vcm_prepare(r, det, ppm_radius);
     if (s != ORX_OK) return s;
+    overlap = overlap && r->vcm_vb.dq0;
+    if (overlap) { /* this iteration's light image and entry list: the ones the last resolve does not read */
+        HIPCHK(r, r->d_vsplat2.ensure(r->d_vsplat.bytes));
+        HIPCHK(r, r->d_vdq2.ensure(r->d_vdq.bytes));
+        HIPCHK(r, r->d_vdpx2.ensure(r->d_vdpx.bytes));
+        swap_buf(r->d_vsplat, r->d_vsplat2);
+        swap_buf(r->d_vdq, r->d_vdq2);
+        swap_buf(r->d_vdpx, r->d_vdpx2);
+        r->vcm_dpar ^= 1u;
+        VcmBufs& vb = r->vcm_vb;
+        vb.splat = r->d_vsplat.as<float>();
+        vb.splat_in = vb.splat + (size_t)r->rank * r->max_rows * r->W * 3;
+        const size_t cap = r->vcm_dqcap;
+        vb.dq0 = r->d_vdq.as<float4>();
+        vb.dq1 = vb.dq0 + cap;
+        vb.dq2 = vb.dq1 + cap;
+        vb.docc = (uint8_t*)(vb.dq2 + cap);
+        vb.demis = r->d_vdpx.as<float4>();
+        vb.dhead = (uint32_t*)(vb.demis + (size_t)r->W * r->rows);
+        vb.dctl = vb.work + (r->vcm_dpar ? 8 : 4);
+    }
     if ((s = vcm_light(r)) != ORX_OK) return s;
-    return vcm_camera(r);
+    r->last_vcm_overlap = overlap;
+    return vcm_camera(r, overlap);
 }
 
 /* One PPM iteration whose gather and output are left running on gstream, overlapping the next
@@ -1727,7 +1809,15 @@ static orx_status render_next_iteration(orx_renderer* r, uint64_t local_iteratio
     const int pipe_on = r->pipe_mode >= 0 ? r->pipe_mode : pipeline_env;
     const bool pipelined = pipe_on && det->method == ORX_METHOD_PROGRESSIVE_PHOTON_MAPPING && r->world == 1 &&
                            !r->use_ext && !r->media;
-    orx_status s0 = begin_iteration(r, local_iteration_number, det, pipelined);
+    /* VCM: the camera pass's resolve half beside the next light pass (ORX_VCM_OVERLAP=0: serial) */
+    static const int vcm_overlap_env = [] {
+        const char* e = getenv("ORX_VCM_OVERLAP");
+        return e ? atoi(e) : 1;
+    }();
+    const bool vcm_overlap = pipe_on && vcm_overlap_env && det->method == ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING &&
+                             r->world == 1 && !r->use_ext;
+    orx_status s0 = begin_iteration(r, local_iteration_number, det, pipelined, vcm_overlap);
+    r->last_vcm_overlap = false;
     if (s0 != ORX_OK) return s0;
     if (pipelined && (s0 = ensure_second_set(r)) != ORX_OK) return s0;
     r->last_pipelined = pipelined && r->pipe_bufs;
@@ -1741,7 +1831,7 @@ static orx_status render_next_iteration(orx_renderer* r, uint64_t local_iteratio
         launch_pt(st, r->scene, cam, r->px, c);
         ev_end(r, P_PT);
     } else if (det->method == ORX_METHOD_VCM_BIDIRECTIONAL_PATH_TRACING) {
-        orx_status sv = vcm_iteration(r, det, ppm_radius);
+        orx_status sv = vcm_iteration(r, det, ppm_radius, vcm_overlap);
         if (sv != ORX_OK) return sv;
     } else {
         /* the direct pass on the aux stream beside the grid build and the gather; the output
@@ -2415,7 +2505,7 @@ orx_status orx_get_stats(orx_renderer* r, orx_stats* out) {
     return check_grid_error(r);
 }
 
-int orx_ppm_pipelined(const orx_renderer* r) { return r && r->last_pipelined ? 1 : 0; }
+int orx_ppm_pipelined(const orx_renderer* r) { return r && (r->last_pipelined || r->last_vcm_overlap) ? 1 : 0; }
 orx_status orx_set_iteration_pipelining(orx_renderer* r, int mode) {
     if (!r || mode < -1 || mode > 1) return ORX_ERR_INVALID_ARGUMENT;
     r->pipe_mode = mode;

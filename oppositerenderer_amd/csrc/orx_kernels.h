@@ -360,6 +360,11 @@ struct VcmConsts {
 };
 void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c, bool estimate);
 void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c);
+/* its parts, in this order: the walk (RNG, light vertices, constants), the rerun after an entry-list overflow,
+ * the resolve (deferred shadow rays, colours) */
+void launch_vcm_camera_walk(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c);
+void launch_vcm_camera_rerun(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c);
+void launch_vcm_camera_resolve(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c);
 uint32_t vcm_camera_waves(uint32_t tiles); /* persistent camera-pass waves for `tiles` 8x8 tiles */
 uint32_t vcm_light_waves(uint32_t items);  /* persistent light-pass waves for `items` 64-subpath items */
 

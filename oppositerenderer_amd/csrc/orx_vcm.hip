@@ -1310,8 +1310,13 @@ static void launch_camera_kernel(hipStream_t s, const DevScene& S, const VcmBufs
  * rays (k_vcm_shadow), the colours (k_vcm_accum).  Should the entry list overflow (more than
  * vb.dcap connections in all, ORX_VCM_DEFER per own pixel), the pass is redone with the shadow rays traced in
  * place from the saved RNG planes (k_vcm_rng_restore, k_vcm_camera<., 2>); both exit at once
- * otherwise.  vb.dq0 == NULL: in place only. */
-void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
+ * otherwise, as k_vcm_shadow and k_vcm_accum do after an overflow.  vb.dq0 == NULL: in place only.
+ * Three parts: the walk (everything that reads or advances the RNG planes, the light vertices and
+ * the pass constants), the rerun (the in-place pass after an overflow, which accumulates into the
+ * output), and the resolve (the deferred shadow rays and the colours), which reads only the entry
+ * list and control words the walk wrote, the light image (vb.splat_in) and the output it accumulates
+ * into, so it can run beside the next iteration's light pass and walk (orx_capi.hip vcm_camera). */
+void launch_vcm_camera_walk(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
     hipLaunchKernelGGL(k_vcm_consts, dim3(1), dim3(1), 0, s, c, vb.consts);
     const uint32_t blocks = vcm_camera_waves(((c.W + 7) / 8) * ((c.rows + 7) / 8));
     if (blocks == 0) return;
@@ -1324,6 +1329,16 @@ void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, cons
         hipMemcpyAsync(vb.rng_save + (size_t)k * nslot, vb.rng.p[k], (size_t)nslot * 4, hipMemcpyDeviceToDevice, s);
     hipMemsetAsync(vb.dctl, 0, 16, s);
     launch_camera_kernel<1>(s, S, vb, blocks);
+}
+void launch_vcm_camera_rerun(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
+    const uint32_t blocks = vcm_camera_waves(((c.W + 7) / 8) * ((c.rows + 7) / 8));
+    if (blocks == 0 || !vb.dq0) return;
+    const uint32_t nslot = c.rows * vb.RW;
+    hipLaunchKernelGGL(k_vcm_rng_restore, dim3((nslot + 255) / 256), dim3(256), 0, s, vb, nslot);
+    launch_camera_kernel<2>(s, S, vb, blocks);
+}
+void launch_vcm_camera_resolve(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
+    if (!vb.dq0 || c.W == 0 || c.rows == 0) return;
     static const uint32_t cus = [] {
         int dev = 0, n = 256;
         hipGetDevice(&dev);
@@ -1337,8 +1352,11 @@ void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, cons
     const uint32_t sblocks = std::min(cus * std::max(1u, per_cu), vb.shstk_lanes / 64u);
     hipLaunchKernelGGL(k_vcm_shadow, dim3(sblocks), dim3(64), lds, s, S, vb);
     hipLaunchKernelGGL(k_vcm_accum, dim3((c.lcount + 255) / 256), dim3(256), 0, s, vb, c.lcount);
-    hipLaunchKernelGGL(k_vcm_rng_restore, dim3((nslot + 255) / 256), dim3(256), 0, s, vb, nslot);
-    launch_camera_kernel<2>(s, S, vb, blocks);
+}
+void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
+    launch_vcm_camera_walk(s, S, vb, c);
+    launch_vcm_camera_rerun(s, S, vb, c);
+    launch_vcm_camera_resolve(s, S, vb, c);
 }
 
 }  // namespace orx

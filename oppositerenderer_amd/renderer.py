@@ -197,11 +197,13 @@ class OptixRenderer:
         return s
 
     def pipelined(self) -> bool:
-        """Whether the last PPM iteration overlapped its gather + output with the next passes."""
+        """Whether the last iteration overlapped part of its work with the next one's passes (PPM: the
+        gather + output; VCM: the deferred shadow rays + colours)."""
         return bool(self._lib.orx_ppm_pipelined(self._h))
 
     def set_iteration_pipelining(self, mode: int):
-        """Single-device PPM pipelining: 1 on, 0 serial passes, -1 the ORX_PIPELINE default."""
+        """Single-device PPM pipelining and VCM shadow-ray overlap: 1 on, 0 serial passes, -1 the
+        ORX_PIPELINE default."""
         self._check(self._lib.orx_set_iteration_pipelining(self._h, mode))
 
     def reset_timing(self):

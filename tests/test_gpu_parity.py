@@ -584,6 +584,41 @@ def test_method_switches_without_reads():
 
 
 @pytest.mark.gpu
+def test_vcm_shadow_overlap_schedules():
+    """VCM's deferred shadow rays and colours of iteration i run beside the light pass and camera
+    subpaths of i+1 (the light images and entry lists alternate, orx_capi.hip vcm_camera): overlapped
+    iterations, a serial stretch (orx_set_iteration_pipelining(0)), overlap again, a PPM iteration in
+    between and VCM once more, every camera colour and RNG word bit-exact and the output matching the
+    oracle after each step."""
+    scene = scenes.cornell()
+    W, H, P = 48, 40, 64
+    gpu, ora, _ = make_pair(scene, W, H, P, _abi.VCM_BIDIRECTIONAL_PATH_TRACING)
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    radius = scene.initial_ppm_radius()
+    seen = []
+    steps = [(_abi.VCM_BIDIRECTIONAL_PATH_TRACING, 0, -1), (_abi.VCM_BIDIRECTIONAL_PATH_TRACING, 1, -1),
+             (_abi.VCM_BIDIRECTIONAL_PATH_TRACING, 2, -1), (_abi.VCM_BIDIRECTIONAL_PATH_TRACING, 3, 0),
+             (_abi.VCM_BIDIRECTIONAL_PATH_TRACING, 4, 1), (_abi.PROGRESSIVE_PHOTON_MAPPING, 0, -1),
+             (_abi.VCM_BIDIRECTIONAL_PATH_TRACING, 0, -1), (_abi.VCM_BIDIRECTIONAL_PATH_TRACING, 1, -1)]
+    for it, (method, local, mode) in enumerate(steps):
+        gpu.set_iteration_pipelining(mode)
+        det = RenderRequestDetails(cam, scene.name, method, W, H)
+        gpu.renderNextIteration(it, local, radius, True, det)
+        ora.render_next_iteration(it, local, radius, det.to_abi())
+        seen.append(gpu.pipelined())
+        if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING:
+            for buf in (_abi.BUF_RNG, _abi.BUF_VCM_CAMERA):
+                g, o = gpu.read_buffer(buf, np.uint32), ora.read_buffer(buf, np.uint32)
+                assert np.array_equal(g, o), (it, buf, int(np.count_nonzero(g != o)))
+        g, o = gpu.getOutputBuffer(), ora.output()
+        assert rel_l2(g, o) < 1e-5 and g.mean() > 0, (it, rel_l2(g, o))
+        radius = next_ppm_radius(radius, it)
+    assert seen == [True, True, True, False, True, True, True, True], seen
+    gpu.destroy()
+    ora.close()
+
+
+@pytest.mark.gpu
 def test_pipelining_starts_after_other_methods():
     """The second buffer set of PPM pipelining is allocated on the first pipelined iteration, not
     at the resize: PT first (no second set), then PPM at the same size pipelines, then a serial

@@ -88,7 +88,8 @@ def test_bench_schedule_configs2_hall_ppm_six_pipelined_iterations():
 
 
 def test_bench_schedule_configs3_hall_vcm_three_iterations():
-    gpu, ora, _ = _bench_schedule(_abi.VCM_BIDIRECTIONAL_PATH_TRACING, 3)
+    gpu, ora, overlapped = _bench_schedule(_abi.VCM_BIDIRECTIONAL_PATH_TRACING, 3)
+    assert overlapped, "bench.py's VCM schedule overlaps the shadow rays with the next light pass"
     for buf, name in ((_abi.BUF_RNG, "rng"), (_abi.BUF_VCM_CAMERA, "camera colours"),
                       (_abi.BUF_VCM_VERTEX_COUNT, "vertex counts")):
         g, o = gpu.read_buffer(buf, np.uint32), ora.read_buffer(buf, np.uint32)
