@@ -514,8 +514,9 @@ def test_vcm_camera_shadow_modes(defer):
     default, ORX_VCM_DEFER=16 entries per pixel; ~6.5 rays per pixel on the hall), traced in place
     inside the camera kernel (ORX_VCM_DEFER=0), and
     deferred into a list too small for them (1 per pixel: the pass overflows, restores the RNG planes
-    and reruns in place).  Camera colours, RNG and vertex counts bit-exact against the oracle, two
-    iterations back to back, and the overflow flag as expected."""
+    and reruns in place).  Camera colours, RNG and vertex counts bit-exact against the oracle, three
+    iterations back to back (the overlapped schedule cycles both entry lists and light images and
+    reruns each overflow after the previous iteration's colours), and the overflow flag as expected."""
     import subprocess, sys, os, json
     code = r'''
 import json, sys, numpy as np
@@ -532,7 +533,7 @@ ora.init_scene(scene)
 cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
 det = RenderRequestDetails(cam, scene.name, _abi.VCM_BIDIRECTIONAL_PATH_TRACING, W, H)
 r = scene.initial_ppm_radius()
-for it in range(2):
+for it in range(3):
     gpu.renderNextIteration(it, it, r, True, det)
     ora.render_next_iteration(it, it, r, det.to_abi())
     r = next_ppm_radius(r, it)
