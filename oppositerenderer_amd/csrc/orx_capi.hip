@@ -433,7 +433,7 @@ struct orx_renderer {
      * colours) of iteration i runs on aux beside the light pass and walk of i+1; the light images and
      * the entry lists with their control words alternate (d_vsplat2, d_vdq2, d_vdpx2, vcm_dpar),
      * ev_vcam ends the walk, ev_vacc the resolve, vcm_pend: one in flight */
-    DevBuf d_vsplat2, d_vdq2, d_vdpx2;
+    DevBuf d_vsplat2, d_vdq2, d_vdpx2, d_vlcq, d_vlcq2; /* d_vlcq: the light pass's deferred camera connections */
     uint32_t vcm_dpar = 0;
     bool last_vcm_overlap = false;
     size_t vcm_dqcap = 0; /* entries per list (ORX_VCM_DEFER per own pixel) */
@@ -1541,6 +1541,9 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
     }
     VcmBufs& vb = r->vcm_vb;
     vb.RW = r->RW;
+    vb.lcq = nullptr; /* the light pass traces its camera connections itself unless vcm_iteration defers them */
+    vb.lctl = nullptr;
+    vb.lcap = 0;
     vb.rng = r->px.rng;
     vb.vcount = r->d_vcount.as<uint32_t>();
     const size_t plane = lpx * VCM_MAX_VERTS;
@@ -1648,6 +1651,7 @@ static orx_status vcm_light(orx_renderer* r) {
         r->vcm_estimated = true;
     }
     HIPCHK(r, hipMemsetAsync(r->vcm_vb.splat, 0, r->vcm_spx * 12, st));
+    if (r->vcm_vb.lcq) HIPCHK(r, hipMemsetAsync(r->vcm_vb.lctl, 0, 8, st));
     launch_vcm_light(st, r->scene, r->vcm_vb, r->vcm_c, false);
     ev_end(r, P_VCM_LIGHT);
     return ORX_OK;
@@ -1715,6 +1719,23 @@ static orx_status vcm_iteration(orx_renderer* r, const orx_request* det, float p
         vb.demis = r->d_vdpx.as<float4>();
         vb.dhead = (uint32_t*)(vb.demis + (size_t)r->W * r->rows);
         vb.dctl = vb.work + (r->vcm_dpar ? 8 : 4);
+        /* the light pass's camera connections go with the resolve too (hall 536 -> 568 Mpaths/s,
+         * profiles/r05r_vcm_light_defer_ab.txt): room for 4 per own subpath, against the hall's ~3 stored
+         * light vertices per subpath with at most one connection each (a wave whose queue does not fit
+         * traces it in place; ORX_VCM_LIGHT_DEFER=0: all in place) */
+        static const uint32_t lper = [] {
+            const char* e = getenv("ORX_VCM_LIGHT_DEFER");
+            return e ? (uint32_t)std::max(0, atoi(e)) : 4u;
+        }();
+        if (lper) {
+            const size_t lcap = std::min<size_t>((size_t)r->W * r->rows * lper, 0x0ffffff0u);
+            HIPCHK(r, r->d_vlcq.ensure(lcap * 48 + 64));
+            HIPCHK(r, r->d_vlcq2.ensure(lcap * 48 + 64));
+            swap_buf(r->d_vlcq, r->d_vlcq2);
+            vb.lcq = r->d_vlcq.as<float4>();
+            vb.lcap = (uint32_t)lcap;
+            vb.lctl = vb.work + (r->vcm_dpar ? 14 : 12);
+        }
     }
     if ((s = vcm_light(r)) != ORX_OK) return s;
     r->last_vcm_overlap = overlap;

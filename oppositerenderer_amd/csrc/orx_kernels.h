@@ -347,6 +347,12 @@ struct VcmBufs {
     uint32_t* shstk;    /* k_vcm_shadow's traversal-stack entries below its LDS part: [block][shdeep][64] */
     uint32_t shstk_lanes, shdeep;
     struct VcmConsts* consts; /* device copy of the pass constants (written by the launches) */
+    /* the light pass's camera connections (connectCameraT1), deferred to k_vcm_light_shadow with the
+     * camera pass's resolve (the overlapped single-device schedule; NULL: traced in the light pass).
+     * A wave whose queue does not fit traces it in place, as without the list. */
+    float4* lcq = nullptr;  /* [lcap][3] queue entries (LightShadowRays' layout) */
+    uint32_t* lctl = nullptr; /* [2] entries written, entries dropped to in-place tracing */
+    uint32_t lcap = 0;
 };
 struct VcmConsts {
     f3 eye, lookdir, u, v;          /* Camera (Camera.cpp:333-345) */

@@ -501,6 +501,7 @@ struct LightShadowRays {
     const float4* q;
     float* splat;
     uint32_t e, total, cur;
+    uint32_t stride = 64;
     __device__ __forceinline__ void add(uint32_t k) const {
         const float4 b = q[3 * k + 1], cc = q[3 * k + 2];
         float* o = splat + __float_as_uint(b.w);
@@ -511,7 +512,7 @@ struct LightShadowRays {
     __device__ __forceinline__ bool next(f3& o, f3& d, float& tmin, float& tmax) {
         while (e < total) {
             cur = e;
-            e += 64;
+            e += stride;
             const float4 a = q[3 * cur], b = q[3 * cur + 1];
             if (a.w < 3.f * VCM_EPS_RAY) { /* occluded() without a walk: not occluded */
                 add(cur);
@@ -529,6 +530,29 @@ struct LightShadowRays {
         if (!occluded) add(cur);
     }
 };
+
+/* A wave's queue of camera connections (lq, n entries): appended to the deferred list vb.lcq when
+ * there is one and it has room, else traced here and splatted at once */
+__device__ __forceinline__ void light_queue_flush(const DevScene& S, const VcmBufs& vb, const float4* lq, uint32_t n,
+                                                  uint32_t lane, uint32_t* stk) {
+    __threadfence_block();
+    if (vb.lcq) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&vb.lctl[0], n);
+        base = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)base, 0, 64));
+        if (base <= vb.lcap && n <= vb.lcap - base) {
+            for (uint32_t k = lane; k < 3 * n; k += 64) vb.lcq[3 * (size_t)base + k] = lq[k];
+            return;
+        }
+        /* no room: the part of the reserved range below lcap gets inert entries (distance 0: no walk;
+         * contribution 0 added to splat[0..2], which leaves every value as it is) */
+        for (uint32_t k = lane; k < 3 * n; k += 64)
+            if ((size_t)base * 3 + k < (size_t)vb.lcap * 3) vb.lcq[3 * (size_t)base + k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (lane == 0) atomicAdd(&vb.lctl[1], n);
+    }
+    LightShadowRays R{lq, vb.splat, lane, n, 0u};
+    trace_any_chain(S, R, stk);
+}
 
 /* lightPass (VCMLightPass.cu:52-93), initLightPayload (:120-176), lightHit (vcm.h:210-309)
  *
@@ -728,19 +752,14 @@ __global__ __launch_bounds__(64, ORX_VCM_LIGHT_WAVES) void k_vcm_light(DevScene 
             }
             lqn += (uint32_t)__popcll(m);
             if (lqn >= 64) {
-                __threadfence_block();
-                LightShadowRays R{lq, vb.splat, lane, lqn, 0u};
-                trace_any_chain(S, R, stk);
+                light_queue_flush(S, vb, lq, lqn, lane, stk);
                 lqn = 0;
             }
         }
     }
-    if (!ESTIMATE && lqn) {
-        __threadfence_block();
-        LightShadowRays R{lq, vb.splat, lane, lqn, 0u};
-        trace_any_chain(S, R, stk);
-    }
+    if (!ESTIMATE && lqn) light_queue_flush(S, vb, lq, lqn, lane, stk);
 }
+
 
 /* connectVertices (vcm.h:315-400) against light vertex k of this subpath */
 template <bool TEX>
@@ -1220,6 +1239,15 @@ struct DeferredShadowRays {
 #endif
 constexpr int VCM_SHADOW_LDS_STACK = 16; /* LDS entries per lane; deeper ones in vb.shstk */
 uint32_t vcm_shadow_stack_deep(uint32_t entries) { return StackH<VCM_SHADOW_LDS_STACK>::deep(entries); }
+/* the light pass's deferred camera connections (vb.lcq), traced and splatted before the camera
+ * pass's colours read the light image (launch_vcm_camera_resolve) */
+__global__ __launch_bounds__(64, ORX_VCM_SHADOW_WAVES) void k_vcm_light_shadow(DevScene S, VcmBufs vb) {
+    ORX_STACK_DECL;
+    const uint32_t n = min(vb.lctl[0], vb.lcap);
+    LightShadowRays R{vb.lcq, vb.splat, blockIdx.x * 64u + threadIdx.x, n, 0u, gridDim.x * 64u};
+    const StackH<VCM_SHADOW_LDS_STACK> stk{ORX_STACK_PTR, vb.shstk, blockIdx.x, vb.shdeep, threadIdx.x};
+    trace_any_chain_t(S, R, stk);
+}
 __global__ __launch_bounds__(64, ORX_VCM_SHADOW_WAVES) void k_vcm_shadow(DevScene S, VcmBufs vb) {
     if (vb.dctl[1]) return; /* out of entries: the camera pass reruns in place */
     ORX_STACK_DECL;
@@ -1350,6 +1378,7 @@ void launch_vcm_camera_resolve(hipStream_t s, const DevScene& S, const VcmBufs& 
     const size_t lds = (size_t)(VCM_SHADOW_LDS_STACK + 2) * 64 * 4;
     const uint32_t per_cu = std::min<uint32_t>(4u * ORX_VCM_SHADOW_WAVES, (uint32_t)((160u << 10) / lds));
     const uint32_t sblocks = std::min(cus * std::max(1u, per_cu), vb.shstk_lanes / 64u);
+    if (vb.lcq) hipLaunchKernelGGL(k_vcm_light_shadow, dim3(sblocks), dim3(64), lds, s, S, vb);
     hipLaunchKernelGGL(k_vcm_shadow, dim3(sblocks), dim3(64), lds, s, S, vb);
     hipLaunchKernelGGL(k_vcm_accum, dim3((c.lcount + 255) / 256), dim3(256), 0, s, vb, c.lcount);
 }
