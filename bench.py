@@ -398,7 +398,9 @@ def main():
     if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING:
         light_vertices = int(np.minimum(r.read_buffer(_abi.BUF_VCM_VERTEX_COUNT, np.uint32), 9).sum())
     pbytes = roofline.pass_bytes(method, W, H, P * P, valid_avg, st.num_cells, light_vertices, photon_map=pmap,
-                                 vcm_entries=st.vcm_shadow_rays if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING else 0)
+                                 vcm_entries=st.vcm_shadow_rays if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING else 0,
+                                 vcm_light_entries=st.vcm_light_connections
+                                 if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING else 0)
     key = (f"{scene.name}:{W}x{H}:{args.method}" + (f":P{P}" if method == 2 else "")
            + (f":{args.photon_map}" if pmap else ""))
     dominant, roof = roofline_block(per_pass, pbytes, key, pmap, serial, overlapped)

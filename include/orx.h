@@ -277,6 +277,8 @@ typedef struct {
     uint32_t timed_iterations;   /* iterations since orx_reset_timing */
     uint32_t bvh_stack_entries;  /* LDS traversal stack depth bound of the scene's BVH4 */
     float pass_ms[16];           /* device time per orx_pass summed since orx_reset_timing */
+    uint32_t vcm_light_connections; /* VCM: the last light pass's camera connections deferred to the resolve */
+    uint32_t vcm_light_inplace;     /* VCM: of its connections, those traced in the light pass (list full) */
 } orx_stats;
 orx_status orx_get_stats(orx_renderer* r, orx_stats* out);
 /* starts a new timed region for orx_get_stats' *_total and pass_ms fields */

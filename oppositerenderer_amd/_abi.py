@@ -123,7 +123,8 @@ class OrxStats(C.Structure):
                 ("photons_visited", C.c_uint64), ("cells_visited", C.c_uint64),
                 ("photons_visited_total", C.c_uint64), ("cells_visited_total", C.c_uint64),
                 ("valid_photons_total", C.c_uint64), ("vcm_shadow_rays", C.c_uint32), ("vcm_shadow_overflow", C.c_uint32),
-                ("timed_iterations", C.c_uint32), ("bvh_stack_entries", C.c_uint32), ("pass_ms", C.c_float * 16)]
+                ("timed_iterations", C.c_uint32), ("bvh_stack_entries", C.c_uint32), ("pass_ms", C.c_float * 16),
+                ("vcm_light_connections", C.c_uint32), ("vcm_light_inplace", C.c_uint32)]
 
 
 PASS_NAMES = ["ppm_eye", "ppm_photon", "grid_hash", "grid_scan", "grid_scatter", "ppm_gather", "ppm_direct_output",

@@ -2513,6 +2513,12 @@ orx_status orx_get_stats(orx_renderer* r, orx_stats* out) {
         out->vcm_shadow_rays = ctl[0];
         out->vcm_shadow_overflow = ctl[1];
     }
+    if (r->vcm_vb.lcq && r->vcm_vb.lctl) { /* the last light pass's deferred camera connections */
+        uint32_t ctl[2] = {0, 0};
+        HIPCHK(r, hipMemcpy(ctl, r->vcm_vb.lctl, 8, hipMemcpyDeviceToHost));
+        out->vcm_light_connections = std::min(ctl[0], r->vcm_vb.lcap);
+        out->vcm_light_inplace = ctl[1];
+    }
     for (int p = 0; p < P_COUNT; p++) {
         double tot = 0.0;
         for (int k = 0; k < r->ev_n[p]; k++) {

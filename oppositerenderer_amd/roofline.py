@@ -30,7 +30,7 @@ KERNELS_OF_PASS = {
     "pt": ["k_pt"],
     "vcm_light": ["k_vcm_light"],
     "vcm_camera": ["k_vcm_camera"],
-    "vcm_shadow": ["k_vcm_shadow", "k_vcm_accum"],
+    "vcm_shadow": ["k_vcm_light_shadow", "k_vcm_shadow", "k_vcm_accum"],
 }
 
 
@@ -56,13 +56,14 @@ def paths_per_iteration(method: int, W: int, H: int, photons: int) -> int:
 
 def pass_bytes(method: int, W: int, H: int, photons: int, valid: float = 0.0, cells: int = 0,
                light_vertices: float = 0.0, deposits_max: int = 4, grid_max: int = 1000000,
-               photon_map: int = 0, vcm_entries: float = 0.0) -> dict:
+               photon_map: int = 0, vcm_entries: float = 0.0, vcm_light_entries: float = 0.0) -> dict:
     """Bytes per launch of each pass.
 
     valid: grid-resident photons (deposits with power > 0); cells: grid cells G;
     light_vertices: stored VCM light vertices per iteration; deposits_max: D
     slots per emitted photon; grid_max: PHOTON_GRID_MAX_SIZE (bucket table size); vcm_entries: the
-    camera pass's deferred connection shadow rays per iteration (0: traced in place)."""
+    camera pass's deferred connection shadow rays per iteration (0: traced in place); vcm_light_entries:
+    the light pass's camera connections deferred to the same resolve."""
     N = W * H
     slots = photons * deposits_max
     table = ((cells + 1023) // 1024) * ((slots + 16383) // 16384)
@@ -98,14 +99,16 @@ def pass_bytes(method: int, W: int, H: int, photons: int, valid: float = 0.0, ce
         }
     if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING and vcm_entries:
         return {
-            # RNG RMW, vertex count, 64 B per stored light vertex
-            "vcm_light": N * (R2 + 4) + light_vertices * 64,
+            # RNG RMW, vertex count, 64 B per stored light vertex, a 48-B entry per deferred camera connection
+            "vcm_light": N * (R2 + 4) + light_vertices * 64 + vcm_light_entries * 48,
             # RNG RMW, vertex count, every stored vertex read once, a 49-B entry per connection, the
             # pixel's list head and emitter term
             "vcm_camera": N * (R2 + 4 + 4 + 16) + light_vertices * 64 + vcm_entries * 49,
             # entries read by the shadow rays (ray, occlusion byte written) and by the colour sums (link,
             # byte, contribution); list head, emitter term, splat read, camera colour, output RMW per pixel
-            "vcm_shadow": vcm_entries * (32 + 1 + 16 + 1 + 16) + N * (4 + 16 + 12 + 12 + 24),
+            # and the light pass's connections read (48 B) with their splat (12 B read + written)
+            "vcm_shadow": vcm_entries * (32 + 1 + 16 + 1 + 16) + N * (4 + 16 + 12 + 12 + 24)
+                          + vcm_light_entries * (48 + 24),
         }
     if method == _abi.VCM_BIDIRECTIONAL_PATH_TRACING:
         return {
