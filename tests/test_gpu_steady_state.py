@@ -97,6 +97,10 @@ def test_bench_schedule_configs3_hall_vcm_three_iterations():
     g, o = gpu.getOutputBuffer(), ora.output()
     assert np.isfinite(g).all() and g.mean() > 0
     assert rel_l2(g, o) < 1e-4, rel_l2(g, o)
+    # the light pass's camera connections went to the resolve, none back to in-place tracing
+    st = gpu.stats()
+    assert st.vcm_light_connections > 0 and st.vcm_light_inplace == 0, (st.vcm_light_connections, st.vcm_light_inplace)
+    assert st.vcm_shadow_rays > 0 and st.vcm_shadow_overflow == 0
     gpu.destroy()
     ora.close()
 
