@@ -558,11 +558,12 @@ orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out)
 void orx_destroy(orx_renderer* r) {
     if (!r) return;
     hipSetDevice(r->device);
+    /* every stream first: the pass timing events are recorded on all of them */
     if (r->stream) hipStreamSynchronize(r->stream);
-    for (int p = 0; p < P_COUNT; p++)
-        for (hipEvent_t e : r->ev[p]) hipEventDestroy(e);
     if (r->aux) hipStreamSynchronize(r->aux);
     if (r->gstream) hipStreamSynchronize(r->gstream);
+    for (int p = 0; p < P_COUNT; p++)
+        for (hipEvent_t e : r->ev[p]) hipEventDestroy(e);
     for (hipEvent_t e : {r->ev_grid_done, r->ev_gdone[0], r->ev_gdone[1]})
         if (e) hipEventDestroy(e);
     if (r->gstream) hipStreamDestroy(r->gstream);
