@@ -506,19 +506,7 @@ print(json.dumps({"errs": errs, "pipelined": gpu.pipelined()}))
     assert res["pipelined"] == (pipeline == "1"), res  # no silent fallback to the serial schedule
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("defer", ["16", "0", "1"])
-def test_vcm_camera_shadow_modes(defer):
-    """The VCM camera pass's connection shadow rays (vcm.h:315-400, connectLightSourceS1 :406-488):
-    deferred to k_vcm_shadow with the colours summed by k_vcm_accum in the reference's order (the
-    default, ORX_VCM_DEFER=16 entries per pixel; ~6.5 rays per pixel on the hall), traced in place
-    inside the camera kernel (ORX_VCM_DEFER=0), and
-    deferred into a list too small for them (1 per pixel: the pass overflows, restores the RNG planes
-    and reruns in place).  Camera colours, RNG and vertex counts bit-exact against the oracle, three
-    iterations back to back (the overlapped schedule cycles both entry lists and light images and
-    reruns each overflow after the previous iteration's colours), and the overflow flag as expected."""
-    import subprocess, sys, os, json
-    code = r'''
+_VCM_CHILD = r'''
 import json, sys, numpy as np
 sys.path.insert(0, "tests")
 import oracle_lib
@@ -544,10 +532,25 @@ for buf, name in ((_abi.BUF_RNG, "rng"), (_abi.BUF_VCM_CAMERA, "camera"), (_abi.
 g, o = gpu.getOutputBuffer().astype(np.float64), ora.output().astype(np.float64)
 st = gpu.stats()
 print(json.dumps({"bad": bad, "err": float(np.sqrt(((g - o) ** 2).sum() / (o ** 2).sum())), "mean": float(g.mean()),
-                  "rays": int(st.vcm_shadow_rays), "overflow": int(st.vcm_shadow_overflow)}))
+                  "rays": int(st.vcm_shadow_rays), "overflow": int(st.vcm_shadow_overflow),
+                  "lconn": int(st.vcm_light_connections), "linplace": int(st.vcm_light_inplace)}))
 '''
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("defer", ["16", "0", "1"])
+def test_vcm_camera_shadow_modes(defer):
+    """The VCM camera pass's connection shadow rays (vcm.h:315-400, connectLightSourceS1 :406-488):
+    deferred to k_vcm_shadow with the colours summed by k_vcm_accum in the reference's order (the
+    default, ORX_VCM_DEFER=16 entries per pixel; ~6.5 rays per pixel on the hall), traced in place
+    inside the camera kernel (ORX_VCM_DEFER=0), and
+    deferred into a list too small for them (1 per pixel: the pass overflows, restores the RNG planes
+    and reruns in place).  Camera colours, RNG and vertex counts bit-exact against the oracle, three
+    iterations back to back (the overlapped schedule cycles both entry lists and light images and
+    reruns each overflow after the previous iteration's colours), and the overflow flag as expected."""
+    import subprocess, sys, os, json
     env = dict(os.environ, ORX_VCM_DEFER=defer)
-    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110,
+    out = subprocess.run([sys.executable, "-c", _VCM_CHILD], env=env, capture_output=True, text=True, timeout=110,
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads(out.stdout.strip().splitlines()[-1])
@@ -557,6 +560,29 @@ print(json.dumps({"bad": bad, "err": float(np.sqrt(((g - o) ** 2).sum() / (o ** 
         assert res["rays"] > 0 and res["overflow"] == 0, res
     elif defer == "1":
         assert res["overflow"] == 1, res  # the rerun path ran
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ldefer", ["4", "1", "0"])
+def test_vcm_light_connection_modes(ldefer):
+    """The light pass's camera connections (connectCameraT1, vcm.h:52-150) deferred to the overlapped
+    resolve (ORX_VCM_LIGHT_DEFER=4 per subpath, the default), into a list too small for them (1: the
+    waves whose queue does not fit trace it in place and fill their reserved entries with inert ones),
+    and traced in the light pass (0).  Three iterations back to back; RNG, camera colours and vertex
+    counts bit-exact, the output (light-image splats are float atomics in every mode) within 1e-5."""
+    import subprocess, sys, os, json
+    env = dict(os.environ, ORX_VCM_LIGHT_DEFER=ldefer)
+    out = subprocess.run([sys.executable, "-c", _VCM_CHILD], env=env, capture_output=True, text=True, timeout=110,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert all(v == 0 for v in res["bad"].values()), res
+    assert res["err"] < 1e-5 and res["mean"] > 0, res
+    if ldefer == "4":
+        assert res["lconn"] > 0 and res["linplace"] == 0, res
+    elif ldefer == "1":
+        assert res["lconn"] > 0 and res["linplace"] > 0, res  # both paths ran
+    else:
+        assert res["lconn"] == 0 and res["linplace"] == 0, res
 
 
 @pytest.mark.gpu
