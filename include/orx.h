@@ -214,6 +214,11 @@ void orx_destroy(orx_renderer* r);
  * the next resize or initScene sizes it again), so that the next PPM photon pass must return
  * ORX_ERR_STATE instead of launching past the buffer (OptixRenderer.cpp:816-820 throws) */
 orx_status orx_debug_limit_photon_stack(orx_renderer* r, uint32_t lanes);
+/* test hook: rerun the last VCM iteration's resolve (deferred shadow rays, colours) with stale list
+ * state -- entry count past the capacity, odd pixels' list heads past the entries, light-connection
+ * entries whose pixel offsets lie past the light image -- which the resolve's device-side bounds must
+ * absorb; synchronous, colours in ORX_BUF_VCM_CAMERA (the output is accumulated once more) */
+orx_status orx_debug_vcm_stale_resolve(orx_renderer* r);
 typedef enum {
     ORX_BUF_RNG = 0,        /* uint32 [slots][6]: xorwow v0..v4, d */
     ORX_BUF_HITPOINTS = 1,  /* float  [W*H][13]: pos3 normal3 atten3 radiance3 flags(bits) */

@@ -434,6 +434,9 @@ struct orx_renderer {
      * the entry lists with their control words alternate (d_vsplat2, d_vdq2, d_vdpx2, vcm_dpar),
      * ev_vcam ends the walk, ev_vacc the resolve, vcm_pend: one in flight */
     DevBuf d_vsplat2, d_vdq2, d_vdpx2, d_vlcq, d_vlcq2; /* d_vlcq: the light pass's deferred camera connections */
+    /* the other set of what the resolve's in-place rerun reads while the next iteration runs: light
+     * vertices, their counts and texel colours, the walk's RNG start words */
+    DevBuf d_vverts2, d_vcount2, d_vkd2, d_vrngsave2;
     uint32_t vcm_dpar = 0;
     bool last_vcm_overlap = false;
     size_t vcm_dqcap = 0; /* entries per list (ORX_VCM_DEFER per own pixel) */
@@ -1559,15 +1562,19 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
     vb.vE = r->has_tex ? r->d_vkd.as<float4>() : nullptr;
     vb.splat = r->d_vsplat.as<float>();
     vb.splat_in = vb.splat + (size_t)r->rank * r->max_rows * r->W * 3;
+    vb.splat_n = (uint32_t)std::min<size_t>(spx * 3, 0xffffffffu);
     {
         const size_t waves = std::max(vcm_camera_waves(((r->W + 7) / 8) * ((r->rows + 7) / 8)),
                                       vcm_light_waves((uint32_t)((lpx + 63) / 64)));
-        HIPCHK(r, r->d_vshq.ensure(waves * VCM_SHQ_PER_WAVE * 16 + 16));
+        /* [waves] queues for the light pass and walk, [waves] for the resolve's rerun beside them */
+        HIPCHK(r, r->d_vshq.ensure(2 * waves * VCM_SHQ_PER_WAVE * 16 + 16));
         vb.shq = r->d_vshq.as<float4>();
+        vb.shq_rerun = vb.shq + waves * VCM_SHQ_PER_WAVE;
         HIPCHK(r, r->d_vwork.ensure(64)); /* [0..1] work counters, [4..7] / [8..11] entry-list control words */
         vb.work = r->d_vwork.as<uint32_t>();
-        HIPCHK(r, r->d_vconst.ensure(sizeof(VcmConsts)));
+        HIPCHK(r, r->d_vconst.ensure(3 * sizeof(VcmConsts))); /* [0] the launches', [1 + set] the resolve's */
         vb.consts = r->d_vconst.as<VcmConsts>();
+        vb.consts_keep = vb.consts + 1 + r->vcm_dpar;
     }
     vb.cam = r->d_vcam.as<float>();
     vb.output = r->d_out.as<float>();
@@ -1597,7 +1604,7 @@ static orx_status vcm_prepare(orx_renderer* r, const orx_request* det, float ppm
             vb.dhead = (uint32_t*)(vb.demis + lpx);
             vb.dctl = vb.work + 4; /* d_vwork: [0..1] work counters, [4..7] the deferred-entry control words */
             vb.dcap = (uint32_t)std::min<size_t>(cap, 0xfffffff0u);
-            vb.rng_save = r->d_vrngsave.as<uint32_t>();
+            for (int k = 0; k < 6; k++) vb.rsave.p[k] = r->d_vrngsave.as<uint32_t>() + (size_t)k * nslot;
             /* the shadow kernel's deep stack entries: (stack bound + 2 - 16) per lane of the largest grid */
             int dev = 0, cus = 256;
             hipGetDevice(&dev);
@@ -1652,7 +1659,6 @@ static orx_status vcm_light(orx_renderer* r) {
         r->vcm_estimated = true;
     }
     HIPCHK(r, hipMemsetAsync(r->vcm_vb.splat, 0, r->vcm_spx * 12, st));
-    if (r->vcm_vb.lcq) HIPCHK(r, hipMemsetAsync(r->vcm_vb.lctl, 0, 8, st));
     launch_vcm_light(st, r->scene, r->vcm_vb, r->vcm_c, false);
     ev_end(r, P_VCM_LIGHT);
     return ORX_OK;
@@ -1663,24 +1669,22 @@ static orx_status vcm_camera(orx_renderer* r, bool overlap = false) {
         hipStream_t st = cur_stream(r);
         ev_begin(r, P_VCM_CAMERA);
         launch_vcm_camera_walk(st, r->scene, r->vcm_vb, r->vcm_c);
-        launch_vcm_camera_rerun(st, r->scene, r->vcm_vb, r->vcm_c);
         ev_end(r, P_VCM_CAMERA);
         ev_begin(r, P_VCM_SHADOW);
         launch_vcm_camera_resolve(st, r->scene, r->vcm_vb, r->vcm_c);
         ev_end(r, P_VCM_SHADOW);
         return ORX_OK;
     }
-    /* the walk on the renderer's stream (its entry list is the one the last resolve does not read);
-     * the rerun after an overflow accumulates into the output, so it follows the last resolve; the
-     * resolve on aux, beside the next iteration's light pass and walk (the pass interval ends with
-     * the resolve) */
+    /* the walk on the renderer's stream, the resolve (with the rerun an overflow needs) on aux beside the
+     * next iteration's light pass and walk (the pass interval ends with the resolve); the stream then
+     * waits for the previous iteration's resolve, since the next light pass and walk write the set it
+     * reads (light image, light vertices, entry list, RNG start words, constants copy) */
     hipStream_t st = cur_stream(r);
     ev_begin(r, P_VCM_CAMERA);
     launch_vcm_camera_walk(st, r->scene, r->vcm_vb, r->vcm_c);
     ev_end(r, P_VCM_CAMERA);
     HIPCHK(r, hipEventRecord(r->ev_vcam, st));
     if (r->vcm_pend) HIPCHK(r, hipStreamWaitEvent(st, r->ev_vacc, 0));
-    launch_vcm_camera_rerun(st, r->scene, r->vcm_vb, r->vcm_c);
     HIPCHK(r, hipStreamWaitEvent(r->aux, r->ev_vcam, 0));
     ev_begin_on(r, P_VCM_SHADOW, r->aux);
     launch_vcm_camera_resolve(r->aux, r->scene, r->vcm_vb, r->vcm_c);
@@ -1720,6 +1724,27 @@ static orx_status vcm_iteration(orx_renderer* r, const orx_request* det, float p
         vb.demis = r->d_vdpx.as<float4>();
         vb.dhead = (uint32_t*)(vb.demis + (size_t)r->W * r->rows);
         vb.dctl = vb.work + (r->vcm_dpar ? 8 : 4);
+        vb.consts_keep = vb.consts + 1 + r->vcm_dpar;
+        /* the light vertices (with counts and texel colours) and the walk's RNG start words: the resolve's
+         * in-place rerun after an overflow reads this iteration's while the next one writes the other set */
+        HIPCHK(r, r->d_vverts2.ensure(r->d_vverts.bytes));
+        HIPCHK(r, r->d_vcount2.ensure(r->d_vcount.bytes));
+        HIPCHK(r, r->d_vrngsave2.ensure(r->d_vrngsave.bytes));
+        swap_buf(r->d_vverts, r->d_vverts2);
+        swap_buf(r->d_vcount, r->d_vcount2);
+        swap_buf(r->d_vrngsave, r->d_vrngsave2);
+        const size_t lpx = (size_t)r->W * r->rows, plane = lpx * VCM_MAX_VERTS, nslot = (size_t)r->rows * r->RW;
+        vb.vcount = r->d_vcount.as<uint32_t>();
+        vb.vA = r->d_vverts.as<float4>();
+        vb.vB = vb.vA + plane;
+        vb.vC = vb.vB + plane;
+        vb.vD = vb.vC + plane;
+        if (vb.vE) {
+            HIPCHK(r, r->d_vkd2.ensure(r->d_vkd.bytes));
+            swap_buf(r->d_vkd, r->d_vkd2);
+            vb.vE = r->d_vkd.as<float4>();
+        }
+        for (int k = 0; k < 6; k++) vb.rsave.p[k] = r->d_vrngsave.as<uint32_t>() + (size_t)k * nslot;
         /* the light pass's camera connections go with the resolve too (hall 536 -> 568 Mpaths/s,
          * profiles/r05r_vcm_light_defer_ab.txt): room for 4 per own subpath, against the hall's ~3 stored
          * light vertices per subpath with at most one connection each (a wave whose queue does not fit
@@ -2086,6 +2111,50 @@ orx_status orx_ppm_slab_import(orx_renderer* r, const void* recv, uint64_t n, co
 orx_status orx_debug_limit_photon_stack(orx_renderer* r, uint32_t lanes) {
     if (!r) return ORX_ERR_INVALID_ARGUMENT;
     if (lanes < r->pb.tlanes) r->pb.tlanes = lanes;
+    return ORX_OK;
+}
+
+/* test hook: drive the last VCM iteration's resolve again with stale list state -- the entry count
+ * past the capacity, every odd own pixel's list head past the entries, and 64 light-connection entries
+ * appended whose pixel offsets lie past the light image -- as a walk or light pass that did not write
+ * this set's control words would leave them (vcm.h:315-400 / :43-58 have no such state: the device-side
+ * bounds in k_vcm_accum and k_vcm_light_shadow are ours).  Synchronous; the colours land in
+ * ORX_BUF_VCM_CAMERA (the output is accumulated once more: not a render) */
+orx_status orx_debug_vcm_stale_resolve(orx_renderer* r) {
+    if (!r) return ORX_ERR_INVALID_ARGUMENT;
+    const VcmBufs& vb = r->vcm_vb;
+    if (!vb.dq0 || !r->vcm_npx) return set_err(r, ORX_ERR_STATE, "no VCM iteration with deferred lists");
+    HIPCHK(r, hipSetDevice(r->device));
+    flush_pipeline(r);
+    HIPCHK(r, hipStreamSynchronize(cur_stream(r)));
+    HIPCHK(r, hipDeviceSynchronize());
+    const size_t lpx = r->vcm_npx;
+    std::vector<uint32_t> head(lpx);
+    HIPCHK(r, hipMemcpy(head.data(), vb.dhead, lpx * 4, hipMemcpyDeviceToHost));
+    for (size_t p = 1; p < lpx; p += 2) head[p] = vb.dcap + (uint32_t)p;
+    HIPCHK(r, hipMemcpy(vb.dhead, head.data(), lpx * 4, hipMemcpyHostToDevice));
+    const uint32_t stale = 0xfffffff0u;
+    HIPCHK(r, hipMemcpy(vb.dctl, &stale, 4, hipMemcpyHostToDevice));
+    if (vb.lcq && vb.lcap >= 64) {
+        uint32_t lc[2] = {0, 0};
+        HIPCHK(r, hipMemcpy(lc, vb.lctl, 8, hipMemcpyDeviceToHost));
+        const uint32_t base = std::min(lc[0], vb.lcap - 64);
+        std::vector<float4> e(3 * 64);
+        for (uint32_t k = 0; k < 64; k++) {
+            const uint32_t at = vb.splat_n + 3 * k; /* past the light image */
+            float w;
+            memcpy(&w, &at, 4);
+            e[3 * k + 0] = make_float4(0.f, 0.f, 0.f, 0.f); /* distance 0: unoccluded without a walk */
+            e[3 * k + 1] = make_float4(0.f, 0.f, 1.f, w);
+            e[3 * k + 2] = make_float4(1.f, 1.f, 1.f, 0.f);
+        }
+        HIPCHK(r, hipMemcpy(vb.lcq + 3 * (size_t)base, e.data(), e.size() * 16, hipMemcpyHostToDevice));
+        lc[0] = base + 64;
+        HIPCHK(r, hipMemcpy(vb.lctl, lc, 4, hipMemcpyHostToDevice));
+    }
+    launch_vcm_camera_resolve(cur_stream(r), r->scene, vb, r->vcm_c);
+    HIPCHK(r, hipGetLastError());
+    HIPCHK(r, hipStreamSynchronize(cur_stream(r)));
     return ORX_OK;
 }
 
@@ -2517,7 +2586,9 @@ orx_status orx_get_stats(orx_renderer* r, orx_stats* out) {
     if (r->vcm_vb.lcq && r->vcm_vb.lctl) { /* the last light pass's deferred camera connections */
         uint32_t ctl[2] = {0, 0};
         HIPCHK(r, hipMemcpy(ctl, r->vcm_vb.lctl, 8, hipMemcpyDeviceToHost));
-        out->vcm_light_connections = std::min(ctl[0], r->vcm_vb.lcap);
+        /* entries reserved minus those a wave could not fit and traced in place (their reserved range
+         * below lcap holds inert placeholders): the connections the resolve traced */
+        out->vcm_light_connections = ctl[0] - std::min(ctl[0], ctl[1]);
         out->vcm_light_inplace = ctl[1];
     }
     for (int p = 0; p < P_COUNT; p++) {

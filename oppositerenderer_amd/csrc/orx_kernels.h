@@ -341,12 +341,19 @@ struct VcmBufs {
     uint8_t* docc;      /* [dcap] 1: occluded (k_vcm_shadow) */
     uint32_t* dhead;    /* [lcount] the pixel's first entry, or VCM_END */
     float4* demis;      /* [lcount] the emitter contribution ending the subpath xyz | 1 if there is one */
-    uint32_t* dctl;     /* [4] entries written, overflow flag (more entries than dcap: the pass reruns in place) */
+    uint32_t* dctl;     /* [4] entries written, overflow flag (more entries than dcap: the resolve reruns in place) */
     uint32_t dcap;
-    uint32_t* rng_save; /* [6][rows*RW] the RNG planes before the camera pass (restored for the in-place rerun) */
+    /* the RNG words each camera subpath starts from, stored by the walk (k_vcm_camera<., 1>) as it loads
+     * them: the in-place rerun after an overflow starts its subpaths from here */
+    RngPlanes rsave;
     uint32_t* shstk;    /* k_vcm_shadow's traversal-stack entries below its LDS part: [block][shdeep][64] */
     uint32_t shstk_lanes, shdeep;
     struct VcmConsts* consts; /* device copy of the pass constants (written by the launches) */
+    /* this iteration's constants as the resolve's rerun reads them: the next iteration's launches
+     * rewrite `consts` while the resolve runs beside them (one copy per entry-list set) */
+    struct VcmConsts* consts_keep;
+    float4* shq_rerun;  /* the rerun's shadow-ray queues (it runs beside the light pass and walk using shq) */
+    uint32_t splat_n;   /* floats in `splat` (the light-image bound of k_vcm_light_shadow's splats) */
     /* the light pass's camera connections (connectCameraT1), deferred to k_vcm_light_shadow with the
      * camera pass's resolve (the overlapped single-device schedule; NULL: traced in the light pass).
      * A wave whose queue does not fit traces it in place, as without the list. */
@@ -366,10 +373,9 @@ struct VcmConsts {
 };
 void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c, bool estimate);
 void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c);
-/* its parts, in this order: the walk (RNG, light vertices, constants), the rerun after an entry-list overflow,
- * the resolve (deferred shadow rays, colours) */
+/* its parts, in this order: the walk (RNG, light vertices, constants, entry lists), the resolve (deferred
+ * shadow rays, colours, and the in-place rerun should the entry list have overflowed) */
 void launch_vcm_camera_walk(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c);
-void launch_vcm_camera_rerun(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c);
 void launch_vcm_camera_resolve(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c);
 uint32_t vcm_camera_waves(uint32_t tiles); /* persistent camera-pass waves for `tiles` 8x8 tiles */
 uint32_t vcm_light_waves(uint32_t items);  /* persistent light-pass waves for `items` 64-subpath items */

@@ -502,9 +502,13 @@ struct LightShadowRays {
     float* splat;
     uint32_t e, total, cur;
     uint32_t stride = 64;
+    uint32_t splat_n = 0xffffffffu; /* floats in splat: a pixel offset past it is dropped (a list entry the
+                                     * light pass did not write this iteration, k_vcm_light_shadow) */
     __device__ __forceinline__ void add(uint32_t k) const {
         const float4 b = q[3 * k + 1], cc = q[3 * k + 2];
-        float* o = splat + __float_as_uint(b.w);
+        const uint32_t at = __float_as_uint(b.w);
+        if (at >= splat_n || splat_n - at < 3u) return;
+        float* o = splat + at;
         unsafeAtomicAdd(o + 0, cc.x);
         unsafeAtomicAdd(o + 1, cc.y);
         unsafeAtomicAdd(o + 2, cc.z);
@@ -931,12 +935,14 @@ struct CamPixel {
     size_t slot;
     uint32_t nverts;
 };
+template <int MODE>
 __device__ __forceinline__ void camera_start(const VcmBufs& vb, const VcmConsts& c, uint32_t x, uint32_t j,
                                              CamPixel& px, Rng& rs, Subpath& C) {
     const uint32_t y = c.rank + j * c.world; /* own row j = image row rank + j*world */
     px.p = x + j * c.W;
     px.slot = (size_t)j * vb.RW + x;
-    rs = rng_load(vb.rng, px.slot);
+    rs = rng_load(vb.rng, px.slot); /* MODE 2: vb.rng are the walk's rsave planes */
+    if (MODE == 1) rng_store(vb.rsave, px.slot, rs); /* where an in-place rerun would start */
     C.throughput = mk1(1.0f);
     C.color = mk1(0.f);
     C.depth = 0;
@@ -957,6 +963,8 @@ __device__ __forceinline__ void camera_start(const VcmBufs& vb, const VcmConsts&
     C.dVCM = (float)c.count / cameraPdfW;
     px.nverts = vb.vcount[px.p];
 }
+/* STORE_RNG false: the rerun, whose walk already left the RNG where the next light pass continues */
+template <bool STORE_RNG>
 __device__ __forceinline__ void camera_finish(const VcmBufs& vb, const CamPixel& px, const Rng& rs, const Subpath& C) {
     const size_t o3 = 3 * (size_t)px.p;
     vb.cam[o3 + 0] = C.color.x;
@@ -968,11 +976,15 @@ __device__ __forceinline__ void camera_finish(const VcmBufs& vb, const CamPixel&
     vb.output[o3 + 0] = ox + C.color.x;
     vb.output[o3 + 1] = oy + C.color.y;
     vb.output[o3 + 2] = oz + C.color.z;
-    rng_store(vb.rng, px.slot, rs);
+    if (STORE_RNG) rng_store(vb.rng, px.slot, rs);
 }
 
-/* MODE 0: connection shadow rays traced in place (below); 1: deferred to k_vcm_shadow, the colour
- * summed by k_vcm_accum; 2: in place, only if the deferred pass ran out of entries (vb.dctl[1]) */
+/* MODE 0: connection shadow rays traced in place (below); 1: the walk, connections deferred to
+ * k_vcm_shadow and the colour summed by k_vcm_accum; 2: in place, only if the walk ran out of entries
+ * (vb.dctl[1]), from the RNG words the walk started from (vb.rng = its rsave planes), without storing
+ * the RNG.  A walk that runs out of entries finishes its subpaths without writing entries: its RNG use
+ * does not depend on the shadow tests or the colour, so the RNG planes it leaves are right either way,
+ * and only the colours need the rerun, which therefore runs in the resolve, off the RNG chain. */
 #ifndef ORX_VCM_CAMERA_DEFER_WAVES
 #define ORX_VCM_CAMERA_DEFER_WAVES 3 /* the deferred form (no traversal of the shadow rays inside) */
 #endif
@@ -1005,6 +1017,7 @@ __global__ __launch_bounds__(64, MODE == 1 ? ORX_VCM_CAMERA_DEFER_WAVES : ORX_VC
     bool alive = false;
     uint32_t tail = VCM_END;  /* DEFER: the pixel's last entry so far */
     bool emis = false;        /* DEFER: the subpath ended on an emitter (its contribution is in C.color) */
+    bool ovf = false;         /* DEFER: the entry list is full (wave-uniform); no more entries */
     uint32_t next = 0, end = 0; /* the wave's current work item range (uniform) */
     bool exhausted = false;
     for (;;) {
@@ -1030,7 +1043,7 @@ __global__ __launch_bounds__(64, MODE == 1 ? ORX_VCM_CAMERA_DEFER_WAVES : ORX_VC
                 const uint32_t item = next + rank, tile = item >> 6;
                 const uint32_t x = (tile % tilesX) * 8 + (item & 7), j = (tile / tilesX) * 8 + ((item >> 3) & 7);
                 if (x < c.W && j < c.rows) {
-                    camera_start(vb, c, x, j, px, rs, C);
+                    camera_start<MODE>(vb, c, x, j, px, rs, C);
                     alive = true;
                     tail = VCM_END;
                     emis = false;
@@ -1145,28 +1158,32 @@ __global__ __launch_bounds__(64, MODE == 1 ? ORX_VCM_CAMERA_DEFER_WAVES : ORX_VC
             if (DEFER) {
                 /* the wave's connections go to the global entry list, each lane's in its reference order
                  * (light sample, then light vertices 0..n-1), linked behind the pixel's earlier ones */
-                uint32_t base = 0;
-                if (lane == 0 && total_p) base = atomicAdd(&vb.dctl[0], total_p);
-                base = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)base, 0, 64));
-                if (total_p && (base > vb.dcap || total_p > vb.dcap - base)) {
-                    /* out of entries: the pass is rerun in place (MODE 2) after restoring the RNG; stop */
-                    if (lane == 0) atomicOr(&vb.dctl[1], 1u);
-                    return;
-                }
-                const uint32_t first = base + pbase;
-                const float4 hp4 = qhit[lane];
-                for (uint32_t k = 0; k < npend; ++k) {
-                    const float4 r0 = q[2 * (qbase + k)];
-                    const float4 r1 = q[2 * (qbase + k) + 1];
-                    const uint32_t e = first + k;
-                    vb.dq0[e] = make_float4(hp4.x, hp4.y, hp4.z, r0.w);
-                    vb.dq1[e] = make_float4(r0.x, r0.y, r0.z, __uint_as_float(k + 1 < npend ? e + 1 : VCM_END));
-                    vb.dq2[e] = make_float4(r1.x, r1.y, r1.z, 0.f);
-                }
-                if (npend) {
-                    if (tail == VCM_END) vb.dhead[px.p] = first;
-                    else reinterpret_cast<uint32_t*>(vb.dq1 + tail)[3] = first;
-                    tail = first + npend - 1;
+                if (!ovf && total_p) {
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(&vb.dctl[0], total_p);
+                    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)base, 0, 64));
+                    if (base > vb.dcap || total_p > vb.dcap - base) {
+                        /* out of entries: the resolve reruns the pass in place (MODE 2); the wave walks on
+                         * without entries, for the RNG the next light pass continues */
+                        if (lane == 0) atomicOr(&vb.dctl[1], 1u);
+                        ovf = true;
+                    } else {
+                        const uint32_t first = base + pbase;
+                        const float4 hp4 = qhit[lane];
+                        for (uint32_t k = 0; k < npend; ++k) {
+                            const float4 r0 = q[2 * (qbase + k)];
+                            const float4 r1 = q[2 * (qbase + k) + 1];
+                            const uint32_t e = first + k;
+                            vb.dq0[e] = make_float4(hp4.x, hp4.y, hp4.z, r0.w);
+                            vb.dq1[e] = make_float4(r0.x, r0.y, r0.z, __uint_as_float(k + 1 < npend ? e + 1 : VCM_END));
+                            vb.dq2[e] = make_float4(r1.x, r1.y, r1.z, 0.f);
+                        }
+                        if (npend) {
+                            if (tail == VCM_END) vb.dhead[px.p] = first;
+                            else reinterpret_cast<uint32_t*>(vb.dq1 + tail)[3] = first;
+                            tail = first + npend - 1;
+                        }
+                    }
                 }
                 if (was_alive && !alive) {
                     /* camera_finish without the colour: RNG, the emitter term, the list end */
@@ -1199,7 +1216,7 @@ __global__ __launch_bounds__(64, MODE == 1 ? ORX_VCM_CAMERA_DEFER_WAVES : ORX_VC
                 if (r0.w == -3.f) C.color = C.color + mk(r1.x, r1.y, r1.z);
             }
         }
-        if (was_alive && !alive) camera_finish(vb, px, rs, C);
+        if (was_alive && !alive) camera_finish<MODE != 2>(vb, px, rs, C);
     }
 }
 
@@ -1244,11 +1261,12 @@ uint32_t vcm_shadow_stack_deep(uint32_t entries) { return StackH<VCM_SHADOW_LDS_
 __global__ __launch_bounds__(64, ORX_VCM_SHADOW_WAVES) void k_vcm_light_shadow(DevScene S, VcmBufs vb) {
     ORX_STACK_DECL;
     const uint32_t n = min(vb.lctl[0], vb.lcap);
-    LightShadowRays R{vb.lcq, vb.splat, blockIdx.x * 64u + threadIdx.x, n, 0u, gridDim.x * 64u};
+    LightShadowRays R{vb.lcq, vb.splat, blockIdx.x * 64u + threadIdx.x, n, 0u, gridDim.x * 64u, vb.splat_n};
     const StackH<VCM_SHADOW_LDS_STACK> stk{ORX_STACK_PTR, vb.shstk, blockIdx.x, vb.shdeep, threadIdx.x};
     trace_any_chain_t(S, R, stk);
 }
 __global__ __launch_bounds__(64, ORX_VCM_SHADOW_WAVES) void k_vcm_shadow(DevScene S, VcmBufs vb) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) vb.work[2] = 0; /* the rerun's work counter (it follows on this stream) */
     if (vb.dctl[1]) return; /* out of entries: the camera pass reruns in place */
     ORX_STACK_DECL;
     const uint32_t n = min(vb.dctl[0], vb.dcap);
@@ -1260,11 +1278,16 @@ __global__ __launch_bounds__(64, ORX_VCM_SHADOW_WAVES) void k_vcm_shadow(DevScen
 /* the colour of every own pixel's camera subpath from its deferred entries, in the order the
  * in-place pass adds them (C.color = C.color + contribution for each unoccluded connection, then the
  * emitter term), then camera_finish's writes */
-__global__ __launch_bounds__(256) void k_vcm_accum(VcmBufs vb, uint32_t lcount) {
+__global__ __launch_bounds__(256) void k_vcm_accum(VcmBufs vb, uint32_t lcount, uint32_t max_per_px) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= lcount || vb.dctl[1]) return;
+    /* the walk writes every own pixel's head and links only to entries below the count it reserved, so
+     * these bounds hold by construction; they keep a list the walk did not write this pass (stale heads,
+     * a stale count) from leading the loop outside the entries or round a cycle */
+    const uint32_t n = min(vb.dctl[0], vb.dcap);
     f3 color = mk1(0.f);
-    for (uint32_t e = vb.dhead[p]; e != VCM_END; e = __float_as_uint(vb.dq1[e].w))
+    uint32_t steps = 0;
+    for (uint32_t e = vb.dhead[p]; e < n && steps < max_per_px; e = __float_as_uint(vb.dq1[e].w), ++steps)
         if (!vb.docc[e]) {
             const float4 a = vb.dq2[e];
             color = color + mk(a.x, a.y, a.z);
@@ -1282,13 +1305,6 @@ __global__ __launch_bounds__(256) void k_vcm_accum(VcmBufs vb, uint32_t lcount) 
     vb.output[o3 + 1] = oy + color.y;
     vb.output[o3 + 2] = oz + color.z;
 }
-/* before the in-place rerun: the RNG planes as they were before the deferred pass */
-__global__ __launch_bounds__(256) void k_vcm_rng_restore(VcmBufs vb, uint32_t n) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !vb.dctl[1]) return;
-    for (int k = 0; k < 6; k++) vb.rng.p[k][i] = vb.rng_save[(size_t)k * n + i];
-}
-
 /* persistent light-pass waves: as many as can be resident at once (4 per SIMD) */
 uint32_t vcm_light_waves(uint32_t items) {
     static uint32_t resident = 0;
@@ -1312,13 +1328,31 @@ uint32_t vcm_camera_waves(uint32_t tiles) {
     return tiles < resident ? tiles : resident;
 }
 
-__global__ void k_vcm_consts(VcmConsts c, VcmConsts* dst) { *dst = c; }
+/* a pass's prologue, one thread: the constants' device copies and the small control words the pass
+ * counts in (work-item counters, entry-list control words), zeroed here instead of by separate
+ * fill dispatches on the iteration's critical chain */
+struct VcmZero {
+    uint32_t* p[2] = {nullptr, nullptr};
+    uint32_t n[2] = {0, 0};
+};
+__global__ void k_vcm_consts(VcmConsts c, VcmConsts* dst, VcmConsts* keep, VcmZero z) {
+    *dst = c;
+    if (keep) *keep = c;
+    for (int i = 0; i < 2; i++)
+        for (uint32_t k = 0; k < z.n[i]; k++) z.p[i][k] = 0;
+}
 
 void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c, bool estimate) {
-    hipLaunchKernelGGL(k_vcm_consts, dim3(1), dim3(1), 0, s, c, vb.consts);
+    VcmZero z;
+    z.p[0] = vb.work + 1; /* the light pass's work counter */
+    z.n[0] = 1;
+    if (!estimate && vb.lcq) { /* the deferred camera connections: entries reserved, entries traced in place */
+        z.p[1] = vb.lctl;
+        z.n[1] = 2;
+    }
+    hipLaunchKernelGGL(k_vcm_consts, dim3(1), dim3(1), 0, s, c, vb.consts, (VcmConsts*)nullptr, z);
     const uint32_t blocks = vcm_light_waves((c.lcount + 63) / 64);
     if (blocks == 0) return;
-    hipMemsetAsync(vb.work + 1, 0, 4, s);
     const size_t lds = ORX_STACK_BYTES(S);
     if (vb.vE) {
         if (estimate) hipLaunchKernelGGL((k_vcm_light<true, true>), dim3(blocks), dim3(64), lds, s, S, vb, vb.consts);
@@ -1329,41 +1363,35 @@ void launch_vcm_light(hipStream_t s, const DevScene& S, const VcmBufs& vb, const
     }
 }
 template <int MODE>
-static void launch_camera_kernel(hipStream_t s, const DevScene& S, const VcmBufs& vb, uint32_t blocks) {
-    hipMemsetAsync(vb.work, 0, 4, s);
-    if (vb.vE) hipLaunchKernelGGL((k_vcm_camera<true, MODE>), dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, vb.consts);
-    else hipLaunchKernelGGL((k_vcm_camera<false, MODE>), dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, vb.consts);
+static void launch_camera_kernel(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts* cp,
+                                 uint32_t blocks) {
+    if (vb.vE) hipLaunchKernelGGL((k_vcm_camera<true, MODE>), dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, cp);
+    else hipLaunchKernelGGL((k_vcm_camera<false, MODE>), dim3(blocks), dim3(64), ORX_STACK_BYTES(S), s, S, vb, cp);
 }
-/* The camera pass: the subpaths with their connections (k_vcm_camera<., 1>), the connections' shadow
- * rays (k_vcm_shadow), the colours (k_vcm_accum).  Should the entry list overflow (more than
- * vb.dcap connections in all, ORX_VCM_DEFER per own pixel), the pass is redone with the shadow rays traced in
- * place from the saved RNG planes (k_vcm_rng_restore, k_vcm_camera<., 2>); both exit at once
- * otherwise, as k_vcm_shadow and k_vcm_accum do after an overflow.  vb.dq0 == NULL: in place only.
- * Three parts: the walk (everything that reads or advances the RNG planes, the light vertices and
- * the pass constants), the rerun (the in-place pass after an overflow, which accumulates into the
- * output), and the resolve (the deferred shadow rays and the colours), which reads only the entry
- * list and control words the walk wrote, the light image (vb.splat_in) and the output it accumulates
- * into, so it can run beside the next iteration's light pass and walk (orx_capi.hip vcm_camera). */
+/* The camera pass in two parts.  The walk (k_vcm_camera<., 1>): everything that reads or advances the RNG
+ * planes, reads the light vertices or the pass constants -- the subpaths, their connections written to the
+ * entry list, and the RNG words each subpath starts from (vb.rsave).  The resolve: the light pass's
+ * deferred camera connections (k_vcm_light_shadow, splats into the light image), the entries' shadow rays
+ * (k_vcm_shadow), the colours (k_vcm_accum), and -- only if the walk ran out of entries (more than vb.dcap
+ * connections in all, ORX_VCM_DEFER per own pixel) -- the in-place rerun k_vcm_camera<., 2>, which starts
+ * from vb.rsave, reads this iteration's light vertices and constants (vb.consts_keep) and the finished light
+ * image, and accumulates into the output; k_vcm_shadow and k_vcm_accum exit at once after an overflow, the
+ * rerun otherwise.  The resolve reads nothing the next iteration's light pass and walk write (their light
+ * vertices, light image, entry list, rsave and constants copy are the other set, orx_capi.hip
+ * vcm_iteration), so it runs beside them (orx_capi.hip vcm_camera).  vb.dq0 == NULL: in place only. */
 void launch_vcm_camera_walk(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
-    hipLaunchKernelGGL(k_vcm_consts, dim3(1), dim3(1), 0, s, c, vb.consts);
+    VcmZero z;
+    z.p[0] = vb.work; /* the camera pass's work counter */
+    z.n[0] = 1;
+    if (vb.dq0) { /* entries reserved, overflow flag */
+        z.p[1] = vb.dctl;
+        z.n[1] = 4;
+    }
+    hipLaunchKernelGGL(k_vcm_consts, dim3(1), dim3(1), 0, s, c, vb.consts, vb.dq0 ? vb.consts_keep : nullptr, z);
     const uint32_t blocks = vcm_camera_waves(((c.W + 7) / 8) * ((c.rows + 7) / 8));
     if (blocks == 0) return;
-    if (!vb.dq0) {
-        launch_camera_kernel<0>(s, S, vb, blocks);
-        return;
-    }
-    const uint32_t nslot = c.rows * vb.RW;
-    for (int k = 0; k < 6; k++)
-        hipMemcpyAsync(vb.rng_save + (size_t)k * nslot, vb.rng.p[k], (size_t)nslot * 4, hipMemcpyDeviceToDevice, s);
-    hipMemsetAsync(vb.dctl, 0, 16, s);
-    launch_camera_kernel<1>(s, S, vb, blocks);
-}
-void launch_vcm_camera_rerun(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
-    const uint32_t blocks = vcm_camera_waves(((c.W + 7) / 8) * ((c.rows + 7) / 8));
-    if (blocks == 0 || !vb.dq0) return;
-    const uint32_t nslot = c.rows * vb.RW;
-    hipLaunchKernelGGL(k_vcm_rng_restore, dim3((nslot + 255) / 256), dim3(256), 0, s, vb, nslot);
-    launch_camera_kernel<2>(s, S, vb, blocks);
+    if (!vb.dq0) launch_camera_kernel<0>(s, S, vb, vb.consts, blocks);
+    else launch_camera_kernel<1>(s, S, vb, vb.consts, blocks);
 }
 void launch_vcm_camera_resolve(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
     if (!vb.dq0 || c.W == 0 || c.rows == 0) return;
@@ -1379,12 +1407,20 @@ void launch_vcm_camera_resolve(hipStream_t s, const DevScene& S, const VcmBufs& 
     const uint32_t per_cu = std::min<uint32_t>(4u * ORX_VCM_SHADOW_WAVES, (uint32_t)((160u << 10) / lds));
     const uint32_t sblocks = std::min(cus * std::max(1u, per_cu), vb.shstk_lanes / 64u);
     if (vb.lcq) hipLaunchKernelGGL(k_vcm_light_shadow, dim3(sblocks), dim3(64), lds, s, S, vb);
-    hipLaunchKernelGGL(k_vcm_shadow, dim3(sblocks), dim3(64), lds, s, S, vb);
-    hipLaunchKernelGGL(k_vcm_accum, dim3((c.lcount + 255) / 256), dim3(256), 0, s, vb, c.lcount);
+    hipLaunchKernelGGL(k_vcm_shadow, dim3(sblocks), dim3(64), lds, s, S, vb); /* also zeroes work[2] */
+    /* a pixel's list holds at most (1 + VCM_MAX_VERTS) connections per camera vertex */
+    const uint32_t max_per_px = (c.maxPathLen + 1) * (1 + VCM_MAX_VERTS);
+    hipLaunchKernelGGL(k_vcm_accum, dim3((c.lcount + 255) / 256), dim3(256), 0, s, vb, c.lcount, max_per_px);
+    const uint32_t blocks = vcm_camera_waves(((c.W + 7) / 8) * ((c.rows + 7) / 8));
+    if (blocks == 0) return;
+    VcmBufs rv = vb; /* the rerun: RNG from the walk's start words, its own queues and work counter */
+    rv.rng = vb.rsave;
+    rv.shq = vb.shq_rerun;
+    rv.work = vb.work + 2;
+    launch_camera_kernel<2>(s, S, rv, vb.consts_keep, blocks);
 }
 void launch_vcm_camera(hipStream_t s, const DevScene& S, const VcmBufs& vb, const VcmConsts& c) {
     launch_vcm_camera_walk(s, S, vb, c);
-    launch_vcm_camera_rerun(s, S, vb, c);
     launch_vcm_camera_resolve(s, S, vb, c);
 }
 

@@ -560,6 +560,10 @@ def test_vcm_camera_shadow_modes(defer):
         assert res["rays"] > 0 and res["overflow"] == 0, res
     elif defer == "1":
         assert res["overflow"] == 1, res  # the rerun path ran
+        # with the light pass's camera connections deferred into the same resolve: the rerun reads the
+        # light image those splats land in, so it must follow k_vcm_light_shadow (it runs in the resolve,
+        # in stream order after it)
+        assert res["lconn"] > 0, res
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("ldefer", ["4", "1", "0"])
@@ -583,6 +587,38 @@ def test_vcm_light_connection_modes(ldefer):
         assert res["lconn"] > 0 and res["linplace"] > 0, res  # both paths ran
     else:
         assert res["lconn"] == 0 and res["linplace"] == 0, res
+
+
+@pytest.mark.gpu
+def test_vcm_resolve_bounds_stale_lists():
+    """The VCM resolve driven with stale list state (orx_debug_vcm_stale_resolve): an entry count past
+    the list's capacity, every odd pixel's list head past the entries, and light-connection entries whose
+    pixel offsets lie past the light image -- what a walk or light pass that did not write the set's
+    control words would leave (the round-5 timing variant that faulted in k_vcm_accum).
+    The resolve must complete: even pixels' colours bit-identical to the real resolve (their lists are
+    intact), odd pixels' colours at most the real ones (the sum stops at the bad head), all finite."""
+    import ctypes as C
+    scene = scenes.scene_by_name("CornellSmall")
+    W, H = 96, 72
+    r = OptixRenderer(_abi.default_config(seed=SEED, photon_launch_width=64, photon_launch_height=64))
+    r.initialize(0)
+    r.initScene(scene)
+    cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
+    det = RenderRequestDetails(cam, scene.name, _abi.VCM_BIDIRECTIONAL_PATH_TRACING, W, H)
+    radius = scene.initial_ppm_radius()
+    for it in range(2):
+        r.renderNextIteration(it, it, radius, True, det)
+    before = r.read_buffer(_abi.BUF_VCM_CAMERA, np.float32).reshape(-1, 3).copy()
+    assert r.stats().vcm_light_connections > 0
+    f = r._lib.orx_debug_vcm_stale_resolve
+    f.argtypes, f.restype = [C.c_void_p], C.c_int
+    assert f(r._h) == 0, r._lib.orx_last_error(r._h)
+    after = r.read_buffer(_abi.BUF_VCM_CAMERA, np.float32).reshape(-1, 3)
+    assert np.isfinite(after).all() and np.isfinite(r.getOutputBuffer()).all()
+    assert np.array_equal(after[0::2], before[0::2])
+    assert (after[1::2] <= before[1::2]).all()
+    assert (after[1::2] < before[1::2]).any()  # the bad heads were read and stopped the sums
+    r.destroy()
 
 
 @pytest.mark.gpu
