@@ -348,6 +348,12 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hitpoints_device
 /* indirect_device: max_local_rows * W * 3 floats for the own rows: the summed unattenuated
  * estimates (times each own hit point's attenuation here) */
 orx_status orx_ppm_finish(orx_renderer* r, const void* indirect_device, size_t indirect_bytes);
+/* orx_ppm_finish on `stream` (a hipStream_t; NULL: as orx_ppm_finish).  Pipelined (orx_set_ppm_pipeline), the
+ * finish of iteration i may be issued after iteration i+1's orx_ppm_local_eye -- behind i+1's hit-point
+ * all-gather, so that the reduce-scatter of i does not hold that all-gather back on RCCL's in-order stream --
+ * and then finishes i (its pixel buffers and constants are held for it); at most one such finish may be
+ * outstanding when the next eye pass is issued (ORX_ERR_STATE otherwise) */
+orx_status orx_ppm_finish_on(orx_renderer* r, const void* indirect_device, size_t indirect_bytes, void* stream);
 /* Pipelined sharded PPM (uniform grid or kd-tree: the hash is single-device, and pipelines on
  * its own without this call; call before the first iteration, like orx_set_shard):
  * orx_ppm_gather_external and orx_ppm_finish of iteration i run on `side_stream` (a hipStream_t

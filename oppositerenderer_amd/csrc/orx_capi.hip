@@ -372,6 +372,13 @@ struct orx_renderer {
     bool pipe_bufs = false, pend = false, last_pipelined = false;
     /* sharded PPM pipelining (orx_set_ppm_pipeline): gather + finish on the caller's side stream */
     bool shard_pipe = false;
+    /* its finishes (orx_ppm_finish / _on): fin_due, the current iteration's is outstanding; fin_snap, the
+     * previous iteration's is, its pixel buffers, constants and buffer set held here (the caller may issue
+     * it after the next iteration's eye pass, behind that iteration's hit-point all-gather) */
+    bool fin_due = false, fin_snap = false;
+    PixelBufs fin_px{};
+    Consts fin_consts{};
+    uint32_t fin_pp = 0;
     /* slab mode (orx_set_slab_partition): photon buffers sized for the imported slab photons */
     bool slab = false;
     size_t S_cap = 0;
@@ -928,6 +935,7 @@ static orx_status resize(orx_renderer* r, uint32_t W, uint32_t H) {
     /* slots per emitted photon: the deposit limit (uniform grid), or room for every non-specular
      * hit at depth 1..max depth - 1 (stochastic hash: store_photon.h never counts deposits) */
     const uint32_t D = hash ? std::min(r->cfg.max_photon_trace_depth, 8u) : r->cfg.max_photon_deposits;
+    r->fin_due = r->fin_snap = false; /* a finish held back across a resize is dropped with its buffers */
     r->W = W;
     r->H = H;
     r->RW = std::max(PW, W);
@@ -1941,6 +1949,14 @@ orx_status orx_ppm_local_eye(orx_renderer* r, uint64_t iteration_number, uint64_
     Consts c = make_consts(r, ppm_radius, local_iteration_number);
     r->last_pipelined = r->shard_pipe && r->pipe_bufs;
     if (r->last_pipelined) {
+        if (r->fin_due) { /* the previous iteration's finish comes later: hold its set */
+            if (r->fin_snap) return set_err(r, ORX_ERR_STATE, "two sharded PPM finishes outstanding");
+            r->fin_px = r->px;
+            r->fin_consts = r->last_consts;
+            r->fin_pp = r->pp;
+            r->fin_snap = true;
+        }
+        r->fin_due = true;
         /* the other buffer set; its last gather + finish (two iterations back) and, through the
          * RNG chain, the last direct pass precede this eye pass */
         swap_sets(r);
@@ -2214,30 +2230,44 @@ orx_status orx_ppm_gather_external(orx_renderer* r, const void* hp, uint32_t seg
     return ORX_OK;
 }
 
-orx_status orx_ppm_finish(orx_renderer* r, const void* indirect, size_t bytes) {
+orx_status orx_ppm_finish_on(orx_renderer* r, const void* indirect, size_t bytes, void* stream) {
     if (!r || !indirect) return ORX_ERR_INVALID_ARGUMENT;
     size_t need = (size_t)r->max_rows * r->W * 12;
     if (bytes < need) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "indirect buffer too small");
     HIPCHK(r, hipSetDevice(r->device));
-    if (r->last_pipelined) { /* output only (direct ran beside the grid build), on the side stream */
-        hipStream_t g = gather_stream(r);
-        launch_indirect_atten(g, r->px, (uint32_t)(need / 12), (const float*)indirect);
+    if (r->last_pipelined) {
+        /* output only (direct ran beside the grid build), on `stream` (NULL: the side stream): the oldest
+         * outstanding iteration, i.e. the one before the last eye pass if its finish was held back */
+        if (!r->fin_snap && !r->fin_due) return set_err(r, ORX_ERR_STATE, "no sharded PPM iteration to finish");
+        const bool prev = r->fin_snap;
+        const PixelBufs px = prev ? r->fin_px : r->px;
+        const Consts c = prev ? r->fin_consts : r->last_consts;
+        const uint32_t k = prev ? r->fin_pp : r->pp;
+        hipStream_t g = stream ? (hipStream_t)stream : gather_stream(r);
+        launch_indirect_atten(g, px, (uint32_t)(need / 12), (const float*)indirect);
+        /* the direct pass of that iteration: not yet overwritten, since the next one's photon pass (which
+         * records the event again) is issued after this finish */
         HIPCHK(r, hipStreamWaitEvent(g, r->ev_direct_done, 0));
         ev_begin_on(r, P_DIRECT, g);
-        launch_ppm_direct_output(g, r->scene, r->px, r->last_consts, 2);
+        launch_ppm_direct_output(g, r->scene, px, c, 2);
         ev_end_on(r, P_DIRECT, g);
-        HIPCHK(r, hipEventRecord(r->ev_gdone[r->pp], g));
+        HIPCHK(r, hipEventRecord(r->ev_gdone[k], g));
+        if (prev) r->fin_snap = false;
+        else r->fin_due = false;
         r->pend = true;
         HIPCHK(r, hipGetLastError());
         return ORX_OK;
     }
-    hipStream_t st = cur_stream(r);
+    hipStream_t st = stream ? (hipStream_t)stream : cur_stream(r);
     launch_indirect_atten(st, r->px, (uint32_t)(need / 12), (const float*)indirect);
-    ev_begin(r, P_DIRECT);
+    ev_begin_on(r, P_DIRECT, st);
     launch_ppm_direct_output(st, r->scene, r->px, r->last_consts);
-    ev_end(r, P_DIRECT);
+    ev_end_on(r, P_DIRECT, st);
     HIPCHK(r, hipGetLastError());
     return ORX_OK;
+}
+orx_status orx_ppm_finish(orx_renderer* r, const void* indirect, size_t bytes) {
+    return orx_ppm_finish_on(r, indirect, bytes, nullptr);
 }
 
 orx_status orx_set_ppm_pipeline(orx_renderer* r, void* side_stream, int enable) {
@@ -2249,6 +2279,7 @@ orx_status orx_set_ppm_pipeline(orx_renderer* r, void* side_stream, int enable) 
     if (s0 != ORX_OK) return s0;
     r->shard_pipe = enable != 0;
     r->side = enable ? (hipStream_t)side_stream : nullptr;
+    r->fin_due = r->fin_snap = false;
     r->rng_ready = false; /* re-allocate the frame with the second buffer set (as orx_set_shard) */
     return ORX_OK;
 }

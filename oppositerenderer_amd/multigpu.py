@@ -257,8 +257,15 @@ class ShardedPPM:
                      for _ in range(nsets)]
         self.hp_local, self.hp_all, self.ind_partial, self.ind_local = self.sets[0]
         self.k = 0
+        self.pending = None  # pipelined: the last gather's (partial, summed indirect, done event), not yet reduced
         if self.pipe:
             backend.enable_pipeline()
+            # the reduce-scatter + finish of iteration i run here, issued after iteration i+1's all-gather:
+            # RCCL runs one communicator's collectives in issue order, so a reduce-scatter issued right
+            # after the gather of i would hold the all-gather of i+1 until that gather ends, and the side
+            # stream would wait for it before the next gather (tools/shard_model.py --interfere: configs[4]
+            # N=8 per-rank frame 7.96 -> 6.74 ms with the collectives' local side emulated)
+            self.fin = backend.torch.cuda.Stream(backend.device)
 
     def slab_exchange(self, radius):
         """histograms -> plan (host) -> pack -> all-to-all of the photon records -> import + grid"""
@@ -283,25 +290,46 @@ class ShardedPPM:
         b.slab_import(recv, nr, box, axis, self.nb, own)
         self.last_plan = (axis, bin_dest, counts)
 
+    def _gather_async(self, work, hp_all, ind_partial, ind_local):
+        """pipelined: the gather of this iteration on the side stream once its all-gather is in; its
+        reduce-scatter + finish wait for the next iteration's all-gather to be issued (drain)"""
+        torch = self.b.torch
+        with torch.cuda.stream(self.b.side):
+            work.wait()
+            self.b.gather_external(hp_all, self.world, ind_partial)
+            done = torch.cuda.Event()
+            done.record(self.b.side)
+        self.pending = (ind_partial, ind_local, done)
+
+    def drain(self):
+        """Issue the outstanding reduce-scatter + finish (pipelined schedule; a no-op otherwise): called by
+        the next iteration right after its all-gather, and before anything reads the output."""
+        if self.pending is None:
+            return
+        ind_partial, ind_local, done = self.pending
+        self.pending = None
+        torch = self.b.torch
+        with torch.cuda.stream(self.fin):
+            self.fin.wait_event(done)
+            self.dist.reduce_scatter_tensor(ind_local, ind_partial)
+            self.b.finish_on(ind_local, self.fin)
+
     def iteration(self, it, local_it, radius, request):
         d = self.dist
         if self.slab:
             return self._iteration_slab(it, local_it, radius, request)
         if self.pipe:
-            # iteration i's gather, reduce-scatter and output on the side stream while the next
-            # iteration's eye, photon and grid passes run on the compute stream (buffer sets
+            # iteration i's gather on the side stream and its reduce-scatter + output on the finish stream
+            # while the next iteration's eye, photon and grid passes run on the compute stream (buffer sets
             # alternate; the renderer orders the RNG chain and the buffer reuse with events)
             hp_local, hp_all, ind_partial, ind_local = self.sets[self.k]
             self.k ^= 1
             self.b.local_eye(it, local_it, radius, request)
             self.b.export_hitpoints(hp_local)
             work = d.all_gather_into_tensor(hp_all, hp_local, async_op=True)
+            self.drain()  # the previous iteration's reduce-scatter + finish, behind this all-gather
             self.b.local_photons()
-            with self.b.torch.cuda.stream(self.b.side):
-                work.wait()
-                self.b.gather_external(hp_all, self.world, ind_partial)
-                d.reduce_scatter_tensor(ind_local, ind_partial)
-                self.b.finish(ind_local)
+            self._gather_async(work, hp_all, ind_partial, ind_local)
             return
         if self.gloo or not hasattr(self.b, "local_eye"):
             self.b.local_passes(it, local_it, radius, request)
@@ -336,13 +364,10 @@ class ShardedPPM:
             self.b.local_eye(it, local_it, radius, request)
             self.b.export_hitpoints(hp_local)
             work = d.all_gather_into_tensor(hp_all, hp_local, async_op=True)
+            self.drain()
             self.b.local_photon_trace()
             self.slab_exchange(radius)
-            with self.b.torch.cuda.stream(self.b.side):
-                work.wait()
-                self.b.gather_external(hp_all, self.world, ind_partial)
-                d.reduce_scatter_tensor(ind_local, ind_partial)
-                self.b.finish(ind_local)
+            self._gather_async(work, hp_all, ind_partial, ind_local)
             return
         self.b.local_trace(it, local_it, radius, request)
         self.b.export_hitpoints(self.hp_local)
@@ -362,6 +387,8 @@ class ShardedPPM:
 
     def image(self):
         """Full running-sum image on every rank (collective)."""
+        if hasattr(self, "drain"):
+            self.drain()
         out = self.b.output_local_tensor(self.max_rows)
         parts = [out.clone() for _ in range(self.world)]
         self.dist.all_gather(parts, out)
@@ -430,6 +457,7 @@ class DeviceShard:
             ("orx_export_hitpoints", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
             ("orx_ppm_gather_external", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t], C.c_int),
             ("orx_ppm_finish", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
+            ("orx_ppm_finish_on", [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p], C.c_int),
             ("orx_set_ppm_pipeline", [C.c_void_p, C.c_void_p, C.c_int], C.c_int),
             ("orx_vcm_local_light", [C.c_void_p, C.c_uint64, C.c_uint64, C.c_float, C.c_void_p], C.c_int),
             ("orx_export_vcm_splats", [C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
@@ -523,6 +551,11 @@ class DeviceShard:
 
     def finish(self, ind_local):
         self.r._check(self.lib.orx_ppm_finish(self.r._h, C.c_void_p(ind_local.data_ptr()), ind_local.numel() * 4))
+
+    def finish_on(self, ind_local, stream):
+        """orx_ppm_finish_on: the oldest outstanding pipelined iteration's finish, on `stream`"""
+        self.r._check(self.lib.orx_ppm_finish_on(self.r._h, C.c_void_p(ind_local.data_ptr()), ind_local.numel() * 4,
+                                                 C.c_void_p(stream.cuda_stream)))
 
     def render_next(self, it, local_it, radius, request):
         self.r._check(self.lib.orx_render_next_iteration(self.r._h, it, local_it, radius, 1, C.byref(request)))
@@ -685,10 +718,12 @@ def bench_main(args, metric, cpu_baseline=None):
         it = batch_iteration(i, rank, world) if batch else i
         sharded.iteration(it, i, radii[it], req)
 
+    drain = getattr(sharded, "drain", lambda: None)  # pipelined rows/slab: the last reduce-scatter + finish
     i = 0
     for _ in range(max(1, args.warmup)):
         step(i)
         i += 1
+    drain()
     sync()
     dist.barrier()
     if hasattr(r, "reset_timing"):
@@ -701,6 +736,7 @@ def bench_main(args, metric, cpu_baseline=None):
         i += 1
     if batch and sharded.reduce_every > 0 and sharded.n % sharded.reduce_every:
         sharded.reduce()  # the timed job ends with its radiance merged on rank 0
+    drain()  # the timed job ends with the last iteration's reduce-scatter and output
     sync()
     dist.barrier()
     elapsed = time.perf_counter() - t0

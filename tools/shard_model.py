@@ -247,7 +247,22 @@ def full_hitpoints(scene, W, H, world, n_iters, dev, req):
     return out
 
 
-def run_pipelined(world, W=1920, H=1080, P=2048, warm=4, steps=32, scene=None):
+_EMUL = None
+
+
+def xgmi_emul():
+    """tools/libxgmi_emul.so (built by __graft_entry__.build()): a paced copy / add kernel with an RCCL
+    collective's footprint (tools/xgmi_emul.hip)."""
+    global _EMUL
+    if _EMUL is None:
+        import ctypes as C
+        _EMUL = C.CDLL(os.path.join(ROOT, "tools", "libxgmi_emul.so"))
+        _EMUL.xgmi_emul.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_double, C.c_int, C.c_int, C.c_void_p]
+        _EMUL.xgmi_emul.restype = C.c_int
+    return _EMUL
+
+
+def run_pipelined(world, W=1920, H=1080, P=2048, warm=4, steps=32, scene=None, interfere=None):
     """Rank 0 of N in the pipelined row-partition schedule ShardedPPM(pipeline=True) runs
     (multigpu.py): per iteration the local eye pass and hit-point export on the compute stream, an
     event standing for the all-gather's completion (work.wait()), the local photon pass + grid
@@ -256,7 +271,14 @@ def run_pipelined(world, W=1920, H=1080, P=2048, warm=4, steps=32, scene=None):
     photons, the own block's copy (the reduce-scatter's place) and the finish -- so the gather of
     iteration i runs beside iteration i+1's local passes, as on the real ranks.  The iteration
     window is the bench's (warmup `warm`, `steps` timed iterations, the global radius sequence), and
-    the wall time between two synchronisations gives the per-rank frame without the collectives."""
+    the wall time between two synchronisations gives the per-rank frame without the collectives.
+
+    interfere = (link GB/s, workgroups): the collectives' local side is run too, on a stream of its own
+    at the points RCCL runs them -- the all-gather after the export, the side stream's gather waiting for
+    it (work.wait()), the reduce-scatter after the gather, the finish waiting for it -- as paced kernels
+    (tools/xgmi_emul.hip) that hold `workgroups` workgroups for the link time of the bytes a rank receives
+    ((N-1)/N of each collective) and move those bytes through HBM (all-gather: a copy; reduce-scatter: an
+    add of the received chunk into the local one)."""
     dev = torch.device("cuda", 0)
     scene = scene or synthetic.synthetic_hall()
     cam = scene.default_camera.set_aspect_ratio(float(np.float32(W) / np.float32(H)))
@@ -276,6 +298,36 @@ def run_pipelined(world, W=1920, H=1080, P=2048, warm=4, steps=32, scene=None):
     mr = (H + world - 1) // world
     sets = [(b.alloc(multigpu.hp_export_floats(mr, W)), b.alloc(world * mr * W * 3), b.alloc(mr * W * 3))
             for _ in range(2)]
+    ag_bytes = world * 4 * multigpu.hp_export_floats(mr, W) * (world - 1) // world // 16 * 16
+    rs_bytes = world * mr * W * 12 * (world - 1) // world // 16 * 16
+    if interfere and world > 1:
+        link_gbs, wgs = interfere
+        rccl = torch.cuda.Stream(dev)
+        ag_src = torch.zeros(ag_bytes // 4, device=dev)
+        ag_dst = [torch.zeros(ag_bytes // 4, device=dev) for _ in range(2)]
+        rs_in = torch.zeros(rs_bytes // 4, device=dev)
+        rs_acc = [torch.zeros(rs_bytes // 4, device=dev) for _ in range(2)]
+        ag_ns, rs_ns = ag_bytes / link_gbs, rs_bytes / link_gbs  # bytes / (GB/s) = ns
+
+    # ShardedPPM's schedule (MODEL_RS_DEFER=1, the default): the reduce-scatter of iteration i is issued after
+    # the all-gather of i+1 (so that one does not queue behind the gather of i on RCCL's in-order stream), and
+    # the finish (orx_ppm_finish_on) waits for it on a stream of its own, so that the side stream goes on to the
+    # next gather; MODEL_RS_DEFER=0: the round-5 schedule (reduce-scatter and finish on the side stream)
+    rs_defer = interfere and world > 1 and os.environ.get("MODEL_RS_DEFER", "1") == "1"
+    if rs_defer:
+        fin = torch.cuda.Stream(dev)
+    pending = []
+
+    def issue_rs(j, gdone):
+        _, part_j, own_j = sets[j % 2]
+        rccl.wait_event(gdone)
+        xgmi_emul().xgmi_emul(rs_in.data_ptr(), rs_acc[j % 2].data_ptr(), rs_bytes, rs_ns, 1, wgs, rccl.cuda_stream)
+        rdone = torch.cuda.Event()
+        rdone.record(rccl)
+        fin.wait_event(rdone)
+        with torch.cuda.stream(fin):
+            own_j.copy_(part_j[:mr * W * 3])
+            b.finish_on(own_j, fin)
 
     def step(it):
         hp_loc, part, own = sets[it % 2]
@@ -283,20 +335,55 @@ def run_pipelined(world, W=1920, H=1080, P=2048, warm=4, steps=32, scene=None):
         b.export_hitpoints(hp_loc)
         ready = torch.cuda.Event()
         ready.record(main)
+        if rs_defer:
+            rccl.wait_event(ready)
+            xgmi_emul().xgmi_emul(ag_src.data_ptr(), ag_dst[it % 2].data_ptr(), ag_bytes, ag_ns, 0, wgs,
+                                  rccl.cuda_stream)
+            ag_done = torch.cuda.Event()
+            ag_done.record(rccl)
+            if pending:
+                issue_rs(*pending.pop())
+            b.local_photons()
+            with torch.cuda.stream(side):
+                side.wait_event(ag_done)
+                b.gather_external(hps[it], world, part)
+                gdone = torch.cuda.Event()
+                gdone.record(side)
+            pending.append((it, gdone))
+            return
+        if interfere and world > 1:  # the all-gather on RCCL's stream, beside the photon pass + grid build
+            rccl.wait_event(ready)
+            xgmi_emul().xgmi_emul(ag_src.data_ptr(), ag_dst[it % 2].data_ptr(), ag_bytes, ag_ns, 0, wgs,
+                                  rccl.cuda_stream)
+            ready = torch.cuda.Event()
+            ready.record(rccl)
         b.local_photons()
         with torch.cuda.stream(side):
             side.wait_event(ready)
             b.gather_external(hps[it], world, part)
+            if interfere and world > 1:  # the reduce-scatter after the gather, the finish waits for it
+                gdone = torch.cuda.Event()
+                gdone.record(side)
+                rccl.wait_event(gdone)
+                xgmi_emul().xgmi_emul(rs_in.data_ptr(), rs_acc[it % 2].data_ptr(), rs_bytes, rs_ns, 1, wgs,
+                                      rccl.cuda_stream)
+                rdone = torch.cuda.Event()
+                rdone.record(rccl)
+                side.wait_event(rdone)
             own.copy_(part[:mr * W * 3])
             b.finish(own)
 
     for it in range(warm):
         step(it)
+    if pending:
+        issue_rs(*pending.pop())
     torch.cuda.synchronize()
     r.reset_timing()
     t0 = time.perf_counter()
     for it in range(warm, n):
         step(it)
+    if pending:
+        issue_rs(*pending.pop())
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / steps
     st = r.stats()
@@ -336,6 +423,11 @@ if __name__ == "__main__":
     if "--pipelined" in sys.argv:
         # pipelined per-rank schedule against the single-device pipelined frame (bench iteration window)
         args = [a for a in sys.argv[1:] if a != "--pipelined"]
+        interfere = None
+        if "--interfere" in args:  # --interfere LINK_GBS WORKGROUPS: the collectives' local side run too
+            i = args.index("--interfere")
+            interfere = (float(args[i + 1]), int(args[i + 2]))
+            args = args[:i] + args[i + 3:]
         conf = 2
         if args[:1] == ["--config"]:
             conf, args = int(args[1]), args[2:]
@@ -347,7 +439,7 @@ if __name__ == "__main__":
         single = run_single_pipelined(**kw)
         print(f"single device, bench schedule: {single:.3f} ms/frame", flush=True)
         for n in worlds:
-            ms, passes, ag, rs = run_pipelined(n, **kw)
+            ms, passes, ag, rs = run_pipelined(n, interfere=interfere, **kw)
             one, alll = collectives_ms(ag, rs, n)
             # overlap-aware: the all-gather of iteration i runs beside its photon pass + grid build, the
             # reduce-scatter (side stream, after the gather) beside the next iteration's eye + photon
@@ -360,6 +452,12 @@ if __name__ == "__main__":
             exposed = max(0.0, ag1 - win_ag) + max(0.0, rs1 - win_rs)
             ov = ms + exposed
             lo, hi = max(ms, alll), ms + one
+            if interfere and n > 1:
+                print(f"N={n}: per-rank pipelined frame {ms:.3f} ms WITH the collectives' local side run (paced at "
+                      f"{interfere[0]:.0f} GB/s on {interfere[1]} workgroups: all-gather {ag1 * 153.0 / interfere[0]:.3f} ms, "
+                      f"reduce-scatter {rs1 * 153.0 / interfere[0]:.3f} ms) = {single / ms:.2f}x the single-device frame "
+                      f"| passes {passes}", flush=True)
+                continue
             print(f"N={n}: per-rank pipelined frame {ms:.3f} ms (collectives not run) | all-gather {ag:.0f} MB, "
                   f"reduce-scatter {rs:.0f} MB; one link: all-gather {ag1:.3f} ms beside photon+grid {win_ag:.3f} ms, "
                   f"reduce-scatter {rs1:.3f} ms beside eye+photon {win_rs:.3f} ms -> exposed {exposed:.3f} ms; "
