@@ -316,19 +316,33 @@ def launch_ranks(n, argv):
     return rc
 
 
+def hw_queues():
+    """HIP hardware queues for the multi-GPU paths, before the first HIP call: the pipelined row partition keeps
+    torch's compute stream, the renderer's aux stream, the gather side stream, the finish stream and RCCL's busy at
+    once; with HIP's default of 4 queues the side stream could share the compute stream's queue and the two
+    serialise (configs[4] N=8 per-rank frame 8.05 against 6.56 ms with 8 queues, tools/shard_model.py --pipelined).
+    Below 8 (or unset) it is raised to 16 (the pool allows 32) with a note on stderr -- the GPU boxes export 4 --
+    unless ORX_KEEP_HW_QUEUES=1 keeps the caller's value; the bench line records the inherited and the used value
+    (config.hw_queues)."""
+    v = os.environ.get("GPU_MAX_HW_QUEUES")
+    os.environ["ORX_INHERITED_HW_QUEUES"] = v if v is not None else "unset"
+    if os.environ.get("ORX_KEEP_HW_QUEUES", "0") == "1":
+        return
+    if v is None or int(v or 0) < 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "16"
+        print(f"bench.py: GPU_MAX_HW_QUEUES {v if v is not None else 'unset'} -> 16 for the multi-GPU schedule "
+              "(ORX_KEEP_HW_QUEUES=1 keeps it)", file=sys.stderr)
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))  # inherited by the ranks (see below)
+        hw_queues()  # inherited by the ranks
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus > 1 or world > 1 or args.force_sharded:
-        # before the first HIP call: the pipelined row partition runs five streams at once (torch's compute
-        # stream, the renderer's aux stream, the gather side stream, RCCL's); with HIP's default of 4
-        # hardware queues the side stream could share the compute stream's queue and the two serialise
-        # (configs[4] N=8 per-rank frame 8.05 against 6.56 ms with 8 queues, tools/shard_model.py --pipelined)
-        os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
+        hw_queues()  # before the first HIP call
         from oppositerenderer_amd import multigpu
         return multigpu.bench_main(args, METRIC, cpu_baseline=None if args.no_cpu_baseline else cpu_baseline)
 

@@ -789,6 +789,8 @@ def bench_main(args, metric, cpu_baseline=None):
                                      + f" per GPU, photon-batch partition: each of {world} GPUs renders its own "
                                        "iterations (weak scaling)"),
                         "baseline_config": getattr(args, "config", None),
+                        "hw_queues": {"used": os.environ.get("GPU_MAX_HW_QUEUES"),
+                                      "inherited": os.environ.get("ORX_INHERITED_HW_QUEUES")},
                         "scene": scene.name, "width": W, "height": H, "method": _METHOD[mcode],
                         "photons_per_iteration": 0 if (vcm or pt) else P * P,
                         "paths_per_iteration": paths,
@@ -809,6 +811,8 @@ def bench_main(args, metric, cpu_baseline=None):
                        {"workload": (f"{scene.name} {W}x{H} PPM, {P * P:,} photons/iter per GPU (weak scaling)" if weak
                                      else f"{scene.name} {W}x{H} PPM, {P * PH:,} photons/iter total (strong scaling)"),
                         "baseline_config": getattr(args, "config", None),
+                        "hw_queues": {"used": os.environ.get("GPU_MAX_HW_QUEUES"),
+                                      "inherited": os.environ.get("ORX_INHERITED_HW_QUEUES")},
                         "scene": scene.name, "width": W, "height": H, "photons_per_iteration": P * PH,
                         "paths_per_iteration": paths,
                         "parallelism": (f"row-interleaved RNG/pixel/photon ownership x{world}; "

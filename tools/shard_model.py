@@ -18,7 +18,8 @@ import time
 # the pipelined schedule runs five streams at once (compute, the renderer's aux stream, the gather side
 # stream, and in the bench RCCL's): with HIP's default of 4 hardware queues the gather shared the compute
 # stream's queue and the per-rank frame serialised (configs[4] N=8: 8.05 against 6.56 ms with 8 queues)
-os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))  # before torch loads HIP
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:  # before torch loads HIP (the boxes export 4)
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 
 import numpy as np
