@@ -20,6 +20,7 @@ RenderResultPacketReceiver, and the client's request generator.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import math
 import time
 from dataclasses import dataclass, field
@@ -66,11 +67,19 @@ WIRE_SYMBOLS = (
 )
 
 _declared = False
+_wire_lib = None
 
 
 def _lib():
-    global _declared
-    lib = load_library()
+    """liborx.so (the wire codec and receiver are host code in it), or ORX_WIRE_LIB: a library of the codec
+    alone, e.g. the ASan/UBSan build tests/test_sanitizers.py runs the wire tests against"""
+    global _declared, _wire_lib
+    if os.environ.get("ORX_WIRE_LIB"):
+        if _wire_lib is None:
+            _wire_lib = C.CDLL(os.environ["ORX_WIRE_LIB"])
+        lib = _wire_lib
+    else:
+        lib = load_library()
     if _declared:
         return lib
     P, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int32

@@ -11,7 +11,8 @@ import numpy as np
 from oppositerenderer_amd import _abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "oracle", "liborx_oracle.so")
+# ORACLE_LIB: another build of the same sources (the ASan/UBSan one, tests/test_sanitizers.py)
+LIB = os.environ.get("ORACLE_LIB") or os.path.join(ROOT, "oracle", "liborx_oracle.so")
 _lib = None
 
 

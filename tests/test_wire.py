@@ -130,6 +130,28 @@ def test_malformed_frames_raise():
             wire.RenderResultPacket.decode(r[:cut])
 
 
+def test_mutated_frames_decode_or_raise():
+    """Every truncation and 2000 seeded byte mutations of a request and a result frame: the decoder either
+    returns a frame or raises OrxError -- it never reads past the buffer (tests/test_sanitizers.py runs this
+    under AddressSanitizer, which turns any out-of-bounds read of the codec into a failure)."""
+    rng = np.random.default_rng(5)
+    req = wire.RenderServerRenderRequest(7, [3, 4, 5], [1.0, 0.9, 0.8], wire.RenderServerRenderRequestDetails())
+    res = wire.RenderResultPacket(7, [3, 4, 5], rng.uniform(0, 1, 3 * 17).astype(np.float32))
+    for frame, cls in ((req.encode(), wire.RenderServerRenderRequest), (res.encode(), wire.RenderResultPacket)):
+        for cut in range(len(frame)):
+            with pytest.raises(OrxError):
+                cls.decode(frame[:cut])
+        for _ in range(1000):
+            bad = bytearray(frame)
+            for _ in range(int(rng.integers(1, 4))):
+                k = int(rng.integers(0, len(bad)))
+                bad[k] = int(rng.integers(0, 256)) if rng.random() < 0.5 else bad[k] ^ 0xFF
+            try:
+                cls.decode(bytes(bad))
+            except OrxError:
+                pass
+
+
 # --- receiver == oracle -------------------------------------------------------
 def _packets(rng, n_iters, sizes, n_px):
     its, k, out = list(range(n_iters)), 0, []
