@@ -520,10 +520,19 @@ static bool hash_config_ok(const orx_config& c) {
 
 /* the deferred gather yields to the next iteration's passes (lowest priority; measured equal
  * to normal priority on the hall) */
+/* The deferred gather's stream at the highest priority (ORX_GATHER_PRIO=0: the lowest): at configs[4] (4K) the
+ * gather stream is the frame's long pole (gather 23.7 ms serial, ~42 ms beside the next iteration's eye, photon
+ * and grid passes, which need ~20 ms), and dispatching its workgroups first gains 1.8 % (552 -> 562 Mpaths/s,
+ * 45.4 -> 44.6 ms); on the 1080p hall the frame is unchanged (1014 / 1014 Mpaths/s)
+ * (profiles/r06i_gather_priority_ab.txt) */
 static int gather_stream_priority() {
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
-    return least;
+    static const bool high = [] {
+        const char* e = getenv("ORX_GATHER_PRIO");
+        return !(e && atoi(e) == 0);
+    }();
+    return high ? greatest : least;
 }
 
 orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out) {
