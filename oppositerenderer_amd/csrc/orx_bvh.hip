@@ -306,12 +306,171 @@ __global__ __launch_bounds__(256) void k_bvh_level(BvhBuildBufs B, const BvhTask
     }
 }
 
+/* ---- treelet restructuring of the binary tree (the refinement of OptiX's Trbvh: Karras & Aila 2013) ----
+ * Per inner node, bottom up, the treelet of the seven largest-area subtrees below it (largest-area expansion
+ * from the node) is rebuilt as the SAH-optimal binary tree over them: a dynamic programme over the 127 subsets
+ * (node cost ci x area, leaf cost area x triangles), the partition of each subset scanned once; the rebuilt
+ * treelet reuses its six inner nodes, the treelet root keeps its index.  One thread per node of a level (the
+ * nodes of a level have disjoint subtrees); the levels come from a top-down pass over the current tree before
+ * each bottom-up sweep.  Boxes become the unions of the children's (already conservatively expanded) boxes.
+ * Hall: photon-path node steps 17.71 -> 17.21 per ray, frame +1.7 % (PPM) / +2.1 % (VCM) measured with the same
+ * passes on the host builder (profiles/r06j_bvh_treelet_ab.txt; priced in tools/bvh_quality.cpp). */
+__device__ __forceinline__ float nd_area(const DevBvhNode& n) {
+    return box_area(n.lo[0], n.lo[1], n.lo[2], n.hi[0], n.hi[1], n.hi[2]);
+}
+__device__ __forceinline__ bool nd_leaf(const DevBvhNode& n) { return (n.count_or_right & 0x80000000u) != 0; }
+struct TreeletBufs {
+    DevBvhNode* nodes;
+    float* cost; /* [nodes] SAH cost of the subtree (area-weighted) */
+    float ci;    /* inner-node cost relative to one triangle test (the build's leaf SAH) */
+};
+__device__ void tl_refresh(const TreeletBufs& T, uint32_t n) {
+    DevBvhNode& x = T.nodes[n];
+    if (nd_leaf(x)) {
+        T.cost[n] = nd_area(x) * (float)(x.count_or_right & 0x7fffffffu);
+        return;
+    }
+    const DevBvhNode l = T.nodes[x.left_or_first], r = T.nodes[x.count_or_right];
+    for (int k = 0; k < 3; k++) x.lo[k] = fminf(l.lo[k], r.lo[k]), x.hi[k] = fmaxf(l.hi[k], r.hi[k]);
+    T.cost[n] = T.ci * nd_area(x) + T.cost[x.left_or_first] + T.cost[x.count_or_right];
+}
+__global__ __launch_bounds__(64) void k_bvh_treelet(TreeletBufs T, const uint32_t* __restrict__ list, uint32_t n,
+                                                    int restructure) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t nd = list[t];
+    tl_refresh(T, nd);
+    if (!restructure || nd_leaf(T.nodes[nd])) return;
+    uint32_t lv[7], inner[6];
+    uint32_t m = 2, ni = 1;
+    lv[0] = T.nodes[nd].left_or_first;
+    lv[1] = T.nodes[nd].count_or_right;
+    inner[0] = nd;
+    while (m < 7) {
+        int bi = -1;
+        float ba = -1.f;
+        for (uint32_t i = 0; i < m; i++) {
+            const DevBvhNode& c = T.nodes[lv[i]];
+            if (!nd_leaf(c) && nd_area(c) > ba) ba = nd_area(c), bi = (int)i;
+        }
+        if (bi < 0) break;
+        const uint32_t c = lv[bi];
+        inner[ni++] = c;
+        lv[bi] = T.nodes[c].left_or_first;
+        lv[m++] = T.nodes[c].count_or_right;
+    }
+    if (m < 3) return;
+    const uint32_t full = (1u << m) - 1u;
+    float copt[128], ar[128];
+    uint8_t split[128];
+    for (uint32_t S = 1; S <= full; S++) {
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (uint32_t i = 0; i < m; i++)
+            if (S >> i & 1u) {
+                const DevBvhNode& c = T.nodes[lv[i]];
+                for (int k = 0; k < 3; k++) lo[k] = fminf(lo[k], c.lo[k]), hi[k] = fmaxf(hi[k], c.hi[k]);
+            }
+        ar[S] = box_area(lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]);
+    }
+    for (uint32_t S = 1; S <= full; S++) {
+        if ((S & (S - 1u)) == 0) {
+            copt[S] = T.cost[lv[__builtin_ctz(S)]];
+            split[S] = 0;
+            continue;
+        }
+        float best = INFINITY;
+        uint32_t bp = 0;
+        const uint32_t low = S & (0u - S); /* the part holding the lowest member: each partition once */
+        for (uint32_t P = (S - 1u) & S; P; P = (P - 1u) & S) {
+            if (!(P & low)) continue;
+            const float c = copt[P] + copt[S ^ P];
+            if (c < best) best = c, bp = P;
+        }
+        copt[S] = T.ci * ar[S] + best;
+        split[S] = (uint8_t)bp;
+    }
+    if (!(copt[full] < T.cost[nd] * (1.f - 1e-6f))) return;
+    /* the optimal shape, top down (inner node k takes subset sub[k]), then boxes and costs bottom up */
+    uint32_t sub[6], id[6], cnt = 1, next = 1;
+    sub[0] = full;
+    id[0] = nd;
+    for (uint32_t k = 0; k < cnt; k++) {
+        const uint32_t S = sub[k], P = split[S], Q = S ^ P;
+        uint32_t ch[2];
+        const uint32_t parts[2] = {P, Q};
+        for (int h = 0; h < 2; h++) {
+            const uint32_t X = parts[h];
+            if ((X & (X - 1u)) == 0) {
+                ch[h] = lv[__builtin_ctz(X)];
+            } else {
+                ch[h] = inner[next++];
+                sub[cnt] = X;
+                id[cnt++] = ch[h];
+            }
+        }
+        T.nodes[id[k]].left_or_first = ch[0];
+        T.nodes[id[k]].count_or_right = ch[1];
+    }
+    for (uint32_t k = cnt; k-- > 0;) tl_refresh(T, id[k]);
+}
+/* the current tree's levels, top down: the inner nodes of `cur` append their two children to `next` */
+__global__ void k_bvh_bfs(const DevBvhNode* __restrict__ nodes, const uint32_t* __restrict__ cur, uint32_t n,
+                          uint32_t* __restrict__ next, uint32_t* ctl) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const DevBvhNode x = nodes[cur[t]];
+    if (nd_leaf(x)) return;
+    const uint32_t o = atomicAdd(&ctl[1], 2u);
+    next[o] = x.left_or_first;
+    next[o + 1] = x.count_or_right;
+}
+/* SAH-optimal collapse to four-wide nodes (Ylitie et al. 2017), bottom up: F[n] = the cheapest cover of n's
+ * subtree by at most 1..4 roots (a four-wide node visit costs 2.5 triangle tests x area, a leaf area x
+ * triangles), K[n] = the roots given to the left child for each budget (0: n itself is the one root; for
+ * budget 1, the distribution inside n's own node).  Priced -0.8..-2.0 % photon-ray node steps on its own. */
+__global__ void k_bvh_sahdp(const DevBvhNode* __restrict__ nodes, float4* __restrict__ F, uchar4* __restrict__ K,
+                            const uint32_t* __restrict__ list, uint32_t n) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t nd = list[t];
+    const DevBvhNode x = nodes[nd];
+    const float a = nd_area(x);
+    if (nd_leaf(x)) {
+        const float c = a * (float)(x.count_or_right & 0x7fffffffu);
+        F[nd] = make_float4(c, c, c, c);
+        K[nd] = make_uchar4(0, 0, 0, 0);
+        return;
+    }
+    const float4 fl = F[x.left_or_first], fr = F[x.count_or_right];
+    const float L[5] = {0.f, fl.x, fl.y, fl.z, fl.w}, R[5] = {0.f, fr.x, fr.y, fr.z, fr.w};
+    float f[5];
+    uint8_t kk[5];
+    auto G = [&](int i, uint8_t& kb) {
+        float best = INFINITY;
+        for (int k = 1; k < i; k++)
+            if (L[k] + R[i - k] < best) best = L[k] + R[i - k], kb = (uint8_t)k;
+        return best;
+    };
+    uint8_t k = 1;
+    f[1] = 2.5f * a + G(4, k);
+    kk[1] = k;
+    for (int i = 2; i <= 4; i++) {
+        const float g = G(i, k);
+        if (g < f[1]) f[i] = g, kk[i] = k;
+        else f[i] = f[1], kk[i] = 0;
+    }
+    F[nd] = make_float4(f[1], f[2], f[3], f[4]);
+    K[nd] = make_uchar4(kk[1], kk[2], kk[3], kk[4]);
+}
+__device__ __forceinline__ uint8_t kget(const uchar4 k, int i) { return i == 1 ? k.x : i == 2 ? k.y : i == 3 ? k.z : k.w; }
+
 /* ---- collapse to quantised BVH4 ---- */
 struct CollapseItem {
     uint32_t n2, out;
 };
 struct CollapseBufs {
     const DevBvhNode* b2;
+    const uchar4* K;       /* SAH-optimal collapse decisions (k_bvh_sahdp), or NULL: largest-area opening */
     DevBvh4* out;
     uint8_t* nch;          /* [out] children per BVH4 node */
     uint32_t* ctl;         /* [0] BVH4 node count, [1] next item count, [3] error */
@@ -343,6 +502,21 @@ __global__ void k_bvh_collapse(CollapseBufs C, const CollapseItem* __restrict__ 
     uint32_t nc = 0;
     if (b2leaf(B[it.n2])) {
         ch[nc++] = it.n2;
+    } else if (C.K) { /* the roots of the cheapest cover: budget K[n].x to the left child, the rest to the right */
+        uint32_t sn[4], sb[4], sp = 0;
+        const uint8_t k1 = C.K[it.n2].x;
+        sn[sp] = B[it.n2].count_or_right, sb[sp++] = 4u - k1;
+        sn[sp] = B[it.n2].left_or_first, sb[sp++] = k1;
+        while (sp) {
+            const uint32_t n = sn[--sp], b = sb[sp];
+            const uint8_t kb = b > 1 && !b2leaf(B[n]) ? kget(C.K[n], (int)b) : (uint8_t)0;
+            if (kb == 0) {
+                ch[nc++] = n;
+            } else {
+                sn[sp] = B[n].count_or_right, sb[sp++] = b - kb;
+                sn[sp] = B[n].left_or_first, sb[sp++] = kb;
+            }
+        }
     } else {
         ch[nc++] = B[it.n2].left_or_first;
         ch[nc++] = B[it.n2].count_or_right;
@@ -436,8 +610,9 @@ __global__ void k_bvh_bound(const DevBvh4* __restrict__ out, const uint8_t* __re
  * Outputs: out4[cap4] BVH4 nodes, leaf_order[nt] (position k holds the
  * original id of the k-th triangle in leaf order). */
 hipError_t device_build_bvh4(hipStream_t s, const float* V, const uint32_t* I, uint32_t nt, int bins, uint32_t leaf_max,
-                             float leaf_sah, DevBvh4* out4, uint32_t cap4, uint32_t* leaf_order, uint32_t* nodes4,
-                             uint32_t* stack_bound, uint32_t* max_depth, bool* ok) {
+                             float leaf_sah, int treelet_passes, bool sah_collapse, DevBvh4* out4, uint32_t cap4,
+                             uint32_t* leaf_order, uint32_t* nodes4, uint32_t* stack_bound, uint32_t* max_depth,
+                             bool* ok) {
     *ok = false;
     if (nt == 0) return hipSuccess;
     hipError_t e;
@@ -476,6 +651,52 @@ hipError_t device_build_bvh4(hipStream_t s, const float* V, const uint32_t* I, u
         std::swap(ta, tn);
     }
     *max_depth = hctl[2];
+    /* treelet restructuring sweeps and the SAH-optimal collapse's covers, each over the current tree's levels */
+    float* cost = nullptr;
+    float4* F = nullptr;
+    uchar4* K = nullptr;
+    uint32_t* lvl = nullptr;
+    if (good && (treelet_passes > 0 || sah_collapse)) {
+        good = chk(hipMalloc(&cost, cap2 * 4)) && chk(hipMalloc(&F, cap2 * sizeof(float4))) &&
+               chk(hipMalloc(&K, cap2 * sizeof(uchar4))) && chk(hipMalloc(&lvl, cap2 * 4));
+        std::vector<uint32_t> off;
+        auto levels = [&]() { /* lvl = the nodes by depth, off[d] .. off[d + 1] */
+            const uint32_t zero = 0;
+            off.assign({0u, 1u});
+            bool g = chk(hipMemcpyAsync(lvl, &zero, 4, hipMemcpyHostToDevice, s));
+            uint32_t cur = 0, n = 1;
+            while (g && n) {
+                g = chk(hipMemcpyAsync(ctl + 1, &zero, 4, hipMemcpyHostToDevice, s));
+                hipLaunchKernelGGL(k_bvh_bfs, dim3((n + 255) / 256), dim3(256), 0, s, nodes, lvl + cur, n, lvl + cur + n,
+                                   ctl);
+                g = g && chk(hipMemcpyAsync(hctl, ctl, 16, hipMemcpyDeviceToHost, s)) && chk(hipStreamSynchronize(s));
+                cur += n;
+                n = hctl[1];
+                if (n) off.push_back(cur + n);
+                if (cur + n > cap2) g = false;
+            }
+            return g;
+        };
+        const TreeletBufs T{nodes, cost, leaf_sah > 0.f ? leaf_sah : 0.6f};
+        for (int p = 0; good && p < treelet_passes; p++) {
+            good = levels();
+            for (size_t d = off.size() - 1; good && d-- > 0;) {
+                const uint32_t n = off[d + 1] - off[d];
+                hipLaunchKernelGGL(k_bvh_treelet, dim3((n + 63) / 64), dim3(64), 0, s, T, lvl + off[d], n, 1);
+            }
+        }
+        if (good && sah_collapse) {
+            good = levels();
+            for (size_t d = off.size() - 1; good && d-- > 0;) {
+                const uint32_t n = off[d + 1] - off[d];
+                hipLaunchKernelGGL(k_bvh_sahdp, dim3((n + 255) / 256), dim3(256), 0, s, nodes, F, K, lvl + off[d], n);
+            }
+        }
+        if (good && treelet_passes > 0) {
+            if (!sah_collapse) good = levels();
+            *max_depth = (uint32_t)off.size() - 2u; /* the restructured tree's depth */
+        }
+    }
     /* collapse, level by level from the root */
     uint32_t nitems = 1;
     if (good) {
@@ -484,7 +705,7 @@ hipError_t device_build_bvh4(hipStream_t s, const float* V, const uint32_t* I, u
         good = chk(hipMemcpyAsync(ctl, c0, 16, hipMemcpyHostToDevice, s)) &&
                chk(hipMemcpyAsync(citems, &root, sizeof root, hipMemcpyHostToDevice, s));
     }
-    CollapseBufs CB{nodes, out4, nch, ctl, cap4};
+    CollapseBufs CB{nodes, sah_collapse ? K : nullptr, out4, nch, ctl, cap4};
     uint32_t off = 0;
     while (good && nitems) {
         if (off + nitems > cap4) {
@@ -522,6 +743,10 @@ hipError_t device_build_bvh4(hipStream_t s, const float* V, const uint32_t* I, u
     hipFree(citems);
     hipFree(nch);
     hipFree(bound);
+    hipFree(cost);
+    hipFree(F);
+    hipFree(K);
+    hipFree(lvl);
     return good ? hipSuccess : (e != hipSuccess ? e : hipErrorUnknown);
 }
 

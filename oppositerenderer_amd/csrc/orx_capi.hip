@@ -13,6 +13,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -182,6 +183,110 @@ struct BvhBuilder {
     }
 };
 
+/* Treelet restructuring of the binary tree (Karras & Aila 2013, the refinement of OptiX's Trbvh; the host
+ * counterpart of the device builder's k_bvh_treelet, priced in tools/bvh_quality.cpp): per inner node, bottom
+ * up, the treelet of its 7 largest-area descendants' subtrees is rebuilt as the SAH-optimal binary tree over
+ * them (dynamic programme over the 127 subsets; node cost leaf_sah x area, leaf cost area x triangles), reusing
+ * the treelet's inner nodes.  Boxes are unions of the children's (already conservatively expanded) boxes. */
+struct TreeletOpt {
+    std::vector<DevBvhNode>& B;
+    float ci;
+    std::vector<double> cost;
+    explicit TreeletOpt(std::vector<DevBvhNode>& b, float c) : B(b), ci(c), cost(b.size(), 0.0) {}
+    static bool leaf(const DevBvhNode& n) { return (n.count_or_right & 0x80000000u) != 0; }
+    static float area(const float* lo, const float* hi) {
+        float dx = std::max(0.f, hi[0] - lo[0]), dy = std::max(0.f, hi[1] - lo[1]), dz = std::max(0.f, hi[2] - lo[2]);
+        return dx * dy + dy * dz + dz * dx;
+    }
+    void refresh(uint32_t n) {
+        DevBvhNode& x = B[n];
+        if (leaf(x)) {
+            cost[n] = (double)area(x.lo, x.hi) * (double)(x.count_or_right & 0x7fffffffu);
+            return;
+        }
+        const DevBvhNode &l = B[x.left_or_first], &r = B[x.count_or_right];
+        for (int k = 0; k < 3; k++) x.lo[k] = std::min(l.lo[k], r.lo[k]), x.hi[k] = std::max(l.hi[k], r.hi[k]);
+        cost[n] = (double)ci * area(x.lo, x.hi) + cost[x.left_or_first] + cost[x.count_or_right];
+    }
+    uint32_t emit(int S, uint32_t hint, const std::vector<uint32_t>& inner, size_t& next, const std::vector<int>& split,
+                  const std::vector<uint32_t>& lv) {
+        if ((S & (S - 1)) == 0) return lv[__builtin_ctz(S)];
+        const uint32_t id = hint != 0xffffffffu ? hint : inner[next++];
+        const uint32_t l = emit(split[S], 0xffffffffu, inner, next, split, lv);
+        const uint32_t r = emit(S ^ split[S], 0xffffffffu, inner, next, split, lv);
+        B[id].left_or_first = l;
+        B[id].count_or_right = r;
+        refresh(id);
+        return id;
+    }
+    bool restructure(uint32_t n) {
+        if (leaf(B[n])) return false;
+        std::vector<uint32_t> lv = {B[n].left_or_first, B[n].count_or_right}, inner = {n};
+        while (lv.size() < 7) {
+            int bi = -1;
+            float ba = -1.f;
+            for (size_t i = 0; i < lv.size(); i++)
+                if (!leaf(B[lv[i]]) && area(B[lv[i]].lo, B[lv[i]].hi) > ba) ba = area(B[lv[i]].lo, B[lv[i]].hi), bi = (int)i;
+            if (bi < 0) break;
+            const uint32_t c = lv[bi];
+            inner.push_back(c);
+            lv[bi] = B[c].left_or_first;
+            lv.push_back(B[c].count_or_right);
+        }
+        const int m = (int)lv.size();
+        if (m < 3) return false;
+        const int full = (1 << m) - 1;
+        std::vector<double> copt(1 << m, 0.0);
+        std::vector<float> ar(1 << m, 0.f);
+        std::vector<int> split(1 << m, 0);
+        for (int S = 1; S <= full; S++) {
+            float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int i = 0; i < m; i++)
+                if (S >> i & 1)
+                    for (int k = 0; k < 3; k++) lo[k] = std::min(lo[k], B[lv[i]].lo[k]), hi[k] = std::max(hi[k], B[lv[i]].hi[k]);
+            ar[S] = area(lo, hi);
+        }
+        for (int S = 1; S <= full; S++) {
+            if ((S & (S - 1)) == 0) {
+                copt[S] = cost[lv[__builtin_ctz(S)]];
+                continue;
+            }
+            double best = INFINITY;
+            int bp = 0;
+            const int low = S & -S;
+            for (int P = (S - 1) & S; P; P = (P - 1) & S) {
+                if (!(P & low)) continue;
+                const double c = copt[P] + copt[S ^ P];
+                if (c < best) best = c, bp = P;
+            }
+            copt[S] = (double)ci * ar[S] + best;
+            split[S] = bp;
+        }
+        if (!(copt[full] < cost[n] * (1.0 - 1e-6))) return false;
+        size_t next = 1;
+        emit(full, n, inner, next, split, lv);
+        return true;
+    }
+    uint32_t pass() {
+        std::vector<uint32_t> order, st = {0u};
+        while (!st.empty()) {
+            const uint32_t n = st.back();
+            st.pop_back();
+            order.push_back(n);
+            if (!leaf(B[n])) st.push_back(B[n].left_or_first), st.push_back(B[n].count_or_right);
+        }
+        uint32_t changed = 0;
+        for (auto it = order.rbegin(); it != order.rend(); ++it) {
+            refresh(*it);
+            changed += restructure(*it);
+        }
+        return changed;
+    }
+    uint32_t depth(uint32_t n) const {
+        return leaf(B[n]) ? 0u : 1u + std::max(depth(B[n].left_or_first), depth(B[n].count_or_right));
+    }
+};
+
 /* Collapse the binary SAH tree into the four-wide quantised BVH the kernels
  * traverse (DevBvh4).  Each node opens its largest-area inner children until
  * it has four; child boxes are quantised outward on an 8-bit grid per axis.
@@ -192,6 +297,46 @@ struct Bvh4Builder {
     std::vector<DevBvh4> out;
     std::vector<DevBvh4F> outf; /* same topology, fp32 child boxes */
     bool ok = true;
+    /* the SAH-optimal collapse (Ylitie et al. 2017; the device builder's k_bvh_sahdp): F[n][i], the cheapest cover of n's
+     * subtree by at most i roots (a four-wide node visit costing 2.5 triangle tests x area, a leaf area x
+     * triangles), and K[n][i] the roots given to the left child (0: n is one root) */
+    std::vector<std::array<double, 5>> F;
+    std::vector<std::array<uint8_t, 5>> K;
+    void dp(uint32_t n) {
+        const std::vector<DevBvhNode>& B = *b2;
+        if (F.empty()) F.assign(B.size(), {}), K.assign(B.size(), {});
+        const float a = area(B[n]);
+        if (leaf(B[n])) {
+            for (int i = 1; i <= 4; i++) F[n][i] = (double)a * (double)(B[n].count_or_right & 0x7fffffffu), K[n][i] = 0;
+            return;
+        }
+        const uint32_t l = B[n].left_or_first, r = B[n].count_or_right;
+        dp(l);
+        dp(r);
+        auto G = [&](int i, int& kb) {
+            double best = INFINITY;
+            for (int k = 1; k < i; k++)
+                if (F[l][k] + F[r][i - k] < best) best = F[l][k] + F[r][i - k], kb = k;
+            return best;
+        };
+        int k = 1;
+        F[n][1] = 2.5 * (double)a + G(4, k);
+        K[n][1] = (uint8_t)k; /* the distribution inside n's own node */
+        for (int i = 2; i <= 4; i++) {
+            const double g = G(i, k);
+            if (g < F[n][1]) F[n][i] = g, K[n][i] = (uint8_t)k;
+            else F[n][i] = F[n][1], K[n][i] = 0;
+        }
+    }
+    void roots(uint32_t n, int i, std::vector<uint32_t>& out_) const {
+        const std::vector<DevBvhNode>& B = *b2;
+        if (i == 1 || leaf(B[n]) || K[n][i] == 0) {
+            out_.push_back(n);
+            return;
+        }
+        roots(B[n].left_or_first, K[n][i], out_);
+        roots(B[n].count_or_right, i - K[n][i], out_);
+    }
 
     static bool leaf(const DevBvhNode& n) { return (n.count_or_right & 0x80000000u) != 0; }
     static float area(const DevBvhNode& n) {
@@ -215,6 +360,9 @@ struct Bvh4Builder {
         std::vector<uint32_t> ch;
         if (leaf(B[n2])) {
             ch.push_back(n2);
+        } else if (!F.empty()) {
+            roots(B[n2].left_or_first, K[n2][1], ch);
+            roots(B[n2].count_or_right, 4 - K[n2][1], ch);
         } else {
             ch = {B[n2].left_or_first, B[n2].count_or_right};
             while (ch.size() < 4) {
@@ -748,6 +896,13 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     if (const char* e = getenv("ORX_BVH_BINS")) bins = std::max(2, std::min(32, atoi(e)));
     if (const char* e = getenv("ORX_BVH_LEAF_MAX")) leaf_max = (uint32_t)std::max(1, std::min(8, atoi(e)));
     if (const char* e = getenv("ORX_BVH_LEAF_SAH")) leaf_sah = (float)atof(e);
+    /* treelet restructuring sweeps of the binary tree and the SAH-optimal four-wide collapse (the refinement
+     * OptiX's Trbvh does, Scene.cpp:353): hall photon-path node steps 17.71 -> 17.21 per ray, PPM frame +1.7 %,
+     * VCM +2.1 % (profiles/r06j_bvh_treelet_ab.txt); ORX_BVH_TREELET=0 / ORX_BVH_COLLAPSE=0: the round-5 tree */
+    int treelet_passes = 3;
+    bool sah_collapse = true;
+    if (const char* e = getenv("ORX_BVH_TREELET")) treelet_passes = std::max(0, std::min(8, atoi(e)));
+    if (const char* e = getenv("ORX_BVH_COLLAPSE")) sah_collapse = atoi(e) != 0;
 #ifdef ORX_BVH_FP32
     const bool device_bvh = false;
 #else
@@ -769,6 +924,7 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
         uint32_t depth = 0;
         bool ok = false;
         HIPCHK(r, device_build_bvh4(r->stream, dV.as<float>(), dI.as<uint32_t>(), nt, bins, leaf_max, leaf_sah,
+                                    treelet_passes, sah_collapse,
                                     r->d_bvh.as<DevBvh4>(), nt, r->d_bvhprims.as<uint32_t>(), &nodes4, &stack_bound,
                                     &depth, &ok));
         if (!ok) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "device BVH build failed (quantisation or capacity)");
@@ -784,10 +940,16 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
         for (uint32_t i = 0; i < nt; i++) bb.prims[i] = i;
         bb.nodes.reserve(2 * (size_t)nt / 2 + 1);
         bb.build(0, nt);
+        if (treelet_passes > 0) { /* the device builder's sweeps, on the host tree (TreeletOpt) */
+            TreeletOpt to(bb.nodes, leaf_sah > 0.f ? leaf_sah : 0.6f);
+            for (int p = 0; p < treelet_passes; p++) to.pass();
+            bb.max_depth = to.depth(0);
+        }
         if (bb.max_depth >= ORX_BVH_STACK)
             return set_err(r, ORX_ERR_INVALID_ARGUMENT, "BVH deeper than the traversal stack");
         b4.b2 = &bb.nodes;
         b4.out.reserve(bb.nodes.size() / 2 + 1);
+        if (sah_collapse) b4.dp(0);
         b4.build(0, stack_bound);
         if (!b4.ok) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "BVH4 quantisation failed");
         leaf_order = bb.prims;
