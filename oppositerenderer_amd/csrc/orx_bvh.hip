@@ -307,14 +307,16 @@ __global__ __launch_bounds__(256) void k_bvh_level(BvhBuildBufs B, const BvhTask
 }
 
 /* ---- treelet restructuring of the binary tree (the refinement of OptiX's Trbvh: Karras & Aila 2013) ----
- * Per inner node, bottom up, the treelet of the seven largest-area subtrees below it (largest-area expansion
- * from the node) is rebuilt as the SAH-optimal binary tree over them: a dynamic programme over the 127 subsets
+ * Per inner node, bottom up, the treelet of the NL (9; Karras & Aila use 7) largest-area subtrees below it
+ * (largest-area expansion from the node) is rebuilt as the SAH-optimal binary tree over them: a dynamic
+ * programme over the 2^NL - 1 subsets
  * (node cost ci x area, leaf cost area x triangles), the partition of each subset scanned once; the rebuilt
  * treelet reuses its six inner nodes, the treelet root keeps its index.  One thread per node of a level (the
  * nodes of a level have disjoint subtrees); the levels come from a top-down pass over the current tree before
  * each bottom-up sweep.  Boxes become the unions of the children's (already conservatively expanded) boxes.
- * Hall: photon-path node steps 17.71 -> 17.21 per ray, frame +1.7 % (PPM) / +2.1 % (VCM) measured with the same
- * passes on the host builder (profiles/r06j_bvh_treelet_ab.txt; priced in tools/bvh_quality.cpp). */
+ * Hall: photon-path node steps 17.71 -> 17.21 (7 leaves) -> 16.91 (9) per ray, hall PPM 1018 -> 1033 -> 1043
+ * Mpaths/s, VCM 561 -> 572 -> 576 (profiles/r06j_bvh_treelet_ab.txt; priced in tools/bvh_quality.cpp, where 11
+ * leaves gain nothing more); scene init 0.1 -> 0.2 s on the hall. */
 __device__ __forceinline__ float nd_area(const DevBvhNode& n) {
     return box_area(n.lo[0], n.lo[1], n.lo[2], n.hi[0], n.hi[1], n.hi[2]);
 }
@@ -334,6 +336,7 @@ __device__ void tl_refresh(const TreeletBufs& T, uint32_t n) {
     for (int k = 0; k < 3; k++) x.lo[k] = fminf(l.lo[k], r.lo[k]), x.hi[k] = fmaxf(l.hi[k], r.hi[k]);
     T.cost[n] = T.ci * nd_area(x) + T.cost[x.left_or_first] + T.cost[x.count_or_right];
 }
+template <uint32_t NL> /* treelet leaves */
 __global__ __launch_bounds__(64) void k_bvh_treelet(TreeletBufs T, const uint32_t* __restrict__ list, uint32_t n,
                                                     int restructure) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -341,12 +344,12 @@ __global__ __launch_bounds__(64) void k_bvh_treelet(TreeletBufs T, const uint32_
     const uint32_t nd = list[t];
     tl_refresh(T, nd);
     if (!restructure || nd_leaf(T.nodes[nd])) return;
-    uint32_t lv[7], inner[6];
+    uint32_t lv[NL], inner[NL - 1];
     uint32_t m = 2, ni = 1;
     lv[0] = T.nodes[nd].left_or_first;
     lv[1] = T.nodes[nd].count_or_right;
     inner[0] = nd;
-    while (m < 7) {
+    while (m < NL) {
         int bi = -1;
         float ba = -1.f;
         for (uint32_t i = 0; i < m; i++) {
@@ -361,8 +364,8 @@ __global__ __launch_bounds__(64) void k_bvh_treelet(TreeletBufs T, const uint32_
     }
     if (m < 3) return;
     const uint32_t full = (1u << m) - 1u;
-    float copt[128], ar[128];
-    uint8_t split[128];
+    float copt[1u << NL], ar[1u << NL];
+    uint16_t split[1u << NL];
     for (uint32_t S = 1; S <= full; S++) {
         float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (uint32_t i = 0; i < m; i++)
@@ -387,11 +390,11 @@ __global__ __launch_bounds__(64) void k_bvh_treelet(TreeletBufs T, const uint32_
             if (c < best) best = c, bp = P;
         }
         copt[S] = T.ci * ar[S] + best;
-        split[S] = (uint8_t)bp;
+        split[S] = (uint16_t)bp;
     }
     if (!(copt[full] < T.cost[nd] * (1.f - 1e-6f))) return;
     /* the optimal shape, top down (inner node k takes subset sub[k]), then boxes and costs bottom up */
-    uint32_t sub[6], id[6], cnt = 1, next = 1;
+    uint32_t sub[NL - 1], id[NL - 1], cnt = 1, next = 1;
     sub[0] = full;
     id[0] = nd;
     for (uint32_t k = 0; k < cnt; k++) {
@@ -610,7 +613,8 @@ __global__ void k_bvh_bound(const DevBvh4* __restrict__ out, const uint8_t* __re
  * Outputs: out4[cap4] BVH4 nodes, leaf_order[nt] (position k holds the
  * original id of the k-th triangle in leaf order). */
 hipError_t device_build_bvh4(hipStream_t s, const float* V, const uint32_t* I, uint32_t nt, int bins, uint32_t leaf_max,
-                             float leaf_sah, int treelet_passes, bool sah_collapse, DevBvh4* out4, uint32_t cap4,
+                             float leaf_sah, int treelet_passes, int treelet_leaves, bool sah_collapse, DevBvh4* out4,
+                             uint32_t cap4,
                              uint32_t* leaf_order, uint32_t* nodes4, uint32_t* stack_bound, uint32_t* max_depth,
                              bool* ok) {
     *ok = false;
@@ -682,7 +686,10 @@ hipError_t device_build_bvh4(hipStream_t s, const float* V, const uint32_t* I, u
             good = levels();
             for (size_t d = off.size() - 1; good && d-- > 0;) {
                 const uint32_t n = off[d + 1] - off[d];
-                hipLaunchKernelGGL(k_bvh_treelet, dim3((n + 63) / 64), dim3(64), 0, s, T, lvl + off[d], n, 1);
+                if (treelet_leaves == 9)
+                    hipLaunchKernelGGL(k_bvh_treelet<9>, dim3((n + 63) / 64), dim3(64), 0, s, T, lvl + off[d], n, 1);
+                else
+                    hipLaunchKernelGGL(k_bvh_treelet<7>, dim3((n + 63) / 64), dim3(64), 0, s, T, lvl + off[d], n, 1);
             }
         }
         if (good && sah_collapse) {

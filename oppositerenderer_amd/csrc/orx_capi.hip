@@ -191,6 +191,7 @@ struct BvhBuilder {
 struct TreeletOpt {
     std::vector<DevBvhNode>& B;
     float ci;
+    size_t nl = 7; /* treelet leaves */
     std::vector<double> cost;
     explicit TreeletOpt(std::vector<DevBvhNode>& b, float c) : B(b), ci(c), cost(b.size(), 0.0) {}
     static bool leaf(const DevBvhNode& n) { return (n.count_or_right & 0x80000000u) != 0; }
@@ -222,7 +223,7 @@ struct TreeletOpt {
     bool restructure(uint32_t n) {
         if (leaf(B[n])) return false;
         std::vector<uint32_t> lv = {B[n].left_or_first, B[n].count_or_right}, inner = {n};
-        while (lv.size() < 7) {
+        while (lv.size() < nl) {
             int bi = -1;
             float ba = -1.f;
             for (size_t i = 0; i < lv.size(); i++)
@@ -897,12 +898,14 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
     if (const char* e = getenv("ORX_BVH_LEAF_MAX")) leaf_max = (uint32_t)std::max(1, std::min(8, atoi(e)));
     if (const char* e = getenv("ORX_BVH_LEAF_SAH")) leaf_sah = (float)atof(e);
     /* treelet restructuring sweeps of the binary tree and the SAH-optimal four-wide collapse (the refinement
-     * OptiX's Trbvh does, Scene.cpp:353): hall photon-path node steps 17.71 -> 17.21 per ray, PPM frame +1.7 %,
-     * VCM +2.1 % (profiles/r06j_bvh_treelet_ab.txt); ORX_BVH_TREELET=0 / ORX_BVH_COLLAPSE=0: the round-5 tree */
+     * OptiX's Trbvh does, Scene.cpp:353): hall photon-path node steps 17.71 -> 16.91 per ray, PPM frame +2.5 %,
+     * VCM +2.6 % (profiles/r06j_bvh_treelet_ab.txt); ORX_BVH_TREELET=0 / ORX_BVH_COLLAPSE=0: the round-5 tree */
     int treelet_passes = 3;
     bool sah_collapse = true;
     if (const char* e = getenv("ORX_BVH_TREELET")) treelet_passes = std::max(0, std::min(8, atoi(e)));
     if (const char* e = getenv("ORX_BVH_COLLAPSE")) sah_collapse = atoi(e) != 0;
+    int treelet_leaves = 9; /* ORX_BVH_TREELET_LEAVES: 9 or 7 (9: hall PPM +0.9 %, VCM +0.6 % over 7; 11 priced: no further gain) */
+    if (const char* e = getenv("ORX_BVH_TREELET_LEAVES")) treelet_leaves = atoi(e) == 7 ? 7 : 9;
 #ifdef ORX_BVH_FP32
     const bool device_bvh = false;
 #else
@@ -924,7 +927,7 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
         uint32_t depth = 0;
         bool ok = false;
         HIPCHK(r, device_build_bvh4(r->stream, dV.as<float>(), dI.as<uint32_t>(), nt, bins, leaf_max, leaf_sah,
-                                    treelet_passes, sah_collapse,
+                                    treelet_passes, treelet_leaves, sah_collapse,
                                     r->d_bvh.as<DevBvh4>(), nt, r->d_bvhprims.as<uint32_t>(), &nodes4, &stack_bound,
                                     &depth, &ok));
         if (!ok) return set_err(r, ORX_ERR_INVALID_ARGUMENT, "device BVH build failed (quantisation or capacity)");
@@ -942,6 +945,7 @@ orx_status orx_init_scene(orx_renderer* r, const orx_scene* s) {
         bb.build(0, nt);
         if (treelet_passes > 0) { /* the device builder's sweeps, on the host tree (TreeletOpt) */
             TreeletOpt to(bb.nodes, leaf_sah > 0.f ? leaf_sah : 0.6f);
+            to.nl = (size_t)treelet_leaves;
             for (int p = 0; p < treelet_passes; p++) to.pass();
             bb.max_depth = to.depth(0);
         }

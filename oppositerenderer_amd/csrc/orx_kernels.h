@@ -192,7 +192,8 @@ void launch_vol_indirect(hipStream_t s, const PixelBufs& px, const float* volR, 
 /* on-device BVH build (orx_bvh.hip): V float3 [n_vertices], I uint3 [nt] on the
  * device; writes out4 (capacity cap4 nodes) and leaf_order [nt] */
 hipError_t device_build_bvh4(hipStream_t s, const float* V, const uint32_t* I, uint32_t nt, int bins, uint32_t leaf_max,
-                             float leaf_sah, int treelet_passes, bool sah_collapse, DevBvh4* out4, uint32_t cap4,
+                             float leaf_sah, int treelet_passes, int treelet_leaves, bool sah_collapse, DevBvh4* out4,
+                             uint32_t cap4,
                              uint32_t* leaf_order, uint32_t* nodes4, uint32_t* stack_bound, uint32_t* max_depth,
                              bool* ok);
 void launch_rng_init(hipStream_t s, RngPlanes rng, uint32_t RW, uint32_t rows, uint32_t rank, uint32_t world,

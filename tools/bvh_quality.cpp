@@ -72,6 +72,9 @@ int LEAF_MAX = 8;
 float LEAF_SAH = 0.6f; /* binary traversal step relative to one triangle test */
 int QBITS = 8;
 int NBINS = 32;
+int TL_LEAVES = 7;   /* treelet size */
+float TL_CI = -1.f;  /* treelet inner cost (< 0: LEAF_SAH) */
+static double CI() { return TL_CI < 0.f ? (double)LEAF_SAH : (double)TL_CI; }
 
 static Box tri_box(uint32_t t) {
     Box b;
@@ -159,14 +162,14 @@ static void annotate(int n, int parent) {
     annotate(x.r, n);
     N2& y = b2[n];
     y.nprim = b2[y.l].nprim + b2[y.r].nprim;
-    y.cost = (double)LEAF_SAH * y.b.area() + b2[y.l].cost + b2[y.r].cost;
+    y.cost = CI() * y.b.area() + b2[y.l].cost + b2[y.r].cost;
 }
 
 /* ---- treelet restructuring (Karras & Aila 2013) ---- */
 static bool restructure(int n) {
     if (b2[n].l < 0) return false;
     std::vector<int> leaves = {b2[n].l, b2[n].r}, inner = {n};
-    while (leaves.size() < 7) {
+    while ((int)leaves.size() < TL_LEAVES) {
         int bi = -1;
         float ba = -1;
         for (size_t i = 0; i < leaves.size(); i++)
@@ -201,7 +204,7 @@ static bool restructure(int n) {
             double c = copt[Pp] + copt[S ^ Pp];
             if (c < best) best = c, bp = Pp;
         }
-        copt[S] = (double)LEAF_SAH * area[S] + best;
+        copt[S] = CI() * area[S] + best;
         split[S] = bp;
     }
     if (!(copt[full] < b2[n].cost * (1 - 1e-6))) return false;
@@ -227,7 +230,7 @@ static bool restructure(int n) {
             x.b = b2[l].b;
             x.b.grow(b2[r].b);
             x.nprim = b2[l].nprim + b2[r].nprim;
-            x.cost = (double)LEAF_SAH * x.b.area() + b2[l].cost + b2[r].cost;
+            x.cost = CI() * x.b.area() + b2[l].cost + b2[r].cost;
             return id;
         }
     };
@@ -252,7 +255,7 @@ static int treelet_pass(int root) {
         x.b = b2[x.l].b;
         x.b.grow(b2[x.r].b);
         x.nprim = b2[x.l].nprim + b2[x.r].nprim;
-        x.cost = (double)LEAF_SAH * x.b.area() + b2[x.l].cost + b2[x.r].cost;
+        x.cost = CI() * x.b.area() + b2[x.l].cost + b2[x.r].cost;
         changed += restructure(n);
     }
     return changed;
@@ -569,20 +572,28 @@ int main(int argc, char** argv) {
         int collapse; /* 0 largest area, 1 SAH DP */
         float c_node;
         int bins = 32;
+        int tl_leaves = 7;
+        float tl_ci = -1.f;
     };
     std::vector<Var> vars = {
-        {"shipped (area collapse)", 1.0, 0, 0, 0},
-        {"sah collapse cn=1.5", 1.0, 0, 1, 1.5f},
+        {"shipped r5 (area collapse)", 1.0, 0, 0, 0},
+        {"r6: treelet x3, sah cn=2.5", 1.0, 3, 1, 2.5f},
+        {"treelet x6, sah", 1.0, 6, 1, 2.5f},
+        {"treelet9 x3, sah", 1.0, 3, 1, 2.5f, 32, 9},
+        {"treelet x3 ci=1.2, sah", 1.0, 3, 1, 2.5f, 32, 7, 1.2f},
+        {"treelet x3 ci=0.3, sah", 1.0, 3, 1, 2.5f, 32, 7, 0.3f},
+        {"treelet9 x6 ci=1.2, sah", 1.0, 6, 1, 2.5f, 32, 9, 1.2f},
+        {"treelet11 x3, sah", 1.0, 3, 1, 2.5f, 32, 11},
+    };
+    if (getenv("BVHQ_ALL")) vars.insert(vars.end(), {
         {"sah collapse cn=2.5", 1.0, 0, 1, 2.5f},
-        {"sah collapse cn=4", 1.0, 0, 1, 4.0f},
         {"treelet x3, area collapse", 1.0, 3, 0, 0},
-        {"treelet x3, sah cn=2.5", 1.0, 3, 1, 2.5f},
         {"presplit 1.10, area", 1.10, 0, 0, 0},
         {"presplit 1.25, area", 1.25, 0, 0, 0},
         {"presplit 1.25 + treelet + sah", 1.25, 3, 1, 2.5f},
         {"256 bins, area", 1.0, 0, 0, 0, 256},
         {"256 bins + treelet x3 + sah", 1.0, 3, 1, 2.5f, 256},
-    };
+    });
     double base_nodes = 0, base_anodes = 0, base_tris = 0;
     for (const Var& v : vars) {
         if (v.split_budget > 1.0) presplit(nt, v.split_budget);
@@ -592,6 +603,8 @@ int main(int argc, char** argv) {
         }
         b2.clear();
         NBINS = v.bins;
+        TL_LEAVES = v.tl_leaves;
+        TL_CI = v.tl_ci;
         build(0, (uint32_t)refs.size());
         annotate(0, -1);
         const double sah0 = b2[0].cost / b2[0].b.area();
