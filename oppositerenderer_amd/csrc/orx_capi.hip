@@ -517,7 +517,10 @@ struct orx_renderer {
      * iteration on one of two buffer sets (hitpoints, direct, grid-ordered photons, offsets,
      * grid parameters); ev_gdone[k] marks the end of the last gather+output on set k */
     hipStream_t gstream = nullptr;
-    hipEvent_t ev_grid_done = nullptr, ev_gdone[2] = {nullptr, nullptr};
+    hipEvent_t ev_grid_done = nullptr, ev_gdone[3] = {nullptr, nullptr, nullptr};
+    /* buffer sets the pipeline cycles through: 3 on one device (the eye pass of i + 1 then waits for the gather
+     * of i - 2, not of i - 1), 2 for the sharded pipeline; set_id: the physical set each view slot holds */
+    uint32_t nsets = 2, set_id[3] = {0, 1, 2};
     bool pipe_bufs = false, pend = false, last_pipelined = false;
     /* sharded PPM pipelining (orx_set_ppm_pipeline): gather + finish on the caller's side stream */
     bool shard_pipe = false;
@@ -560,6 +563,7 @@ struct orx_renderer {
     DevBuf d_hp2, d_dir2, d_sorted2, d_subofs2, d_offsets2, d_grid2; /* second buffer set (pipelining) */
     DevBuf d_kdtree2; /* kd-tree photon map: the second tree */
     DevBuf d_slots2, d_hcount2, d_hwin2; /* stochastic hash: second deposit records and table */
+    DevBuf d_hp3, d_dir3, d_sorted3, d_subofs3, d_offsets3, d_grid3, d_kdtree3, d_slots3, d_hcount3, d_hwin3; /* third */
     /* kd-tree photon map (photon_map = 2, orx_kdtree.hip) */
     DevBuf d_kdtree, d_kdids, d_kdlst, d_kdnkey, d_kdkeys, d_kdnodepos, d_kdseg, d_kdbox, d_kdninfo, d_kdP, d_kdppart,
         d_kdtable, d_kdtpart, d_kdvpart, d_kdcount;
@@ -710,6 +714,7 @@ orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out)
         hipEventCreateWithFlags(&r->ev_grid_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_gdone[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_gdone[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&r->ev_gdone[2], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_photon_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_direct_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_eye_done, hipEventDisableTiming) != hipSuccess ||
@@ -732,7 +737,7 @@ void orx_destroy(orx_renderer* r) {
     if (r->gstream) hipStreamSynchronize(r->gstream);
     for (int p = 0; p < P_COUNT; p++)
         for (hipEvent_t e : r->ev[p]) hipEventDestroy(e);
-    for (hipEvent_t e : {r->ev_grid_done, r->ev_gdone[0], r->ev_gdone[1]})
+    for (hipEvent_t e : {r->ev_grid_done, r->ev_gdone[0], r->ev_gdone[1], r->ev_gdone[2]})
         if (e) hipEventDestroy(e);
     if (r->gstream) hipStreamDestroy(r->gstream);
     if (r->ev_photon_done) hipEventDestroy(r->ev_photon_done);
@@ -1409,31 +1414,68 @@ static orx_status sync_all(orx_renderer* r) {
  * the uniform grid's sorted photons and offsets, or the hash's deposit records and table, or
  * the kd-tree.  Allocated on the first pipelined iteration after a resize, so PT/VCM-only
  * renderers and the serial schedule never hold it. */
-static orx_status ensure_second_set(orx_renderer* r) {
-    if (r->pipe_bufs) return ORX_OK;
+/* one extra set: the views of set `n` (2 or 3) */
+struct SetBufs {
+    DevBuf *hp, *dir, *grid, *sorted, *subofs, *offsets, *hcount, *hwin, *slots, *kdtree;
+};
+static SetBufs set_bufs(orx_renderer* r, int n) {
+    if (n == 2)
+        return SetBufs{&r->d_hp2, &r->d_dir2, &r->d_grid2, &r->d_sorted2, &r->d_subofs2, &r->d_offsets2,
+                       &r->d_hcount2, &r->d_hwin2, &r->d_slots2, &r->d_kdtree2};
+    return SetBufs{&r->d_hp3, &r->d_dir3, &r->d_grid3, &r->d_sorted3, &r->d_subofs3, &r->d_offsets3,
+                   &r->d_hcount3, &r->d_hwin3, &r->d_slots3, &r->d_kdtree3};
+}
+static orx_status ensure_set(orx_renderer* r, const SetBufs& b) {
     const size_t nhp = (size_t)r->max_rows * r->W;
-    HIPCHK(r, r->d_hp2.ensure(nhp * 40));
-    HIPCHK(r, hipMemsetAsync(r->d_hp2.p, 0, nhp * 40, r->stream));
-    HIPCHK(r, r->d_dir2.ensure(nhp * 12));
-    HIPCHK(r, r->d_grid2.ensure(sizeof(GridParams)));
-    HIPCHK(r, hipMemsetAsync(r->d_grid2.p, 0, sizeof(GridParams), r->stream));
+    HIPCHK(r, b.hp->ensure(nhp * 40));
+    HIPCHK(r, hipMemsetAsync(b.hp->p, 0, nhp * 40, r->stream));
+    HIPCHK(r, b.dir->ensure(nhp * 12));
+    HIPCHK(r, b.grid->ensure(sizeof(GridParams)));
+    HIPCHK(r, hipMemsetAsync(b.grid->p, 0, sizeof(GridParams), r->stream));
     const size_t G2 = (size_t)r->cfg.photon_grid_max_size + 2;
     if (r->cfg.photon_map == 0) {
         const size_t bytes = (size_t)SP_PLANES * r->pb.splane * 4;
-        HIPCHK(r, r->d_sorted2.ensure(bytes));
-        HIPCHK(r, hipMemsetAsync(r->d_sorted2.p, 0, bytes, r->stream)); /* tail reads stay finite */
-        HIPCHK(r, r->d_subofs2.ensure(r->d_subofs.bytes));
-        HIPCHK(r, r->d_offsets2.ensure(G2 * 4));
-        HIPCHK(r, hipMemsetAsync(r->d_offsets2.p, 0, G2 * 4, r->stream));
+        HIPCHK(r, b.sorted->ensure(bytes));
+        HIPCHK(r, hipMemsetAsync(b.sorted->p, 0, bytes, r->stream)); /* tail reads stay finite */
+        HIPCHK(r, b.subofs->ensure(r->d_subofs.bytes));
+        HIPCHK(r, b.offsets->ensure(G2 * 4));
+        HIPCHK(r, hipMemsetAsync(b.offsets->p, 0, G2 * 4, r->stream));
     } else if (r->cfg.photon_map == 1) {
-        HIPCHK(r, r->d_hcount2.ensure((size_t)r->pb.hnum * 4));
-        HIPCHK(r, r->d_hwin2.ensure((size_t)r->pb.hnum * 4));
-        HIPCHK(r, r->d_slots2.ensure((size_t)r->pb.S * 64));
+        HIPCHK(r, b.hcount->ensure((size_t)r->pb.hnum * 4));
+        HIPCHK(r, b.hwin->ensure((size_t)r->pb.hnum * 4));
+        HIPCHK(r, b.slots->ensure((size_t)r->pb.S * 64));
     } else {
         const size_t bytes = (size_t)r->kd.tree_size * 48 + 48;
-        HIPCHK(r, r->d_kdtree2.ensure(bytes));
-        HIPCHK(r, hipMemsetAsync(r->d_kdtree2.p, 0, bytes, r->stream));
+        HIPCHK(r, b.kdtree->ensure(bytes));
+        HIPCHK(r, hipMemsetAsync(b.kdtree->p, 0, bytes, r->stream));
     }
+    return ORX_OK;
+}
+/* The further buffer sets of PPM pipelining: only what the photon map of the renderer
+ * alternates between iterations (the buffers the deferred gather of iteration i reads while the
+ * next iterations write their own): hit points, direct light, grid parameters, and the uniform
+ * grid's sorted photons and offsets, or the hash's deposit records and table, or the kd-tree.
+ * Allocated on the first pipelined iteration after a resize, so PT/VCM-only renderers and the
+ * serial schedule never hold them.  One device takes three sets (ORX_PIPE_SETS=2: two): with two,
+ * the eye pass of iteration i + 1 waited for the gather and output of i - 1, which on the hall ran
+ * until the grid build of i had ended, and the photon pass of i + 1 then waited ~1 ms per frame for
+ * that eye pass (kernel trace gpurun_out/r06n_tl); the sharded pipeline keeps two (its finish may
+ * be held back one iteration, orx_ppm_finish_on). */
+static orx_status ensure_second_set(orx_renderer* r) {
+    if (r->pipe_bufs) return ORX_OK;
+    static const uint32_t sets_env = [] {
+        const char* e = getenv("ORX_PIPE_SETS");
+        return e && atoi(e) == 2 ? 2u : 3u;
+    }();
+    r->nsets = r->shard_pipe ? 2u : sets_env;
+    for (uint32_t n = 2; n <= r->nsets; n++) {
+        const orx_status s0 = ensure_set(r, set_bufs(r, (int)n));
+        if (s0 != ORX_OK) return s0;
+    }
+    r->set_id[0] = 0;
+    r->set_id[1] = 1;
+    r->set_id[2] = 2;
+    r->pp = 0;
     /* the zero-fills above ran on the own stream; on a caller stream (the sharded pipeline) the
      * eye pass and grid build of this iteration write these buffers right after swap_sets */
     if (r->use_ext) HIPCHK(r, hipStreamSynchronize(r->stream));
@@ -1445,26 +1487,35 @@ static inline void swap_buf(DevBuf& a, DevBuf& b) {
     std::swap(a.p, b.p);
     std::swap(a.bytes, b.bytes);
 }
-/* switch to the other buffer set and point the kernels' views at it */
+/* the current view slot takes the next buffer set: with two sets the other one, with three the least recently
+ * used ((cur, prev, prev2) -> (prev2, cur, prev)); then point the kernels' views at it */
+static void cycle(orx_renderer* r, DevBuf& a, DevBuf& b, DevBuf& c) {
+    if (r->nsets == 3) {
+        swap_buf(a, c); /* (c, b, a) */
+        swap_buf(b, c); /* (c, a, b) */
+    } else {
+        swap_buf(a, b);
+    }
+}
 static void swap_sets(orx_renderer* r) {
-    swap_buf(r->d_hp, r->d_hp2);
-    swap_buf(r->d_dir, r->d_dir2);
-    swap_buf(r->d_grid, r->d_grid2);
+    cycle(r, r->d_hp, r->d_hp2, r->d_hp3);
+    cycle(r, r->d_dir, r->d_dir2, r->d_dir3);
+    cycle(r, r->d_grid, r->d_grid2, r->d_grid3);
     if (r->cfg.photon_map == 0) {
-        swap_buf(r->d_sorted, r->d_sorted2);
-        swap_buf(r->d_subofs, r->d_subofs2);
-        swap_buf(r->d_offsets, r->d_offsets2);
+        cycle(r, r->d_sorted, r->d_sorted2, r->d_sorted3);
+        cycle(r, r->d_subofs, r->d_subofs2, r->d_subofs3);
+        cycle(r, r->d_offsets, r->d_offsets2, r->d_offsets3);
     }
     if (r->cfg.photon_map == 1) { /* the hash gather reads the deposit records and the table */
-        swap_buf(r->d_slots, r->d_slots2);
-        swap_buf(r->d_hcount, r->d_hcount2);
-        swap_buf(r->d_hwin, r->d_hwin2);
+        cycle(r, r->d_slots, r->d_slots2, r->d_slots3);
+        cycle(r, r->d_hcount, r->d_hcount2, r->d_hcount3);
+        cycle(r, r->d_hwin, r->d_hwin2, r->d_hwin3);
         r->pb.slots = r->d_slots.as<float4>();
         r->pb.hcount = r->d_hcount.as<uint32_t>();
         r->pb.hwin = r->d_hwin.as<uint32_t>();
     }
     if (r->cfg.photon_map == 2) {
-        swap_buf(r->d_kdtree, r->d_kdtree2);
+        cycle(r, r->d_kdtree, r->d_kdtree2, r->d_kdtree3);
         r->kd.tree = r->d_kdtree.as<float4>();
         r->kd.tree_bc = r->kd.tree + r->kd.tree_size + 1;
     }
@@ -1477,7 +1528,15 @@ static void swap_sets(orx_renderer* r) {
     if (r->pb.subofs) r->pb.subofs = r->d_subofs.as<uint32_t>();
     r->pb.offsets = r->d_offsets.as<uint32_t>();
     r->pb.grid = r->d_grid.as<GridParams>();
-    r->pp ^= 1u;
+    if (r->nsets == 3) {
+        const uint32_t t = r->set_id[2];
+        r->set_id[2] = r->set_id[1];
+        r->set_id[1] = r->set_id[0];
+        r->set_id[0] = t;
+    } else {
+        std::swap(r->set_id[0], r->set_id[1]);
+    }
+    r->pp = r->set_id[0];
 }
 
 static Consts make_consts(orx_renderer* r, float ppm_radius, uint64_t local_iteration_number) {
@@ -2775,9 +2834,10 @@ orx_status orx_get_stats(orx_renderer* r, orx_stats* out) {
         out->photons_visited_total = g.photons_visited_total;
         out->cells_visited_total = g.cells_visited_total;
         out->valid_photons_total = g.valid_total;
-        if (r->pipe_bufs && r->d_grid2.p) { /* the other buffer set's share of the totals */
+        for (const DevBuf* b : {&r->d_grid2, &r->d_grid3}) { /* the other buffer sets' share of the totals */
+            if (!r->pipe_bufs || !b->p || (b == &r->d_grid3 && r->nsets < 3)) continue;
             GridParams g2;
-            HIPCHK(r, hipMemcpy(&g2, r->d_grid2.p, sizeof g2, hipMemcpyDeviceToHost));
+            HIPCHK(r, hipMemcpy(&g2, b->p, sizeof g2, hipMemcpyDeviceToHost));
             out->photons_visited_total += g2.photons_visited_total;
             out->cells_visited_total += g2.cells_visited_total;
             out->valid_photons_total += g2.valid_total;
@@ -2826,8 +2886,8 @@ orx_status orx_reset_timing(orx_renderer* r) {
     }
     for (int p = 0; p < P_COUNT; p++) r->ev_n[p] = 0;
     r->timed_iterations = 0;
-    for (DevBuf* b : {&r->d_grid, &r->d_grid2}) {
-        if (!b->p || (b == &r->d_grid2 && !r->pipe_bufs)) continue;
+    for (DevBuf* b : {&r->d_grid, &r->d_grid2, &r->d_grid3}) {
+        if (!b->p || (b != &r->d_grid && !r->pipe_bufs) || (b == &r->d_grid3 && r->nsets < 3)) continue;
         GridParams g;
         HIPCHK(r, hipMemcpy(&g, b->p, sizeof g, hipMemcpyDeviceToHost));
         g.photons_visited_total = 0;
