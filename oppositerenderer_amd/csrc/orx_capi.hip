@@ -506,6 +506,15 @@ struct orx_renderer {
     hipStream_t aux = nullptr;   /* PPM direct pass, overlapped with the grid build and gather */
     hipEvent_t ev_photon_done = nullptr, ev_direct_done = nullptr;
     bool overlap_direct = false;
+    /* one device, three buffer sets, uniform grid: the grid build of iteration i on a stream of its own (gridq)
+     * beside the photon pass of i + 1, the photon pass's outputs (deposit records, positions, validity bits,
+     * AABB replicas) alternating between two sets (d_slotsB ...; po: the set the last photon pass wrote);
+     * ev_gsrc[set]: the last grid build that read that set */
+    bool async_grid = false;
+    uint32_t po = 0;
+    hipStream_t gridq = nullptr;
+    hipEvent_t ev_gsrc[2] = {nullptr, nullptr};
+    DevBuf d_slotsB, d_vmaskB, d_bboxB, d_pos4B;
     /* pipelined PPM: the eye pass of iteration i+1 runs on aux right behind the direct pass of i
      * (the RNG chain), beside the grid build of i; ev_eye_done orders the photon pass after it.
      * eye_chain: aux is already ordered after every earlier renderer-stream write the eye pass
@@ -688,6 +697,17 @@ static int gather_stream_priority() {
     return high ? greatest : least;
 }
 
+/* the asynchronous grid build's stream: the gather's priority, or the least (ORX_GRIDQ_PRIO=0) */
+static int grid_stream_priority() {
+    static const bool low = [] {
+        const char* e = getenv("ORX_GRIDQ_PRIO");
+        return e && atoi(e) == 0;
+    }();
+    int least = 0, greatest = 0;
+    if (low && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess) return least;
+    return gather_stream_priority();
+}
+
 orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out) {
     if (!out) return ORX_ERR_INVALID_ARGUMENT;
     *out = nullptr;
@@ -711,6 +731,9 @@ orx_status orx_create(int hip_device, const orx_config* cfg, orx_renderer** out)
         hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&r->aux, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithPriority(&r->gstream, hipStreamNonBlocking, gather_stream_priority()) != hipSuccess ||
+        hipStreamCreateWithPriority(&r->gridq, hipStreamNonBlocking, grid_stream_priority()) != hipSuccess ||
+        hipEventCreateWithFlags(&r->ev_gsrc[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&r->ev_gsrc[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_grid_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_gdone[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&r->ev_gdone[1], hipEventDisableTiming) != hipSuccess ||
@@ -739,7 +762,11 @@ void orx_destroy(orx_renderer* r) {
         for (hipEvent_t e : r->ev[p]) hipEventDestroy(e);
     for (hipEvent_t e : {r->ev_grid_done, r->ev_gdone[0], r->ev_gdone[1], r->ev_gdone[2]})
         if (e) hipEventDestroy(e);
+    if (r->gridq) hipStreamSynchronize(r->gridq);
     if (r->gstream) hipStreamDestroy(r->gstream);
+    if (r->gridq) hipStreamDestroy(r->gridq);
+    for (hipEvent_t e : {r->ev_gsrc[0], r->ev_gsrc[1]})
+        if (e) hipEventDestroy(e);
     if (r->ev_photon_done) hipEventDestroy(r->ev_photon_done);
     if (r->ev_direct_done) hipEventDestroy(r->ev_direct_done);
     if (r->ev_eye_done) hipEventDestroy(r->ev_eye_done);
@@ -1404,6 +1431,7 @@ static orx_status sync_all(orx_renderer* r) {
     HIPCHK(r, hipStreamSynchronize(r->aux));
     if (r->use_ext) HIPCHK(r, hipStreamSynchronize(r->ext_stream));
     if (r->gstream) HIPCHK(r, hipStreamSynchronize(r->gstream));
+    if (r->gridq) HIPCHK(r, hipStreamSynchronize(r->gridq));
     if (r->shard_pipe) HIPCHK(r, hipStreamSynchronize(r->side));
     return ORX_OK;
 }
@@ -1471,6 +1499,24 @@ static orx_status ensure_second_set(orx_renderer* r) {
     for (uint32_t n = 2; n <= r->nsets; n++) {
         const orx_status s0 = ensure_set(r, set_bufs(r, (int)n));
         if (s0 != ORX_OK) return s0;
+    }
+    /* The asynchronous grid build (ORX_GRID_ASYNC=1) pays where the chain eye -> photon -> grid -> next
+     * photon sets the frame (hall: 1059 -> 1071 Mpaths/s); where the gather does it only reorders a
+     * throughput-bound frame and costs 1-2 % (Cornell 2056 -> 2012, conference 4K 585 -> 578;
+     * profiles/r06p_grid_async_ab.txt), so it is off by default. */
+    static const bool async_env = [] {
+        const char* e = getenv("ORX_GRID_ASYNC");
+        return e && atoi(e) != 0;
+    }();
+    r->async_grid = async_env && r->nsets == 3 && r->cfg.photon_map == 0 && !r->media;
+    if (r->async_grid) { /* the photon pass's second output set (the first is resize's) */
+        HIPCHK(r, r->d_slotsB.ensure(r->d_slots.bytes));
+        HIPCHK(r, r->d_vmaskB.ensure(r->d_vmask.bytes));
+        HIPCHK(r, hipMemsetAsync(r->d_vmaskB.p, 0, r->d_vmaskB.bytes, r->stream));
+        HIPCHK(r, r->d_pos4B.ensure(r->d_pos4.bytes));
+        HIPCHK(r, r->d_bboxB.ensure(r->d_bbox.bytes));
+        HIPCHK(r, hipMemsetAsync(r->d_bboxB.p, 0xff, 3 * BBOX_REPLICAS * 4, r->stream));
+        HIPCHK(r, hipMemsetAsync(r->d_bboxB.as<uint32_t>() + 3 * BBOX_REPLICAS, 0, 3 * BBOX_REPLICAS * 4, r->stream));
     }
     r->set_id[0] = 0;
     r->set_id[1] = 1;
@@ -1701,7 +1747,7 @@ static HashParams hash_params(const orx_renderer* r, float ppm_radius) {
     hp.mask = r->pb.hnum - 1u;
     return hp;
 }
-static void ppm_grid_build(orx_renderer* r, const PhotonBufs& pb, const GridBox& gb = GridBox{});
+static void ppm_grid_build(orx_renderer* r, const PhotonBufs& pb, const GridBox& gb = GridBox{}, hipStream_t on = nullptr);
 /* photon pass (+ the overlapped direct pass), then the photon map (build_map: false in slab
  * mode, whose grid is built over the imported photons by orx_ppm_slab_import) */
 static orx_status ppm_photons_grid(orx_renderer* r, const Consts& c, bool build_map = true) {
@@ -1745,19 +1791,32 @@ static orx_status ppm_photons_grid(orx_renderer* r, const Consts& c, bool build_
     return ORX_OK;
 }
 /* grid build: the atomic-free bucket sort (an atomic-rank counting sort measured slower:
- * one device-scope atomic per photon into a 4 MB histogram) */
-static void ppm_grid_build(orx_renderer* r, const PhotonBufs& pb, const GridBox& gb) {
-    hipStream_t st = cur_stream(r);
-    ev_begin(r, P_SETUP_HASH);
+ * one device-scope atomic per photon into a 4 MB histogram); on `on`, or the
+ * renderer's stream */
+static void ppm_grid_build(orx_renderer* r, const PhotonBufs& pb, const GridBox& gb, hipStream_t on) {
+    hipStream_t st = on ? on : cur_stream(r);
+    ev_begin_on(r, P_SETUP_HASH, st);
     launch_grid_setup(st, pb, gb);
     launch_grid_bucket_count(st, pb);
-    ev_end(r, P_SETUP_HASH);
-    ev_begin(r, P_SCAN);
+    ev_end_on(r, P_SETUP_HASH, st);
+    ev_begin_on(r, P_SCAN, st);
     launch_grid_bucket_scan(st, pb);
-    ev_end(r, P_SCAN);
-    ev_begin(r, P_SCATTER);
+    ev_end_on(r, P_SCAN, st);
+    ev_begin_on(r, P_SCATTER, st);
     launch_grid_bucket_place(st, pb);
-    ev_end(r, P_SCATTER);
+    ev_end_on(r, P_SCATTER, st);
+}
+/* async grid build: the photon pass writes the other output set */
+static void swap_photon_out(orx_renderer* r) {
+    swap_buf(r->d_slots, r->d_slotsB);
+    swap_buf(r->d_vmask, r->d_vmaskB);
+    swap_buf(r->d_pos4, r->d_pos4B);
+    swap_buf(r->d_bbox, r->d_bboxB);
+    r->pb.slots = r->d_slots.as<float4>();
+    r->pb.vmask = r->d_vmask.as<uint8_t>();
+    r->pb.pos4 = r->d_pos4.as<float4>();
+    r->pb.bbox = r->d_bbox.as<uint32_t>();
+    r->po ^= 1u;
 }
 static orx_status ppm_local_passes(orx_renderer* r, const DevCamera& cam, const Consts& c) {
     ppm_eye(r, cam, c);
@@ -2020,6 +2079,10 @@ static orx_status ppm_pipelined_iteration(orx_renderer* r, const orx_request* de
     hipStream_t st = r->stream;
     swap_sets(r);
     const uint32_t k = r->pp;
+    if (r->async_grid) { /* the other photon-output set: its last reader, the grid build two iterations back */
+        swap_photon_out(r);
+        HIPCHK(r, hipStreamWaitEvent(st, r->ev_gsrc[r->po], 0));
+    }
     /* the set's previous gather + output (two iterations back) and, through the RNG chain
      * (slot (x,y) is advanced by eye, photon and direct in turn), the last direct pass */
     HIPCHK(r, hipStreamWaitEvent(st, r->ev_gdone[k], 0));
@@ -2039,10 +2102,19 @@ static orx_status ppm_pipelined_iteration(orx_renderer* r, const orx_request* de
     HIPCHK(r, hipEventRecord(r->ev_eye_done, r->aux));
     HIPCHK(r, hipStreamWaitEvent(st, r->ev_eye_done, 0));
     r->overlap_direct = true;
-    const orx_status sp = ppm_photons_grid(r, c); /* photon, direct (aux), grid */
+    const orx_status sp = ppm_photons_grid(r, c, !r->async_grid); /* photon, direct (aux), grid */
     r->overlap_direct = false;
     if (sp != ORX_OK) return sp;
-    HIPCHK(r, hipEventRecord(r->ev_grid_done, st));
+    if (r->async_grid) {
+        /* the grid build on its own stream: the photon pass of i + 1 waits only for the RNG chain (eye of i + 1
+         * after the direct pass of i) and for this build's end of reading the output set two iterations on */
+        HIPCHK(r, hipStreamWaitEvent(r->gridq, r->ev_photon_done, 0));
+        ppm_grid_build(r, r->pb, GridBox{}, r->gridq);
+        HIPCHK(r, hipEventRecord(r->ev_gsrc[r->po], r->gridq));
+        HIPCHK(r, hipEventRecord(r->ev_grid_done, r->gridq));
+    } else {
+        HIPCHK(r, hipEventRecord(r->ev_grid_done, st));
+    }
     hipStream_t g = r->gstream;
     HIPCHK(r, hipStreamWaitEvent(g, r->ev_grid_done, 0));
     ev_begin_on(r, P_GATHER, g);

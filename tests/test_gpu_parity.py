@@ -460,13 +460,15 @@ def test_kdtree_parity(scene_name, W, H, P):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pipeline,photon_map,large", [("1", 0, False), ("0", 0, False), ("1", 1, False),
-                                                       ("1", 2, False), ("1", 1, True), ("1", 0, True)])
-def test_ppm_back_to_back_iterations(pipeline, photon_map, large, monkeypatch):
+@pytest.mark.parametrize("pipeline,photon_map,large,gasync", [
+    ("1", 0, False, "0"), ("0", 0, False, "0"), ("1", 1, False, "0"), ("1", 2, False, "0"), ("1", 1, True, "0"),
+    ("1", 0, True, "0"), ("1", 0, False, "1"), ("1", 0, True, "1")])
+def test_ppm_back_to_back_iterations(pipeline, photon_map, large, gasync, monkeypatch):
     """Iterations issued back to back with no read in between: with pipelining on (default) the
-    gather + output of iteration i run beside the eye/photon/grid passes of i+1 on the other
+    gather + output of iteration i run beside the eye/photon/grid passes of i+1 on another
     buffer set; the running sum after five iterations (and a resolution change in between)
-    matches the oracle as the serial schedule does."""
+    matches the oracle as the serial schedule does.  gasync = "1": the grid build of i runs on a
+    stream of its own beside the photon pass of i+1 (ORX_GRID_ASYNC=1, photon outputs alternate)."""
     import subprocess, sys, os, json
     code = r'''
 import json, sys, numpy as np
@@ -496,7 +498,7 @@ for W, H, n in sizes:
     errs.append(float(np.sqrt(((g - o) ** 2).sum() / (o ** 2).sum())))
 print(json.dumps({"errs": errs, "pipelined": gpu.pipelined()}))
 '''
-    env = dict(os.environ, ORX_PIPELINE=pipeline)
+    env = dict(os.environ, ORX_PIPELINE=pipeline, ORX_GRID_ASYNC=gasync)
     out = subprocess.run([sys.executable, "-c", code, str(photon_map), "1" if large else "0"], env=env,
                          capture_output=True, text=True, timeout=110,
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

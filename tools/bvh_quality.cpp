@@ -574,6 +574,8 @@ int main(int argc, char** argv) {
         int bins = 32;
         int tl_leaves = 7;
         float tl_ci = -1.f;
+        float leaf_sah = 0.6f;
+        int leaf_max = 8;
     };
     std::vector<Var> vars = {
         {"shipped r5 (area collapse)", 1.0, 0, 0, 0},
@@ -583,7 +585,10 @@ int main(int argc, char** argv) {
         {"treelet x3 ci=1.2, sah", 1.0, 3, 1, 2.5f, 32, 7, 1.2f},
         {"treelet x3 ci=0.3, sah", 1.0, 3, 1, 2.5f, 32, 7, 0.3f},
         {"treelet9 x6 ci=1.2, sah", 1.0, 6, 1, 2.5f, 32, 9, 1.2f},
-        {"treelet11 x3, sah", 1.0, 3, 1, 2.5f, 32, 11},
+        {"t9 sah leafsah 0.4", 1.0, 3, 1, 2.5f, 32, 9, -1.f, 0.4f},
+        {"t9 sah leafsah 0.9", 1.0, 3, 1, 2.5f, 32, 9, -1.f, 0.9f},
+        {"t9 sah leafsah 1.3", 1.0, 3, 1, 2.5f, 32, 9, -1.f, 1.3f},
+        {"t9 sah leafmax 4", 1.0, 3, 1, 2.5f, 32, 9, -1.f, 0.6f, 4},
     };
     if (getenv("BVHQ_ALL")) vars.insert(vars.end(), {
         {"sah collapse cn=2.5", 1.0, 0, 1, 2.5f},
@@ -605,6 +610,8 @@ int main(int argc, char** argv) {
         NBINS = v.bins;
         TL_LEAVES = v.tl_leaves;
         TL_CI = v.tl_ci;
+        LEAF_SAH = v.leaf_sah;
+        LEAF_MAX = v.leaf_max;
         build(0, (uint32_t)refs.size());
         annotate(0, -1);
         const double sah0 = b2[0].cost / b2[0].b.area();
