@@ -546,8 +546,8 @@ def test_vcm_camera_shadow_modes(defer):
     deferred to k_vcm_shadow with the colours summed by k_vcm_accum in the reference's order (the
     default, ORX_VCM_DEFER=16 entries per pixel; ~6.5 rays per pixel on the hall), traced in place
     inside the camera kernel (ORX_VCM_DEFER=0), and
-    deferred into a list too small for them (1 per pixel: the pass overflows, restores the RNG planes
-    and reruns in place).  Camera colours, RNG and vertex counts bit-exact against the oracle, three
+    deferred into a list too small for them (1 per pixel: the walk overflows, walks on without entries,
+    and the resolve's last kernel reruns the colours from the saved RNG start words).  Camera colours, RNG and vertex counts bit-exact against the oracle, three
     iterations back to back (the overlapped schedule cycles both entry lists and light images and
     reruns each overflow after the previous iteration's colours), and the overflow flag as expected."""
     import subprocess, sys, os, json
