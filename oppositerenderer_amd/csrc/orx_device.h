@@ -515,14 +515,20 @@ struct StackL {
     __device__ __forceinline__ uint32_t pop(int& sp) const { return s[(--sp) * 64]; }
     /* write entry k without moving the stack pointer (k may run two past the bound) */
     __device__ __forceinline__ void put(int k, uint32_t v) const { s[k * 64] = v; }
+    /* the whole stack is in LDS: every wave is shallow */
+    __device__ __forceinline__ bool shallow(int, int) const { return true; }
+    __device__ __forceinline__ void put_l(int k, uint32_t v) const { put(k, v); }
+    __device__ __forceinline__ uint32_t pop_l(int& sp) const { return pop(sp); }
 };
 /* A short LDS stack continued in global memory: entries k < NL in the lane's LDS column, deeper
  * ones in the block's own global array [depth][64] at column `lane` (g_ = the block's base, so the
  * 32-bit buffer offsets stay below depth * 256 B whatever the launch size), through buffer
  * loads/stores (kept apart from the LDS accesses, which the compiler would otherwise merge with
  * them into flat loads).  The LDS column holds NL + 1 entries: a push always writes LDS, at min(k, NL) (entry
- * NL is a dump slot), and only a push or pop past NL takes the branch to global memory, so a wave
- * whose lanes all stay shallow runs one skipped branch per operation.  For kernels whose occupancy
+ * NL is a dump slot), and only a push or pop past NL takes the branch to global memory.  The traversal
+ * loops test once per node step whether any lane of the wave could pass NL (shallow(): one ballot) and
+ * otherwise push and pop through put_l / pop_l, LDS only, without the clamp and the per-entry branch
+ * (hall photon pass 3.555 -> 3.494 ms serial, frame +1.1 %, profiles/r06za_stack_fast_path_ab.txt).  For kernels whose occupancy
  * the full-depth LDS stack limits (k_vcm_shadow: 61 VGPRs, 4 waves per SIMD with 35 LDS entries,
  * 8 with 16; k_ppm_photon). */
 template <int NL>
@@ -549,6 +555,11 @@ struct StackH {
         s[(k < NL ? k : NL) * 64] = v;
         if (k >= NL) __builtin_amdgcn_raw_buffer_store_b32(v, g, (int)(((uint32_t)(k - NL) * gstride + lane) * 4u), 0, 0);
     }
+    /* wave-uniform: no lane's next `n` entries (from sp) reach past the LDS column, so put_l / pop_l
+     * (LDS only, no clamp and no per-entry branch to global memory) serve this step */
+    __device__ __forceinline__ bool shallow(int sp, int n) const { return !__ballot(sp + n > NL); }
+    __device__ __forceinline__ void put_l(int k, uint32_t v) const { s[k * 64] = v; }
+    __device__ __forceinline__ uint32_t pop_l(int& sp) const { return s[(--sp) * 64]; }
 };
 struct NodesG {
     __device__ __forceinline__ void test(const DevScene& S, uint32_t idx, const RayBox& rb, float tmin, float tmax,
@@ -655,11 +666,19 @@ __device__ inline bool trace_closest_t(const DevScene& S, f3 o, f3 d, float tmin
                      * their final positions (misses sort last), then the pointer moves by the
                      * hits (photon pass 4.03 -> 3.98 ms against one branch per push) */
                     const int n3 = ct[3] != INFINITY, n2 = ct[2] != INFINITY, n1 = ct[1] != INFINITY;
-                    stk.put(sp, cc[3]);
-                    stk.put(sp + n3, cc[2]);
-                    stk.put(sp + n3 + n2, cc[1]);
-                    sp += n3 + n2 + n1;
-                    ref = ct[0] != INFINITY ? cc[0] : (sp ? stk.pop(sp) : ORX_DONE);
+                    if (stk.shallow(sp, 3)) { /* the common case: the three entries in LDS */
+                        stk.put_l(sp, cc[3]);
+                        stk.put_l(sp + n3, cc[2]);
+                        stk.put_l(sp + n3 + n2, cc[1]);
+                        sp += n3 + n2 + n1;
+                        ref = ct[0] != INFINITY ? cc[0] : (sp ? stk.pop_l(sp) : ORX_DONE);
+                    } else {
+                        stk.put(sp, cc[3]);
+                        stk.put(sp + n3, cc[2]);
+                        stk.put(sp + n3 + n2, cc[1]);
+                        sp += n3 + n2 + n1;
+                        ref = ct[0] != INFINITY ? cc[0] : (sp ? stk.pop(sp) : ORX_DONE);
+                    }
                 }
                 if ((ref & ORX_LEAF) && !(lf & ORX_LEAF)) {
                     lf = ref;
@@ -739,17 +758,30 @@ __device__ inline bool trace_any_t(const DevScene& S, f3 o, f3 d, float tmin, fl
                  * matter for any hit), the last one is taken back from registers */
                 const int h0 = ct[0] != INFINITY, h1 = ct[1] != INFINITY, h2 = ct[2] != INFINITY,
                           h3 = ct[3] != INFINITY;
-                stk.put(sp, cc[0]);
-                sp += h0;
-                stk.put(sp, cc[1]);
-                sp += h1;
-                stk.put(sp, cc[2]);
-                sp += h2;
-                stk.put(sp, cc[3]);
-                sp += h3;
                 const uint32_t next = h3 ? cc[3] : h2 ? cc[2] : h1 ? cc[1] : h0 ? cc[0] : ORX_DONE;
-                sp -= next != ORX_DONE;
-                ref = next != ORX_DONE ? next : (sp ? stk.pop(sp) : ORX_DONE);
+                if (stk.shallow(sp, 4)) { /* the common case: the four entries in LDS */
+                    stk.put_l(sp, cc[0]);
+                    sp += h0;
+                    stk.put_l(sp, cc[1]);
+                    sp += h1;
+                    stk.put_l(sp, cc[2]);
+                    sp += h2;
+                    stk.put_l(sp, cc[3]);
+                    sp += h3;
+                    sp -= next != ORX_DONE;
+                    ref = next != ORX_DONE ? next : (sp ? stk.pop_l(sp) : ORX_DONE);
+                } else {
+                    stk.put(sp, cc[0]);
+                    sp += h0;
+                    stk.put(sp, cc[1]);
+                    sp += h1;
+                    stk.put(sp, cc[2]);
+                    sp += h2;
+                    stk.put(sp, cc[3]);
+                    sp += h3;
+                    sp -= next != ORX_DONE;
+                    ref = next != ORX_DONE ? next : (sp ? stk.pop(sp) : ORX_DONE);
+                }
                 if ((ref & ORX_LEAF) && !(lf & ORX_LEAF)) {
                     lf = ref;
                     ref = sp ? stk.pop(sp) : ORX_DONE;
@@ -831,17 +863,30 @@ __device__ __forceinline__ void trace_any_chain_t(const DevScene& S, RAYS& R, co
             uint32_t cc[4];
             node_test(S.bvh4, ref, rb, tmin, tmax, ct, cc);
             const int h0 = ct[0] != INFINITY, h1 = ct[1] != INFINITY, h2 = ct[2] != INFINITY, h3 = ct[3] != INFINITY;
-            stk.put(sp, cc[0]);
-            sp += h0;
-            stk.put(sp, cc[1]);
-            sp += h1;
-            stk.put(sp, cc[2]);
-            sp += h2;
-            stk.put(sp, cc[3]);
-            sp += h3;
             const uint32_t next = h3 ? cc[3] : h2 ? cc[2] : h1 ? cc[1] : h0 ? cc[0] : ORX_DONE;
-            sp -= next != ORX_DONE;
-            ref = next != ORX_DONE ? next : (sp ? stk.pop(sp) : ORX_DONE);
+            if (stk.shallow(sp, 4)) { /* the common case: the four entries in LDS */
+                stk.put_l(sp, cc[0]);
+                sp += h0;
+                stk.put_l(sp, cc[1]);
+                sp += h1;
+                stk.put_l(sp, cc[2]);
+                sp += h2;
+                stk.put_l(sp, cc[3]);
+                sp += h3;
+                sp -= next != ORX_DONE;
+                ref = next != ORX_DONE ? next : (sp ? stk.pop_l(sp) : ORX_DONE);
+            } else {
+                stk.put(sp, cc[0]);
+                sp += h0;
+                stk.put(sp, cc[1]);
+                sp += h1;
+                stk.put(sp, cc[2]);
+                sp += h2;
+                stk.put(sp, cc[3]);
+                sp += h3;
+                sp -= next != ORX_DONE;
+                ref = next != ORX_DONE ? next : (sp ? stk.pop(sp) : ORX_DONE);
+            }
             if ((ref & ORX_LEAF) && !(lf & ORX_LEAF)) {
                 lf = ref;
                 ref = sp ? stk.pop(sp) : ORX_DONE;
