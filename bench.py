@@ -386,6 +386,9 @@ def main():
     # passes, so every pass time is wall time under interference; a few serial iterations after
     # the timed region give each pass's stand-alone time
     pipelined = r.pipelined()
+    # the pipelined PPM grid build's schedule, chosen by the renderer from its first pipelined iteration
+    # (orx.h orx_ppm_grid_schedule); read before the serial legs below
+    gsched, gprobe = r.grid_schedule() if method == _abi.PROGRESSIVE_PHOTON_MAPPING else (0, (0.0, 0.0))
     # pipelined (single device): gather + output of iteration i beside iteration i+1's passes, the
     # direct pass beside the grid build, and the eye pass of i+1 on the direct pass's stream beside
     # the grid build of i, so the chain per frame is photon pass + grid build
@@ -456,6 +459,10 @@ def main():
         "dominant_pass": dominant,
         "overlapped_passes": overlapped,
     }
+    if pipelined and method == _abi.PROGRESSIVE_PHOTON_MAPPING:
+        out["config"]["grid_build"] = {-1: "not chosen", 0: "synchronous", 1: "asynchronous"}.get(gsched, "n/a")
+        out["config"]["grid_build_measured_ms"] = {"photon_and_grid": round(gprobe[0], 4),
+                                                   "gather": round(gprobe[1], 4)}
     if not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(scene, method, W, H, P, args.cpu_seconds, photon_map=pmap)

@@ -293,6 +293,14 @@ orx_status orx_reset_timing(orx_renderer* r);
  * grid passes; VCM, its deferred shadow rays and colours (ORX_PASS_VCM_SHADOW) beside the next
  * iteration's light pass and camera subpaths; so those pass_ms are overlapped wall time; 0 otherwise */
 int orx_ppm_pipelined(const orx_renderer* r);
+/* The single-device pipelined PPM schedule's grid build (uniform grid): 0 on the renderer's stream before
+ * the next photon pass, 1 on a stream of its own beside it, -1 not chosen yet.  By default (ORX_GRID_ASYNC
+ * unset) the renderer chooses after the first pipelined iterations following a resize: the first is timed
+ * (its photon pass + grid build, and its gather, which the next photon pass then waits for), and the
+ * asynchronous build is taken when photon + grid exceed 1.15x the gather; ORX_GRID_ASYNC=0 / 1 fixes it.
+ * probe_ms (optional, 2 floats): the measured photon + grid and gather times (ms; 0 when not measured).
+ * No reference counterpart (OptiX schedules its own launches); images are identical either way. */
+int orx_ppm_grid_schedule(const orx_renderer* r, float* probe_ms);
 /* Single-device PPM iteration pipelining and VCM shadow-ray overlap: 1 on, 0 off (serial passes), -1
  * the ORX_PIPELINE environment default (on).  Takes effect at the next iteration (an outstanding pipelined
  * iteration is finished first); images are identical either way. */

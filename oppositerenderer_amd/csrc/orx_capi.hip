@@ -515,6 +515,15 @@ struct orx_renderer {
     hipStream_t gridq = nullptr;
     hipEvent_t ev_gsrc[2] = {nullptr, nullptr};
     DevBuf d_slotsB, d_vmaskB, d_bboxB, d_pos4B;
+    bool out_b = false; /* set B allocated: the asynchronous build may run */
+    /* the schedule chosen from the workload (ORX_GRID_ASYNC unset): the first pipelined iteration after a
+     * resize times its photon pass + grid build on the renderer's stream and its gather, the next one's
+     * photon pass waits for that gather (so nothing overlaps it), and the iteration after that picks the
+     * asynchronous build if photon + grid take more than GRID_CHAIN_RATIO x the gather (the chain, not the
+     * gather, then sets the frame).  probe_stage: 0 decided, 1 measure, 2 isolate, 3 decide */
+    uint32_t probe_stage = 0, probe_k = 0;
+    float probe_ms[2] = {0.f, 0.f}; /* photon + grid, gather of the measured iteration */
+    hipEvent_t ev_pm[4] = {};
     /* pipelined PPM: the eye pass of iteration i+1 runs on aux right behind the direct pass of i
      * (the RNG chain), beside the grid build of i; ev_eye_done orders the photon pass after it.
      * eye_chain: aux is already ordered after every earlier renderer-stream write the eye pass
@@ -766,6 +775,8 @@ void orx_destroy(orx_renderer* r) {
     if (r->gstream) hipStreamDestroy(r->gstream);
     if (r->gridq) hipStreamDestroy(r->gridq);
     for (hipEvent_t e : {r->ev_gsrc[0], r->ev_gsrc[1]})
+        if (e) hipEventDestroy(e);
+    for (hipEvent_t e : r->ev_pm)
         if (e) hipEventDestroy(e);
     if (r->ev_photon_done) hipEventDestroy(r->ev_photon_done);
     if (r->ev_direct_done) hipEventDestroy(r->ev_direct_done);
@@ -1504,12 +1515,16 @@ static orx_status ensure_second_set(orx_renderer* r) {
      * photon sets the frame (hall: 1059 -> 1071 Mpaths/s); where the gather does it only reorders a
      * throughput-bound frame and costs 1-2 % (Cornell 2056 -> 2012, conference 4K 585 -> 578;
      * profiles/r06p_grid_async_ab.txt), so it is off by default. */
-    static const bool async_env = [] {
+    static const int async_env = [] {
         const char* e = getenv("ORX_GRID_ASYNC");
-        return e && atoi(e) != 0;
+        return e ? atoi(e) : -1;
     }();
-    r->async_grid = async_env && r->nsets == 3 && r->cfg.photon_map == 0 && !r->media;
-    if (r->async_grid) { /* the photon pass's second output set (the first is resize's) */
+    const bool eligible = r->nsets == 3 && r->cfg.photon_map == 0 && !r->media;
+    r->async_grid = eligible && async_env > 0;
+    r->probe_stage = eligible && async_env < 0 ? 1u : 0u;
+    r->probe_ms[0] = r->probe_ms[1] = 0.f;
+    r->out_b = eligible && async_env != 0;
+    if (r->out_b) { /* the photon pass's second output set (the first is resize's) */
         HIPCHK(r, r->d_slotsB.ensure(r->d_slots.bytes));
         HIPCHK(r, r->d_vmaskB.ensure(r->d_vmask.bytes));
         HIPCHK(r, hipMemsetAsync(r->d_vmaskB.p, 0, r->d_vmaskB.bytes, r->stream));
@@ -1517,6 +1532,11 @@ static orx_status ensure_second_set(orx_renderer* r) {
         HIPCHK(r, r->d_bboxB.ensure(r->d_bbox.bytes));
         HIPCHK(r, hipMemsetAsync(r->d_bboxB.p, 0xff, 3 * BBOX_REPLICAS * 4, r->stream));
         HIPCHK(r, hipMemsetAsync(r->d_bboxB.as<uint32_t>() + 3 * BBOX_REPLICAS, 0, 3 * BBOX_REPLICAS * 4, r->stream));
+        /* both sets' last-reader events exist from here on, so a wait on either is valid */
+        HIPCHK(r, hipEventRecord(r->ev_gsrc[0], r->stream));
+        HIPCHK(r, hipEventRecord(r->ev_gsrc[1], r->stream));
+        for (hipEvent_t& e : r->ev_pm)
+            if (!e) HIPCHK(r, hipEventCreate(&e));
     }
     r->set_id[0] = 0;
     r->set_id[1] = 1;
@@ -2069,6 +2089,13 @@ static orx_status vcm_iteration(orx_renderer* r, const orx_request* det, float p
     return vcm_camera(r, overlap);
 }
 
+/* the asynchronous grid build when the measured photon pass + grid build exceed this multiple of the gather.
+ * Measured on the first pipelined iteration (its radius is the largest, so its gather the dearest): hall
+ * 5.59 / 3.44 ms = 1.62 (the asynchronous build gains 1.2-1.8 % there), Cornell 0.79 / 0.98 = 0.81 and
+ * conference 4K 19.2 / 51.0 = 0.38 (it loses 1-2 %); the threshold sits at their geometric middle
+ * (profiles/r06p_grid_async_ab.txt, r06zh_grid_schedule_choice.txt) */
+constexpr float GRID_CHAIN_RATIO = 1.15f;
+
 /* One PPM iteration whose gather and output are left running on gstream, overlapping the next
  * iteration's eye, photon and grid passes (orx_render_next_iteration, single device).  Every
  * kernel and its inputs are those of the serial schedule; only the buffer set alternates. */
@@ -2079,10 +2106,22 @@ static orx_status ppm_pipelined_iteration(orx_renderer* r, const orx_request* de
     hipStream_t st = r->stream;
     swap_sets(r);
     const uint32_t k = r->pp;
-    if (r->async_grid) { /* the other photon-output set: its last reader, the grid build two iterations back */
-        swap_photon_out(r);
-        HIPCHK(r, hipStreamWaitEvent(st, r->ev_gsrc[r->po], 0));
+    const bool measure = r->probe_stage == 1;
+    if (r->probe_stage == 2) { /* after the measured iteration: this photon pass waits for its gather */
+        HIPCHK(r, hipStreamWaitEvent(st, r->ev_gdone[r->probe_k], 0));
+        r->probe_stage = 3;
+    } else if (r->probe_stage == 3) { /* the device still holds the previous iteration: no bubble */
+        HIPCHK(r, hipEventSynchronize(r->ev_pm[3]));
+        HIPCHK(r, hipEventElapsedTime(&r->probe_ms[0], r->ev_pm[0], r->ev_pm[1]));
+        HIPCHK(r, hipEventElapsedTime(&r->probe_ms[1], r->ev_pm[2], r->ev_pm[3]));
+        r->async_grid = r->probe_ms[0] > GRID_CHAIN_RATIO * r->probe_ms[1];
+        r->probe_stage = 0;
     }
+    /* asynchronous build: the photon pass writes the other output set, whose last reader is the grid build
+     * two iterations back; synchronous after asynchronous iterations: the current set, last read by the
+     * previous iteration's build on gridq (else an event long complete) */
+    if (r->async_grid) swap_photon_out(r);
+    if (r->out_b) HIPCHK(r, hipStreamWaitEvent(st, r->ev_gsrc[r->po], 0));
     /* the set's previous gather + output (two iterations back) and, through the RNG chain
      * (slot (x,y) is advanced by eye, photon and direct in turn), the last direct pass */
     HIPCHK(r, hipStreamWaitEvent(st, r->ev_gdone[k], 0));
@@ -2102,7 +2141,9 @@ static orx_status ppm_pipelined_iteration(orx_renderer* r, const orx_request* de
     HIPCHK(r, hipEventRecord(r->ev_eye_done, r->aux));
     HIPCHK(r, hipStreamWaitEvent(st, r->ev_eye_done, 0));
     r->overlap_direct = true;
+    if (measure) HIPCHK(r, hipEventRecord(r->ev_pm[0], st));
     const orx_status sp = ppm_photons_grid(r, c, !r->async_grid); /* photon, direct (aux), grid */
+    if (measure) HIPCHK(r, hipEventRecord(r->ev_pm[1], st));
     r->overlap_direct = false;
     if (sp != ORX_OK) return sp;
     if (r->async_grid) {
@@ -2118,9 +2159,15 @@ static orx_status ppm_pipelined_iteration(orx_renderer* r, const orx_request* de
     hipStream_t g = r->gstream;
     HIPCHK(r, hipStreamWaitEvent(g, r->ev_grid_done, 0));
     ev_begin_on(r, P_GATHER, g);
+    if (measure) HIPCHK(r, hipEventRecord(r->ev_pm[2], g));
     if (r->cfg.photon_map == 2) launch_ppm_gather_kd(g, local_gather_in(r), r->pb, r->kd, c);
     else if (r->pb.hash) launch_ppm_gather_hash(g, local_gather_in(r), r->pb, hash_params(r, c.ppm_radius), c);
     else launch_ppm_gather(g, local_gather_in(r), r->pb, c);
+    if (measure) {
+        HIPCHK(r, hipEventRecord(r->ev_pm[3], g));
+        r->probe_stage = 2;
+        r->probe_k = k;
+    }
     ev_end_on(r, P_GATHER, g);
     HIPCHK(r, hipStreamWaitEvent(g, r->ev_direct_done, 0));
     ev_begin_on(r, P_DIRECT, g);
@@ -2943,6 +2990,14 @@ orx_status orx_get_stats(orx_renderer* r, orx_stats* out) {
 }
 
 int orx_ppm_pipelined(const orx_renderer* r) { return r && (r->last_pipelined || r->last_vcm_overlap) ? 1 : 0; }
+int orx_ppm_grid_schedule(const orx_renderer* r, float* probe_ms) {
+    if (!r) return -2;
+    if (probe_ms) {
+        probe_ms[0] = r->probe_ms[0];
+        probe_ms[1] = r->probe_ms[1];
+    }
+    return r->probe_stage ? -1 : r->async_grid ? 1 : 0;
+}
 orx_status orx_set_iteration_pipelining(orx_renderer* r, int mode) {
     if (!r || mode < -1 || mode > 1) return ORX_ERR_INVALID_ARGUMENT;
     r->pipe_mode = mode;

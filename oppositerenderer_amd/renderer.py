@@ -58,6 +58,8 @@ def load_library(path: str = LIB_PATH):
     lib.orx_reset_timing.restype = C.c_int
     lib.orx_ppm_pipelined.argtypes = [C.c_void_p]
     lib.orx_ppm_pipelined.restype = C.c_int
+    lib.orx_ppm_grid_schedule.argtypes = [C.c_void_p, C.POINTER(C.c_float)]
+    lib.orx_ppm_grid_schedule.restype = C.c_int
     lib.orx_set_iteration_pipelining.argtypes = [C.c_void_p, C.c_int]
     lib.orx_set_iteration_pipelining.restype = C.c_int
     lib.orx_stream.argtypes = [C.c_void_p]
@@ -70,7 +72,7 @@ EXPORTED_SYMBOLS = (
     "orx_default_config", "orx_create", "orx_init_scene", "orx_render_next_iteration", "orx_get_output",
     "orx_get_output_device", "orx_width", "orx_height", "orx_output_bytes", "orx_emitted_photons_per_iteration",
     "orx_last_error", "orx_destroy", "orx_read_buffer", "orx_get_stats", "orx_reset_timing", "orx_ppm_pipelined",
-    "orx_set_iteration_pipelining",
+    "orx_set_iteration_pipelining", "orx_ppm_grid_schedule",
     "orx_set_shard", "orx_set_ppm_pipeline",
     "orx_stream",
 )
@@ -200,6 +202,13 @@ class OptixRenderer:
         """Whether the last iteration overlapped part of its work with the next one's passes (PPM: the
         gather + output; VCM: the deferred shadow rays + colours)."""
         return bool(self._lib.orx_ppm_pipelined(self._h))
+
+    def grid_schedule(self):
+        """The pipelined PPM grid build's schedule (orx_ppm_grid_schedule): (0 synchronous / 1 asynchronous /
+        -1 not chosen yet, (photon + grid ms, gather ms) as measured, or zeros)."""
+        ms = (C.c_float * 2)()
+        mode = self._lib.orx_ppm_grid_schedule(self._h, ms)
+        return mode, (float(ms[0]), float(ms[1]))
 
     def set_iteration_pipelining(self, mode: int):
         """Single-device PPM pipelining and VCM shadow-ray overlap: 1 on, 0 serial passes, -1 the

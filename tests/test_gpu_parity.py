@@ -462,13 +462,15 @@ def test_kdtree_parity(scene_name, W, H, P):
 @pytest.mark.gpu
 @pytest.mark.parametrize("pipeline,photon_map,large,gasync", [
     ("1", 0, False, "0"), ("0", 0, False, "0"), ("1", 1, False, "0"), ("1", 2, False, "0"), ("1", 1, True, "0"),
-    ("1", 0, True, "0"), ("1", 0, False, "1"), ("1", 0, True, "1")])
+    ("1", 0, True, "0"), ("1", 0, False, "1"), ("1", 0, True, "1"), ("1", 0, False, "auto")])
 def test_ppm_back_to_back_iterations(pipeline, photon_map, large, gasync, monkeypatch):
     """Iterations issued back to back with no read in between: with pipelining on (default) the
     gather + output of iteration i run beside the eye/photon/grid passes of i+1 on another
     buffer set; the running sum after five iterations (and a resolution change in between)
     matches the oracle as the serial schedule does.  gasync = "1": the grid build of i runs on a
-    stream of its own beside the photon pass of i+1 (ORX_GRID_ASYNC=1, photon outputs alternate)."""
+    stream of its own beside the photon pass of i+1 (ORX_GRID_ASYNC=1, photon outputs alternate);
+    "auto" (the default, ORX_GRID_ASYNC unset): the renderer times its first pipelined iteration and
+    chooses, choosing again after the resize -- the images still match the oracle."""
     import subprocess, sys, os, json
     code = r'''
 import json, sys, numpy as np
@@ -480,6 +482,7 @@ scene = scenes.cornell()
 pm, large = int(sys.argv[1]), sys.argv[2] == "1"
 P = 256 if large else (64 if pm == 1 else 96)  # the hash table needs a power-of-two deposit count
 sizes = ((1920, 24, 4), (1280, 16, 2)) if large else ((64, 48, 5), (40, 40, 3))  # 1080p-class rows
+sched = []
 cfg = _abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P, photon_map=pm)
 gpu = OptixRenderer(cfg); gpu.initialize(0); gpu.initScene(scene)
 ora = oracle_lib.OracleRenderer(_abi.default_config(seed=1645301512, photon_launch_width=P, photon_launch_height=P,
@@ -494,11 +497,14 @@ for W, H, n in sizes:
         gpu.renderNextIteration(it, it, r, True, det)
         ora.render_next_iteration(it, it, r, det.to_abi())
         r = next_ppm_radius(r, it)
+    sched.append(gpu.grid_schedule()[0])
     g, o = gpu.getOutputBuffer().astype(np.float64), ora.output().astype(np.float64)
     errs.append(float(np.sqrt(((g - o) ** 2).sum() / (o ** 2).sum())))
-print(json.dumps({"errs": errs, "pipelined": gpu.pipelined()}))
+print(json.dumps({"errs": errs, "pipelined": gpu.pipelined(), "sched": sched}))
 '''
     env = dict(os.environ, ORX_PIPELINE=pipeline, ORX_GRID_ASYNC=gasync)
+    if gasync == "auto":
+        env.pop("ORX_GRID_ASYNC")
     out = subprocess.run([sys.executable, "-c", code, str(photon_map), "1" if large else "0"], env=env,
                          capture_output=True, text=True, timeout=110,
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -506,6 +512,10 @@ print(json.dumps({"errs": errs, "pipelined": gpu.pipelined()}))
     res = json.loads(out.stdout.strip().splitlines()[-1])
     assert all(e < 1e-5 for e in res["errs"]), res
     assert res["pipelined"] == (pipeline == "1"), res  # no silent fallback to the serial schedule
+    if gasync == "auto":  # chosen within each size's iterations (the first pipelined one is timed)
+        assert all(m in (0, 1) for m in res["sched"]), res
+    elif pipeline == "1" and photon_map == 0:
+        assert res["sched"] == [int(gasync)] * 2, res
 
 
 _VCM_CHILD = r'''
