@@ -1401,11 +1401,19 @@ void launch_vcm_camera_resolve(hipStream_t s, const DevScene& S, const VcmBufs& 
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
         return (uint32_t)n;
     }();
-    /* as many one-wave blocks as are resident at once: the register cap, or the short LDS stacks (160 KB
-     * per CU); vb.shstk holds the deeper entries of that many lanes */
+    /* persistent one-wave blocks: half as many as can be resident at once (the register cap, or the short
+     * LDS stacks, 160 KB per CU), so the next iteration's light pass and camera walk beside them keep room:
+     * the stand-alone resolve is as fast, the overlapped frame +0.3 % (hall 581.5 -> 583.3 Mpaths/s over four
+     * alternating runs; a quarter is 9 % slower; profiles/r06zm_vcm_shadow_frac_ab.txt, ORX_VCM_SHADOW_FRAC);
+     * vb.shstk holds the deeper entries of that many lanes */
     const size_t lds = (size_t)(VCM_SHADOW_LDS_STACK + 2) * 64 * 4;
     const uint32_t per_cu = std::min<uint32_t>(4u * ORX_VCM_SHADOW_WAVES, (uint32_t)((160u << 10) / lds));
-    const uint32_t sblocks = std::min(cus * std::max(1u, per_cu), vb.shstk_lanes / 64u);
+    static const float frac = [] { /* the fraction of the resident capacity */
+        const char* e = getenv("ORX_VCM_SHADOW_FRAC");
+        const float f = e ? (float)atof(e) : 0.5f;
+        return f > 0.f && f <= 1.f ? f : 1.f;
+    }();
+    const uint32_t sblocks = std::max(1u, (uint32_t)((float)std::min(cus * std::max(1u, per_cu), vb.shstk_lanes / 64u) * frac));
     if (vb.lcq) hipLaunchKernelGGL(k_vcm_light_shadow, dim3(sblocks), dim3(64), lds, s, S, vb);
     hipLaunchKernelGGL(k_vcm_shadow, dim3(sblocks), dim3(64), lds, s, S, vb); /* also zeroes work[2] */
     /* a pixel's list holds at most (1 + VCM_MAX_VERTS) connections per camera vertex */
