@@ -1382,7 +1382,10 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
         in3 = in3 && q3 <= DIRQ_BAND;
         const bool u0 = in0 && q0 >= -DIRQ_BAND, u1 = in1 && q1 >= -DIRQ_BAND;
         const bool u2 = in2 && q2 >= -DIRQ_BAND, u3 = in3 && q3 >= -DIRQ_BAND;
-        if (wave_any(u0 | u1 | u2 | u3)) { /* inside the band: the exact test (rare) */
+        /* The two tests below are lane-divergent ifs, not wave_any: the exec-mask save and skip is
+         * scalar, where a ballot of these combined masks compiled to a select and a compare (two
+         * VALU each, of ~56 per batch).  A lane that skips the sums adds fma(w, 0, acc) = acc. */
+        if (u0 | u1 | u2 | u3) { /* inside the band: the exact test (rare) */
             const uint32_t ku = (uint32_t)__builtin_amdgcn_readfirstlane((int)kb);
             const f4u DX = sload4(k.SDX, ku), DY = sload4(k.SDY, ku), DZ = sload4(k.SDZ, ku);
             const v2f nd0 = (pk_mul_bhi(lo2(DX), k.pzn) + pk_mul_blo(lo2(DY), k.nyz)) + pk_mul_bhi(lo2(DZ), k.nyz);
@@ -1392,19 +1395,20 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
             in2 = in2 && (!u2 || nd1.x <= 0.f);
             in3 = in3 && (!u3 || nd1.y <= 0.f);
         }
-        if (!wave_any(in0 | in1 | in2 | in3)) continue;
-        const float4 WX = L4[64 + (e >> 2)], WY = L4[80 + (e >> 2)], WZ = L4[96 + (e >> 2)];
-        v2f w0 = weight2u(pk_mul_blo(d20, k.irr)), w1 = weight2u(pk_mul_blo(d21, k.irr));
-        w0.x = in0 ? w0.x : 0.f;
-        w0.y = in1 ? w0.y : 0.f;
-        w1.x = in2 ? w1.x : 0.f;
-        w1.y = in3 ? w1.y : 0.f;
-        a.accx = __builtin_elementwise_fma(lo2(WX), w0, a.accx);
-        a.accy = __builtin_elementwise_fma(lo2(WY), w0, a.accy);
-        a.accz = __builtin_elementwise_fma(lo2(WZ), w0, a.accz);
-        a.accx = __builtin_elementwise_fma(hi2(WX), w1, a.accx);
-        a.accy = __builtin_elementwise_fma(hi2(WY), w1, a.accy);
-        a.accz = __builtin_elementwise_fma(hi2(WZ), w1, a.accz);
+        if (in0 | in1 | in2 | in3) {
+            const float4 WX = L4[64 + (e >> 2)], WY = L4[80 + (e >> 2)], WZ = L4[96 + (e >> 2)];
+            v2f w0 = weight2u(pk_mul_blo(d20, k.irr)), w1 = weight2u(pk_mul_blo(d21, k.irr));
+            w0.x = in0 ? w0.x : 0.f;
+            w0.y = in1 ? w0.y : 0.f;
+            w1.x = in2 ? w1.x : 0.f;
+            w1.y = in3 ? w1.y : 0.f;
+            a.accx = __builtin_elementwise_fma(lo2(WX), w0, a.accx);
+            a.accy = __builtin_elementwise_fma(lo2(WY), w0, a.accy);
+            a.accz = __builtin_elementwise_fma(lo2(WZ), w0, a.accz);
+            a.accx = __builtin_elementwise_fma(hi2(WX), w1, a.accx);
+            a.accy = __builtin_elementwise_fma(hi2(WY), w1, a.accy);
+            a.accz = __builtin_elementwise_fma(hi2(WZ), w1, a.accz);
+        }
     }
 }
 
