@@ -1025,6 +1025,19 @@ __device__ __forceinline__ v2f weight2u(v2f u) {
     p = __builtin_elementwise_fma(p, u, v2f{ORX_W5_C1, ORX_W5_C1});
     return __builtin_elementwise_fma(p, u, v2f{ORX_W5_C0, ORX_W5_C0});
 }
+/* The union gather's form: the same polynomial in d^2, coefficients c_k / r^(2k) (one radius per
+ * launch: uniform, in SGPRs), so the u = d^2 / r^2 multiply per pair leaves the batch.  The host
+ * takes it only where every scaled coefficient is a finite float (launch_ppm_gather). */
+struct WPoly {
+    float c[6];
+};
+__device__ __forceinline__ v2f weight2d(v2f d2, const WPoly& w) {
+    v2f p = __builtin_elementwise_fma(v2f{w.c[5], w.c[5]}, d2, v2f{w.c[4], w.c[4]});
+    p = __builtin_elementwise_fma(p, d2, v2f{w.c[3], w.c[3]});
+    p = __builtin_elementwise_fma(p, d2, v2f{w.c[2], w.c[2]});
+    p = __builtin_elementwise_fma(p, d2, v2f{w.c[1], w.c[1]});
+    return __builtin_elementwise_fma(p, d2, v2f{w.c[0], w.c[0]});
+}
 /* int8 facing prefilter dot products of four photons' direction words with the hit point's nq.
  * gfx950 runs v_dot* like its matrix-core instructions: another VALU instruction may read a dot's
  * result only three wait states after it.  The compiler pads the instructions it emits but not
@@ -1352,9 +1365,9 @@ struct UConst {
  * is farther than r from the lane's hit point (the margin argument of the chord
  * trimming), so the distance test alone decides, as the per-lane kernel's chord +
  * distance tests do. */
-template <bool RANGE>
+template <bool RANGE, bool DF>
 __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uint32_t c, uint32_t ce, uint32_t lo,
-                                                uint32_t len, float r2, const UConst& k, UAcc& a) {
+                                                uint32_t len, float r2, const UConst& k, const WPoly& wp, UAcc& a) {
     const float4* L4 = reinterpret_cast<const float4*>(L);
     for (uint32_t e = 0; e < ce; e += 4) {
         const uint32_t kb = c + e;
@@ -1397,7 +1410,14 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
         }
         if (in0 | in1 | in2 | in3) {
             const float4 WX = L4[64 + (e >> 2)], WY = L4[80 + (e >> 2)], WZ = L4[96 + (e >> 2)];
-            v2f w0 = weight2u(pk_mul_blo(d20, k.irr)), w1 = weight2u(pk_mul_blo(d21, k.irr));
+            v2f w0, w1;
+            if (DF) {
+                w0 = weight2d(d20, wp);
+                w1 = weight2d(d21, wp);
+            } else {
+                w0 = weight2u(pk_mul_blo(d20, k.irr));
+                w1 = weight2u(pk_mul_blo(d21, k.irr));
+            }
             w0.x = in0 ? w0.x : 0.f;
             w0.y = in1 ? w0.y : 0.f;
             w1.x = in2 ? w1.x : 0.f;
@@ -1427,9 +1447,9 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
 #ifndef ORX_UNION_WAVES
 #define ORX_UNION_WAVES 7 /* waves per SIMD the union gather is register-capped for (at 8 it spills 37-49 VGPRs) */
 #endif
-template <uint32_t NSUB>
+template <uint32_t NSUB, bool DF>
 __global__ __launch_bounds__(256, ORX_UNION_WAVES) void k_ppm_gather_union(GatherIn gi, PhotonBufs pb, Consts c, uint32_t ntx,
-                                                          uint32_t ntiles) {
+                                                          uint32_t ntiles, WPoly wp) {
     __shared__ float ulds[4][7 * 64];
     const uint32_t tid = threadIdx.x, w = tid >> 6, l = tid & 63;
     uint32_t tile;
@@ -1573,8 +1593,8 @@ __global__ __launch_bounds__(256, ORX_UNION_WAVES) void k_ppm_gather_union(Gathe
                     L[320 + l] = cur.WY;
                     L[384 + l] = cur.WZ;
                     __builtin_amdgcn_wave_barrier();
-                    if (range) union_chunk_lds<true>(L, cc, ce, lo, len, r2, UK, UA);
-                    else union_chunk_lds<false>(L, cc, ce, lo, len, r2, UK, UA);
+                    if (range) union_chunk_lds<true, DF>(L, cc, ce, lo, len, r2, UK, wp, UA);
+                    else union_chunk_lds<false, DF>(L, cc, ce, lo, len, r2, UK, wp, UA);
                     __builtin_amdgcn_wave_barrier();
                     cc = cn;
                 }
@@ -1727,8 +1747,30 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
         else hipLaunchKernelGGL((k_ppm_gather<SUBR * SUBR>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
         return;
     }
-    if (pb.nsub == 1) hipLaunchKernelGGL((k_ppm_gather_union<1>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
-    else hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
+    /* the weight polynomial in d^2 (weight2d) where its scaled coefficients are finite floats */
+    static const int dform_env = [] {
+        const char* e = getenv("ORX_GATHER_DFORM");
+        return e ? atoi(e) : 1;
+    }();
+    WPoly wp{};
+    bool df = dform_env != 0;
+    {
+        const double irr = (double)(1.0f / c.ppm_radius2);
+        const double ck[6] = {ORX_W5_C0, ORX_W5_C1, ORX_W5_C2, ORX_W5_C3, ORX_W5_C4, ORX_W5_C5};
+        double sc = 1.0;
+        for (int k = 0; k < 6; k++, sc *= irr) {
+            const double v = ck[k] * sc;
+            df = df && std::isfinite(v) && std::fabs(v) < 1e37 && (v == 0.0 || std::fabs(v) > 1e-37);
+            wp.c[k] = (float)v;
+        }
+    }
+    if (pb.nsub == 1) {
+        if (df) hipLaunchKernelGGL((k_ppm_gather_union<1, true>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles, wp);
+        else hipLaunchKernelGGL((k_ppm_gather_union<1, false>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles, wp);
+    } else {
+        if (df) hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR, true>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles, wp);
+        else hipLaunchKernelGGL((k_ppm_gather_union<SUBR * SUBR, false>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles, wp);
+    }
 }
 
 /* ------------------------------------------------------------------ */
