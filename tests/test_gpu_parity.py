@@ -99,6 +99,49 @@ def test_ppm_parity(scene_name, W, H, P, gather_variant):
     ora.close()
 
 
+@pytest.mark.parametrize("radius", [None, 5000.0])
+def test_ppm_union_weight_forms(radius):
+    """The union gather evaluates its weight polynomial in d^2 with per-launch coefficients c_k / r^(2k)
+    (launch_ppm_gather), falling back to the polynomial in u = d^2 / r^2 where a scaled coefficient
+    leaves the normal float range: a 5000-unit radius over the 550-unit Cornell box takes the fallback
+    (c_5 / r^10 ~ 1e-39; every photon is a candidate of every pixel).  Both forms against the oracle
+    (accepted sets exact), and the u form forced (ORX_GATHER_DFORM=0) in a child process."""
+    import subprocess, sys, os, json
+    if radius is None:
+        code = r'''
+import json, sys
+sys.path.insert(0, "tests")
+import test_gpu_parity as t
+from oppositerenderer_amd import _abi, scenes
+from oppositerenderer_amd.renderer import next_ppm_radius
+scene = scenes.scene_by_name("Cornell")
+gpu, ora, det = t.make_pair(scene, 64, 48, 64, _abi.PROGRESSIVE_PHOTON_MAPPING)
+r = scene.initial_ppm_radius()
+for it in range(2):
+    gpu.renderNextIteration(it, it, r, True, det)
+    ora.render_next_iteration(it, it, r, det.to_abi())
+    t.check_ppm_iteration(gpu, ora)
+    r = next_ppm_radius(r, it)
+print(json.dumps({"err": t.rel_l2(gpu.getOutputBuffer(), ora.output())}))
+'''
+        env = dict(os.environ, ORX_GATHER_DFORM="0")
+        out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110,
+                             cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert out.returncode == 0, out.stderr[-2000:]
+        assert json.loads(out.stdout.strip().splitlines()[-1])["err"] < 1e-4
+        return
+    scene = scenes.scene_by_name("Cornell")
+    gpu, ora, det = make_pair(scene, 48, 40, 64, _abi.PROGRESSIVE_PHOTON_MAPPING)
+    req = det.to_abi()
+    for it in range(2):
+        gpu.renderNextIteration(it, it, radius, True, det)
+        ora.render_next_iteration(it, it, radius, req)
+        check_ppm_iteration(gpu, ora)
+    assert rel_l2(gpu.getOutputBuffer(), ora.output()) < 1e-4
+    gpu.destroy()
+    ora.close()
+
+
 @pytest.mark.parametrize("scene_name,W,H", [("Cornell", 64, 64), ("CornellSmallLargeSphere", 48, 48),
                                             ("CornellSmallSmallSpheres", 48, 40)])
 def test_pt_parity(scene_name, W, H):
