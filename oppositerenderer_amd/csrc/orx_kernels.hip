@@ -1025,18 +1025,22 @@ __device__ __forceinline__ v2f weight2u(v2f u) {
     p = __builtin_elementwise_fma(p, u, v2f{ORX_W5_C1, ORX_W5_C1});
     return __builtin_elementwise_fma(p, u, v2f{ORX_W5_C0, ORX_W5_C0});
 }
-/* The union gather's form: the same polynomial in d^2, coefficients c_k / r^(2k) (one radius per
- * launch: uniform, in SGPRs), so the u = d^2 / r^2 multiply per pair leaves the batch.  The host
- * takes it only where every scaled coefficient is a finite float (launch_ppm_gather). */
+/* The union gather's form: the same polynomial in d^2 with coefficients c_k / r^(2k) (one radius per
+ * launch: uniform, in SGPRs), so the u = d^2 / r^2 multiply per pair leaves the batch, and divided
+ * through by the d^8 coefficient c_4 / r^8 (`scale`), so the first Horner step adds the inline
+ * constant 1 (a coefficient pair in the first step would need a VGPR copy per batch: the packed
+ * FMA reads one SGPR operand); the lane's sums are multiplied by `scale` once at the end.  The host
+ * takes it only where the coefficients and the scale keep the sums in range (launch_ppm_gather). */
 struct WPoly {
-    float c[6];
+    float k[6]; /* k[4] = 1 */
+    float scale;
 };
 __device__ __forceinline__ v2f weight2d(v2f d2, const WPoly& w) {
-    v2f p = __builtin_elementwise_fma(v2f{w.c[5], w.c[5]}, d2, v2f{w.c[4], w.c[4]});
-    p = __builtin_elementwise_fma(p, d2, v2f{w.c[3], w.c[3]});
-    p = __builtin_elementwise_fma(p, d2, v2f{w.c[2], w.c[2]});
-    p = __builtin_elementwise_fma(p, d2, v2f{w.c[1], w.c[1]});
-    return __builtin_elementwise_fma(p, d2, v2f{w.c[0], w.c[0]});
+    v2f p = __builtin_elementwise_fma(v2f{w.k[5], w.k[5]}, d2, v2f{1.f, 1.f});
+    p = __builtin_elementwise_fma(p, d2, v2f{w.k[3], w.k[3]});
+    p = __builtin_elementwise_fma(p, d2, v2f{w.k[2], w.k[2]});
+    p = __builtin_elementwise_fma(p, d2, v2f{w.k[1], w.k[1]});
+    return __builtin_elementwise_fma(p, d2, v2f{w.k[0], w.k[0]});
 }
 /* int8 facing prefilter dot products of four photons' direction words with the hit point's nq.
  * gfx950 runs v_dot* like its matrix-core instructions: another VALU instruction may read a dot's
@@ -1612,7 +1616,12 @@ __global__ __launch_bounds__(256, ORX_UNION_WAVES) void k_ppm_gather_union(Gathe
     atomicAdd((unsigned long long*)&pb.grid->st_accepted, (unsigned long long)ts_tris);
 #endif
     if (live) {
-        const float ax = accx.x + accx.y, ay = accy.x + accy.y, az = accz.x + accz.y;
+        float ax = accx.x + accx.y, ay = accy.x + accy.y, az = accz.x + accz.y;
+        if (DF) {
+            ax *= wp.scale;
+            ay *= wp.scale;
+            az *= wp.scale;
+        }
         const f3 att = mk(B.w, Cc.x, Cc.y);
         const float s1 = 1.0f / (ORX_PI_F * c.ppm_radius2);
         const float s2 = 1.0f / c.emitted_f;
@@ -1757,12 +1766,17 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
     {
         const double irr = (double)(1.0f / c.ppm_radius2);
         const double ck[6] = {ORX_W5_C0, ORX_W5_C1, ORX_W5_C2, ORX_W5_C3, ORX_W5_C4, ORX_W5_C5};
+        const double c4 = ck[4] * irr * irr * irr * irr;
+        /* sums of powers times weights / scale stay far inside fp32 for scale in [1e-20, 1e20] */
+        df = df && std::isfinite(c4) && std::fabs(c4) >= 1e-20 && std::fabs(c4) <= 1e20;
         double sc = 1.0;
         for (int k = 0; k < 6; k++, sc *= irr) {
-            const double v = ck[k] * sc;
-            df = df && std::isfinite(v) && std::fabs(v) < 1e37 && (v == 0.0 || std::fabs(v) > 1e-37);
-            wp.c[k] = (float)v;
+            const double v = ck[k] * sc / c4;
+            df = df && std::isfinite(v) && std::fabs(v) < 1e37 && std::fabs(v) > 1e-37;
+            wp.k[k] = (float)v;
         }
+        wp.k[4] = 1.f;
+        wp.scale = (float)c4;
     }
     if (pb.nsub == 1) {
         if (df) hipLaunchKernelGGL((k_ppm_gather_union<1, true>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles, wp);

@@ -102,9 +102,9 @@ def test_ppm_parity(scene_name, W, H, P, gather_variant):
 @pytest.mark.parametrize("radius", [None, 5000.0])
 def test_ppm_union_weight_forms(radius):
     """The union gather evaluates its weight polynomial in d^2 with per-launch coefficients c_k / r^(2k)
-    (launch_ppm_gather), falling back to the polynomial in u = d^2 / r^2 where a scaled coefficient
-    leaves the normal float range: a 5000-unit radius over the 550-unit Cornell box takes the fallback
-    (c_5 / r^10 ~ 1e-39; every photon is a candidate of every pixel).  Both forms against the oracle
+    divided through by c_4 / r^8 (launch_ppm_gather), falling back to the polynomial in u = d^2 / r^2 where
+    that scale leaves [1e-20, 1e20]: a 5000-unit radius over the 550-unit Cornell box takes the fallback
+    (c_4 / r^8 ~ 2e-31; every photon is a candidate of every pixel).  Both forms against the oracle
     (accepted sets exact), and the u form forced (ORX_GATHER_DFORM=0) in a child process."""
     import subprocess, sys, os, json
     if radius is None:
