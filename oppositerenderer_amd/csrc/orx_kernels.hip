@@ -1373,7 +1373,9 @@ template <bool RANGE, bool DF>
 __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uint32_t c, uint32_t ce, uint32_t lo,
                                                 uint32_t len, float r2, const UConst& k, const WPoly& wp, UAcc& a) {
     const float4* L4 = reinterpret_cast<const float4*>(L);
-    for (uint32_t e = 0; e < ce; e += 4) {
+    /* one batch of four; two per loop step, so the second batch's LDS reads take the first's address
+     * plus an offset (one address increment per two batches) */
+    auto batch = [&](const uint32_t e) {
         const uint32_t kb = c + e;
         const float4 X = L4[e >> 2], Y = L4[16 + (e >> 2)], Z = L4[32 + (e >> 2)];
         const v2f dx0 = pk_sub_blo(k.pxy, lo2(X)), dx1 = pk_sub_blo(k.pxy, hi2(X));
@@ -1389,7 +1391,7 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
             in2 = in2 && t + 2 < len;
             in3 = in3 && t + 3 < len;
         }
-        if (!wave_any(in0 | in1 | in2 | in3)) continue;
+        if (!wave_any(in0 | in1 | in2 | in3)) return;
         const uint4 Q = reinterpret_cast<const uint4*>(L4)[48 + (e >> 2)];
         int32_t q0, q1, q2, q3;
         sdot4x4(Q.x, Q.y, Q.z, Q.w, k.nq, q0, q1, q2, q3);
@@ -1433,6 +1435,10 @@ __device__ __forceinline__ void union_chunk_lds(const float* __restrict__ L, uin
             a.accy = __builtin_elementwise_fma(hi2(WY), w1, a.accy);
             a.accz = __builtin_elementwise_fma(hi2(WZ), w1, a.accz);
         }
+    };
+    for (uint32_t e = 0; e < ce; e += 8) {
+        batch(e);
+        if (e + 4 < ce) batch(e + 4);
     }
 }
 
