@@ -1762,7 +1762,8 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
         else hipLaunchKernelGGL((k_ppm_gather<SUBR * SUBR>), grid, dim3(256), 0, s, gi, pb, c, ntx, ntiles);
         return;
     }
-    /* the weight polynomial in d^2 (weight2d) where its scaled coefficients are finite floats */
+    /* the weight polynomial in d^2 divided through by c_4 / r^8 (weight2d) where that scale and the
+     * coefficients are normal floats; else in u = d^2 / r^2 (weight2u) */
     static const int dform_env = [] {
         const char* e = getenv("ORX_GATHER_DFORM");
         return e ? atoi(e) : 1;
@@ -1773,7 +1774,7 @@ void launch_ppm_gather(hipStream_t s, const GatherIn& gi, const PhotonBufs& pb, 
         const double irr = (double)(1.0f / c.ppm_radius2);
         const double ck[6] = {ORX_W5_C0, ORX_W5_C1, ORX_W5_C2, ORX_W5_C3, ORX_W5_C4, ORX_W5_C5};
         const double c4 = ck[4] * irr * irr * irr * irr;
-        /* sums of powers times weights / scale stay far inside fp32 for scale in [1e-20, 1e20] */
+        /* a lane's sums carry a factor 1 / scale until the end: far inside fp32 for a scale in [1e-20, 1e20] */
         df = df && std::isfinite(c4) && std::fabs(c4) >= 1e-20 && std::fabs(c4) <= 1e20;
         double sc = 1.0;
         for (int k = 0; k < 6; k++, sc *= irr) {
